@@ -1,0 +1,205 @@
+/*
+ * marshrutka_pf.h — C ABI of the MI355X-native grid shortest-path engine.
+ *
+ * This is the drop-in boundary for marshrutka's pathfinder hot path
+ * (SURVEY.md §8b).  In the reference the path is a crate-private Rust API:
+ *
+ *   pub struct FindPath<'a> { .. }                 src/pathfinder.rs:183-196
+ *   pub fn eval(self, from, to) -> Option<TotalCost>  src/pathfinder.rs:199-248
+ *   fn MapGrid::parse(&str) -> Result<MapGrid>       src/grid.rs:47-237
+ *
+ * Every entry point below names the reference item it replaces.  Types are
+ * plain C PODs (no torch / HIP types in any signature) so a Rust `extern "C"`
+ * block, ctypes or a C++ caller can bind them directly.
+ *
+ * Conventions
+ *  - All functions return an int status (mr_status); they never abort.
+ *  - The caller owns every buffer it passes in.
+ *  - A grid handle is immutable after creation; concurrent queries on one
+ *    grid from several host threads are safe.
+ *  - Widths: the reference stores homeland positions / border shifts in u8
+ *    and cell coordinates in i8 (src/index.rs:35-46, src/cell.rs:33-34), which
+ *    caps the grid at odd S <= 255.  This ABI widens them to u16 so the
+ *    BASELINE sizes (S = 1025, 4097) are representable; for S <= 255 every
+ *    result is identical to the reference's.
+ */
+#ifndef MARSHRUTKA_PF_H
+#define MARSHRUTKA_PF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MR_ABI_VERSION 1u
+
+/* ---- status codes ------------------------------------------------------ */
+typedef enum mr_status {
+    MR_OK = 0,
+    MR_NOT_FOUND = 1,          /* eval() returned None (src/pathfinder.rs:247) */
+    MR_ERR_INVALID_ARG = -1,   /* null pointer, bad enum value, ...            */
+    MR_ERR_INVALID_GRID = -2,  /* MapGrid::parse would fail (src/grid.rs:60-133) or
+                                  the cell labels are not a consistent 4-grid     */
+    MR_ERR_INVALID_INDEX = -3, /* a CellIndex that is not in the grid; the
+                                  reference panics here (src/grid.rs:288-290)    */
+    MR_ERR_CAPACITY = -4,      /* caller's command buffer too small; n written   */
+    MR_ERR_DEVICE = -5,        /* HIP runtime error                              */
+    MR_ERR_LIMIT = -6,         /* grid or label exceeds an engine limit           */
+    MR_ERR_NO_DEVICE = -7      /* no gfx950 device visible: the engine has no CPU
+                                  fallback and fails loudly                       */
+} mr_status;
+
+/* ---- vertex naming (src/index.rs:23-46, src/homeland.rs:26-32) ---------- */
+enum { MR_CELL_CENTER = 0, MR_CELL_HOMELAND = 1, MR_CELL_BORDER = 2 };
+enum { MR_HOMELAND_BLUE = 0, MR_HOMELAND_RED = 1, MR_HOMELAND_GREEN = 2, MR_HOMELAND_YELLOW = 3 };
+enum { MR_BORDER_BR = 0, MR_BORDER_RG = 1, MR_BORDER_GY = 2, MR_BORDER_YB = 3 };
+
+/* CellIndex (src/index.rs:41-46).  kind = MR_CELL_*;
+ *   CENTER:   sub = x = y = 0
+ *   HOMELAND: sub = homeland, x/y = Pos{x,y} (both >= 1 once canonical)
+ *   BORDER:   sub = border, x = shift (>= 1), y = 0
+ * Field order gives the derived Ord of the reference (variant, then fields). */
+typedef struct mr_cell_index {
+    uint8_t kind;
+    uint8_t sub;
+    uint16_t x;
+    uint16_t y;
+    uint16_t reserved; /* must be 0 */
+} mr_cell_index;
+
+/* ---- grid construction (replaces MapGrid::parse's output, src/grid.rs:31-38) */
+enum { MR_POI_NONE = 0, MR_POI_CAMPFIRE = 1, MR_POI_FOUNTAIN = 2, MR_POI_FORUM = 3 };
+
+/* One map cell.  Cells are passed row-major exactly as MapGrid::parse scans
+ * them (src/grid.rs:64-77): cell i sits at x = i % S - S/2, y = i / S - S/2. */
+typedef struct mr_cell {
+    mr_cell_index index;
+    uint8_t poi;          /* MR_POI_*  (src/cell.rs:192-201) */
+    uint8_t reserved[7];
+} mr_cell;
+
+typedef struct mr_grid mr_grid; /* opaque, immutable */
+
+/* Builds the grid and its per-cell precompute (nearest campfire per homeland,
+ * src/grid.rs:134-230,297-325).  n_cells must be S*S for odd S.
+ * Errors: MR_ERR_INVALID_GRID for the reference's parse errors (not square,
+ * Center missing / not at (0,0)) and for cell labels whose index adjacency
+ * (src/pathfinder.rs:24-138) is not the geometric 4-neighbourhood. */
+int mr_grid_create(const mr_cell *cells, uint32_t n_cells, mr_grid **out);
+void mr_grid_destroy(mr_grid *grid);
+/* MapGrid::square_size / homeland_size (src/grid.rs:280-282) */
+uint32_t mr_grid_square_size(const mr_grid *grid);
+
+/* ---- query parameters: every FindPath field (src/pathfinder.rs:183-196) -- */
+enum { MR_SORT_LEGS = 0, MR_SORT_TIME = 1, MR_SORT_MONEY = 2 }; /* CostComparator, src/cost.rs:76-81 */
+
+typedef struct mr_params {
+    uint32_t scroll_of_escape_cost;        /* SoE money  */
+    uint32_t scroll_of_escape_hq_cost;     /* SHQ money  */
+    uint32_t scroll_of_escape_forum_cost;  /* SFm money  */
+    uint8_t use_soe;
+    uint8_t use_sfm;
+    uint8_t use_caravans;
+    uint8_t has_hq;                        /* hq_position: Option<CellIndex> */
+    mr_cell_index hq_position;
+    uint32_t route_guru;                   /* RouteGuru(u32); >5 behaves as 0 (src/skill.rs:21-30) */
+    uint32_t fleetfoot;                    /* Fleetfoot(u32); >3 behaves as 0 */
+    uint8_t sort_by[2];                    /* (CostComparator, CostComparator) */
+    uint8_t homeland;                      /* MR_HOMELAND_* */
+    uint8_t reserved;
+} mr_params;
+
+/* The app's defaults (src/app.rs:782-811, update_path :704-731):
+ * sort (Legs, Money); SoE 50, SHQ 75, SFm 100; use_soe, use_caravans; no HQ;
+ * skills 0; homeland Blue. */
+void mr_params_default(mr_params *p);
+
+/* ---- results (TotalCost / Command, src/cost.rs:83-206) ------------------ */
+enum {
+    MR_CMD_NO_MOVE = 0, MR_CMD_CENTRAL = 1, MR_CMD_STANDARD = 2, MR_CMD_CARAVAN = 3,
+    MR_CMD_SOE = 4, MR_CMD_SHQ = 5, MR_CMD_SFM = 6
+}; /* AggregatedCost variants in declaration (= Ord) order, src/cost.rs:90-110 */
+
+/* Command { aggregated_cost, from, to }.  Only the fields of the variant are
+ * meaningful, the rest are 0:  CENTRAL{time}; STANDARD{time(raw, before the
+ * Fleetfoot ceil), legs, fleetfoot}; CARAVAN{time, money}; SOE/SHQ/SFM{money}. */
+typedef struct mr_command {
+    uint8_t kind;
+    uint8_t reserved[3];
+    uint32_t legs;
+    uint32_t money;
+    uint32_t fleetfoot;
+    int64_t time_s;
+    mr_cell_index from;
+    mr_cell_index to;
+} mr_command;
+
+/* TotalCost { legs, money, time, commands }.  status is the per-query
+ * mr_status (MR_OK, MR_NOT_FOUND, MR_ERR_INVALID_INDEX, MR_ERR_CAPACITY). */
+typedef struct mr_result {
+    uint32_t legs;
+    uint32_t money;
+    int64_t time_s;
+    uint32_t n_commands;
+    uint32_t command_offset; /* into the batch's command pool */
+    int32_t status;
+    uint32_t reserved;
+} mr_result;
+
+typedef struct mr_query {
+    mr_cell_index from;
+    mr_cell_index to;
+} mr_query;
+
+/* ---- single query: FindPath { params.., grid }.eval(from, to) ------------
+ * Replaces src/pathfinder.rs:199-248.  Writes the label into *out and up to
+ * cap commands into cmds.  Returns MR_OK, MR_NOT_FOUND (None), or an error;
+ * MR_ERR_CAPACITY means out->n_commands > cap (nothing truncated silently). */
+int mr_find_path(const mr_grid *grid, const mr_params *params, mr_cell_index from,
+                 mr_cell_index to, mr_result *out, mr_command *cmds, uint32_t cap);
+
+/* ---- batched queries (the GPU hot path) ---------------------------------
+ * Answers n independent (from,to) queries.  Queries sharing a source share one
+ * single-source solve on the device.  results[i].command_offset indexes pool;
+ * the call returns MR_ERR_CAPACITY if pool_cap is smaller than the total number
+ * of commands (results[] are still filled so the caller can size the pool). */
+int mr_find_path_batch(const mr_grid *grid, const mr_params *params, const mr_query *queries,
+                       uint32_t n, mr_result *results, mr_command *pool, uint64_t pool_cap);
+
+/* ---- device-resident plans (bench / multi-GPU) -------------------------- */
+typedef struct mr_plan mr_plan;
+
+/* Uploads the grid and the query batch to the current HIP device and groups
+ * queries by source.  Inputs stay resident in HBM across mr_plan_run calls. */
+int mr_plan_create(const mr_grid *grid, const mr_params *params, const mr_query *queries,
+                   uint32_t n, mr_plan **out);
+/* Enqueues one full pass of the hot path on `stream` (a hipStream_t, or NULL
+ * for the plan's own stream).  Asynchronous. */
+int mr_plan_run(mr_plan *plan, void *stream);
+/* Waits for the plan's work and copies results/commands to host buffers. */
+int mr_plan_fetch(mr_plan *plan, mr_result *results, mr_command *pool, uint64_t pool_cap);
+/* Device pointers of the compact per-query output records (for an RCCL
+ * gather): n * 16 B result records and n * max_cmds * 16 B command slots. */
+int mr_plan_device_outputs(mr_plan *plan, void **d_results, uint64_t *results_bytes,
+                           void **d_commands, uint64_t *commands_bytes);
+/* Number of unique sources (= single-source solves per pass). */
+uint32_t mr_plan_num_sources(const mr_plan *plan);
+/* Average device time (ms) of the main solve kernel over the last
+ * mr_plan_run calls since the previous call to this function, measured with
+ * HIP events on the stream the kernel is launched on. */
+double mr_plan_kernel_ms(mr_plan *plan, uint32_t *n_launches);
+void mr_plan_destroy(mr_plan *plan);
+
+/* ---- misc ---------------------------------------------------------------- */
+uint32_t mr_abi_version(void);
+/* Human-readable description of the last error on this thread. */
+const char *mr_last_error(void);
+/* 1 if a gfx950 device is visible to this process. */
+int mr_device_available(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MARSHRUTKA_PF_H */
