@@ -1,0 +1,116 @@
+// mr_engine.hpp — data layout shared by the host planner and the gfx950 kernels.
+//
+// Algorithm: a single-source solve computes the unique fixed
+// point L(v) = min_u extend(L(u), u->v) of the reference's Dijkstra
+// (src/pathfinder.rs:199-248; uniqueness: SURVEY.md §8a).  Two facts shape the
+// layout:
+//  * every vertex that is not a "special" (Center, the four border-1 cells,
+//    campfires, HQ) has only StandardMove in-edges, so its label is a walk
+//    L(b).commands ++ [StandardMove{k} b->v] from a *boundary* b that is the
+//    source or a special (src/cost.rs:246-264 merges the run).  Such a label is
+//    stored in ONE 32-bit word: (b, k).
+//  * specials (<= ~300) keep full labels in an LDS table as a parent pointer
+//    plus <= 2 tail commands; command lists compare by walking parents.
+// Vertices are settled bucket by bucket on the comparator's leading metric
+// (plain vertices of one bucket are independent), specials inside a bucket by
+// an exact one-wave Dijkstra.
+#pragma once
+#include <stdint.h>
+
+namespace mr {
+
+constexpr uint32_t kNone10 = 0x3FFu;          // "no index" in a 10-bit field
+constexpr uint32_t kMaxSpecials = 1021u;      // table indices 1..1021 (0 = source)
+constexpr uint32_t kStSettled = 0x80000000u;  // grid state word flags
+constexpr uint32_t kStDirty = 0x40000000u;
+constexpr uint32_t kStBShift = 20u;
+constexpr uint32_t kStKMask = 0xFFFFFu;       // walk run length k < 2^20
+constexpr uint32_t kStUntouched = kNone10 << kStBShift;
+
+// command kinds = AggregatedCost variant order (src/cost.rs:90-110)
+enum : uint32_t { kNoMove = 0, kCentral = 1, kStandard = 2, kCaravan = 3, kSoE = 4, kSHQ = 5, kSFm = 6 };
+
+// A command: kp = kind << 29 | payload.  payload: Standard k (legs of the run),
+// Central j (moves merged), Caravan (d << 1 | coef==5), scrolls/NoMove 0.
+// Comparing kp as an unsigned integer is the derived Ord of AggregatedCost for
+// one query (time = 180k / 10j / d*rgt are monotone in the payload; the
+// Caravan money d*coef orders by the coef bit at equal d).
+struct Cmd {
+    uint32_t kp;
+    uint32_t from;  // vertex id (row-major)
+    uint32_t to;
+};
+
+// A full label of a special (or the source), src/cost.rs:187-206:
+//   commands = full(parent) ++ tail[0..ntail)   (parent 0 = empty prefix)
+struct Rec {
+    uint32_t m[3];     // legs, money, time  (metric index order)
+    uint16_t len;      // commands.len()
+    uint8_t ntail;     // 1 or 2
+    uint8_t state;     // 0 none, 1 tentative, 2 settled
+    uint16_t parent;   // table index of the prefix label, 0 = root
+    uint16_t pad;
+    Cmd tail[2];
+};
+static_assert(sizeof(Rec) == 44, "Rec layout");
+
+// Static per-special info (one entry per table index 1..NS; entry 0 unused).
+struct SpecialStatic {
+    uint32_t v;       // vertex id
+    int32_t x, y;     // geometric coordinates
+    uint32_t flags;   // bit0 center, bit1 border-1, bit2 caravan hub
+    uint32_t region;  // table index of this cell's nearest campfire (query homeland), kNone10 if none
+    uint32_t coef5;   // 1 if a caravan INTO this special costs 5/distance (else 2)
+};
+constexpr uint32_t kSpCenter = 1u, kSpBorder1 = 2u, kSpHub = 4u;
+
+// bucket modes: leading comparator metric(s) used as the settle bucket
+enum : uint32_t { kBucketLegs = 0, kBucketTime = 1, kBucketMoneyLegs = 2, kBucketMoneyTime = 3 };
+
+struct DevParams {
+    uint32_t S, H, V, vc;         // side, half side, vertices, Center vertex id
+    uint32_t perm[3];             // comparator metrics c1,c2,c3 as indices into m[] (0 legs, 1 money, 2 time)
+    uint32_t bucket_mode;
+    uint32_t W;                   // time bucket width = min StandardMove time increment
+    uint32_t ff;                  // Fleetfoot level stored in Standard commands
+    uint32_t ff_num, ff_den;      // Fleetfoot ratio (1/1 when level 0 or out of range)
+    uint32_t rgt;                 // caravan seconds per distance unit (RouteGuru applied)
+    uint32_t soe_cost, shq_cost, sfm_cost;
+    uint32_t use_soe, use_sfm, use_caravans;
+    uint32_t hq_t;                // table index of HQ, 0 if no SHQ
+    uint32_t NS;                  // number of specials
+    uint32_t n_hubs;              // caravan hubs (Center + campfires), table indices in hubs[]
+    uint32_t max_cmds;            // command slots per query in the output
+};
+
+// compact per-query output (expanded to mr_result/mr_command on the host)
+struct OutResult {
+    uint32_t legs, money, time;
+    uint32_t ncmd_status;  // low 16 bits: n_commands; high 16 bits: status code + 16
+};
+struct OutCmd {
+    uint32_t kp, from, to, pad;
+};
+
+// kernel arguments (one solve launch)
+struct KArgs {
+    DevParams p;
+    const uint32_t *sinfo;       // V words: special idx (10b) | region idx << 10
+    const uint32_t *rank;        // V words: position in CellIndex order
+    const SpecialStatic *sp;     // NS+1 entries
+    const uint16_t *hubs;        // n_hubs caravan endpoints (table indices)
+    const uint32_t *src_v;       // nsrc source vertices
+    const uint32_t *q_begin;     // nsrc+1 offsets into q_dst/q_id
+    const uint32_t *q_dst;       // destinations grouped by source
+    const uint32_t *q_id;        // query id of each grouped destination
+    OutResult *out_res;          // per query id
+    OutCmd *out_cmd;             // per query id * max_cmds
+    uint32_t *ws;                // grid-in-HBM mode: per-workgroup slots of 5*V words
+    uint32_t *counter;           // [0] source dequeue, [1] error flags
+    uint32_t nsrc;
+    uint32_t early_exit_max;     // early exit if a source has <= this many destinations (<= 64)
+};
+
+constexpr uint32_t kErrKOverflow = 1u, kErrMetricOverflow = 2u, kErrBucket = 4u, kErrChain = 8u;
+
+}  // namespace mr

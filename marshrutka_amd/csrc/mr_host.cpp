@@ -1,0 +1,729 @@
+// mr_host.cpp — host side of libmarshrutka_pf.so: grid construction and
+// validation, per-query planning, the C ABI of include/marshrutka_pf.h.
+//
+// There is no CPU fallback: every query runs on the gfx950 device; without one
+// the entry points return MR_ERR_NO_DEVICE (include/marshrutka_pf.h).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/marshrutka_pf.h"
+#include "mr_engine.hpp"
+
+namespace mr {
+uint32_t lds_bytes(uint32_t NS, uint32_t V, bool grid_in_lds);
+hipError_t launch_sssp(const KArgs &a, bool grid_in_lds, uint32_t blocks, hipStream_t stream);
+int max_blocks_per_cu(bool grid_in_lds, uint32_t bytes);
+}  // namespace mr
+
+
+using namespace mr;
+
+static thread_local std::string g_last_error;
+static int fail(int code, const std::string &msg) {
+    g_last_error = msg;
+    return code;
+}
+
+// ------------------------------------------------------------------ CellIndex
+static inline uint64_t ci_key(const mr_cell_index &c) {
+    return (uint64_t(c.kind) << 48) | (uint64_t(c.sub) << 40) | (uint64_t(c.x) << 20) | uint64_t(c.y);
+}
+static inline mr_cell_index ci_make(uint8_t kind, uint8_t sub, uint16_t x, uint16_t y) {
+    mr_cell_index c;
+    c.kind = kind;
+    c.sub = sub;
+    c.x = x;
+    c.y = y;
+    c.reserved = 0;
+    return c;
+}
+// CellIndexBuilder::build (src/index.rs:257-312)
+static mr_cell_index build_homeland(int h, int x, int y) {
+    if (x == 0 && y == 0) return ci_make(MR_CELL_CENTER, 0, 0, 0);
+    if (x == 0) return ci_make(MR_CELL_BORDER, (h == MR_HOMELAND_YELLOW || h == MR_HOMELAND_BLUE) ? MR_BORDER_YB : MR_BORDER_RG, uint16_t(y), 0);
+    if (y == 0) return ci_make(MR_CELL_BORDER, (h == MR_HOMELAND_BLUE || h == MR_HOMELAND_RED) ? MR_BORDER_BR : MR_BORDER_GY, uint16_t(x), 0);
+    return ci_make(MR_CELL_HOMELAND, uint8_t(h), uint16_t(x), uint16_t(y));
+}
+static mr_cell_index build_border(int b, int s) {
+    if (s == 0) return ci_make(MR_CELL_CENTER, 0, 0, 0);
+    return ci_make(MR_CELL_BORDER, uint8_t(b), uint16_t(s), 0);
+}
+static bool canonical(const mr_cell_index &c) {
+    if (c.reserved) return false;
+    if (c.kind == MR_CELL_CENTER) return c.sub == 0 && c.x == 0 && c.y == 0;
+    if (c.kind == MR_CELL_HOMELAND) return c.sub < 4 && c.x >= 1 && c.y >= 1;
+    if (c.kind == MR_CELL_BORDER) return c.sub < 4 && c.x >= 1 && c.y == 0;
+    return false;
+}
+// The StandardMove/CentralMove neighbours the reference generates for a cell
+// (Inflight::edges, src/pathfinder.rs:24-138), used to validate that the map's
+// labels form the geometric 4-grid the kernels traverse implicitly.
+static void index_neighbours(const mr_cell_index &v, int H, std::vector<uint64_t> &out) {
+    static const int bn[4][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 0}};  // Border::neighbours
+    static const int hb[4][2] = {{MR_BORDER_BR, MR_BORDER_YB}, {MR_BORDER_BR, MR_BORDER_RG},
+                                 {MR_BORDER_GY, MR_BORDER_RG}, {MR_BORDER_GY, MR_BORDER_YB}};  // [h][hor, vert]
+    out.clear();
+    if (v.kind == MR_CELL_CENTER) {
+        for (int b = 0; b < 4; ++b) out.push_back(ci_key(build_border(b, 1)));
+    } else if (v.kind == MR_CELL_BORDER) {
+        int b = v.sub, s = v.x;
+        out.push_back(ci_key(build_border(b, s - 1)));
+        if (s < H) out.push_back(ci_key(build_border(b, s + 1)));
+        bool horizontal = (b == MR_BORDER_BR || b == MR_BORDER_GY);
+        for (int k = 0; k < 2; ++k)
+            out.push_back(ci_key(horizontal ? build_homeland(bn[b][k], s, 1) : build_homeland(bn[b][k], 1, s)));
+    } else {
+        int h = v.sub, x = v.x, y = v.y;
+        out.push_back(ci_key(x == 1 ? build_border(hb[h][1], y) : build_homeland(h, x - 1, y)));
+        out.push_back(ci_key(y == 1 ? build_border(hb[h][0], x) : build_homeland(h, x, y - 1)));
+        if (x < H) out.push_back(ci_key(build_homeland(h, x + 1, y)));
+        if (y < H) out.push_back(ci_key(build_homeland(h, x, y + 1)));
+    }
+    std::sort(out.begin(), out.end());
+}
+
+// ------------------------------------------------------------------ grid
+struct mr_grid {
+    uint32_t S = 0, H = 0, V = 0, vc = 0;
+    std::vector<mr_cell_index> idx;
+    std::vector<uint8_t> poi;
+    std::unordered_map<uint64_t, uint32_t> index;
+    std::vector<uint32_t> rank;
+    std::vector<uint32_t> campfires;       // vertex ids, CellIndex order
+    std::vector<uint32_t> nearest[4];      // nearest campfire vertex per homeland (kNone32)
+    int32_t gx(uint32_t v) const { return int32_t(v % S) - int32_t(H); }
+    int32_t gy(uint32_t v) const { return int32_t(v / S) - int32_t(H); }
+    bool find(const mr_cell_index &c, uint32_t &v) const {
+        if (!canonical(c)) return false;
+        auto it = index.find(ci_key(c));
+        if (it == index.end()) return false;
+        v = it->second;
+        return true;
+    }
+};
+
+static constexpr uint32_t kNone32 = 0xFFFFFFFFu;
+
+extern "C" int mr_grid_create(const mr_cell *cells, uint32_t n, mr_grid **out) {
+    if (!cells || !out) return fail(MR_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    uint64_t s = 0;
+    while ((s + 1) * (s + 1) <= n) ++s;
+    if (s * s != n) return fail(MR_ERR_INVALID_GRID, "map grid is not square (src/grid.rs:60-63)");
+    if (s < 3 || s % 2 == 0) return fail(MR_ERR_INVALID_GRID, "square size must be odd and >= 3");
+    if (s > 65535) return fail(MR_ERR_LIMIT, "square size above 65535");
+    auto g = new mr_grid();
+    g->S = uint32_t(s);
+    g->H = g->S / 2;
+    g->V = n;
+    g->idx.resize(n);
+    g->poi.resize(n);
+    g->index.reserve(n * 2);
+    for (uint32_t i = 0; i < n; ++i) {
+        mr_cell_index c = cells[i].index;
+        // MapGrid::parse builds every index canonically (src/index.rs:419-431)
+        if (c.kind == MR_CELL_HOMELAND && c.sub < 4) c = build_homeland(c.sub, c.x, c.y);
+        else if (c.kind == MR_CELL_BORDER && c.sub < 4 && c.y == 0) c = build_border(c.sub, c.x);
+        if (!canonical(c) || cells[i].poi > MR_POI_FORUM || cells[i].index.reserved) {
+            delete g;
+            return fail(MR_ERR_INVALID_GRID, "invalid cell index or poi at cell " + std::to_string(i));
+        }
+        if (!g->index.emplace(ci_key(c), i).second) {
+            delete g;
+            return fail(MR_ERR_INVALID_GRID, "duplicate cell index at cell " + std::to_string(i));
+        }
+        g->idx[i] = c;
+        g->poi[i] = cells[i].poi;
+    }
+    uint32_t vc;
+    if (!g->find(ci_make(MR_CELL_CENTER, 0, 0, 0), vc) || g->gx(vc) != 0 || g->gy(vc) != 0) {
+        delete g;
+        return fail(MR_ERR_INVALID_GRID, "Center missing or not at (0,0) (src/grid.rs:122-133)");
+    }
+    g->vc = vc;
+    // the index adjacency must be the geometric 4-neighbourhood
+    std::vector<uint64_t> a, b;
+    const int S_ = int(g->S);
+    for (uint32_t v = 0; v < n; ++v) {
+        const mr_cell_index &c = g->idx[v];
+        if ((c.kind == MR_CELL_HOMELAND && (c.x > g->H || c.y > g->H)) || (c.kind == MR_CELL_BORDER && c.x > g->H)) {
+            delete g;
+            return fail(MR_ERR_INVALID_GRID, "cell index outside the homeland size");
+        }
+        index_neighbours(c, int(g->H), a);
+        b.clear();
+        int x = int(v % g->S), y = int(v / g->S);
+        if (x > 0) b.push_back(ci_key(g->idx[v - 1]));
+        if (x + 1 < S_) b.push_back(ci_key(g->idx[v + 1]));
+        if (y > 0) b.push_back(ci_key(g->idx[v - g->S]));
+        if (y + 1 < S_) b.push_back(ci_key(g->idx[v + g->S]));
+        std::sort(b.begin(), b.end());
+        if (a != b) {
+            delete g;
+            return fail(MR_ERR_INVALID_GRID, "cell labels are not a consistent 4-grid at cell " + std::to_string(v));
+        }
+    }
+    // rank = position in the derived Ord of CellIndex (src/index.rs:41-46)
+    {
+        std::vector<std::pair<uint64_t, uint32_t>> keys(n);
+        for (uint32_t v = 0; v < n; ++v) keys[v] = {ci_key(g->idx[v]), v};
+        std::sort(keys.begin(), keys.end());
+        g->rank.resize(n);
+        for (uint32_t r = 0; r < n; ++r) g->rank[keys[r].second] = r;
+        for (uint32_t r = 0; r < n; ++r)
+            if (g->poi[keys[r].second] == MR_POI_CAMPFIRE) g->campfires.push_back(keys[r].second);
+    }
+    // nearest campfire per homeland (src/grid.rs:134-230, 297-325): the argmin
+    // of (manhattan distance, |x|!=|y|, |x|+|y|, |x|, |y|) over the homeland's
+    // Homeland-indexed campfires, computed by one multi-source BFS per homeland
+    // (lexicographic (dist, key) minima propagate along shortest paths).
+    for (int h = 0; h < 4; ++h) {
+        std::vector<uint32_t> dist(n, kNone32), nc(n, kNone32);
+        std::vector<uint64_t> key(n, ~0ull);
+        std::vector<uint32_t> cur, nxt;
+        for (uint32_t v : g->campfires) {
+            const mr_cell_index &c = g->idx[v];
+            if (c.kind != MR_CELL_HOMELAND || c.sub != h) continue;
+            uint64_t ax = uint64_t(std::abs(g->gx(v))), ay = uint64_t(std::abs(g->gy(v)));
+            dist[v] = 0;
+            nc[v] = v;
+            key[v] = (uint64_t(ax != ay) << 62) | ((ax + ay) << 40) | (ax << 20) | ay;
+            cur.push_back(v);
+        }
+        if (cur.empty()) {
+            delete g;
+            // MapGrid::parse reaches unreachable!() in this case (src/grid.rs:209)
+            return fail(MR_ERR_INVALID_GRID, "a homeland has no campfire (the reference panics, src/grid.rs:209)");
+        }
+        for (uint32_t d = 0; !cur.empty(); ++d) {
+            nxt.clear();
+            for (uint32_t u : cur) {
+                int x = int(u % g->S), y = int(u / g->S);
+                uint32_t nb[4] = {x > 0 ? u - 1 : kNone32, x + 1 < S_ ? u + 1 : kNone32,
+                                  y > 0 ? u - g->S : kNone32, y + 1 < S_ ? u + g->S : kNone32};
+                for (uint32_t w : nb) {
+                    if (w == kNone32) continue;
+                    if (dist[w] == kNone32) {
+                        dist[w] = d + 1;
+                        key[w] = key[u];
+                        nc[w] = nc[u];
+                        nxt.push_back(w);
+                    } else if (dist[w] == d + 1 && key[u] < key[w]) {
+                        key[w] = key[u];
+                        nc[w] = nc[u];
+                    }
+                }
+            }
+            cur.swap(nxt);
+        }
+        g->nearest[h] = std::move(nc);
+    }
+    *out = g;
+    return MR_OK;
+}
+
+extern "C" void mr_grid_destroy(mr_grid *g) { delete g; }
+extern "C" uint32_t mr_grid_square_size(const mr_grid *g) { return g ? g->S : 0; }
+
+extern "C" void mr_params_default(mr_params *p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->scroll_of_escape_cost = 50;
+    p->scroll_of_escape_hq_cost = 75;
+    p->scroll_of_escape_forum_cost = 100;
+    p->use_soe = 1;
+    p->use_sfm = 0;
+    p->use_caravans = 1;
+    p->has_hq = 0;
+    p->route_guru = 0;
+    p->fleetfoot = 0;
+    p->sort_by[0] = MR_SORT_LEGS;
+    p->sort_by[1] = MR_SORT_MONEY;
+    p->homeland = MR_HOMELAND_BLUE;
+}
+
+extern "C" uint32_t mr_abi_version(void) { return MR_ABI_VERSION; }
+extern "C" const char *mr_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" int mr_device_available(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
+    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+}
+
+// ------------------------------------------------------------------ planning
+namespace {
+
+struct HostPlan {
+    DevParams p{};
+    std::vector<uint32_t> sinfo;
+    std::vector<SpecialStatic> sp;
+    std::vector<uint16_t> hubs;
+    std::vector<uint32_t> src_v, q_begin, q_dst, q_id;
+    std::vector<int32_t> q_status;  // per query: MR_OK or a host-side error
+    uint32_t nq = 0;
+    uint32_t fleetfoot_raw = 0;
+};
+
+// (c1, c2) -> (c1, c2', c3): CostComparator::eval_next (src/cost.rs:387-405)
+static void comparator_order(uint8_t s1, uint8_t s2, uint8_t out[3]) {
+    uint8_t c2 = s2;
+    if (s1 == s2) c2 = (s1 == MR_SORT_LEGS) ? MR_SORT_TIME : MR_SORT_LEGS;
+    uint8_t c3 = uint8_t(3 - s1 - c2);  // the remaining one of {0,1,2}
+    out[0] = s1;
+    out[1] = c2;
+    out[2] = c3;
+}
+static uint32_t metric_index(uint8_t c) { return c == MR_SORT_LEGS ? 0u : (c == MR_SORT_MONEY ? 1u : 2u); }
+
+static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs, uint32_t n, uint32_t max_cmds,
+                      HostPlan &hp) {
+    if (!g || !prm) return fail(MR_ERR_INVALID_ARG, "null grid or params");
+    if (prm->sort_by[0] > 2 || prm->sort_by[1] > 2 || prm->homeland > 3)
+        return fail(MR_ERR_INVALID_ARG, "invalid sort_by or homeland");
+    DevParams &p = hp.p;
+    p.S = g->S;
+    p.H = g->H;
+    p.V = g->V;
+    p.vc = g->vc;
+    uint8_t ord[3];
+    comparator_order(prm->sort_by[0], prm->sort_by[1], ord);
+    for (int i = 0; i < 3; ++i) p.perm[i] = metric_index(ord[i]);
+    if (ord[0] == MR_SORT_LEGS) p.bucket_mode = kBucketLegs;
+    else if (ord[0] == MR_SORT_TIME) p.bucket_mode = kBucketTime;
+    else p.bucket_mode = (ord[1] == MR_SORT_LEGS) ? kBucketMoneyLegs : kBucketMoneyTime;
+    // Fleetfoot (src/skill.rs:65-71): out-of-range levels leave the time raw
+    static const uint32_t ffn[4] = {1, 50, 100, 25}, ffd[4] = {1, 53, 109, 28};
+    uint32_t ff = prm->fleetfoot <= 3 ? prm->fleetfoot : 0;
+    p.ff = prm->fleetfoot;
+    hp.fleetfoot_raw = prm->fleetfoot;
+    p.ff_num = ffn[ff];
+    p.ff_den = ffd[ff];
+    p.W = uint32_t((180ull * p.ff_num) / p.ff_den);  // floor(r*180): min StandardMove increment
+    // RouteGuru (src/skill.rs:43-52) on CARAVAN_TIME = 240 s
+    static const uint32_t rgn[6] = {1, 19, 7, 73, 31, 51}, rgd[6] = {1, 24, 10, 120, 60, 120};
+    uint32_t rg = prm->route_guru <= 5 ? prm->route_guru : 0;
+    p.rgt = uint32_t((240ull * rgn[rg] + rgd[rg] - 1) / rgd[rg]);
+    p.soe_cost = prm->scroll_of_escape_cost;
+    p.shq_cost = prm->scroll_of_escape_hq_cost;
+    p.sfm_cost = prm->scroll_of_escape_forum_cost;
+    p.use_soe = prm->use_soe ? 1 : 0;
+    p.use_sfm = prm->use_sfm ? 1 : 0;
+    p.use_caravans = prm->use_caravans ? 1 : 0;
+    p.max_cmds = max_cmds;
+    // specials: 1 Center, 2..5 border-1 cells, campfires, HQ
+    const uint32_t V = g->V;
+    std::vector<uint32_t> tix(V, kNone10);
+    std::vector<uint32_t> order;
+    order.push_back(0);  // entry 0 = source (dynamic)
+    auto add = [&](uint32_t v) {
+        if (tix[v] != kNone10) return tix[v];
+        tix[v] = uint32_t(order.size());
+        order.push_back(v);
+        return tix[v];
+    };
+    add(g->vc);
+    for (int b = 0; b < 4; ++b) {
+        uint32_t v;
+        g->find(build_border(b, 1), v);
+        add(v);
+    }
+    for (uint32_t v : g->campfires) add(v);
+    uint32_t hq_v = kNone32;
+    if (prm->has_hq) {
+        if (!g->find(prm->hq_position, hq_v)) return fail(MR_ERR_INVALID_INDEX, "hq_position is not a grid cell");
+        add(hq_v);
+    }
+    const uint32_t NS = uint32_t(order.size()) - 1;
+    if (NS > kMaxSpecials) return fail(MR_ERR_LIMIT, "too many campfires (special table limit)");
+    p.NS = NS;
+    p.hq_t = prm->has_hq ? tix[hq_v] : 0;
+    const std::vector<uint32_t> &near = g->nearest[prm->homeland];
+    hp.sp.assign(NS + 1, SpecialStatic{});
+    hp.hubs.clear();
+    for (uint32_t t = 1; t <= NS; ++t) {
+        uint32_t v = order[t];
+        SpecialStatic &s = hp.sp[t];
+        s.v = v;
+        s.x = g->gx(v);
+        s.y = g->gy(v);
+        bool is_cf = g->poi[v] == MR_POI_CAMPFIRE;
+        s.flags = (t == 1 ? kSpCenter : 0u) | ((t >= 2 && t <= 5) ? kSpBorder1 : 0u) | ((t == 1 || is_cf) ? kSpHub : 0u);
+        s.region = near[v] == kNone32 ? kNone10 : tix[near[v]];
+        const mr_cell_index &c = g->idx[v];
+        bool coef2 = c.kind == MR_CELL_CENTER || (c.kind == MR_CELL_HOMELAND && c.sub == prm->homeland);
+        s.coef5 = coef2 ? 0u : 1u;
+        if (s.flags & kSpHub) hp.hubs.push_back(uint16_t(t));
+    }
+    p.n_hubs = uint32_t(hp.hubs.size());
+    hp.sinfo.resize(V);
+    for (uint32_t v = 0; v < V; ++v) {
+        uint32_t r = near[v] == kNone32 ? kNone10 : tix[near[v]];
+        hp.sinfo[v] = (tix[v] & kNone10) | (r << 10);
+    }
+    // queries grouped by source (counting sort on the source vertex)
+    hp.nq = n;
+    hp.q_status.assign(n, MR_OK);
+    std::vector<uint32_t> qs_src(n), qs_dst(n);
+    std::vector<uint32_t> count(V + 1, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t a, b;
+        if (!g->find(qs[i].from, a) || !g->find(qs[i].to, b)) {
+            hp.q_status[i] = MR_ERR_INVALID_INDEX;
+            qs_src[i] = kNone32;
+            continue;
+        }
+        qs_src[i] = a;
+        qs_dst[i] = b;
+        count[a]++;
+    }
+    hp.src_v.clear();
+    hp.q_begin.clear();
+    std::vector<uint32_t> start(V, 0);
+    uint32_t off = 0;
+    for (uint32_t v = 0; v < V; ++v) {
+        if (!count[v]) continue;
+        hp.src_v.push_back(v);
+        hp.q_begin.push_back(off);
+        start[v] = off;
+        off += count[v];
+    }
+    hp.q_begin.push_back(off);
+    hp.q_dst.resize(off);
+    hp.q_id.resize(off);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (qs_src[i] == kNone32) continue;
+        uint32_t k = start[qs_src[i]]++;
+        hp.q_dst[k] = qs_dst[i];
+        hp.q_id[k] = i;
+    }
+    return MR_OK;
+}
+
+#define HIPCHK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) return fail(MR_ERR_DEVICE, std::string(#x ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+static int upload(T *&dptr, const std::vector<T> &h) {
+    dptr = nullptr;
+    size_t bytes = std::max<size_t>(h.size(), 1) * sizeof(T);
+    HIPCHK(hipMalloc(reinterpret_cast<void **>(&dptr), bytes));
+    if (!h.empty()) HIPCHK(hipMemcpy(dptr, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+    return MR_OK;
+}
+
+}  // namespace
+
+struct mr_plan {
+    const mr_grid *grid = nullptr;
+    HostPlan hp;
+    KArgs ka{};
+    bool grid_in_lds = false;
+    uint32_t blocks = 0;
+    uint32_t *d_sinfo = nullptr, *d_rank = nullptr, *d_src = nullptr, *d_qb = nullptr, *d_qd = nullptr, *d_qi = nullptr;
+    SpecialStatic *d_sp = nullptr;
+    uint16_t *d_hubs = nullptr;
+    OutResult *d_res = nullptr;
+    OutCmd *d_cmd = nullptr;
+    uint32_t *d_ws = nullptr, *d_counter = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;  // pending event pairs
+    int device = 0;
+    ~mr_plan() {
+        for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_src, (void *)d_qb, (void *)d_qd, (void *)d_qi,
+                        (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws, (void *)d_counter})
+            if (p) (void)hipFree(p);
+        for (auto &e : timed) {
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *qs, uint32_t n, uint32_t max_cmds,
+                       mr_plan **out) {
+    if (!out || (n && !qs)) return fail(MR_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    if (!mr_device_available()) return fail(MR_ERR_NO_DEVICE, "no gfx950 device visible (no CPU fallback)");
+    auto pl = new mr_plan();
+    pl->grid = g;
+    int st = build_plan(g, prm, qs, n, max_cmds, pl->hp);
+    if (st != MR_OK) {
+        delete pl;
+        return st;
+    }
+    HostPlan &hp = pl->hp;
+    auto bail = [&](int code) {
+        delete pl;
+        return code;
+    };
+    if (hipGetDevice(&pl->device) != hipSuccess) return bail(fail(MR_ERR_DEVICE, "hipGetDevice"));
+    if ((st = upload(pl->d_sinfo, hp.sinfo)) || (st = upload(pl->d_rank, g->rank)) || (st = upload(pl->d_sp, hp.sp)) ||
+        (st = upload(pl->d_hubs, hp.hubs)) || (st = upload(pl->d_src, hp.src_v)) || (st = upload(pl->d_qb, hp.q_begin)) ||
+        (st = upload(pl->d_qd, hp.q_dst)) || (st = upload(pl->d_qi, hp.q_id)))
+        return bail(st);
+    size_t nres = std::max<uint32_t>(n, 1);
+    if (hipMalloc(reinterpret_cast<void **>(&pl->d_res), nres * sizeof(OutResult)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&pl->d_cmd), nres * size_t(max_cmds) * sizeof(OutCmd)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&pl->d_counter), 16) != hipSuccess)
+        return bail(fail(MR_ERR_DEVICE, "hipMalloc outputs"));
+    // grid state in LDS when it fits 3 workgroups per CU, else per-workgroup HBM slots
+    const uint32_t NS = hp.p.NS, V = hp.p.V;
+    const uint32_t nsrc = uint32_t(hp.src_v.size());
+    uint32_t lds_full = lds_bytes(NS, V, true);
+    pl->grid_in_lds = V <= 65535 && lds_full <= 53 * 1024;
+    // MR_GRID_STATE=hbm|lds overrides the choice (tests cover both kernel variants)
+    if (const char *e = std::getenv("MR_GRID_STATE")) {
+        if (!std::strcmp(e, "hbm")) pl->grid_in_lds = false;
+        else if (!std::strcmp(e, "lds") && V <= 65535 && lds_full <= 160 * 1024) pl->grid_in_lds = true;
+    }
+    uint32_t bytes = lds_bytes(NS, V, pl->grid_in_lds);
+    if (bytes > 160 * 1024) return bail(fail(MR_ERR_LIMIT, "special table exceeds LDS"));
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, pl->device) != hipSuccess) return bail(fail(MR_ERR_DEVICE, "props"));
+    int per_cu = std::max(1, max_blocks_per_cu(pl->grid_in_lds, bytes));
+    uint64_t resident = uint64_t(per_cu) * uint64_t(prop.multiProcessorCount);
+    uint64_t blocks = std::min<uint64_t>(std::max<uint32_t>(nsrc, 1), resident);
+    if (!pl->grid_in_lds) {
+        const uint64_t slot_bytes = 5ull * V * 4ull;
+        const uint64_t budget = 64ull << 30;  // HBM budget for solve slots
+        blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, budget / slot_bytes));
+        if (hipMalloc(reinterpret_cast<void **>(&pl->d_ws), blocks * slot_bytes) != hipSuccess)
+            return bail(fail(MR_ERR_DEVICE, "hipMalloc workspace"));
+    }
+    pl->blocks = uint32_t(blocks);
+    if (hipStreamCreateWithFlags(&pl->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(MR_ERR_DEVICE, "stream"));
+    KArgs &ka = pl->ka;
+    ka.p = hp.p;
+    ka.sinfo = pl->d_sinfo;
+    ka.rank = pl->d_rank;
+    ka.sp = pl->d_sp;
+    ka.hubs = pl->d_hubs;
+    ka.src_v = pl->d_src;
+    ka.q_begin = pl->d_qb;
+    ka.q_dst = pl->d_qd;
+    ka.q_id = pl->d_qi;
+    ka.out_res = pl->d_res;
+    ka.out_cmd = pl->d_cmd;
+    ka.ws = pl->d_ws;
+    ka.counter = pl->d_counter;
+    ka.nsrc = nsrc;
+    ka.early_exit_max = 64;
+    *out = pl;
+    return MR_OK;
+}
+
+extern "C" int mr_plan_create(const mr_grid *g, const mr_params *prm, const mr_query *qs, uint32_t n, mr_plan **out) {
+    return plan_create(g, prm, qs, n, 16, out);
+}
+
+extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
+    if (!pl) return fail(MR_ERR_INVALID_ARG, "null plan");
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : pl->stream;
+    if (hipMemsetAsync(pl->d_counter, 0, 16, s) != hipSuccess) return fail(MR_ERR_DEVICE, "memset");
+    if (pl->ka.nsrc == 0) return MR_OK;
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return fail(MR_ERR_DEVICE, "event");
+    (void)hipEventRecord(e0, s);
+    hipError_t e = launch_sssp(pl->ka, pl->grid_in_lds, pl->blocks, s);
+    (void)hipEventRecord(e1, s);
+    pl->timed.push_back({e0, e1});
+    if (e != hipSuccess) return fail(MR_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(e));
+    return MR_OK;
+}
+
+extern "C" double mr_plan_kernel_ms(mr_plan *pl, uint32_t *n_launches) {
+    if (!pl) return 0.0;
+    double tot = 0.0;
+    uint32_t k = 0;
+    for (auto &e : pl->timed) {
+        (void)hipEventSynchronize(e.second);
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) {
+            tot += ms;
+            ++k;
+        }
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    pl->timed.clear();
+    if (n_launches) *n_launches = k;
+    return k ? tot / k : 0.0;
+}
+
+extern "C" uint32_t mr_plan_num_sources(const mr_plan *pl) { return pl ? pl->ka.nsrc : 0; }
+
+extern "C" int mr_plan_device_outputs(mr_plan *pl, void **d_results, uint64_t *rb, void **d_commands, uint64_t *cb) {
+    if (!pl) return fail(MR_ERR_INVALID_ARG, "null plan");
+    if (d_results) *d_results = pl->d_res;
+    if (rb) *rb = uint64_t(pl->hp.nq) * sizeof(OutResult);
+    if (d_commands) *d_commands = pl->d_cmd;
+    if (cb) *cb = uint64_t(pl->hp.nq) * pl->hp.p.max_cmds * sizeof(OutCmd);
+    return MR_OK;
+}
+
+// expand one compact command (mr_engine.hpp) into the ABI's mr_command
+static void expand_cmd(const mr_grid *g, const HostPlan &hp, const OutCmd &c, mr_command &o) {
+    std::memset(&o, 0, sizeof(o));
+    uint32_t kind = c.kp >> 29, pay = c.kp & 0x1FFFFFFFu;
+    o.kind = uint8_t(kind);
+    const DevParams &p = hp.p;
+    switch (kind) {
+        case kCentral: o.time_s = int64_t(10) * pay; break;
+        case kStandard:
+            o.legs = pay;
+            o.time_s = int64_t(180) * pay;
+            o.fleetfoot = hp.fleetfoot_raw;
+            break;
+        case kCaravan: {
+            uint32_t d = pay >> 1;
+            o.time_s = int64_t(p.rgt) * d;
+            o.money = d * ((pay & 1u) ? 5u : 2u);
+            break;
+        }
+        case kSoE: o.money = p.soe_cost; break;
+        case kSHQ: o.money = p.shq_cost; break;
+        case kSFm: o.money = p.sfm_cost; break;
+        default: break;
+    }
+    o.from = g->idx[c.from];
+    o.to = g->idx[c.to];
+}
+
+static int check_device_errors(mr_plan *pl, uint32_t &flags) {
+    uint32_t ctr[4] = {0, 0, 0, 0};
+    if (hipMemcpy(ctr, pl->d_counter, 16, hipMemcpyDeviceToHost) != hipSuccess) return fail(MR_ERR_DEVICE, "copy counter");
+    flags = ctr[1];
+    if (flags & (kErrKOverflow | kErrMetricOverflow))
+        return fail(MR_ERR_LIMIT, "a label exceeds the engine's 32-bit metric or run-length limits");
+    if (flags) return fail(MR_ERR_DEVICE, "internal invariant violated on device (flags " + std::to_string(flags) + ")");
+    return MR_OK;
+}
+
+// Copies the compact outputs and expands them.  Queries whose label needs more
+// than max_cmds commands come back with status MR_ERR_CAPACITY in *over.
+static int plan_collect(mr_plan *pl, std::vector<OutResult> &res, std::vector<OutCmd> &cmd) {
+    if (hipStreamSynchronize(pl->stream) != hipSuccess) return fail(MR_ERR_DEVICE, "sync");
+    if (hipDeviceSynchronize() != hipSuccess) return fail(MR_ERR_DEVICE, "device sync");
+    uint32_t flags = 0;
+    int st = check_device_errors(pl, flags);
+    if (st != MR_OK) return st;
+    const uint32_t n = pl->hp.nq, mc = pl->hp.p.max_cmds;
+    res.resize(n);
+    cmd.resize(size_t(n) * mc);
+    if (n) {
+        if (hipMemcpy(res.data(), pl->d_res, n * sizeof(OutResult), hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(cmd.data(), pl->d_cmd, size_t(n) * mc * sizeof(OutCmd), hipMemcpyDeviceToHost) != hipSuccess)
+            return fail(MR_ERR_DEVICE, "copy outputs");
+    }
+    return MR_OK;
+}
+
+extern "C" int mr_plan_fetch(mr_plan *pl, mr_result *results, mr_command *pool, uint64_t pool_cap) {
+    if (!pl || (pl->hp.nq && !results)) return fail(MR_ERR_INVALID_ARG, "null argument");
+    std::vector<OutResult> res;
+    std::vector<OutCmd> cmd;
+    int st = plan_collect(pl, res, cmd);
+    if (st != MR_OK) return st;
+    const HostPlan &hp = pl->hp;
+    const uint32_t mc = hp.p.max_cmds;
+    uint64_t off = 0;
+    int ret = MR_OK;
+    for (uint32_t i = 0; i < hp.nq; ++i) {
+        mr_result &r = results[i];
+        std::memset(&r, 0, sizeof(r));
+        if (hp.q_status[i] != MR_OK) {
+            r.status = hp.q_status[i];
+            if (ret == MR_OK) ret = hp.q_status[i];
+            continue;
+        }
+        const OutResult &o = res[i];
+        int status = int(o.ncmd_status >> 16) - 16;
+        r.legs = o.legs;
+        r.money = o.money;
+        r.time_s = int64_t(o.time);
+        r.n_commands = o.ncmd_status & 0xFFFFu;
+        r.status = status;
+        r.command_offset = uint32_t(off);
+        if (status == MR_NOT_FOUND) {
+            r.n_commands = 0;
+            continue;
+        }
+        if (status != MR_OK) {
+            if (ret == MR_OK) ret = status;
+            continue;
+        }
+        if (off + r.n_commands <= pool_cap && pool) {
+            for (uint32_t j = 0; j < r.n_commands; ++j) expand_cmd(pl->grid, hp, cmd[size_t(i) * mc + j], pool[off + j]);
+        } else {
+            ret = MR_ERR_CAPACITY;
+        }
+        off += r.n_commands;
+    }
+    return ret;
+}
+
+extern "C" void mr_plan_destroy(mr_plan *pl) { delete pl; }
+
+extern "C" int mr_find_path_batch(const mr_grid *g, const mr_params *prm, const mr_query *qs, uint32_t n,
+                                  mr_result *results, mr_command *pool, uint64_t pool_cap) {
+    if (!g || !prm || (n && (!qs || !results))) return fail(MR_ERR_INVALID_ARG, "null argument");
+    uint32_t max_cmds = 16;
+    for (int attempt = 0; attempt < 4; ++attempt) {
+        mr_plan *pl = nullptr;
+        int st = plan_create(g, prm, qs, n, max_cmds, &pl);
+        if (st != MR_OK) return st;
+        st = mr_plan_run(pl, nullptr);
+        if (st != MR_OK) {
+            mr_plan_destroy(pl);
+            return st;
+        }
+        st = mr_plan_fetch(pl, results, pool, pool_cap);
+        mr_plan_destroy(pl);
+        // a label longer than the device command slots: re-run with more slots
+        uint32_t need = 0;
+        for (uint32_t i = 0; i < n; ++i)
+            if (results[i].status == MR_ERR_CAPACITY) need = std::max(need, results[i].n_commands);
+        if (need == 0) return st;
+        max_cmds = std::max(need, max_cmds * 4);
+    }
+    return fail(MR_ERR_LIMIT, "label length");
+}
+
+extern "C" int mr_find_path(const mr_grid *g, const mr_params *prm, mr_cell_index from, mr_cell_index to,
+                            mr_result *out, mr_command *cmds, uint32_t cap) {
+    if (!out) return fail(MR_ERR_INVALID_ARG, "null result");
+    mr_query q;
+    q.from = from;
+    q.to = to;
+    std::vector<mr_command> pool(std::max<uint32_t>(cap, 64));
+    int st = mr_find_path_batch(g, prm, &q, 1, out, pool.data(), pool.size());
+    if (st < 0 && st != MR_ERR_CAPACITY) return st;
+    if (out->status != MR_OK) return out->status;
+    out->command_offset = 0;
+    if (out->n_commands > cap) {
+        out->status = MR_ERR_CAPACITY;
+        return MR_ERR_CAPACITY;
+    }
+    if (cmds) std::memcpy(cmds, pool.data(), out->n_commands * sizeof(mr_command));
+    return MR_OK;
+}

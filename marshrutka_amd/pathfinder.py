@@ -1,0 +1,241 @@
+"""Host-side mirror of the reference's pathfinder API over the C ABI.
+
+    FindPath { scroll_of_escape_cost, .., sort_by, homeland, grid }.eval(from, to)
+        -> Option<TotalCost>                          (src/pathfinder.rs:183-248)
+
+`FindPath(...).eval(a, b)` returns a TotalCost or None exactly like the
+reference; `FindPath(...).eval_batch(pairs)` is the batched GPU hot path.  All
+compute runs in libmarshrutka_pf.so on a gfx950 device; without one every call
+raises EngineError (there is no CPU fallback).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+from . import abi
+from .abi import (MR_ERR_CAPACITY, MR_NOT_FOUND, MR_OK, CellIndex, Params, TotalCost, cells_to_c,
+                  mr_cell, mr_cell_index, mr_command, mr_params, mr_query, mr_result, queries_to_c,
+                  result_from_c)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmarshrutka_pf.so")
+
+EXPORTED_SYMBOLS = [
+    "mr_grid_create", "mr_grid_destroy", "mr_grid_square_size", "mr_params_default", "mr_find_path",
+    "mr_find_path_batch", "mr_plan_create", "mr_plan_run", "mr_plan_fetch", "mr_plan_device_outputs",
+    "mr_plan_num_sources", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_abi_version", "mr_last_error",
+    "mr_device_available",
+]
+
+
+class EngineError(RuntimeError):
+    def __init__(self, status: int, msg: str = ""):
+        super().__init__(f"{abi.STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+_lib = None
+
+
+def lib():
+    """Loads the in-tree HIP library (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise EngineError(abi.MR_ERR_NO_DEVICE, f"{LIB_PATH} missing: run python -m marshrutka_amd.build")
+        L = C.CDLL(LIB_PATH)
+        vp = C.c_void_p
+        L.mr_grid_create.argtypes = [C.POINTER(mr_cell), C.c_uint32, C.POINTER(vp)]
+        L.mr_grid_create.restype = C.c_int
+        L.mr_grid_destroy.argtypes = [vp]
+        L.mr_grid_square_size.argtypes = [vp]
+        L.mr_grid_square_size.restype = C.c_uint32
+        L.mr_params_default.argtypes = [C.POINTER(mr_params)]
+        L.mr_find_path.argtypes = [vp, C.POINTER(mr_params), mr_cell_index, mr_cell_index,
+                                   C.POINTER(mr_result), C.POINTER(mr_command), C.c_uint32]
+        L.mr_find_path.restype = C.c_int
+        L.mr_find_path_batch.argtypes = [vp, C.POINTER(mr_params), C.POINTER(mr_query), C.c_uint32,
+                                         C.POINTER(mr_result), C.POINTER(mr_command), C.c_uint64]
+        L.mr_find_path_batch.restype = C.c_int
+        L.mr_plan_create.argtypes = [vp, C.POINTER(mr_params), C.POINTER(mr_query), C.c_uint32, C.POINTER(vp)]
+        L.mr_plan_create.restype = C.c_int
+        L.mr_plan_run.argtypes = [vp, vp]
+        L.mr_plan_run.restype = C.c_int
+        L.mr_plan_fetch.argtypes = [vp, C.POINTER(mr_result), C.POINTER(mr_command), C.c_uint64]
+        L.mr_plan_fetch.restype = C.c_int
+        L.mr_plan_device_outputs.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_uint64), C.POINTER(vp),
+                                             C.POINTER(C.c_uint64)]
+        L.mr_plan_device_outputs.restype = C.c_int
+        L.mr_plan_num_sources.argtypes = [vp]
+        L.mr_plan_num_sources.restype = C.c_uint32
+        L.mr_plan_kernel_ms.argtypes = [vp, C.POINTER(C.c_uint32)]
+        L.mr_plan_kernel_ms.restype = C.c_double
+        L.mr_plan_destroy.argtypes = [vp]
+        L.mr_abi_version.restype = C.c_uint32
+        L.mr_last_error.restype = C.c_char_p
+        L.mr_device_available.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return (lib().mr_last_error() or b"").decode()
+
+
+def device_available() -> bool:
+    return bool(lib().mr_device_available())
+
+
+class MapGrid:
+    """The immutable grid handle (MapGrid, src/grid.rs:31-38)."""
+
+    def __init__(self, cells: Sequence[Tuple[CellIndex, int]]):
+        self._cells = cells_to_c(cells)
+        h = C.c_void_p()
+        st = lib().mr_grid_create(self._cells, len(cells), C.byref(h))
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+        self.handle = h
+
+    @property
+    def square_size(self) -> int:
+        return lib().mr_grid_square_size(self.handle)
+
+    def homeland_size(self) -> int:  # src/grid.rs:280-282
+        return self.square_size // 2
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and _lib is not None:
+            _lib.mr_grid_destroy(h)
+            self.handle = None
+
+
+@dataclass
+class FindPath:
+    """Same fields and defaults as the reference's FindPath (src/pathfinder.rs:183-196)."""
+    grid: MapGrid
+    scroll_of_escape_cost: int = 50
+    scroll_of_escape_hq_cost: int = 75
+    scroll_of_escape_forum_cost: int = 100
+    use_soe: bool = True
+    use_sfm: bool = False
+    use_caravans: bool = True
+    hq_position: Optional[CellIndex] = None
+    route_guru: int = 0
+    fleetfoot: int = 0
+    sort_by: Tuple[int, int] = (abi.SORT_LEGS, abi.SORT_MONEY)
+    homeland: int = abi.BLUE
+
+    def params(self) -> Params:
+        return Params(self.scroll_of_escape_cost, self.scroll_of_escape_hq_cost,
+                      self.scroll_of_escape_forum_cost, self.use_soe, self.use_sfm, self.use_caravans,
+                      self.hq_position, self.route_guru, self.fleetfoot, tuple(self.sort_by), self.homeland)
+
+    @staticmethod
+    def with_params(grid: MapGrid, p: Params) -> "FindPath":
+        return FindPath(grid, p.scroll_of_escape_cost, p.scroll_of_escape_hq_cost,
+                        p.scroll_of_escape_forum_cost, p.use_soe, p.use_sfm, p.use_caravans,
+                        p.hq_position, p.route_guru, p.fleetfoot, tuple(p.sort_by), p.homeland)
+
+    def eval(self, from_: CellIndex, to: CellIndex) -> Optional[TotalCost]:
+        """FindPath::eval (src/pathfinder.rs:199-248); None when unreachable."""
+        p = self.params().to_c()
+        res = mr_result()
+        cap = 64
+        while True:
+            cmds = (mr_command * cap)()
+            st = lib().mr_find_path(self.grid.handle, C.byref(p), from_.to_c(), to.to_c(), C.byref(res), cmds, cap)
+            if st == MR_ERR_CAPACITY:
+                cap = res.n_commands
+                continue
+            break
+        if st == MR_NOT_FOUND:
+            return None
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+        res.command_offset = 0
+        return result_from_c(res, cmds)
+
+    def eval_batch_raw(self, pairs: Sequence[Tuple[CellIndex, CellIndex]]):
+        n = len(pairs)
+        qs = queries_to_c(pairs)
+        p = self.params().to_c()
+        res = (mr_result * max(n, 1))()
+        cap = max(1, n * 8)
+        while True:
+            pool = (mr_command * cap)()
+            st = lib().mr_find_path_batch(self.grid.handle, C.byref(p), qs, n, res, pool, cap)
+            if st == MR_ERR_CAPACITY and any(res[i].status == MR_OK for i in range(n)):
+                total = sum(res[i].n_commands for i in range(n) if res[i].status == MR_OK)
+                if total > cap:
+                    cap = total
+                    continue
+            break
+        if st < 0 and st != abi.MR_ERR_INVALID_INDEX:
+            raise EngineError(st, last_error())
+        return res, pool
+
+    def eval_batch(self, pairs: Sequence[Tuple[CellIndex, CellIndex]]) -> List[Optional[TotalCost]]:
+        res, pool = self.eval_batch_raw(pairs)
+        out = []
+        for i in range(len(pairs)):
+            r = res[i]
+            if r.status == MR_OK or r.status == MR_NOT_FOUND:
+                out.append(result_from_c(r, pool))
+            else:
+                raise EngineError(r.status, f"query {i}")
+        return out
+
+
+class Plan:
+    """Device-resident batch: inputs uploaded once, `run()` enqueues one pass."""
+
+    def __init__(self, grid: MapGrid, params: Params, pairs: Sequence[Tuple[CellIndex, CellIndex]]):
+        self.grid = grid
+        self.n = len(pairs)
+        self._qs = queries_to_c(pairs)
+        self._p = params.to_c()
+        h = C.c_void_p()
+        st = lib().mr_plan_create(grid.handle, C.byref(self._p), self._qs, self.n, C.byref(h))
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+        self.handle = h
+
+    @property
+    def num_sources(self) -> int:
+        return lib().mr_plan_num_sources(self.handle)
+
+    def run(self, stream: int = 0) -> None:
+        st = lib().mr_plan_run(self.handle, C.c_void_p(stream) if stream else None)
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+
+    def kernel_ms(self) -> Tuple[float, int]:
+        n = C.c_uint32()
+        ms = lib().mr_plan_kernel_ms(self.handle, C.byref(n))
+        return ms, n.value
+
+    def device_outputs(self):
+        r, rb, c, cb = C.c_void_p(), C.c_uint64(), C.c_void_p(), C.c_uint64()
+        st = lib().mr_plan_device_outputs(self.handle, C.byref(r), C.byref(rb), C.byref(c), C.byref(cb))
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+        return r.value, rb.value, c.value, cb.value
+
+    def fetch(self) -> List[Optional[TotalCost]]:
+        res = (mr_result * max(self.n, 1))()
+        cap = max(1, self.n * 16)
+        pool = (mr_command * cap)()
+        st = lib().mr_plan_fetch(self.handle, res, pool, cap)
+        if st < 0 and st != abi.MR_ERR_INVALID_INDEX:
+            raise EngineError(st, last_error())
+        return [result_from_c(res[i], pool) for i in range(self.n)]
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and _lib is not None:
+            _lib.mr_plan_destroy(h)
+            self.handle = None

@@ -1,0 +1,108 @@
+"""CPU-side checks of the C-ABI library: it builds, loads, exports every
+function include/marshrutka_pf.h declares, validates grids on the host, and
+fails loudly (MR_ERR_NO_DEVICE) instead of falling back to the CPU."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from marshrutka_amd import abi
+from marshrutka_amd.abi import BLUE, CellIndex, Params
+from marshrutka_amd.mapgen import SyntheticMap, to_html
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from marshrutka_amd import build, pathfinder
+    build.build()
+    return pathfinder
+
+
+def declared_functions():
+    names = []
+    for fn in os.listdir(os.path.join(ROOT, "include")):
+        if fn.endswith(".h"):
+            src = open(os.path.join(ROOT, "include", fn)).read()
+            src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+            names += re.findall(r"^[A-Za-z_][\w \*]*?\b(mr_\w+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_api():
+    names = declared_functions()
+    assert "mr_find_path" in names and "mr_find_path_batch" in names and "mr_grid_create" in names
+    assert len(names) >= 15
+
+
+def test_library_exports_every_declared_symbol(eng):
+    L = C.CDLL(eng.LIB_PATH)
+    for name in declared_functions():
+        assert hasattr(L, name), name
+    assert sorted(declared_functions()) == sorted(eng.EXPORTED_SYMBOLS)
+
+
+def test_abi_version_and_defaults(eng):
+    L = eng.lib()
+    assert L.mr_abi_version() == 1
+    p = abi.mr_params()
+    L.mr_params_default(C.byref(p))
+    d = Params().to_c()
+    for f, _ in abi.mr_params._fields_:
+        if f in ("hq_position", "sort_by", "reserved"):
+            continue
+        assert getattr(p, f) == getattr(d, f), f
+    assert list(p.sort_by) == [abi.SORT_LEGS, abi.SORT_MONEY]
+
+
+def test_grid_validation_on_host(eng):
+    m = SyntheticMap(9, campfires_per_homeland=2, seed=1)
+    g = eng.MapGrid(m.cells())
+    assert g.square_size == 9 and g.homeland_size() == 4
+    cells = m.cells()
+    # not square
+    with pytest.raises(eng.EngineError, match="INVALID_GRID"):
+        eng.MapGrid(cells[:-1])
+    # duplicate index
+    bad = list(cells)
+    bad[0] = bad[1]
+    with pytest.raises(eng.EngineError, match="INVALID_GRID"):
+        eng.MapGrid(bad)
+    # labels that are not a consistent 4-grid (two homeland cells swapped)
+    bad = list(cells)
+    bad[0], bad[10] = bad[10], bad[0]
+    with pytest.raises(eng.EngineError, match="INVALID_GRID"):
+        eng.MapGrid(bad)
+    # a homeland without campfires: the reference panics (src/grid.rs:209)
+    m2 = SyntheticMap(7, campfires_per_homeland=0, seed=0,
+                      extra_campfires=[CellIndex.homeland(h, 3, 3) for h in range(3)])
+    with pytest.raises(eng.EngineError, match="INVALID_GRID"):
+        eng.MapGrid(m2.cells())
+
+
+def test_rotated_layout_is_accepted(eng):
+    # any orientation whose labels are consistent with the index adjacency is a valid map
+    m = SyntheticMap(7, campfires_per_homeland=1, seed=4)
+    S = 7
+    cells = m.cells()
+    rot = [cells[(S - 1 - (i % S)) * S + (i // S)] for i in range(S * S)]  # transpose + flip
+    eng.MapGrid(rot)
+
+
+def test_no_cpu_fallback_without_device(eng):
+    if eng.device_available():
+        pytest.skip("a device is visible")
+    m = SyntheticMap(7, campfires_per_homeland=1, seed=4)
+    g = eng.MapGrid(m.cells())
+    fp = eng.FindPath(g)
+    with pytest.raises(eng.EngineError, match="NO_DEVICE"):
+        fp.eval(CellIndex.homeland(BLUE, 1, 1), CellIndex.center())
+
+
+def test_html_writer_schema():
+    m = SyntheticMap(5, campfires_per_homeland=1, seed=2)
+    html = to_html(m)
+    assert html.count('class="map-cell"') == 25
+    assert '<div class="top-right-text">0#0</div>' in html

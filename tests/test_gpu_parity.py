@@ -1,0 +1,144 @@
+"""Parity of the HIP engine (through the C ABI) with the CPU oracle and the
+committed golden vectors.  Integer/index work: the bar is bit-exact equality of
+(legs, money, time, every command)."""
+import os
+import random
+
+import pytest
+
+from golden_util import as_expected, fixture_names, load
+from marshrutka_amd.abi import (BLUE, GREEN, RED, SORT_LEGS, SORT_MONEY, SORT_TIME, YELLOW,
+                                CellIndex, Params)
+from marshrutka_amd.mapgen import SyntheticMap, random_queries
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from marshrutka_amd import build, pathfinder
+    build.build()
+    if not pathfinder.device_available():
+        pytest.fail("no gfx950 device visible to the GPU tests")
+    return pathfinder
+
+
+@pytest.fixture(params=["lds", "hbm"])
+def grid_state(request, monkeypatch):
+    monkeypatch.setenv("MR_GRID_STATE", request.param)
+    return request.param
+
+
+def check(eng, oracle_lib, m, params, queries, label=""):
+    g = eng.MapGrid(m.cells())
+    og = oracle_lib.OracleGrid(m.cells())
+    got = eng.FindPath.with_params(g, params).eval_batch(queries)
+    exp = og.find_path_batch(params, queries, threads=0)
+    bad = [(q, e, r) for q, e, r in zip(queries, exp, got) if as_expected(e) != as_expected(r)]
+    assert not bad, f"{label}: {len(bad)}/{len(queries)} mismatches; first: {bad[0]}"
+
+
+@pytest.mark.parametrize("name", fixture_names())
+def test_golden(eng, grid_state, name):
+    m, queries, runs = load(name)
+    g = eng.MapGrid(m.cells())
+    for params, expected in runs:
+        got = eng.FindPath.with_params(g, params).eval_batch(queries)
+        bad = [(q, e, as_expected(r)) for q, e, r in zip(queries, expected, got) if as_expected(r) != e]
+        assert not bad, f"{name} {params}: {len(bad)} mismatches; first {bad[0]}"
+
+
+def test_kat_single_query_api(eng, oracle_lib):
+    # KAT5 through the single-query entry point (src/pathfinder.rs:199)
+    m = SyntheticMap(7, campfires_per_homeland=0, seed=0, fountains=0, forums=0,
+                     extra_campfires=[CellIndex.homeland(h, 3, 3) for h in range(4)])
+    g = eng.MapGrid(m.cells())
+    r = eng.FindPath(g, use_soe=False, use_caravans=False, fleetfoot=2).eval(
+        CellIndex.parse("B 2#2"), CellIndex.parse("G 2#2"))
+    assert (r.legs, r.money, r.time_s) == (6, 0, 1012)
+    assert [str(c.to) for c in r.commands] == ["BR 1", "RG 1", "G 2#2"]
+    r = eng.FindPath(g).eval(CellIndex.parse("B 3#3"), CellIndex.parse("G 3#3"))
+    assert (r.legs, r.money, r.time_s) == (0, 42, 2880)
+    r = eng.FindPath(g).eval(CellIndex.center(), CellIndex.center())
+    assert (r.legs, r.money, r.time_s, len(r.commands)) == (0, 0, 0, 1)
+
+
+SORTS = [(a, b) for a in (SORT_LEGS, SORT_TIME, SORT_MONEY) for b in (SORT_LEGS, SORT_TIME, SORT_MONEY)]
+
+
+def random_params(rng, m):
+    hq = None
+    if rng.random() < 0.3:
+        hq = rng.choice(m.all_indices())
+    return Params(scroll_of_escape_cost=rng.choice([0, 1, 50, 500]),
+                  scroll_of_escape_hq_cost=rng.choice([0, 75, 3]),
+                  scroll_of_escape_forum_cost=rng.choice([0, 100, 7]),
+                  use_soe=rng.random() < 0.8, use_sfm=rng.random() < 0.3,
+                  use_caravans=rng.random() < 0.8, hq_position=hq,
+                  route_guru=rng.choice([0, 1, 2, 3, 4, 5, 6]), fleetfoot=rng.choice([0, 1, 2, 3, 4]),
+                  sort_by=rng.choice(SORTS), homeland=rng.choice([BLUE, RED, GREEN, YELLOW]))
+
+
+@pytest.mark.parametrize("size,k,clustered", [(5, 1, False), (7, 2, False), (11, 3, False),
+                                              (15, 4, False), (21, 6, True), (33, 4, False),
+                                              (65, 4, False)])
+def test_random_params_vs_oracle(eng, oracle_lib, grid_state, size, k, clustered):
+    rng = random.Random(size * 1000 + k)
+    for trial in range(4):
+        m = SyntheticMap(size, campfires_per_homeland=k, seed=rng.randrange(1 << 30), clustered=clustered)
+        params = random_params(rng, m)
+        queries = random_queries(m, 200 if size <= 33 else 120, rng.randrange(1 << 30))
+        check(eng, oracle_lib, m, params, queries, f"S={size} trial={trial} {params}")
+
+
+def test_default_params_c2_sample(eng, oracle_lib):
+    # configs[1]: 64x64 -> odd S = 65, uniform queries, default (app) parameters
+    m = SyntheticMap(65, campfires_per_homeland=4, seed=2024)
+    check(eng, oracle_lib, m, Params(), random_queries(m, 400, 7), "c2 sample")
+
+
+def test_hbm_regime_mid_grid(eng, oracle_lib):
+    m = SyntheticMap(129, campfires_per_homeland=4, seed=77)
+    for params in (Params(), Params(fleetfoot=3, sort_by=(SORT_TIME, SORT_MONEY)),
+                   Params(sort_by=(SORT_MONEY, SORT_LEGS), use_sfm=True)):
+        check(eng, oracle_lib, m, params, random_queries(m, 60, 3), f"S=129 {params}")
+
+
+def test_edge_cases(eng, oracle_lib):
+    m = SyntheticMap(9, campfires_per_homeland=2, seed=3)
+    cf = m.campfires()
+    specials = [CellIndex.center()] + [CellIndex.border(b, 1) for b in range(4)] + cf
+    qs = [(a, b) for a in specials for b in specials]
+    qs += [(a, a) for a in m.all_indices()[:20]]
+    for params in (Params(), Params(hq_position=cf[0], use_sfm=True),
+                   Params(scroll_of_escape_cost=0, hq_position=CellIndex.center(), use_sfm=True,
+                          scroll_of_escape_forum_cost=0, scroll_of_escape_hq_cost=0),
+                   Params(sort_by=(SORT_TIME, SORT_TIME), fleetfoot=1)):
+        check(eng, oracle_lib, m, params, qs, f"edges {params}")
+
+
+def test_invalid_queries_report_errors(eng):
+    from marshrutka_amd.abi import MR_ERR_INVALID_INDEX, MR_OK
+    m = SyntheticMap(7, campfires_per_homeland=1, seed=3)
+    g = eng.MapGrid(m.cells())
+    fp = eng.FindPath(g)
+    res, _ = fp.eval_batch_raw([(CellIndex.center(), CellIndex.homeland(BLUE, 9, 9)),
+                                (CellIndex.center(), CellIndex.homeland(BLUE, 1, 1))])
+    assert res[0].status == MR_ERR_INVALID_INDEX and res[1].status == MR_OK
+    with pytest.raises(eng.EngineError, match="INVALID_INDEX"):
+        fp.eval(CellIndex.homeland(BLUE, 0, 4), CellIndex.center())  # non-canonical
+
+
+def test_plan_rerun_is_identical(eng):
+    m = SyntheticMap(33, campfires_per_homeland=3, seed=5)
+    g = eng.MapGrid(m.cells())
+    qs = random_queries(m, 300, 9)
+    plan = eng.Plan(g, Params(), qs)
+    plan.run()
+    a = [as_expected(r) for r in plan.fetch()]
+    plan.run()
+    plan.run()
+    b = [as_expected(r) for r in plan.fetch()]
+    assert a == b
+    ms, n = plan.kernel_ms()
+    assert n == 3 and ms > 0
