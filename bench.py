@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""bench.py — queries/sec of the gfx950 pathfinder hot path.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c4]
+
+One "step" = one pass of the hot path over one batch: every query of the
+rank's shard is answered (one single-source solve per unique source, all
+destinations of that source read off it) and, for N > 1, the fixed-size
+result records are gathered to rank 0 over RCCL.  Inputs are resident in HBM
+before the timed region starts.
+
+Workloads (BASELINE.json configs; odd sides per SURVEY.md §8a A14):
+  c2 (default) 10k uniform (src,dst) queries per GPU on a 65x65 synthetic map
+               (configs[1]: "10k random (src,dst) batch on 64x64")
+  c4           the 1025x1025 map with 1M/8 = 125k queries per GPU
+               (configs[3] shard; weak scaling up to the 1M batch at N=8)
+
+N>1 is launched by the driver as
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+one process per GPU; each rank owns the sources of its shard (weak scaling).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "shortest-path queries/sec on N×N weighted grid; bit-exact vs CPU pathfinder"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: Chip-level parameters)
+BYTES_PER_VERTEX_SOLVE = 20  # per full single-source solve, V x 20 B
+
+WORKLOADS = {
+    "c2": dict(size=65, queries_per_gpu=10_000, campfires=4, seed=2024,
+               desc="configs[1]: 10k uniform (src,dst) per GPU on a 65x65 synthetic map (64x64 -> odd 65), "
+                    "default FindPath params"),
+    "c4": dict(size=1025, queries_per_gpu=125_000, campfires=4, seed=4096,
+               desc="configs[3] shard: 125k uniform (src,dst) per GPU on a 1025x1025 synthetic map "
+                    "(1024 -> odd 1025), default FindPath params; N=8 is the 1M batch"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--queries", type=int, default=0, help="override queries per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline budget (CPU-seconds)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc", default="", help="JSON with PMC-derived HBM bytes per launch (profiles/)")
+    return ap.parse_args()
+
+
+def cpu_baseline_leg(m, params, queries, gpu_results, budget_s):
+    """Oracle (C++ restatement of the reference, oracle/) on host cores over a
+    bounded sample of the same workload; also checks the sample's GPU results."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_lib
+    oracle_lib.build()
+    og = oracle_lib.OracleGrid(m.cells())
+    threads = max(1, min(16, os.cpu_count() or 1))
+    # calibrate on a small single-threaded sample, then size the run to ~budget CPU-seconds
+    cal = queries[:64]
+    t0 = time.perf_counter()
+    og.find_path_batch_raw(params, cal, threads=1)
+    per_q = max((time.perf_counter() - t0) / len(cal), 1e-6)
+    n = int(min(len(queries), max(256, budget_s / per_q)))
+    sample = queries[:n]
+    t0 = time.perf_counter()
+    labels = og.find_path_batch(params, sample, threads=threads)
+    wall = time.perf_counter() - t0
+    mism = sum(1 for e, g in zip(labels, gpu_results[:n]) if as_expected(e) != as_expected(g))
+    return ({"value": n / wall, "unit": "queries/s", "cores": threads, "kind": "port",
+             "sample": f"first {n} queries of the rank-0 batch, oracle/mr_oracle.cpp (binary heap of full "
+                       f"labels + hash map, as the reference) on {threads} host threads, {wall:.2f} s wall; "
+                       f"cpu model: {cpu_model()}; nproc {os.cpu_count()}"},
+            {"checked": n, "mismatches": mism})
+
+
+def as_expected(label):
+    if label is None:
+        return None
+    return (label.legs, label.money, label.time_s, tuple(c.as_tuple() for c in label.commands))
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from marshrutka_amd import build, pathfinder
+    from marshrutka_amd.abi import Params
+    from marshrutka_amd.mapgen import SyntheticMap, random_queries
+    from marshrutka_amd.shard import gather_rows_to_root, shard_by_source
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    # a dedicated stream: the solve kernel and the RCCL gather are ordered on it
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+    build.build()
+    if not pathfinder.device_available():
+        raise SystemExit("no gfx950 device visible: the engine has no CPU fallback")
+
+    wl = dict(WORKLOADS[args.workload])
+    qpg = args.queries or wl["queries_per_gpu"]
+    m = SyntheticMap(wl["size"], campfires_per_homeland=wl["campfires"], seed=wl["seed"])
+    params = Params()  # the app's defaults (src/app.rs:782-811)
+    all_q = random_queries(m, qpg * world, wl["seed"] + 17)
+    keys = [(a.kind << 40) | (a.sub << 32) | (a.x << 16) | a.y for a, _ in all_q]
+    shards = shard_by_source(keys, world)
+    mine = [all_q[i] for i in shards[rank]]
+    counts = [len(s) for s in shards]
+
+    grid = pathfinder.MapGrid(m.cells())
+    plan = pathfinder.Plan(grid, params, mine)
+    n_src = plan.num_sources
+    _, rbytes, _, cbytes = plan.device_outputs()
+    if world > 1:
+        # compact result records and command slots in torch-owned device buffers,
+        # padded to the largest shard so the gather moves equal-sized rows
+        rows, nq = max(counts), max(1, len(mine))
+        res_t = torch.zeros((rows, rbytes // nq // 4), dtype=torch.int32, device="cuda")
+        cmd_t = torch.zeros((rows, cbytes // nq // 4), dtype=torch.int32, device="cuda")
+        plan.bind_outputs(res_t.data_ptr(), cmd_t.data_ptr())
+
+    def step():
+        plan.run(stream.cuda_stream)
+        if world > 1:
+            gather_rows_to_root(res_t, counts, rank, world)
+            gather_rows_to_root(cmd_t, counts, rank, world)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    plan.kernel_ms()  # reset the per-launch event window to the timed region
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kms, nl = plan.kernel_ms()
+    if world > 1:
+        t = torch.tensor([elapsed, kms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kms = float(t[0]), float(t[1])
+        tot_src = torch.tensor([n_src], dtype=torch.int64, device="cuda")
+        dist.all_reduce(tot_src)
+        tot_src = int(tot_src)
+    else:
+        tot_src = n_src
+
+    total_queries = sum(counts) * args.steps
+    value = total_queries / elapsed
+    V = wl["size"] ** 2
+    # roofline: SURVEY §8d algorithmic bytes = (unique sources) x V x 20 B per launch,
+    # over the solve kernel's average launch time (HIP events on its stream)
+    alg_bytes = n_src * V * BYTES_PER_VERTEX_SOLVE
+    achieved = alg_bytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
+    traffic = None
+    pmc_path = args.pmc or os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as f:
+                pm = json.load(f)
+            if pm.get("workload") == args.workload and pm.get("queries_per_gpu") == qpg:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    out = {
+        "metric": METRIC, "value": value, "unit": "queries/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": wl["desc"], "grid": f"{wl['size']}x{wl['size']}", "queries_per_gpu": qpg,
+                   "campfires_per_homeland": wl["campfires"], "unique_sources_per_step": tot_src,
+                   "params": "FindPath defaults: sort (Legs,Money), SoE 50, caravans, skills 0, homeland Blue",
+                   "parallelism": f"sources sharded over {world} GPU(s), RCCL gather of results to rank 0"
+                                  if world > 1 else "1 GPU"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "sssp_kernel", "kernel_ms": kms, "launches": nl,
+                     "alg_bytes_per_launch": alg_bytes},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        gpu_res = plan.fetch()
+        cb, parity = cpu_baseline_leg(m, params, mine, gpu_res, args.cpu_seconds)
+        out["cpu_baseline"] = cb
+        out["parity"] = parity
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -184,6 +184,11 @@ int mr_plan_fetch(mr_plan *plan, mr_result *results, mr_command *pool, uint64_t 
  * gather): n * 16 B result records and n * max_cmds * 16 B command slots. */
 int mr_plan_device_outputs(mr_plan *plan, void **d_results, uint64_t *results_bytes,
                            void **d_commands, uint64_t *commands_bytes);
+/* Makes subsequent mr_plan_run calls write their compact outputs into caller
+ * device buffers (e.g. torch tensors that an RCCL collective then gathers)
+ * instead of the plan's own.  Sizes as reported by mr_plan_device_outputs;
+ * the caller keeps the buffers alive while the plan uses them. */
+int mr_plan_bind_outputs(mr_plan *plan, void *d_results, void *d_commands);
 /* Number of unique sources (= single-source solves per pass). */
 uint32_t mr_plan_num_sources(const mr_plan *plan);
 /* Average device time (ms) of the main solve kernel over the last

@@ -570,13 +570,20 @@ extern "C" double mr_plan_kernel_ms(mr_plan *pl, uint32_t *n_launches) {
     return k ? tot / k : 0.0;
 }
 
+extern "C" int mr_plan_bind_outputs(mr_plan *pl, void *d_results, void *d_commands) {
+    if (!pl || !d_results || !d_commands) return fail(MR_ERR_INVALID_ARG, "null argument");
+    pl->ka.out_res = reinterpret_cast<OutResult *>(d_results);
+    pl->ka.out_cmd = reinterpret_cast<OutCmd *>(d_commands);
+    return MR_OK;
+}
+
 extern "C" uint32_t mr_plan_num_sources(const mr_plan *pl) { return pl ? pl->ka.nsrc : 0; }
 
 extern "C" int mr_plan_device_outputs(mr_plan *pl, void **d_results, uint64_t *rb, void **d_commands, uint64_t *cb) {
     if (!pl) return fail(MR_ERR_INVALID_ARG, "null plan");
-    if (d_results) *d_results = pl->d_res;
+    if (d_results) *d_results = pl->ka.out_res;
     if (rb) *rb = uint64_t(pl->hp.nq) * sizeof(OutResult);
-    if (d_commands) *d_commands = pl->d_cmd;
+    if (d_commands) *d_commands = pl->ka.out_cmd;
     if (cb) *cb = uint64_t(pl->hp.nq) * pl->hp.p.max_cmds * sizeof(OutCmd);
     return MR_OK;
 }
@@ -631,8 +638,8 @@ static int plan_collect(mr_plan *pl, std::vector<OutResult> &res, std::vector<Ou
     res.resize(n);
     cmd.resize(size_t(n) * mc);
     if (n) {
-        if (hipMemcpy(res.data(), pl->d_res, n * sizeof(OutResult), hipMemcpyDeviceToHost) != hipSuccess ||
-            hipMemcpy(cmd.data(), pl->d_cmd, size_t(n) * mc * sizeof(OutCmd), hipMemcpyDeviceToHost) != hipSuccess)
+        if (hipMemcpy(res.data(), pl->ka.out_res, n * sizeof(OutResult), hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(cmd.data(), pl->ka.out_cmd, size_t(n) * mc * sizeof(OutCmd), hipMemcpyDeviceToHost) != hipSuccess)
             return fail(MR_ERR_DEVICE, "copy outputs");
     }
     return MR_OK;

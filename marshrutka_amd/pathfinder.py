@@ -25,7 +25,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libm
 EXPORTED_SYMBOLS = [
     "mr_grid_create", "mr_grid_destroy", "mr_grid_square_size", "mr_params_default", "mr_find_path",
     "mr_find_path_batch", "mr_plan_create", "mr_plan_run", "mr_plan_fetch", "mr_plan_device_outputs",
-    "mr_plan_num_sources", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_abi_version", "mr_last_error",
+    "mr_plan_num_sources", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_plan_bind_outputs", "mr_abi_version", "mr_last_error",
     "mr_device_available",
 ]
 
@@ -68,6 +68,8 @@ def lib():
         L.mr_plan_device_outputs.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_uint64), C.POINTER(vp),
                                              C.POINTER(C.c_uint64)]
         L.mr_plan_device_outputs.restype = C.c_int
+        L.mr_plan_bind_outputs.argtypes = [vp, vp, vp]
+        L.mr_plan_bind_outputs.restype = C.c_int
         L.mr_plan_num_sources.argtypes = [vp]
         L.mr_plan_num_sources.restype = C.c_uint32
         L.mr_plan_kernel_ms.argtypes = [vp, C.POINTER(C.c_uint32)]
@@ -224,6 +226,11 @@ class Plan:
         if st != MR_OK:
             raise EngineError(st, last_error())
         return r.value, rb.value, c.value, cb.value
+
+    def bind_outputs(self, d_results: int, d_commands: int) -> None:
+        st = lib().mr_plan_bind_outputs(self.handle, C.c_void_p(d_results), C.c_void_p(d_commands))
+        if st != MR_OK:
+            raise EngineError(st, last_error())
 
     def fetch(self) -> List[Optional[TotalCost]]:
         res = (mr_result * max(self.n, 1))()

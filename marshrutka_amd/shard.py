@@ -1,0 +1,46 @@
+"""Multi-GPU sharding of a query batch.
+
+Queries are independent and the grid is read-only, so a batch shards by
+*source*: all queries of one source go to the same rank (one single-source
+solve answers all of them).  Sources are dealt to ranks by a deterministic
+longest-processing-time greedy on their query counts.  The only collective is
+the final gather of the fixed-size result records to rank 0 (RCCL over xGMI on
+MI355X; gloo in the CPU tests).
+"""
+from __future__ import annotations
+
+import heapq
+from typing import Dict, List, Sequence
+
+
+def shard_by_source(src_keys: Sequence[int], world: int) -> List[List[int]]:
+    """Returns, per rank, the (ascending) query indices it owns."""
+    groups: Dict[int, List[int]] = {}
+    for i, s in enumerate(src_keys):
+        groups.setdefault(s, []).append(i)
+    # LPT: biggest groups first, ties by source key, each to the least-loaded rank
+    order = sorted(groups.items(), key=lambda kv: (-len(kv[1]), kv[0]))
+    heap = [(0, r) for r in range(world)]
+    out: List[List[int]] = [[] for _ in range(world)]
+    for _, idxs in order:
+        load, r = heapq.heappop(heap)
+        out[r].extend(idxs)
+        heapq.heappush(heap, (load + len(idxs), r))
+    for r in range(world):
+        out[r].sort()
+    return out
+
+
+def gather_rows_to_root(local, counts: Sequence[int], rank: int, world: int, group=None):
+    """Gathers each rank's first counts[rank] rows of `local` (a tensor padded to
+    max(counts) rows) to rank 0.  Returns the concatenation on rank 0, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return local[: counts[0]]
+    if rank == 0:
+        bufs = [torch.empty_like(local) for _ in range(world)]
+        dist.gather(local, gather_list=bufs, dst=0, group=group)
+        return torch.cat([b[: counts[r]] for r, b in enumerate(bufs)], dim=0)
+    dist.gather(local, dst=0, group=group)
+    return None
