@@ -97,6 +97,7 @@ struct KArgs {
     DevParams p;
     const uint32_t *sinfo;       // V words: special idx (10b) | region idx << 10
     const uint32_t *rank;        // V words: position in CellIndex order
+    const uint32_t *rank_inv;    // V words: vertex of each rank
     const SpecialStatic *sp;     // NS+1 entries
     const uint16_t *hubs;        // n_hubs caravan endpoints (table indices)
     const uint32_t *src_v;       // nsrc source vertices
@@ -109,7 +110,10 @@ struct KArgs {
     uint32_t *counter;           // [0] source dequeue, [1] error flags
     uint32_t nsrc;
     uint32_t early_exit_max;     // early exit if a source has <= this many destinations (<= 64)
+    uint32_t grid_in_lds;        // 1: grid state in LDS, 0: per-workgroup HBM slots
+    uint32_t algo;               // kAlgoLegs (Legs-first level-synchronous) or kAlgoGeneric
 };
+enum : uint32_t { kAlgoGeneric = 0, kAlgoLegs = 1 };
 
 constexpr uint32_t kErrKOverflow = 1u, kErrMetricOverflow = 2u, kErrBucket = 4u, kErrChain = 8u;
 

@@ -19,9 +19,10 @@
 #include "mr_engine.hpp"
 
 namespace mr {
-uint32_t lds_bytes(uint32_t NS, uint32_t V, bool grid_in_lds);
-hipError_t launch_sssp(const KArgs &a, bool grid_in_lds, uint32_t blocks, hipStream_t stream);
-int max_blocks_per_cu(bool grid_in_lds, uint32_t bytes);
+uint32_t lds_bytes(uint32_t NS, uint32_t V, bool grid_in_lds, uint32_t algo);
+hipError_t launch_solve(const KArgs *d_args, bool grid_in_lds, uint32_t algo, uint32_t NS, uint32_t V,
+                        uint32_t blocks, hipStream_t stream);
+int max_blocks_per_cu(bool grid_in_lds, uint32_t algo, uint32_t bytes);
 }  // namespace mr
 
 
@@ -98,6 +99,7 @@ struct mr_grid {
     std::vector<uint8_t> poi;
     std::unordered_map<uint64_t, uint32_t> index;
     std::vector<uint32_t> rank;
+    std::vector<uint32_t> rank_inv;        // vertex of each rank
     std::vector<uint32_t> campfires;       // vertex ids, CellIndex order
     std::vector<uint32_t> nearest[4];      // nearest campfire vertex per homeland (kNone32)
     int32_t gx(uint32_t v) const { return int32_t(v % S) - int32_t(H); }
@@ -178,7 +180,11 @@ extern "C" int mr_grid_create(const mr_cell *cells, uint32_t n, mr_grid **out) {
         for (uint32_t v = 0; v < n; ++v) keys[v] = {ci_key(g->idx[v]), v};
         std::sort(keys.begin(), keys.end());
         g->rank.resize(n);
-        for (uint32_t r = 0; r < n; ++r) g->rank[keys[r].second] = r;
+        g->rank_inv.resize(n);
+        for (uint32_t r = 0; r < n; ++r) {
+            g->rank[keys[r].second] = r;
+            g->rank_inv[r] = keys[r].second;
+        }
         for (uint32_t r = 0; r < n; ++r)
             if (g->poi[keys[r].second] == MR_POI_CAMPFIRE) g->campfires.push_back(keys[r].second);
     }
@@ -436,7 +442,10 @@ struct mr_plan {
     KArgs ka{};
     bool grid_in_lds = false;
     uint32_t blocks = 0;
-    uint32_t *d_sinfo = nullptr, *d_rank = nullptr, *d_src = nullptr, *d_qb = nullptr, *d_qd = nullptr, *d_qi = nullptr;
+    uint32_t *d_sinfo = nullptr, *d_rank = nullptr, *d_rank_inv = nullptr, *d_src = nullptr, *d_qb = nullptr,
+             *d_qd = nullptr, *d_qi = nullptr;
+    KArgs *d_args = nullptr;
+    uint32_t algo = kAlgoGeneric;
     SpecialStatic *d_sp = nullptr;
     uint16_t *d_hubs = nullptr;
     OutResult *d_res = nullptr;
@@ -447,8 +456,9 @@ struct mr_plan {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;  // pending event pairs
     int device = 0;
     ~mr_plan() {
-        for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_src, (void *)d_qb, (void *)d_qd, (void *)d_qi,
-                        (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws, (void *)d_counter})
+        for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_rank_inv, (void *)d_src, (void *)d_qb, (void *)d_qd,
+                        (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
+                        (void *)d_counter, (void *)d_args})
             if (p) (void)hipFree(p);
         for (auto &e : timed) {
             (void)hipEventDestroy(e.first);
@@ -476,7 +486,8 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         return code;
     };
     if (hipGetDevice(&pl->device) != hipSuccess) return bail(fail(MR_ERR_DEVICE, "hipGetDevice"));
-    if ((st = upload(pl->d_sinfo, hp.sinfo)) || (st = upload(pl->d_rank, g->rank)) || (st = upload(pl->d_sp, hp.sp)) ||
+    if ((st = upload(pl->d_sinfo, hp.sinfo)) || (st = upload(pl->d_rank, g->rank)) ||
+        (st = upload(pl->d_rank_inv, g->rank_inv)) || (st = upload(pl->d_sp, hp.sp)) ||
         (st = upload(pl->d_hubs, hp.hubs)) || (st = upload(pl->d_src, hp.src_v)) || (st = upload(pl->d_qb, hp.q_begin)) ||
         (st = upload(pl->d_qd, hp.q_dst)) || (st = upload(pl->d_qi, hp.q_id)))
         return bail(st);
@@ -485,21 +496,25 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         hipMalloc(reinterpret_cast<void **>(&pl->d_cmd), nres * size_t(max_cmds) * sizeof(OutCmd)) != hipSuccess ||
         hipMalloc(reinterpret_cast<void **>(&pl->d_counter), 16) != hipSuccess)
         return bail(fail(MR_ERR_DEVICE, "hipMalloc outputs"));
-    // grid state in LDS when it fits 3 workgroups per CU, else per-workgroup HBM slots
+    // algorithm: level-synchronous when the comparator leads with Legs (MR_ALGO=generic forces the
+    // bucketed solver, used by the tests to cover both); grid state in LDS when it fits 3
+    // workgroups per CU, else per-workgroup HBM slots (MR_GRID_STATE=hbm|lds overrides)
     const uint32_t NS = hp.p.NS, V = hp.p.V;
     const uint32_t nsrc = uint32_t(hp.src_v.size());
-    uint32_t lds_full = lds_bytes(NS, V, true);
+    pl->algo = hp.p.bucket_mode == kBucketLegs ? kAlgoLegs : kAlgoGeneric;
+    if (const char *e = std::getenv("MR_ALGO"))
+        if (!std::strcmp(e, "generic")) pl->algo = kAlgoGeneric;
+    const uint32_t lds_full = lds_bytes(NS, V, true, pl->algo);
     pl->grid_in_lds = V <= 65535 && lds_full <= 53 * 1024;
-    // MR_GRID_STATE=hbm|lds overrides the choice (tests cover both kernel variants)
     if (const char *e = std::getenv("MR_GRID_STATE")) {
         if (!std::strcmp(e, "hbm")) pl->grid_in_lds = false;
         else if (!std::strcmp(e, "lds") && V <= 65535 && lds_full <= 160 * 1024) pl->grid_in_lds = true;
     }
-    uint32_t bytes = lds_bytes(NS, V, pl->grid_in_lds);
+    uint32_t bytes = lds_bytes(NS, V, pl->grid_in_lds, pl->algo);
     if (bytes > 160 * 1024) return bail(fail(MR_ERR_LIMIT, "special table exceeds LDS"));
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, pl->device) != hipSuccess) return bail(fail(MR_ERR_DEVICE, "props"));
-    int per_cu = std::max(1, max_blocks_per_cu(pl->grid_in_lds, bytes));
+    int per_cu = std::max(1, max_blocks_per_cu(pl->grid_in_lds, pl->algo, bytes));
     uint64_t resident = uint64_t(per_cu) * uint64_t(prop.multiProcessorCount);
     uint64_t blocks = std::min<uint64_t>(std::max<uint32_t>(nsrc, 1), resident);
     if (!pl->grid_in_lds) {
@@ -516,6 +531,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     ka.p = hp.p;
     ka.sinfo = pl->d_sinfo;
     ka.rank = pl->d_rank;
+    ka.rank_inv = pl->d_rank_inv;
     ka.sp = pl->d_sp;
     ka.hubs = pl->d_hubs;
     ka.src_v = pl->d_src;
@@ -528,6 +544,11 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     ka.counter = pl->d_counter;
     ka.nsrc = nsrc;
     ka.early_exit_max = 64;
+    ka.grid_in_lds = pl->grid_in_lds ? 1u : 0u;
+    ka.algo = pl->algo;
+    if (hipMalloc(reinterpret_cast<void **>(&pl->d_args), sizeof(KArgs)) != hipSuccess ||
+        hipMemcpy(pl->d_args, &ka, sizeof(KArgs), hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail(MR_ERR_DEVICE, "kernel args"));
     *out = pl;
     return MR_OK;
 }
@@ -544,7 +565,7 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return fail(MR_ERR_DEVICE, "event");
     (void)hipEventRecord(e0, s);
-    hipError_t e = launch_sssp(pl->ka, pl->grid_in_lds, pl->blocks, s);
+    hipError_t e = launch_solve(pl->d_args, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->blocks, s);
     (void)hipEventRecord(e1, s);
     pl->timed.push_back({e0, e1});
     if (e != hipSuccess) return fail(MR_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(e));
@@ -574,6 +595,8 @@ extern "C" int mr_plan_bind_outputs(mr_plan *pl, void *d_results, void *d_comman
     if (!pl || !d_results || !d_commands) return fail(MR_ERR_INVALID_ARG, "null argument");
     pl->ka.out_res = reinterpret_cast<OutResult *>(d_results);
     pl->ka.out_cmd = reinterpret_cast<OutCmd *>(d_commands);
+    if (hipMemcpy(pl->d_args, &pl->ka, sizeof(KArgs), hipMemcpyHostToDevice) != hipSuccess)
+        return fail(MR_ERR_DEVICE, "kernel args");
     return MR_OK;
 }
 

@@ -8,37 +8,53 @@
 // See mr_engine.hpp for the layout and DESIGN.md §3 for the exactness argument.
 //
 // One 256-thread workgroup solves one source at a time (sources are dequeued
-// from a global counter).  Per bucket B:
-//   1. settle   — every plain vertex listed for B is final: mark it, feed the
-//                 Scroll-of-Escape region argmin, mark its 4 neighbours dirty;
-//   2. specials — wave 0: fire SoE candidates, then an exact Dijkstra over the
-//                 specials whose tentative label lies in bucket B (wave argmin);
-//   3. pull     — every dirty vertex recomputes its best walk label from its
-//                 settled neighbours (deterministic, no label atomics); a plain
-//                 vertex is appended to the list of bucket B+1 or B+2 on first touch;
-//   4. next     — B' = min(non-empty list buckets, tentative specials).
+// from a global counter; no grid-wide barrier, no co-residency assumption).
+// Two solvers share the special-table machinery (Core):
+//
+//  * LegsSolver   (comparator leads with Legs — the app's default): level-
+//    synchronous.  At legs level L every candidate label of a plain vertex is
+//    walk(b, L - legs(b)), so candidates order by the boundary b alone: wave 0
+//    ranks the boundaries once per level (prio[]), and a plain vertex's label
+//    is FINAL the moment it is claimed.  Two barriers per level:
+//      [specials] wave 0: Scroll-of-Escape region argmins fire, an exact
+//                 Dijkstra settles the specials of level L, boundaries are
+//                 ranked for level L+1;
+//      [claim]    every frontier vertex of level L claims the unsettled
+//                 neighbours it owns (lowest-direction frontier neighbour owns;
+//                 a parity bit tells level-L vertices apart), picking the
+//                 best-prio boundary among their level-L neighbours.
+//  * GenericSolver (Time- or Money-first): buckets of the leading metric
+//    (the bucket rises by 1 or 2 per StandardMove): settle -> specials ->
+//    pull -> next, with full label comparisons in the pull.
+//
 // Grid state lives in LDS when it fits (G=false) and in a per-workgroup HBM
-// slot otherwise (G=true; cross-thread words then go through sc1 loads).
+// slot otherwise (G=true; cross-thread words then go through sc1 loads/stores).
 #include <hip/hip_runtime.h>
 
 #include "mr_engine.hpp"
 
 namespace mr {
 
-struct Shared {
-    unsigned long long B;        // current bucket key
-    uint32_t cnt[3];             // list counts per buffer
-    uint32_t lb;                 // list rotation base: L0 = buf[lb]
-    uint32_t nd;                 // dirty count
-    uint32_t sidx;
-    uint32_t done;
-    uint32_t pad[3];
-};
-
 constexpr int kBS = 256;
 constexpr uint32_t kOwn = 0xFFFFu;
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
 constexpr unsigned long long kInf64 = ~0ull;
+constexpr uint32_t kStPar = kStDirty;  // LegsSolver: parity of the settle level (settled words only)
+
+struct Shared {
+    unsigned long long B;   // generic: current bucket
+    unsigned long long smin;
+    uint32_t cnt[3];        // list counts
+    uint32_t lb;            // generic: list rotation base / legs: current frontier buffer
+    uint32_t nd;            // generic: dirty count
+    uint32_t sidx;
+    uint32_t done;
+    uint32_t L;             // legs: current level
+    uint32_t nbnd;          // legs: number of boundaries
+    uint32_t jump;          // legs: 1 if the frontier is empty and L jumps
+    uint32_t ndst;          // destinations of the current source
+    uint32_t ranked;        // legs: nbnd when prio[] was last computed (linear run time)
+};
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
@@ -48,38 +64,33 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// A label viewed for comparison: metrics, length and the last <= 2 commands
-// plus the prefix pointer (table index; 0 = empty prefix).
+// A label viewed for comparison: metrics, length, prefix pointer (table
+// index, 0 = empty prefix) and the last <= 2 commands.  Scalar fields only, so
+// nothing is runtime-indexed (no scratch).
 struct View {
-    uint32_t m[3];
-    uint32_t len;
-    uint32_t parent;
-    uint32_t ntail;
-    Cmd tail[2];
+    uint32_t m0, m1, m2;  // legs, money, time
+    uint32_t len, parent, ntail;
+    Cmd t0, t1;
 };
+// selected with masks rather than ?: so the optimiser cannot turn it into a
+// load through a selected pointer (which would force the View into scratch)
+__device__ __forceinline__ Cmd tail_at(const View &x, int i) {
+    const uint32_t m = 0u - uint32_t(i == 0);
+    return Cmd{(x.t0.kp & m) | (x.t1.kp & ~m), (x.t0.from & m) | (x.t1.from & ~m), (x.t0.to & m) | (x.t1.to & ~m)};
+}
 
-template <bool G, class IdxT>
-struct Solver {
-    const KArgs &a;
-    const DevParams &p;
+template <bool G>
+struct Core {
+    const KArgs *__restrict__ a;
     Shared *sh;
     Rec *R;
-    uint32_t *best;
-    uint32_t *fired;
     uint32_t *state;
-    IdxT *lbuf[3];
-    IdxT *dirty;
+    const SpecialStatic *sp;  // LDS copy of a->sp (loaded once per workgroup)
+    const uint16_t *hubs;     // LDS copy of a->hubs
+    uint32_t *dst;            // LDS: destinations of the current source (<= early_exit_max)
     uint32_t src;
 
-    __device__ Solver(const KArgs &a_, Shared *sh_, Rec *R_, uint32_t *best_, uint32_t *fired_,
-                      uint32_t *state_, IdxT *l0, IdxT *l1, IdxT *l2, IdxT *dirty_)
-        : a(a_), p(a_.p), sh(sh_), R(R_), best(best_), fired(fired_), state(state_), dirty(dirty_), src(0) {
-        lbuf[0] = l0;
-        lbuf[1] = l1;
-        lbuf[2] = l2;
-    }
-
-    // ---- memory helpers ---------------------------------------------------
+    // ---- memory helpers -----------------------------------------------------
     __device__ __forceinline__ uint32_t ld_state(uint32_t v) const {
         if constexpr (G) return __hip_atomic_load(state + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else return state[v];
@@ -92,19 +103,20 @@ struct Solver {
         if constexpr (G) return __hip_atomic_fetch_or(state + v, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else return atomicOr(state + v, x);
     }
+    template <class IdxT>
     __device__ __forceinline__ uint32_t ld_idx(const IdxT *l, uint32_t i) const {
         if constexpr (G) return __hip_atomic_load(l + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else return l[i];
     }
+    template <class IdxT>
     __device__ __forceinline__ void st_idx(IdxT *l, uint32_t i, uint32_t v) const {
         if constexpr (G) __hip_atomic_store(l + i, IdxT(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else l[i] = IdxT(v);
     }
-    __device__ __forceinline__ void flag(uint32_t e) const { atomicOr(a.counter + 1, e); }
-
-    __device__ __forceinline__ uint32_t special_of(uint32_t v) const { return a.sinfo[v] & kNone10; }
-    __device__ __forceinline__ uint32_t region_of(uint32_t v) const { return (a.sinfo[v] >> 10) & kNone10; }
-    __device__ __forceinline__ uint32_t vert_of(uint32_t t) const { return t == 0 ? src : a.sp[t].v; }
+    __device__ __forceinline__ void flag(uint32_t e) const { atomicOr(a->counter + 1, e); }
+    __device__ __forceinline__ uint32_t special_of(uint32_t v) const { return a->sinfo[v] & kNone10; }
+    __device__ __forceinline__ uint32_t region_of(uint32_t v) const { return (a->sinfo[v] >> 10) & kNone10; }
+    __device__ __forceinline__ uint32_t vert_of(uint32_t t) const { return t == 0 ? src : sp[t].v; }
 
     // ---- arithmetic (u32 like the reference; overflow is reported, not wrapped)
     __device__ __forceinline__ uint32_t add32(uint32_t x, uint32_t y) const {
@@ -115,40 +127,43 @@ struct Solver {
     // AggregatedCost::time of a StandardMove run of k legs: Fleetfoot ceil of
     // 180k seconds (src/cost.rs:122-124, src/skill.rs:21-30)
     __device__ __forceinline__ uint32_t run_time(uint32_t k) const {
+        const DevParams &p = a->p;
         unsigned long long t = 180ull * k;
         if (p.ff_num != p.ff_den) t = (t * p.ff_num + p.ff_den - 1) / p.ff_den;
         if (t > 0xFFFFFFFFull) flag(kErrMetricOverflow);
         return uint32_t(t);
     }
-    __device__ __forceinline__ unsigned long long key_of(const uint32_t *m) const {
+    __device__ __forceinline__ unsigned long long key_of(uint32_t m0, uint32_t m1, uint32_t m2) const {
+        const DevParams &p = a->p;
         switch (p.bucket_mode) {
-            case kBucketLegs: return m[0];
-            case kBucketTime: return m[2] / p.W;
-            case kBucketMoneyLegs: return (unsigned long long)m[1] << 32 | m[0];
-            default: return (unsigned long long)m[1] << 32 | (m[2] / p.W);
+            case kBucketLegs: return m0;
+            case kBucketTime: return m2 / p.W;
+            case kBucketMoneyLegs: return (unsigned long long)m1 << 32 | m0;
+            default: return (unsigned long long)m1 << 32 | (m2 / p.W);
         }
     }
+    __device__ __forceinline__ unsigned long long key_rec(uint32_t t) const { return key_of(R[t].m[0], R[t].m[1], R[t].m[2]); }
 
-    // ---- views ------------------------------------------------------------
+    // ---- views ------------------------------------------------------------------
     __device__ __forceinline__ void view_rec(uint32_t t, View &x) const {
         const Rec &r = R[t];
-        x.m[0] = r.m[0];
-        x.m[1] = r.m[1];
-        x.m[2] = r.m[2];
+        x.m0 = r.m[0];
+        x.m1 = r.m[1];
+        x.m2 = r.m[2];
         x.len = r.len;
         x.parent = r.parent;
         x.ntail = r.ntail;
-        x.tail[0] = r.tail[0];
-        x.tail[1] = r.tail[1];
+        x.t0 = r.tail[0];
+        x.t1 = r.tail[1];
     }
     // the start label TotalCost::new(src) (src/cost.rs:196-205)
     __device__ __forceinline__ void view_start(View &x) const {
-        x.m[0] = x.m[1] = x.m[2] = 0;
+        x.m0 = x.m1 = x.m2 = 0;
         x.len = 1;
         x.parent = 0;
         x.ntail = 1;
-        x.tail[0] = Cmd{kNoMove << 29, src, src};
-        x.tail[1] = Cmd{0, 0, 0};
+        x.t0 = Cmd{kNoMove << 29, src, src};
+        x.t1 = Cmd{0, 0, 0};
     }
     // walk label of v: full(b) ++ [StandardMove{k} vert(b) -> v]
     __device__ __forceinline__ void view_walk(uint32_t b, uint32_t k, uint32_t v, View &x) const {
@@ -157,36 +172,41 @@ struct Solver {
             return;
         }
         const Rec &rb = R[b];
-        x.m[0] = add32(rb.m[0], k);
-        x.m[1] = rb.m[1];
-        x.m[2] = add32(rb.m[2], run_time(k));
+        x.m0 = add32(rb.m[0], k);
+        x.m1 = rb.m[1];
+        x.m2 = add32(rb.m[2], run_time(k));
         x.len = (b == 0 ? 0u : rb.len) + 1u;
         x.parent = b;
         x.ntail = 1;
-        x.tail[0] = Cmd{(kStandard << 29) | k, vert_of(b), v};
-        x.tail[1] = Cmd{0, 0, 0};
+        x.t0 = Cmd{(kStandard << 29) | k, vert_of(b), v};
+        x.t1 = Cmd{0, 0, 0};
     }
 
-    // ---- comparator: CostComparator::and_then (src/cost.rs:411-426) --------
+    // ---- comparator: CostComparator::and_then (src/cost.rs:411-426) ------------
     __device__ __forceinline__ int cmp_cmd(const Cmd &x, const Cmd &y) const {
         if (x.kp != y.kp) return x.kp < y.kp ? -1 : 1;
-        if (x.from != y.from) return a.rank[x.from] < a.rank[y.from] ? -1 : 1;
-        if (x.to != y.to) return a.rank[x.to] < a.rank[y.to] ? -1 : 1;
+        if (x.from != y.from) return a->rank[x.from] < a->rank[y.from] ? -1 : 1;
+        if (x.to != y.to) return a->rank[x.to] < a->rank[y.to] ? -1 : 1;
         return 0;
     }
-    // lexicographic compare of two command lists of equal length; xid/yid are
-    // the table entries the views were read from (kOwn for built views).
-    __device__ int cmp_list(const View &x, uint32_t xid, const View &y, uint32_t yid) const {
+    // command i of table entry t, by value (no pointer into LDS escapes)
+    __device__ __forceinline__ Cmd rec_tail(uint32_t t, int i) const {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(&R[t].tail[0]) + 3 * i;
+        return Cmd{w[0], w[1], w[2]};
+    }
+    // lexicographic compare of two command lists of equal length, walking from
+    // the last command towards the first; xid/yid name the table entries the
+    // views were read from (kOwn for built views) so a shared prefix stops the walk.
+    __device__ __forceinline__ int cmp_list(const View &x, uint32_t xid, const View &y, uint32_t yid) const {
         uint32_t xe = xid, ye = yid;
         int xt = int(x.ntail) - 1, yt = int(y.ntail) - 1;
         int res = 0;
-        for (uint32_t guard = 0; guard < 4096u; ++guard) {
-            if (xe != kOwn && xe == ye && xt == yt) return res;  // shared prefix node
-            const Cmd &cx = (xe == kOwn) ? x.tail[xt] : R[xe].tail[xt];
-            const Cmd &cy = (ye == kOwn) ? y.tail[yt] : R[ye].tail[yt];
+        for (uint32_t guard = 0; guard < 8192u; ++guard) {
+            if (xe != kOwn && xe == ye && xt == yt) return res;
+            const Cmd cx = (xe == kOwn) ? tail_at(x, xt) : rec_tail(xe, xt);
+            const Cmd cy = (ye == kOwn) ? tail_at(y, yt) : rec_tail(ye, yt);
             int r = cmp_cmd(cx, cy);
             if (r) res = r;
-            // step to the previous command
             if (xt > 0) --xt;
             else {
                 uint32_t pp = (xe == kOwn) ? x.parent : R[xe].parent;
@@ -205,88 +225,123 @@ struct Solver {
         flag(kErrChain);
         return res;
     }
-    __device__ __forceinline__ int cmp_metrics(const uint32_t *x, const uint32_t *y) const {
+    __device__ __forceinline__ int cmp_metrics(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t y0, uint32_t y1,
+                                               uint32_t y2) const {
+        const DevParams &p = a->p;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            uint32_t u = x[p.perm[i]], w = y[p.perm[i]];
+            const uint32_t pi = p.perm[i];
+            const uint32_t u = pi == 0 ? x0 : (pi == 1 ? x1 : x2);
+            const uint32_t w = pi == 0 ? y0 : (pi == 1 ? y1 : y2);
             if (u != w) return u < w ? -1 : 1;
         }
         return 0;
     }
-    __device__ int cmp_view(const View &x, uint32_t xid, const View &y, uint32_t yid) const {
-        int r = cmp_metrics(x.m, y.m);
+    __device__ __forceinline__ int cmp_view(const View &x, uint32_t xid, const View &y, uint32_t yid) const {
+        int r = cmp_metrics(x.m0, x.m1, x.m2, y.m0, y.m1, y.m2);
         if (r) return r;
         if (x.len != y.len) return x.len < y.len ? -1 : 1;
         return cmp_list(x, xid, y, yid);
     }
     __device__ __forceinline__ int cmp_entries(uint32_t s, uint32_t t) const {
+        const Rec &rs = R[s], &rt = R[t];
+        int r = cmp_metrics(rs.m[0], rs.m[1], rs.m[2], rt.m[0], rt.m[1], rt.m[2]);
+        if (r) return r;
+        if (rs.len != rt.len) return rs.len < rt.len ? -1 : 1;
         View x, y;
         view_rec(s, x);
         view_rec(t, y);
-        return cmp_view(x, s, y, t);
+        return cmp_list(x, s, y, t);
     }
 
-    // ---- special table updates ---------------------------------------------
+    // ---- special table updates --------------------------------------------------
     __device__ __forceinline__ void try_improve(uint32_t t, const View &c) const {
         Rec &r = R[t];
         if (r.state == 2) return;
         if (r.state == 1) {
-            View cur;
-            view_rec(t, cur);
-            if (cmp_view(c, kOwn, cur, t) >= 0) return;
+            int cm = cmp_metrics(c.m0, c.m1, c.m2, r.m[0], r.m[1], r.m[2]);
+            if (cm > 0) return;
+            if (cm == 0) {
+                if (c.len > r.len) return;
+                if (c.len == r.len) {
+                    View cur;
+                    view_rec(t, cur);
+                    if (cmp_list(c, kOwn, cur, t) >= 0) return;
+                }
+            }
         }
-        r.m[0] = c.m[0];
-        r.m[1] = c.m[1];
-        r.m[2] = c.m[2];
+        r.m[0] = c.m0;
+        r.m[1] = c.m1;
+        r.m[2] = c.m2;
         r.len = uint16_t(c.len);
         r.ntail = uint8_t(c.ntail);
         r.parent = uint16_t(c.parent);
-        r.tail[0] = c.tail[0];
-        r.tail[1] = c.tail[1];
+        r.tail[0] = c.t0;
+        r.tail[1] = c.t1;
         r.state = 1;
     }
     // extend the settled label of special s by a non-Standard edge to t
     // (TotalCost += edge, src/cost.rs:208-315)
-    __device__ __forceinline__ void ext_special(uint32_t s, uint32_t kind, uint32_t payload,
-                                                uint32_t dm_money, uint32_t dm_time, uint32_t t, View &c) const {
+    __device__ __forceinline__ void ext_special(uint32_t s, uint32_t kind, uint32_t payload, uint32_t dm_money,
+                                                uint32_t dm_time, uint32_t t, View &c) const {
         const Rec &r = R[s];
-        const Cmd &last = r.tail[r.ntail - 1];
-        uint32_t lk = last.kp >> 29;
-        uint32_t vt = a.sp[t].v;
-        if (lk == kNoMove) {  // the start label: NoMove is replaced, from kept
-            c.m[0] = 0;
-            c.m[1] = dm_money;
-            c.m[2] = dm_time;
+        const Cmd last = r.ntail == 2 ? r.tail[1] : r.tail[0];
+        const uint32_t lk = last.kp >> 29;
+        const uint32_t vt = sp[t].v;
+        c.t1 = Cmd{0, 0, 0};
+        if (lk == kNoMove) {  // the start label: NoMove is replaced, its from kept
+            c.m0 = 0;
+            c.m1 = dm_money;
+            c.m2 = dm_time;
             c.len = 1;
             c.parent = 0;
             c.ntail = 1;
-            c.tail[0] = Cmd{(kind << 29) | payload, last.from, vt};
-        } else if (kind == kCentral && lk == kCentral) {  // central moves merge
-            c.m[0] = r.m[0];
-            c.m[1] = r.m[1];
-            c.m[2] = add32(r.m[2], dm_time);
+            c.t0 = Cmd{(kind << 29) | payload, last.from, vt};
+        } else if (kind == kCentral && lk == kCentral) {  // CentralMoves merge (ntail is 1)
+            c.m0 = r.m[0];
+            c.m1 = r.m[1];
+            c.m2 = add32(r.m[2], dm_time);
             c.len = r.len;
             c.parent = r.parent;
-            c.ntail = r.ntail;
-            c.tail[0] = r.tail[0];
-            c.tail[1] = r.tail[1];
-            c.tail[c.ntail - 1] = Cmd{last.kp + 1u, last.from, vt};
+            c.ntail = 1;
+            c.t0 = Cmd{last.kp + 1u, last.from, vt};
         } else {
-            c.m[0] = r.m[0];
-            c.m[1] = add32(r.m[1], dm_money);
-            c.m[2] = add32(r.m[2], dm_time);
+            c.m0 = r.m[0];
+            c.m1 = add32(r.m[1], dm_money);
+            c.m2 = add32(r.m[2], dm_time);
             c.len = r.len + 1u;
             c.parent = s;
             c.ntail = 1;
-            c.tail[0] = Cmd{(kind << 29) | payload, a.sp[s].v, vt};
+            c.t0 = Cmd{(kind << 29) | payload, sp[s].v, vt};
         }
-        if (c.ntail == 1) c.tail[1] = Cmd{0, 0, 0};
+    }
+    // the SoE candidate for campfire t from plain vertex u with walk label (b,k)
+    __device__ __forceinline__ void soe_from_plain(uint32_t b, uint32_t k, uint32_t u, uint32_t t, View &c) const {
+        const DevParams &p = a->p;
+        const uint32_t vt = sp[t].v;
+        if (b == 0 && k == 0) {  // u is the source: [SoE src->c]
+            c.m0 = 0;
+            c.m1 = p.soe_cost;
+            c.m2 = 0;
+            c.len = 1;
+            c.parent = 0;
+            c.ntail = 1;
+            c.t0 = Cmd{kSoE << 29, src, vt};
+            c.t1 = Cmd{0, 0, 0};
+        } else {  // full(b) ++ [Std{k} b->u, SoE u->c]
+            view_walk(b, k, u, c);
+            c.m1 = add32(c.m1, p.soe_cost);
+            c.len += 1;
+            c.ntail = 2;
+            c.t1 = Cmd{kSoE << 29, u, vt};
+        }
     }
 
-    // ---- grid helpers --------------------------------------------------------
+    // ---- grid helpers -------------------------------------------------------------
     // geometric neighbour d (0:-x 1:+x 2:-y 3:+y) of v, or kNone32
     __device__ __forceinline__ uint32_t nbr(uint32_t v, int d) const {
-        uint32_t x = v % p.S;
+        const DevParams &p = a->p;
+        const uint32_t x = v % p.S;
         switch (d) {
             case 0: return x == 0 ? kNone32 : v - 1;
             case 1: return x + 1 == p.S ? kNone32 : v + 1;
@@ -294,92 +349,37 @@ struct Solver {
             default: return v + p.S >= p.V ? kNone32 : v + p.S;
         }
     }
-    // mark the StandardMove out-neighbours of a freshly settled vertex dirty
-    // (edges touching the Center are CentralMoves and are handled by the table)
-    __device__ __forceinline__ void mark_dirty(uint32_t v, uint32_t n) const {
-        if (n == kNone32 || v == p.vc || n == p.vc) return;
-        uint32_t old = or_state(n, kStDirty);
-        if (old & (kStSettled | kStDirty)) return;
-        uint32_t i = atomicAdd(&sh->nd, 1u);
-        st_idx(dirty, i, n);
-    }
 
-    // ---- phase 1: settle plain vertices of bucket B ---------------------------
-    __device__ void region_offer(uint32_t r, uint32_t v) const {
-        uint32_t cur = best[r];
-        for (;;) {
-            if (cur != kNone32) {
-                uint32_t su = ld_state(cur), sv = ld_state(v);
-                View xu, xv;
-                view_walk((su >> kStBShift) & kNone10, su & kStKMask, cur, xu);
-                view_walk((sv >> kStBShift) & kNone10, sv & kStKMask, v, xv);
-                if (cmp_view(xu, kOwn, xv, kOwn) <= 0) return;
-            }
-            uint32_t prev = atomicCAS(best + r, cur, v);
-            if (prev == cur) return;
-            cur = prev;
-        }
-    }
-    __device__ void settle_plain(uint32_t v) const {
-        or_state(v, kStSettled);
-        if (p.use_soe) {
-            uint32_t r = region_of(v);
-            if (r != kNone10 && !fired[r]) region_offer(r, v);
-        }
-#pragma unroll
-        for (int d = 0; d < 4; ++d) mark_dirty(v, nbr(v, d));
-    }
-
-    // ---- phase 2: specials (one wave) -----------------------------------------
-    __device__ void fire_regions() const {
-        for (uint32_t t = 1 + lane_id(); t <= p.NS; t += 64) {
-            uint32_t u = best[t];
-            if (u == kNone32) continue;
-            best[t] = kNone32;
-            fired[t] = 1;
-            if (R[t].state == 2) continue;
-            uint32_t su = ld_state(u);
-            uint32_t b = (su >> kStBShift) & kNone10, k = su & kStKMask;
-            View c;
-            uint32_t vt = a.sp[t].v;
-            if (b == 0 && k == 0) {  // u is the source: [SoE src->c]
-                c.m[0] = 0;
-                c.m[1] = p.soe_cost;
-                c.m[2] = 0;
-                c.len = 1;
-                c.parent = 0;
-                c.ntail = 1;
-                c.tail[0] = Cmd{kSoE << 29, src, vt};
-                c.tail[1] = Cmd{0, 0, 0};
-            } else {  // full(b) ++ [Std{k} b->u, SoE u->c]
-                view_walk(b, k, u, c);
-                c.m[1] = add32(c.m[1], p.soe_cost);
-                c.len += 1;
-                c.ntail = 2;
-                c.tail[1] = Cmd{kSoE << 29, u, vt};
-            }
-            try_improve(t, c);
-        }
-        wave_sync();
-    }
-
-    __device__ void settle_special(uint32_t s) const {
+    // ---- specials: settle + relax (one wave, uniform s) ----------------------------
+    // Seeds the grid word of s, then relaxes CentralMove (src/pathfinder.rs:30-53),
+    // caravan (:140-160, 251-273) and Scroll-of-Escape (:162-170) edges.
+    // Returns whether s is a boundary (its label does not end in a StandardMove).
+    __device__ __forceinline__ bool settle_special(uint32_t s, uint32_t par_bits) const {
+        const DevParams &p = a->p;
         const uint32_t lane = lane_id();
-        const uint32_t vs = a.sp[s].v;
-        if (lane == 0) {
-            Rec &r = R[s];
-            r.state = 2;
-            const Cmd &last = r.tail[r.ntail - 1];
-            uint32_t lk = last.kp >> 29, seed;
-            if (lk == kNoMove) seed = 0;  // the source itself
-            else if (lk == kStandard) seed = (uint32_t(r.parent) << kStBShift) | (last.kp & kStKMask);
-            else seed = s << kStBShift;   // a boundary: walks restart here
-            st_state(vs, kStSettled | seed);
+        const uint32_t vs = sp[s].v;
+        Rec &r = R[s];
+        const Cmd last = r.ntail == 2 ? r.tail[1] : r.tail[0];
+        const uint32_t lk = last.kp >> 29;
+        uint32_t seed;
+        bool boundary;
+        if (lk == kNoMove) {  // the source itself
+            seed = 0;
+            boundary = false;
+        } else if (lk == kStandard) {  // continues the walk of its parent boundary
+            seed = (uint32_t(r.parent) << kStBShift) | (last.kp & kStKMask);
+            boundary = false;
+        } else {  // a boundary: walks restart here
+            seed = s << kStBShift;
+            boundary = true;
         }
         wave_sync();
-        if (lane < 4) mark_dirty(vs, nbr(vs, int(lane)));
-        const uint32_t fl = a.sp[s].flags;
-        // CentralMove edges (src/pathfinder.rs:30-53)
+        if (lane == 0) {
+            r.state = 2;
+            st_state(vs, kStSettled | par_bits | seed);
+        }
+        wave_sync();
+        const uint32_t fl = sp[s].flags;
         if (fl & kSpCenter) {
             if (lane < 4) {
                 View c;
@@ -394,24 +394,22 @@ struct Solver {
             }
         }
         wave_sync();
-        // caravans between Center and campfires (src/pathfinder.rs:140-160, 251-273)
         if (p.use_caravans && (fl & kSpHub)) {
-            const SpecialStatic &ss = a.sp[s];
+            const SpecialStatic ss = sp[s];
             for (uint32_t h = lane; h < p.n_hubs; h += 64) {
-                uint32_t t = a.hubs[h];
+                const uint32_t t = hubs[h];
                 if (t == s || R[t].state == 2) continue;
-                const SpecialStatic &st = a.sp[t];
-                uint32_t d = uint32_t(abs(ss.x - st.x) + abs(ss.y - st.y));
-                uint32_t coef = st.coef5 ? 5u : 2u;
+                const SpecialStatic st = sp[t];
+                const uint32_t d = uint32_t(abs(ss.x - st.x) + abs(ss.y - st.y));
+                const uint32_t coef = st.coef5 ? 5u : 2u;
                 View c;
                 ext_special(s, kCaravan, (d << 1) | st.coef5, coef * d, p.rgt * d, t, c);
                 try_improve(t, c);
             }
         }
         wave_sync();
-        // Scroll of Escape to this cell's nearest campfire (src/pathfinder.rs:162-170)
         if (p.use_soe && lane == 0) {
-            uint32_t t = a.sp[s].region;
+            const uint32_t t = sp[s].region;
             if (t != kNone10 && t != s) {
                 View c;
                 ext_special(s, kSoE, 0, p.soe_cost, 0, t, c);
@@ -419,46 +417,461 @@ struct Solver {
             }
         }
         wave_sync();
+        return boundary;
     }
 
-    __device__ void specials_in_bucket(unsigned long long B) const {
+    // wave argmin (full comparator) over tentative specials whose key == K
+    __device__ __forceinline__ uint32_t argmin_special(unsigned long long K) const {
+        const DevParams &p = a->p;
         const uint32_t lane = lane_id();
-        for (uint32_t iter = 0; iter <= p.NS + 1; ++iter) {
-            uint32_t mine = kNone32;
-            for (uint32_t t = 1 + lane; t <= p.NS; t += 64) {
-                if (R[t].state != 1) continue;
-                unsigned long long k = key_of(R[t].m);
-                if (k < B) flag(kErrBucket);
-                if (k > B) continue;
-                if (mine == kNone32 || cmp_entries(t, mine) < 0) mine = t;
+        uint32_t mine = kNone32;
+        for (uint32_t t = 1 + lane; t <= p.NS; t += 64) {
+            if (R[t].state != 1) continue;
+            const unsigned long long k = key_rec(t);
+            if (k < K) flag(kErrBucket);
+            if (k > K) continue;
+            if (mine == kNone32 || cmp_entries(t, mine) < 0) mine = t;
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const uint32_t other = __shfl_xor(mine, off, 64);
+            if (other != kNone32 && (mine == kNone32 || cmp_entries(other, mine) < 0)) mine = other;
+        }
+        return mine;
+    }
+    __device__ __forceinline__ unsigned long long min_special_key() const {
+        const DevParams &p = a->p;
+        unsigned long long smin = kInf64;
+        for (uint32_t t = 1 + lane_id(); t <= p.NS; t += 64)
+            if (R[t].state == 1) {
+                const unsigned long long k = key_rec(t);
+                if (k < smin) smin = k;
             }
 #pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) {
-                uint32_t other = __shfl_xor(mine, off, 64);
-                if (other != kNone32 && (mine == kNone32 || cmp_entries(other, mine) < 0)) mine = other;
+        for (int off = 32; off >= 1; off >>= 1) {
+            const unsigned long long o = __shfl_xor(smin, off, 64);
+            if (o < smin) smin = o;
+        }
+        return smin;
+    }
+
+    // ---- per-source init / output ----------------------------------------------------
+    // Untouched grid words carry the vertex's static info in their k field
+    // (special index | region << 10), so a claim needs no extra global load.
+    __device__ __forceinline__ void init_source(uint32_t s_idx) {
+        const DevParams &p = a->p;
+        const uint32_t tid = threadIdx.x;
+        src = a->src_v[s_idx];
+        if constexpr (G) {
+            const uint4 *i4 = reinterpret_cast<const uint4 *>(a->sinfo);
+            uint4 *s4 = reinterpret_cast<uint4 *>(state);
+            for (uint32_t i = tid; i < p.V / 4; i += kBS) {
+                uint4 x = i4[i];
+                x.x |= kStUntouched;
+                x.y |= kStUntouched;
+                x.z |= kStUntouched;
+                x.w |= kStUntouched;
+                s4[i] = x;
             }
-            if (mine == kNone32) return;
-            settle_special(mine);
+            for (uint32_t v = (p.V & ~3u) + tid; v < p.V; v += kBS) state[v] = kStUntouched | a->sinfo[v];
+        } else {
+            for (uint32_t v = tid; v < p.V; v += kBS) state[v] = kStUntouched | a->sinfo[v];
+        }
+        for (uint32_t t = tid; t <= p.NS; t += kBS) R[t].state = 0;
+        const uint32_t q0 = a->q_begin[s_idx], q1 = a->q_begin[s_idx + 1];
+        if (tid == 0) sh->ndst = q1 - q0;
+        if (q1 - q0 <= a->early_exit_max)
+            for (uint32_t i = tid; i < q1 - q0; i += kBS) dst[i] = a->q_dst[q0 + i];
+    }
+    // SHQ / SFm: only the source's own edges can be minimal (any prefix only adds
+    // metrics and length), src/pathfinder.rs:172-178
+    __device__ __forceinline__ void seed_scrolls() const {
+        const DevParams &p = a->p;
+        if (p.hq_t) {
+            View c;
+            view_start(c);
+            c.m1 = p.shq_cost;
+            c.t0 = Cmd{kSHQ << 29, src, sp[p.hq_t].v};
+            try_improve(p.hq_t, c);
+        }
+        if (p.use_sfm) {
+            View c;
+            view_start(c);
+            c.m1 = p.sfm_cost;
+            c.t0 = Cmd{kSFm << 29, src, p.vc};
+            try_improve(1, c);
+        }
+    }
+    __device__ __forceinline__ void write_output(uint32_t w, uint32_t qid) const {
+        const DevParams &p = a->p;
+        OutResult &o = a->out_res[qid];
+        const uint32_t sw = ld_state(w);
+        if (!(sw & kStSettled)) {
+            o = OutResult{0, 0, 0, uint32_t(16 + 1) << 16};  // MR_NOT_FOUND
+            return;
+        }
+        View x;
+        const uint32_t t = special_of(w);
+        if (t != kNone10) view_rec(t, x);
+        else view_walk((sw >> kStBShift) & kNone10, sw & kStKMask, w, x);
+        if (x.len > p.max_cmds) {  // MR_ERR_CAPACITY: the host re-runs with more slots
+            o = OutResult{x.m0, x.m1, x.m2, (uint32_t(16 - 4) << 16) | (x.len & 0xFFFFu)};
+            return;
+        }
+        OutCmd *oc = a->out_cmd + (unsigned long long)qid * p.max_cmds;
+        int pos = int(x.len) - 1;
+        if (x.ntail == 2 && pos >= 0) {
+            oc[pos] = OutCmd{x.t1.kp, x.t1.from, x.t1.to, 0};
+            --pos;
+        }
+        if (pos >= 0) {
+            oc[pos] = OutCmd{x.t0.kp, x.t0.from, x.t0.to, 0};
+            --pos;
+        }
+        uint32_t pp = x.parent;
+        while (pp != 0 && pos >= 0) {
+            const Rec &r = R[pp];
+            for (int j = int(r.ntail) - 1; j >= 0 && pos >= 0; --j, --pos)
+                oc[pos] = OutCmd{r.tail[j].kp, r.tail[j].from, r.tail[j].to, 0};
+            pp = r.parent;
+        }
+        if (pos != -1 || pp != 0) flag(kErrChain);
+        o = OutResult{x.m0, x.m1, x.m2, (uint32_t(16) << 16) | (x.len & 0xFFFFu)};
+    }
+    __device__ __forceinline__ void write_outputs(uint32_t s_idx) const {
+        const uint32_t q0 = a->q_begin[s_idx], q1 = a->q_begin[s_idx + 1];
+        for (uint32_t i = q0 + threadIdx.x; i < q1; i += kBS) write_output(a->q_dst[i], a->q_id[i]);
+    }
+    // 1 if every destination of this source (when <= early_exit_max) is settled
+    __device__ __forceinline__ uint32_t dsts_done() const {
+        const uint32_t lane = lane_id();
+        const uint32_t nd = sh->ndst;
+        if (nd > a->early_exit_max) return 0;
+        bool ok = true;
+        if (lane < nd) ok = (ld_state(dst[lane]) & kStSettled) != 0;
+        return __all(ok) ? 1u : 0u;
+    }
+    __device__ __forceinline__ void seed_root() const {
+        View st;
+        view_start(st);
+        Rec &r0 = R[0];  // entry 0: the source, root of every command chain
+        r0.m[0] = r0.m[1] = r0.m[2] = 0;
+        r0.len = 1;
+        r0.ntail = 1;
+        r0.parent = 0;
+        r0.tail[0] = st.t0;
+        r0.state = 2;
+    }
+};
+
+// ===================================================================================
+// Legs-first level-synchronous solver
+// ===================================================================================
+template <bool G, class IdxT>
+struct LegsSolver : Core<G> {
+    using Core<G>::a;
+    using Core<G>::sh;
+    using Core<G>::R;
+    using Core<G>::state;
+    using Core<G>::src;
+    IdxT *F0, *F1;                 // frontier ping-pong lists
+    uint32_t *prio;                // per boundary rank for the next level
+    uint32_t *bnd;                 // boundary list (table indices), bnd[0] = 0 (the source)
+    unsigned long long *best64;    // per region: (prio << 32 | rank) of the level's best vertex
+    uint32_t *fired;
+
+    __device__ __forceinline__ IdxT *frontier(uint32_t i) const { return i ? F1 : F0; }
+
+    // walk(b1, L - legs(b1)) vs walk(b2, L - legs(b2)) at one vertex: legs tie at L
+    __device__ __forceinline__ int cmp_boundaries(uint32_t b1, uint32_t b2, uint32_t L) const {
+        const Rec &r1 = R[b1], &r2 = R[b2];
+        const uint32_t k1 = L - r1.m[0], k2 = L - r2.m[0];
+        const uint32_t t1 = this->add32(r1.m[2], this->run_time(k1)), t2 = this->add32(r2.m[2], this->run_time(k2));
+        int c = this->cmp_metrics(L, r1.m[1], t1, L, r2.m[1], t2);
+        if (c) return c;
+        const uint32_t l1 = (b1 == 0 ? 0u : r1.len), l2 = (b2 == 0 ? 0u : r2.len);
+        if (l1 != l2) return l1 < l2 ? -1 : 1;
+        if (b1 == b2) return 0;
+        View x, y;  // equal prefix lengths >= 1: both are table entries; compare full(b1), full(b2)
+        this->view_rec(b1, x);
+        this->view_rec(b2, y);
+        return this->cmp_list(x, b1, y, b2);
+    }
+    // wave 0: rank the boundaries for level L (prio[b] = number of better boundaries)
+    __device__ __forceinline__ void rank_boundaries(uint32_t L) const {
+        const uint32_t nb = sh->nbnd;
+        for (uint32_t i = lane_id(); i < nb; i += 64) {
+            const uint32_t b = bnd[i];
+            uint32_t r = 0;
+            for (uint32_t j = 0; j < nb; ++j)
+                if (j != i && cmp_boundaries(bnd[j], b, L) < 0) ++r;
+            prio[b] = r;
+        }
+        wave_sync();
+    }
+    // wave 0: SoE candidates from the level-L region argmins
+    __device__ __forceinline__ void fire_regions() const {
+        const DevParams &p = a->p;
+        for (uint32_t t = 1 + lane_id(); t <= p.NS; t += 64) {
+            const unsigned long long key = best64[t];
+            if (key == kInf64) continue;
+            best64[t] = kInf64;
+            fired[t] = 1;
+            if (R[t].state == 2) continue;
+            const uint32_t u = a->rank_inv[uint32_t(key)];
+            const uint32_t su = this->ld_state(u);
+            View c;
+            this->soe_from_plain((su >> kStBShift) & kNone10, su & kStKMask, u, t, c);
+            this->try_improve(t, c);
+        }
+        wave_sync();
+    }
+    // claim the unsettled StandardMove neighbours of frontier vertex v (level L)
+    __device__ __forceinline__ void claim_from(uint32_t v, uint32_t L, IdxT *Fn, uint32_t cn) const {
+        const DevParams &p = a->p;
+        if (v == p.vc) return;  // the Center's out-edges are CentralMoves
+        const uint32_t parL = (L & 1u) ? kStPar : 0u;
+        const uint32_t parN = parL ^ kStPar;
+        const uint32_t sv = this->ld_state(v);
+        const uint32_t bv = (sv >> kStBShift) & kNone10, kv = sv & kStKMask;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const uint32_t w = this->nbr(v, d);
+            if (w == kNone32 || w == p.vc) continue;
+            const uint32_t sw = this->ld_state(w);
+            if (sw & kStSettled) continue;
+            const int dw = d ^ 1;  // direction of v as seen from w
+            // ownership: the frontier neighbour of w with the lowest direction claims w;
+            // best candidate: lowest prio among w's level-L neighbours
+            bool owner = true;
+            uint32_t bb = bv, bk = kv + 1u, bp = prio[bv];
+#pragma unroll
+            for (int d2 = 0; d2 < 4; ++d2) {
+                if (d2 == dw) continue;
+                const uint32_t u = this->nbr(w, d2);
+                if (u == kNone32 || u == p.vc) continue;
+                const uint32_t su = this->ld_state(u);
+                if (!(su & kStSettled) || (su & kStPar) != parL) continue;
+                if (d2 < dw) owner = false;
+                const uint32_t b = (su >> kStBShift) & kNone10;
+                const uint32_t pr = prio[b];
+                if (pr < bp) {
+                    bp = pr;
+                    bb = b;
+                    bk = (su & kStKMask) + 1u;
+                }
+            }
+            if (!owner) continue;
+            if (bk > kStKMask) {
+                this->flag(kErrKOverflow);
+                continue;
+            }
+            const uint32_t t = sw & kNone10;  // static info of the untouched word
+            if (t != kNone10) {  // a special: offer the walk label to the table
+                View c;
+                this->view_walk(bb, bk, w, c);
+                this->try_improve(t, c);
+                continue;
+            }
+            this->st_state(w, kStSettled | parN | (bb << kStBShift) | bk);
+            const uint32_t i = atomicAdd(&sh->cnt[cn], 1u);
+            this->st_idx(Fn, i, w);
+            if (p.use_soe) {
+                const uint32_t r = (sw >> 10) & kNone10;
+                if (r != kNone10 && !fired[r]) atomicMin(best64 + r, ((unsigned long long)bp << 32) | a->rank[w]);
+            }
         }
     }
 
-    // ---- phase 3: pull -----------------------------------------------------------
-    __device__ void pull(uint32_t w) const {
+    __device__ __forceinline__ void solve(uint32_t s_idx) {
+        const DevParams &p = a->p;
+        const uint32_t tid = threadIdx.x;
+        this->init_source(s_idx);
+        for (uint32_t t = tid; t <= p.NS; t += kBS) {
+            best64[t] = kInf64;
+            fired[t] = 0;
+        }
+        if (tid == 0) {
+            sh->cnt[0] = sh->cnt[1] = 0;
+            sh->lb = 0;
+            sh->L = 0;
+            sh->done = 0;
+            sh->jump = 0;
+            sh->nbnd = 1;
+            sh->ranked = 1;
+            bnd[0] = 0;
+            prio[0] = 0;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            this->seed_root();
+            View st;
+            this->view_start(st);
+            const uint32_t ts = this->special_of(src);
+            if (ts != kNone10) {
+                this->try_improve(ts, st);
+            } else {
+                this->st_state(src, kStSettled);  // level 0 (parity 0), walk (0,0) = the start label
+                sh->cnt[0] = 1;
+                this->st_idx(F0, 0, src);
+                const uint32_t r = this->region_of(src);
+                if (p.use_soe && r != kNone10) {  // [SoE src -> nearest campfire]
+                    View c;
+                    this->soe_from_plain(0, 0, src, r, c);
+                    this->try_improve(r, c);
+                    fired[r] = 1;
+                }
+            }
+            this->seed_scrolls();
+        }
+        __syncthreads();
+        for (uint32_t guard = 0;; ++guard) {
+            // ---- specials of level L (wave 0) ----
+            if (tid < 64) {
+                const uint32_t L = sh->L;
+                const uint32_t cur = sh->lb;
+                if (p.use_soe) fire_regions();
+                for (uint32_t it = 0; it <= p.NS; ++it) {
+                    const uint32_t s = this->argmin_special(L);
+                    if (s == kNone32) break;
+                    const bool boundary = this->settle_special(s, (L & 1u) ? kStPar : 0u);
+                    if (lane_id() == 0) {
+                        const uint32_t i = sh->cnt[cur]++;
+                        this->st_idx(frontier(cur), i, this->sp[s].v);
+                        if (boundary) bnd[sh->nbnd++] = s;
+                    }
+                    wave_sync();
+                }
+                const uint32_t done = this->dsts_done();
+                const uint32_t n = sh->cnt[cur];
+                if (n == 0) {  // empty frontier: jump to the next special level
+                    const unsigned long long smin = this->min_special_key();
+                    if (lane_id() == 0) {
+                        sh->jump = 1;
+                        sh->done = (smin == kInf64 || done) ? 1u : 0u;
+                        if (smin != kInf64) sh->L = uint32_t(smin);
+                    }
+                } else {
+                    // with a linear run time (Fleetfoot 0 / out of range) the order of
+                    // boundaries does not depend on the level: re-rank only when one is added
+                    if (p.ff_num != p.ff_den || sh->ranked != sh->nbnd) {
+                        rank_boundaries(L + 1);
+                        if (lane_id() == 0) sh->ranked = sh->nbnd;
+                    }
+                    if (lane_id() == 0) {
+                        sh->jump = 0;
+                        sh->done = done;
+                        sh->cnt[cur ^ 1u] = 0;
+                    }
+                }
+            }
+            __syncthreads();
+            if (sh->done) break;
+            if (guard > p.V + p.NS + 64u) {
+                this->flag(kErrBucket);
+                break;
+            }
+            if (sh->jump) continue;
+            // ---- claim level L+1 from the level-L frontier (all threads) ----
+            {
+                const uint32_t L = sh->L, cur = sh->lb, n = sh->cnt[cur];
+                const IdxT *Fc = frontier(cur);
+                IdxT *Fn = frontier(cur ^ 1u);
+                for (uint32_t i = tid; i < n; i += kBS) claim_from(this->ld_idx(Fc, i), L, Fn, cur ^ 1u);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                sh->lb ^= 1u;
+                sh->L += 1;
+            }
+            __syncthreads();
+        }
+        this->write_outputs(s_idx);
+        __syncthreads();
+    }
+};
+
+// ===================================================================================
+// Generic bucketed solver (Time- or Money-first comparators)
+// ===================================================================================
+template <bool G, class IdxT>
+struct GenericSolver : Core<G> {
+    using Core<G>::a;
+    using Core<G>::sh;
+    using Core<G>::R;
+    using Core<G>::state;
+    using Core<G>::src;
+    IdxT *L0b, *dirty;  // the three bucket lists are L0b + i * lstride
+    uint32_t lstride;
+    uint32_t *best;
+    uint32_t *fired;
+
+    __device__ __forceinline__ IdxT *lbuf(uint32_t i) const { return L0b + i * lstride; }
+
+    __device__ __forceinline__ void mark_dirty(uint32_t v, uint32_t n) const {
+        const DevParams &p = a->p;
+        if (n == kNone32 || v == p.vc || n == p.vc) return;
+        const uint32_t old = this->or_state(n, kStDirty);
+        if (old & (kStSettled | kStDirty)) return;
+        const uint32_t i = atomicAdd(&sh->nd, 1u);
+        this->st_idx(dirty, i, n);
+    }
+    __device__ __forceinline__ void region_offer(uint32_t r, uint32_t v) const {
+        uint32_t cur = best[r];
+        for (;;) {
+            if (cur != kNone32) {
+                const uint32_t su = this->ld_state(cur), sv = this->ld_state(v);
+                View xu, xv;
+                this->view_walk((su >> kStBShift) & kNone10, su & kStKMask, cur, xu);
+                this->view_walk((sv >> kStBShift) & kNone10, sv & kStKMask, v, xv);
+                if (this->cmp_view(xu, kOwn, xv, kOwn) <= 0) return;
+            }
+            const uint32_t prev = atomicCAS(best + r, cur, v);
+            if (prev == cur) return;
+            cur = prev;
+        }
+    }
+    __device__ __forceinline__ void settle_plain(uint32_t v) const {
+        const DevParams &p = a->p;
+        this->or_state(v, kStSettled);
+        if (p.use_soe) {
+            const uint32_t r = this->region_of(v);
+            if (r != kNone10 && !fired[r]) region_offer(r, v);
+        }
+#pragma unroll
+        for (int d = 0; d < 4; ++d) mark_dirty(v, this->nbr(v, d));
+    }
+    __device__ __forceinline__ void fire_regions() const {
+        const DevParams &p = a->p;
+        for (uint32_t t = 1 + lane_id(); t <= p.NS; t += 64) {
+            const uint32_t u = best[t];
+            if (u == kNone32) continue;
+            best[t] = kNone32;
+            fired[t] = 1;
+            if (R[t].state == 2) continue;
+            const uint32_t su = this->ld_state(u);
+            View c;
+            this->soe_from_plain((su >> kStBShift) & kNone10, su & kStKMask, u, t, c);
+            this->try_improve(t, c);
+        }
+        wave_sync();
+    }
+    __device__ __forceinline__ void pull(uint32_t w) const {
+        const DevParams &p = a->p;
         // a vertex marked dirty may have been settled later in the same bucket
-        // (a plain vertex of bucket B, or a special settled by the table)
-        if (ld_state(w) & kStSettled) return;
-        const uint32_t t = special_of(w);
+        if (this->ld_state(w) & kStSettled) return;
+        const uint32_t t = this->special_of(w);
         uint32_t bb = kNone10, bk = 0;
         if (w != p.vc) {
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
-                uint32_t n = nbr(w, d);
+                const uint32_t n = this->nbr(w, d);
                 if (n == kNone32 || n == p.vc) continue;
-                uint32_t sn = ld_state(n);
+                const uint32_t sn = this->ld_state(n);
                 if (!(sn & kStSettled)) continue;
-                uint32_t b = (sn >> kStBShift) & kNone10, k = (sn & kStKMask) + 1u;
+                const uint32_t b = (sn >> kStBShift) & kNone10, k = (sn & kStKMask) + 1u;
                 if (k > kStKMask) {
-                    flag(kErrKOverflow);
+                    this->flag(kErrKOverflow);
                     continue;
                 }
                 if (bb == kNone10) {
@@ -468,9 +881,9 @@ struct Solver {
                     if (k < bk) bk = k;  // same boundary: fewer legs is smaller in every order
                 } else {
                     View xc, xb;
-                    view_walk(b, k, w, xc);
-                    view_walk(bb, bk, w, xb);
-                    if (cmp_view(xc, kOwn, xb, kOwn) < 0) {
+                    this->view_walk(b, k, w, xc);
+                    this->view_walk(bb, bk, w, xb);
+                    if (this->cmp_view(xc, kOwn, xb, kOwn) < 0) {
                         bb = b;
                         bk = k;
                     }
@@ -478,61 +891,41 @@ struct Solver {
             }
         }
         if (t != kNone10) {
-            st_state(w, kStUntouched);
+            this->st_state(w, this->ld_state(w) & ~kStDirty);
             if (bb != kNone10) {
                 View c;
-                view_walk(bb, bk, w, c);
-                try_improve(t, c);
+                this->view_walk(bb, bk, w, c);
+                this->try_improve(t, c);
             }
             return;
         }
-        uint32_t old = ld_state(w);
+        const uint32_t old = this->ld_state(w);
         if (bb == kNone10) {  // cannot happen: a dirty vertex has a settled StandardMove neighbour
-            st_state(w, old & ~kStDirty);
-            flag(kErrBucket);
+            this->st_state(w, old & ~kStDirty);
+            this->flag(kErrBucket);
             return;
         }
-        st_state(w, (bb << kStBShift) | bk);
-        if (((old >> kStBShift) & kNone10) == kNone10) {  // first touch: list it
+        this->st_state(w, (bb << kStBShift) | bk);
+        if (((old >> kStBShift) & kNone10) == kNone10) {  // first touch: list it (its bucket is final)
             View c;
-            view_walk(bb, bk, w, c);
-            unsigned long long X = key_of(c.m), B = sh->B;
+            this->view_walk(bb, bk, w, c);
+            const unsigned long long X = this->key_of(c.m0, c.m1, c.m2), B = sh->B;
             uint32_t j;
             if (X == B + 1) j = 1;
             else if (X == B + 2) j = 2;
             else {
-                flag(kErrBucket);
+                this->flag(kErrBucket);
                 return;
             }
-            uint32_t buf = (sh->lb + j) % 3u;
-            uint32_t i = atomicAdd(&sh->cnt[buf], 1u);
-            st_idx(lbuf[buf], i, w);
+            const uint32_t buf = (sh->lb + j) % 3u;
+            const uint32_t i = atomicAdd(&sh->cnt[buf], 1u);
+            this->st_idx(lbuf(buf), i, w);
         }
     }
-
-    // ---- phase 4: next bucket ----------------------------------------------------
-    __device__ void next_bucket(uint32_t s) const {
-        const uint32_t lane = lane_id();
-        unsigned long long smin = kInf64;
-        for (uint32_t t = 1 + lane; t <= p.NS; t += 64)
-            if (R[t].state == 1) {
-                unsigned long long k = key_of(R[t].m);
-                if (k < smin) smin = k;
-            }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            unsigned long long o = __shfl_xor(smin, off, 64);
-            if (o < smin) smin = o;
-        }
-        // early exit once every destination of this source is settled
-        uint32_t all_done = 0;
-        const uint32_t q0 = a.q_begin[s], q1 = a.q_begin[s + 1];
-        if (q1 - q0 <= a.early_exit_max) {
-            bool ok = true;
-            if (lane < q1 - q0) ok = (ld_state(a.q_dst[q0 + lane]) & kStSettled) != 0;
-            all_done = __all(ok) ? 1u : 0u;
-        }
-        if (lane == 0) {
+    __device__ __forceinline__ void next_bucket(uint32_t s_idx) const {
+        const unsigned long long smin = this->min_special_key();
+        const uint32_t all_done = this->dsts_done();
+        if (lane_id() == 0) {
             const unsigned long long B = sh->B;
             const uint32_t lb = sh->lb;
             const uint32_t n1 = sh->cnt[(lb + 1) % 3u], n2 = sh->cnt[(lb + 2) % 3u];
@@ -546,51 +939,11 @@ struct Solver {
             sh->done = (nb == kInf64 || all_done) ? 1u : 0u;
         }
     }
-
-    // ---- outputs -----------------------------------------------------------------
-    __device__ void write_output(uint32_t w, uint32_t qid) const {
-        OutResult &o = a.out_res[qid];
-        const uint32_t sw = ld_state(w);
-        if (!(sw & kStSettled)) {
-            o = OutResult{0, 0, 0, uint32_t(16 + 1) << 16};  // MR_NOT_FOUND
-            return;
-        }
-        View x;
-        uint32_t xid = kOwn;
-        const uint32_t t = special_of(w);
-        if (t != kNone10) {
-            view_rec(t, x);
-            xid = t;
-        } else {
-            view_walk((sw >> kStBShift) & kNone10, sw & kStKMask, w, x);
-        }
-        if (x.len > p.max_cmds) {  // MR_ERR_CAPACITY: caller re-runs with more slots
-            o = OutResult{x.m[0], x.m[1], x.m[2], (uint32_t(16 - 4) << 16) | (x.len & 0xFFFFu)};
-            return;
-        }
-        OutCmd *oc = a.out_cmd + (unsigned long long)qid * p.max_cmds;
-        int pos = int(x.len) - 1;
-        for (int j = int(x.ntail) - 1; j >= 0 && pos >= 0; --j, --pos)
-            oc[pos] = OutCmd{x.tail[j].kp, x.tail[j].from, x.tail[j].to, 0};
-        uint32_t pp = x.parent;
-        while (pp != 0 && pos >= 0) {
-            const Rec &r = R[pp];
-            for (int j = int(r.ntail) - 1; j >= 0 && pos >= 0; --j, --pos)
-                oc[pos] = OutCmd{r.tail[j].kp, r.tail[j].from, r.tail[j].to, 0};
-            pp = r.parent;
-        }
-        if (pos != -1 || pp != 0) flag(kErrChain);
-        (void)xid;
-        o = OutResult{x.m[0], x.m[1], x.m[2], (uint32_t(16) << 16) | (x.len & 0xFFFFu)};
-    }
-
-    // ---- one source ----------------------------------------------------------------
-    __device__ void solve(uint32_t s) {
+    __device__ __forceinline__ void solve(uint32_t s_idx) {
+        const DevParams &p = a->p;
         const uint32_t tid = threadIdx.x;
-        src = a.src_v[s];
-        for (uint32_t v = tid; v < p.V; v += kBS) st_state(v, kStUntouched);
+        this->init_source(s_idx);
         for (uint32_t t = tid; t <= p.NS; t += kBS) {
-            R[t].state = 0;
             best[t] = kNone32;
             fired[t] = 0;
         }
@@ -603,166 +956,211 @@ struct Solver {
         }
         __syncthreads();
         if (tid == 0) {
+            this->seed_root();
             View st;
-            view_start(st);
-            // entry 0 = the source (root of every command chain)
-            R[0].m[0] = R[0].m[1] = R[0].m[2] = 0;
-            R[0].len = 1;
-            R[0].ntail = 1;
-            R[0].parent = 0;
-            R[0].tail[0] = st.tail[0];
-            R[0].state = 2;
-            const uint32_t ts = special_of(src);
+            this->view_start(st);
+            const uint32_t ts = this->special_of(src);
             if (ts != kNone10) {
-                try_improve(ts, st);
+                this->try_improve(ts, st);
             } else {
-                st_state(src, 0u);  // walk label (0,0) = the start label
+                this->st_state(src, 0u);  // walk label (0,0) = the start label
                 sh->cnt[0] = 1;
-                st_idx(lbuf[0], 0, src);
+                this->st_idx(L0b, 0, src);
             }
-            // SHQ / SFm: only the source's own edges can be minimal (a prefix only
-            // adds metrics and length), src/pathfinder.rs:172-178
-            if (p.hq_t) {
-                View c;
-                view_start(c);
-                c.m[1] = p.shq_cost;
-                c.tail[0] = Cmd{kSHQ << 29, src, a.sp[p.hq_t].v};
-                try_improve(p.hq_t, c);
-            }
-            if (p.use_sfm) {
-                View c;
-                view_start(c);
-                c.m[1] = p.sfm_cost;
-                c.tail[0] = Cmd{kSFm << 29, src, p.vc};
-                try_improve(1, c);
-            }
+            this->seed_scrolls();
         }
         __syncthreads();
         for (uint32_t guard = 0;; ++guard) {
-            // 1. settle
             {
-                const uint32_t lb = sh->lb;
-                const uint32_t n0 = sh->cnt[lb];
-                const IdxT *L0 = lbuf[lb];
-                for (uint32_t i = tid; i < n0; i += kBS) settle_plain(ld_idx(L0, i));
+                const uint32_t lb = sh->lb, n0 = sh->cnt[lb];
+                const IdxT *L0 = lbuf(lb);
+                for (uint32_t i = tid; i < n0; i += kBS) settle_plain(this->ld_idx(L0, i));
             }
             __syncthreads();
-            // 2. specials
             if (tid < 64) {
                 if (p.use_soe) fire_regions();
-                specials_in_bucket(sh->B);
+                const unsigned long long B = sh->B;
+                for (uint32_t it = 0; it <= p.NS; ++it) {
+                    const uint32_t s = this->argmin_special(B);
+                    if (s == kNone32) break;
+                    this->settle_special(s, 0u);
+                    const uint32_t vs = this->sp[s].v;
+                    if (lane_id() < 4) mark_dirty(vs, this->nbr(vs, int(lane_id())));
+                    wave_sync();
+                }
             }
             __syncthreads();
-            // 3. pull
             {
                 const uint32_t nd = sh->nd;
-                for (uint32_t i = tid; i < nd; i += kBS) pull(ld_idx(dirty, i));
+                for (uint32_t i = tid; i < nd; i += kBS) pull(this->ld_idx(dirty, i));
             }
             __syncthreads();
-            // 4. next bucket
-            if (tid < 64) next_bucket(s);
+            if (tid < 64) next_bucket(s_idx);
             __syncthreads();
             if (sh->done) break;
             if (guard > p.V + p.NS + 64u) {
-                flag(kErrBucket);
+                this->flag(kErrBucket);
                 break;
             }
         }
-        const uint32_t q0 = a.q_begin[s], q1 = a.q_begin[s + 1];
-        for (uint32_t i = q0 + tid; i < q1; i += kBS) write_output(a.q_dst[i], a.q_id[i]);
+        this->write_outputs(s_idx);
         __syncthreads();
     }
 };
 
+// ===================================================================================
+// LDS layout and kernels
+// ===================================================================================
 __host__ __device__ constexpr uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
 
 struct LdsLayout {
-    uint32_t off_R, off_best, off_fired, off_state, off_l0, off_l1, off_l2, off_dirty, total;
+    uint32_t off_R, off_a, off_b, off_c, off_d, off_sp, off_hubs, off_dst, off_state, off_l[4], total;
 };
 
-__host__ __device__ inline LdsLayout lds_layout(uint32_t NS, uint32_t V, bool grid_in_lds) {
+// per-table arrays (NS+1 entries each): a 8 B (legs: best64), b/c/d 4 B
+// (legs: prio, bnd, fired; generic: best, -, fired); grid part (LDS regime):
+// state 4 B/vertex + 2 (legs) or 4 (generic) u16 lists.
+__host__ __device__ inline LdsLayout lds_layout(uint32_t NS, uint32_t V, bool grid_in_lds, uint32_t algo) {
     LdsLayout L{};
+    const uint32_t T = NS + 1;
     uint32_t o = align16(sizeof(Shared));
     L.off_R = o;
-    o = align16(o + (NS + 1) * sizeof(Rec));
-    L.off_best = o;
-    o = align16(o + (NS + 1) * 4);
-    L.off_fired = o;
-    o = align16(o + (NS + 1) * 4);
+    o = align16(o + T * uint32_t(sizeof(Rec)));
+    L.off_a = o;
+    o = align16(o + T * 8);
+    L.off_b = o;
+    o = align16(o + T * 4);
+    L.off_c = o;
+    o = align16(o + T * 4);
+    L.off_d = o;
+    o = align16(o + T * 4);
+    L.off_sp = o;
+    o = align16(o + T * uint32_t(sizeof(SpecialStatic)));
+    L.off_hubs = o;
+    o = align16(o + T * 2);
+    L.off_dst = o;
+    o = align16(o + 64 * 4);
     if (grid_in_lds) {
         L.off_state = o;
         o = align16(o + V * 4);
-        L.off_l0 = o;
-        o = align16(o + V * 2);
-        L.off_l1 = o;
-        o = align16(o + V * 2);
-        L.off_l2 = o;
-        o = align16(o + V * 2);
-        L.off_dirty = o;
-        o = align16(o + V * 2);
+        const uint32_t nl = algo == kAlgoLegs ? 2u : 4u;
+        for (uint32_t i = 0; i < 4; ++i) {
+            L.off_l[i] = o;
+            if (i < nl) o = align16(o + V * 2);
+        }
     }
     L.total = o;
     return L;
 }
 
-template <bool G, class IdxT>
-__global__ __launch_bounds__(kBS) void sssp_kernel(KArgs a) {
+template <bool G, class IdxT, uint32_t ALGO>
+__global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const LdsLayout L = lds_layout(a.p.NS, a.p.V, !G);
+    const uint32_t V = a->p.V, NS = a->p.NS;
+    const LdsLayout L = lds_layout(NS, V, !G, ALGO);
     Shared *sh = reinterpret_cast<Shared *>(smem);
     Rec *R = reinterpret_cast<Rec *>(smem + L.off_R);
-    uint32_t *best = reinterpret_cast<uint32_t *>(smem + L.off_best);
-    uint32_t *fired = reinterpret_cast<uint32_t *>(smem + L.off_fired);
     uint32_t *state;
-    IdxT *l0, *l1, *l2, *dirty;
+    IdxT *l0, *l1, *l2, *l3;
     if constexpr (G) {
-        uint32_t *slot = a.ws + (unsigned long long)blockIdx.x * 5ull * a.p.V;
+        uint32_t *slot = a->ws + (unsigned long long)blockIdx.x * 5ull * V;
         state = slot;
-        l0 = reinterpret_cast<IdxT *>(slot + a.p.V);
-        l1 = reinterpret_cast<IdxT *>(slot + 2ull * a.p.V);
-        l2 = reinterpret_cast<IdxT *>(slot + 3ull * a.p.V);
-        dirty = reinterpret_cast<IdxT *>(slot + 4ull * a.p.V);
+        l0 = reinterpret_cast<IdxT *>(slot + V);
+        l1 = reinterpret_cast<IdxT *>(slot + 2ull * V);
+        l2 = reinterpret_cast<IdxT *>(slot + 3ull * V);
+        l3 = reinterpret_cast<IdxT *>(slot + 4ull * V);
     } else {
         state = reinterpret_cast<uint32_t *>(smem + L.off_state);
-        l0 = reinterpret_cast<IdxT *>(smem + L.off_l0);
-        l1 = reinterpret_cast<IdxT *>(smem + L.off_l1);
-        l2 = reinterpret_cast<IdxT *>(smem + L.off_l2);
-        dirty = reinterpret_cast<IdxT *>(smem + L.off_dirty);
+        l0 = reinterpret_cast<IdxT *>(smem + L.off_l[0]);
+        l1 = reinterpret_cast<IdxT *>(smem + L.off_l[1]);
+        l2 = reinterpret_cast<IdxT *>(smem + L.off_l[2]);
+        l3 = reinterpret_cast<IdxT *>(smem + L.off_l[3]);
     }
-    Solver<G, IdxT> S(a, sh, R, best, fired, state, l0, l1, l2, dirty);
-    for (;;) {
-        if (threadIdx.x == 0) sh->sidx = atomicAdd(a.counter, 1u);
-        __syncthreads();
-        const uint32_t s = sh->sidx;
-        __syncthreads();
-        if (s >= a.nsrc) break;
-        S.solve(s);
-    }
-}
-
-// ---- host-side launch helpers (called from mr_api.cpp) -------------------------
-uint32_t lds_bytes(uint32_t NS, uint32_t V, bool grid_in_lds) { return lds_layout(NS, V, grid_in_lds).total; }
-
-hipError_t launch_sssp(const KArgs &a, bool grid_in_lds, uint32_t blocks, hipStream_t stream) {
-    const uint32_t bytes = lds_bytes(a.p.NS, a.p.V, grid_in_lds);
-    if (grid_in_lds) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&sssp_kernel<false, uint16_t>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
-        hipLaunchKernelGGL((sssp_kernel<false, uint16_t>), dim3(blocks), dim3(kBS), bytes, stream, a);
+    SpecialStatic *spl = reinterpret_cast<SpecialStatic *>(smem + L.off_sp);
+    uint16_t *hubl = reinterpret_cast<uint16_t *>(smem + L.off_hubs);
+    uint32_t *dstl = reinterpret_cast<uint32_t *>(smem + L.off_dst);
+    for (uint32_t t = threadIdx.x; t <= NS; t += kBS) spl[t] = a->sp[t];
+    for (uint32_t h = threadIdx.x; h < a->p.n_hubs; h += kBS) hubl[h] = a->hubs[h];
+    __syncthreads();
+    if constexpr (ALGO == kAlgoLegs) {
+        LegsSolver<G, IdxT> S;
+        S.a = a;
+        S.sh = sh;
+        S.R = R;
+        S.state = state;
+        S.sp = spl;
+        S.hubs = hubl;
+        S.dst = dstl;
+        S.src = 0;
+        S.F0 = l0;
+        S.F1 = l1;
+        S.best64 = reinterpret_cast<unsigned long long *>(smem + L.off_a);
+        S.prio = reinterpret_cast<uint32_t *>(smem + L.off_b);
+        S.bnd = reinterpret_cast<uint32_t *>(smem + L.off_c);
+        S.fired = reinterpret_cast<uint32_t *>(smem + L.off_d);
+        (void)l2;
+        (void)l3;
+        for (;;) {
+            if (threadIdx.x == 0) sh->sidx = atomicAdd(a->counter, 1u);
+            __syncthreads();
+            const uint32_t s = sh->sidx;
+            __syncthreads();
+            if (s >= a->nsrc) break;
+            S.solve(s);
+        }
     } else {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&sssp_kernel<true, uint32_t>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
-        hipLaunchKernelGGL((sssp_kernel<true, uint32_t>), dim3(blocks), dim3(kBS), bytes, stream, a);
+        GenericSolver<G, IdxT> S;
+        S.a = a;
+        S.sh = sh;
+        S.R = R;
+        S.state = state;
+        S.sp = spl;
+        S.hubs = hubl;
+        S.dst = dstl;
+        S.src = 0;
+        S.L0b = l0;
+        S.lstride = uint32_t(l1 - l0);
+        S.dirty = l3;
+        S.best = reinterpret_cast<uint32_t *>(smem + L.off_b);
+        S.fired = reinterpret_cast<uint32_t *>(smem + L.off_d);
+        for (;;) {
+            if (threadIdx.x == 0) sh->sidx = atomicAdd(a->counter, 1u);
+            __syncthreads();
+            const uint32_t s = sh->sidx;
+            __syncthreads();
+            if (s >= a->nsrc) break;
+            S.solve(s);
+        }
     }
-    return hipGetLastError();
 }
 
-int max_blocks_per_cu(bool grid_in_lds, uint32_t bytes) {
+// ---- host-side launch helpers (called from mr_host.cpp) ------------------------------
+uint32_t lds_bytes(uint32_t NS, uint32_t V, bool grid_in_lds, uint32_t algo) {
+    return lds_layout(NS, V, grid_in_lds, algo).total;
+}
+
+template <bool G, class IdxT, uint32_t ALGO>
+static const void *kfn() {
+    return reinterpret_cast<const void *>(&solve_kernel<G, IdxT, ALGO>);
+}
+
+static const void *select_kernel(bool grid_in_lds, uint32_t algo) {
+    if (grid_in_lds) return algo == kAlgoLegs ? kfn<false, uint16_t, kAlgoLegs>() : kfn<false, uint16_t, kAlgoGeneric>();
+    return algo == kAlgoLegs ? kfn<true, uint32_t, kAlgoLegs>() : kfn<true, uint32_t, kAlgoGeneric>();
+}
+
+hipError_t launch_solve(const KArgs *d_args, bool grid_in_lds, uint32_t algo, uint32_t NS, uint32_t V,
+                        uint32_t blocks, hipStream_t stream) {
+    const uint32_t bytes = lds_bytes(NS, V, grid_in_lds, algo);
+    const void *fn = select_kernel(grid_in_lds, algo);
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
+    void *args[] = {const_cast<KArgs **>(&d_args)};
+    return hipLaunchKernel(fn, dim3(blocks), dim3(kBS), args, bytes, stream);
+}
+
+int max_blocks_per_cu(bool grid_in_lds, uint32_t algo, uint32_t bytes) {
     int n = 0;
-    if (grid_in_lds)
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, sssp_kernel<false, uint16_t>, kBS, bytes);
-    else
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, sssp_kernel<true, uint32_t>, kBS, bytes);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, select_kernel(grid_in_lds, algo), kBS, bytes);
     return n;
 }
 

@@ -23,9 +23,16 @@ def eng():
     return pathfinder
 
 
-@pytest.fixture(params=["lds", "hbm"])
+@pytest.fixture(params=["lds-auto", "hbm-auto", "lds-generic", "hbm-generic"])
 def grid_state(request, monkeypatch):
-    monkeypatch.setenv("MR_GRID_STATE", request.param)
+    """Both grid-state regimes x both solvers (Legs-first parameters use the
+    level-synchronous solver unless MR_ALGO=generic forces the bucketed one)."""
+    state, algo = request.param.split("-")
+    monkeypatch.setenv("MR_GRID_STATE", state)
+    if algo == "generic":
+        monkeypatch.setenv("MR_ALGO", "generic")
+    else:
+        monkeypatch.delenv("MR_ALGO", raising=False)
     return request.param
 
 
