@@ -24,6 +24,18 @@ def _stale() -> bool:
     return any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in SOURCES + HEADERS)
 
 
+def build_diag(verbose: bool = False) -> str:
+    """Diagnostic build with per-phase s_memtime stamps (-DMR_STAMPS) into
+    lib/diag/; load it with MR_LIB_PATH=<path>.  Never used by the product path."""
+    out = os.path.join(LIB_DIR, "diag", "libmarshrutka_pf.so")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [HIPCC, *FLAGS, "-DMR_STAMPS", *[os.path.join(CSRC, s) for s in SOURCES], "-o", out]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return out
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB_PATH
@@ -38,5 +50,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, verbose=True)
-    print(LIB_PATH)
+    if "--diag" in sys.argv:
+        print(build_diag(verbose=True))
+    else:
+        build(force="--force" in sys.argv, verbose=True)
+        print(LIB_PATH)

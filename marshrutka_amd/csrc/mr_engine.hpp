@@ -61,6 +61,8 @@ struct SpecialStatic {
     uint32_t flags;   // bit0 center, bit1 border-1, bit2 caravan hub
     uint32_t region;  // table index of this cell's nearest campfire (query homeland), kNone10 if none
     uint32_t coef5;   // 1 if a caravan INTO this special costs 5/distance (else 2)
+    uint32_t rid;     // hub solver: region id if this is a query-homeland campfire, else kNone10
+    uint32_t pad;
 };
 constexpr uint32_t kSpCenter = 1u, kSpBorder1 = 2u, kSpHub = 4u;
 
@@ -107,11 +109,19 @@ struct KArgs {
     OutResult *out_res;          // per query id
     OutCmd *out_cmd;             // per query id * max_cmds
     uint32_t *ws;                // grid-in-HBM mode: per-workgroup slots of 5*V words
-    uint32_t *counter;           // [0] source dequeue, [1] error flags
+    uint32_t *counter;           // [0] source dequeue, [1] error flags, [2] fallback count, [3] fallback dequeue
     uint32_t nsrc;
     uint32_t early_exit_max;     // early exit if a source has <= this many destinations (<= 64)
     uint32_t grid_in_lds;        // 1: grid state in LDS, 0: per-workgroup HBM slots
     uint32_t algo;               // kAlgoLegs (Legs-first level-synchronous) or kAlgoGeneric
+    unsigned long long *dbg;     // diagnostic builds (-DMR_STAMPS): per-workgroup phase cycles
+    // hub solver (linear run time): per vertex and region, the nearest region cell by
+    // walk distance avoiding the Center: near[2*(v*nreg + r)] = {distance, cell}
+    const uint32_t *near;
+    uint32_t nreg;
+    uint32_t *fb_list;           // sources the hub solver hands to the SSSP kernel (counter[2] of them)
+    uint32_t fb_mode;            // 1: this SSSP launch solves fb_list[counter[3]++] only
+    uint32_t fb_all;             // tests: the hub solver hands every source to the SSSP kernel
 };
 enum : uint32_t { kAlgoGeneric = 0, kAlgoLegs = 1 };
 

@@ -23,6 +23,9 @@ uint32_t lds_bytes(uint32_t NS, uint32_t V, bool grid_in_lds, uint32_t algo);
 hipError_t launch_solve(const KArgs *d_args, bool grid_in_lds, uint32_t algo, uint32_t NS, uint32_t V,
                         uint32_t blocks, hipStream_t stream);
 int max_blocks_per_cu(bool grid_in_lds, uint32_t algo, uint32_t bytes);
+uint32_t hub_lds_bytes(uint32_t NS);
+hipError_t launch_hub(const KArgs *d_args, uint32_t NS, uint32_t blocks, hipStream_t stream);
+int hub_blocks_per_cu(uint32_t bytes);
 }  // namespace mr
 
 
@@ -102,6 +105,13 @@ struct mr_grid {
     std::vector<uint32_t> rank_inv;        // vertex of each rank
     std::vector<uint32_t> campfires;       // vertex ids, CellIndex order
     std::vector<uint32_t> nearest[4];      // nearest campfire vertex per homeland (kNone32)
+    // hub solver: per homeland, the regions (campfires of the homeland, CellIndex order) and
+    // for every vertex and region the nearest cell of that region by walk distance avoiding
+    // the Center, ties by CellIndex order: near[2*(v*nreg+r)] = {distance, cell}
+    mutable std::mutex near_mu;
+    mutable std::vector<uint32_t> regions[4];
+    mutable std::vector<uint32_t> near[4];
+    mutable bool near_built[4] = {false, false, false, false};
     int32_t gx(uint32_t v) const { return int32_t(v % S) - int32_t(H); }
     int32_t gy(uint32_t v) const { return int32_t(v / S) - int32_t(H); }
     bool find(const mr_cell_index &c, uint32_t &v) const {
@@ -270,6 +280,65 @@ extern "C" int mr_device_available(void) {
     return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
 }
 
+// Region tables for the hub solver (built lazily, once per grid and homeland).
+// A multi-source BFS per region over the grid minus the Center (walks cannot
+// cross it, src/pathfinder.rs:30-53) propagates (distance, rank of origin)
+// lexicographic minima along shortest paths.
+static const std::vector<uint32_t> &region_table(const mr_grid *g, int h, const std::vector<uint32_t> *&regions) {
+    std::lock_guard<std::mutex> lk(g->near_mu);
+    regions = &g->regions[h];
+    if (g->near_built[h]) return g->near[h];
+    const uint32_t V = g->V, S = g->S;
+    std::vector<uint32_t> regs;
+    for (uint32_t v : g->campfires) {
+        const mr_cell_index &c = g->idx[v];
+        if (c.kind == MR_CELL_HOMELAND && c.sub == h) regs.push_back(v);  // campfires: CellIndex order
+    }
+    const uint32_t nreg = uint32_t(regs.size());
+    std::vector<uint32_t> rid(V, kNone32);
+    for (uint32_t r = 0; r < nreg; ++r) rid[regs[r]] = r;
+    std::vector<uint32_t> tab(size_t(V) * nreg * 2, kNone32);
+    std::vector<uint32_t> dist(V), org(V), cur, nxt;
+    for (uint32_t r = 0; r < nreg; ++r) {
+        std::fill(dist.begin(), dist.end(), kNone32);
+        cur.clear();
+        for (uint32_t v = 0; v < V; ++v) {
+            if (v == g->vc || g->nearest[h][v] != regs[r]) continue;
+            dist[v] = 0;
+            org[v] = v;
+            cur.push_back(v);
+        }
+        for (uint32_t d = 0; !cur.empty(); ++d) {
+            nxt.clear();
+            for (uint32_t u : cur) {
+                const uint32_t x = u % S, y = u / S;
+                const uint32_t nb[4] = {x > 0 ? u - 1 : kNone32, x + 1 < S ? u + 1 : kNone32,
+                                        y > 0 ? u - S : kNone32, y + 1 < S ? u + S : kNone32};
+                for (uint32_t w : nb) {
+                    if (w == kNone32 || w == g->vc) continue;
+                    if (dist[w] == kNone32) {
+                        dist[w] = d + 1;
+                        org[w] = org[u];
+                        nxt.push_back(w);
+                    } else if (dist[w] == d + 1 && g->rank[org[u]] < g->rank[org[w]]) {
+                        org[w] = org[u];
+                    }
+                }
+            }
+            cur.swap(nxt);
+        }
+        for (uint32_t v = 0; v < V; ++v) {
+            tab[(size_t(v) * nreg + r) * 2] = dist[v];
+            tab[(size_t(v) * nreg + r) * 2 + 1] = dist[v] == kNone32 ? kNone32 : org[v];
+        }
+    }
+    g->regions[h] = std::move(regs);
+    g->near[h] = std::move(tab);
+    g->near_built[h] = true;
+    (void)rid;
+    return g->near[h];
+}
+
 // ------------------------------------------------------------------ planning
 namespace {
 
@@ -282,6 +351,9 @@ struct HostPlan {
     std::vector<int32_t> q_status;  // per query: MR_OK or a host-side error
     uint32_t nq = 0;
     uint32_t fleetfoot_raw = 0;
+    bool hub = false;                       // hub solver applicable (linear run time, small tables)
+    const std::vector<uint32_t> *near = nullptr;
+    uint32_t nreg = 0;
 };
 
 // (c1, c2) -> (c1, c2', c3): CostComparator::eval_next (src/cost.rs:387-405)
@@ -375,6 +447,30 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
         if (s.flags & kSpHub) hp.hubs.push_back(uint16_t(t));
     }
     p.n_hubs = uint32_t(hp.hubs.size());
+    for (uint32_t t = 1; t <= NS; ++t) hp.sp[t].rid = kNone10;
+    // hub solver: exact when the StandardMove run time is linear (Fleetfoot level 0 or out
+    // of range) — see DESIGN.md §3b; the one non-isotone case is detected per source
+    // and re-solved by the SSSP kernel.  MR_ALGO=sssp|generic disables it.
+    hp.hub = (p.ff_num == p.ff_den) && NS <= 63;
+    if (const char *e = std::getenv("MR_ALGO"))
+        if (!std::strcmp(e, "sssp") || !std::strcmp(e, "generic")) hp.hub = false;
+    if (hp.hub) {
+        size_t nregs = 0;
+        for (uint32_t v : g->campfires)
+            if (g->idx[v].kind == MR_CELL_HOMELAND && g->idx[v].sub == prm->homeland) ++nregs;
+        if (nregs > 63 || size_t(V) * nregs * 8 > (size_t(2) << 30)) hp.hub = false;  // table budget
+    }
+    if (hp.hub) {
+        const std::vector<uint32_t> *regs = nullptr;
+        const std::vector<uint32_t> &tab = region_table(g, prm->homeland, regs);
+        hp.nreg = uint32_t(regs->size());
+        if (hp.nreg > 63) {
+            hp.hub = false;
+        } else {
+            hp.near = &tab;
+            for (uint32_t r = 0; r < hp.nreg; ++r) hp.sp[tix[(*regs)[r]]].rid = r;
+        }
+    }
     hp.sinfo.resize(V);
     for (uint32_t v = 0; v < V; ++v) {
         uint32_t r = near[v] == kNone32 ? kNone10 : tix[near[v]];
@@ -445,6 +541,10 @@ struct mr_plan {
     uint32_t *d_sinfo = nullptr, *d_rank = nullptr, *d_rank_inv = nullptr, *d_src = nullptr, *d_qb = nullptr,
              *d_qd = nullptr, *d_qi = nullptr;
     KArgs *d_args = nullptr;
+    KArgs *d_args_fb = nullptr;           // SSSP launch over the hub solver's fallback list
+    uint32_t *d_near = nullptr, *d_fb = nullptr;
+    uint32_t hub_blocks = 0, fb_blocks = 0;
+    unsigned long long *d_dbg = nullptr;  // diagnostic builds: per-workgroup phase cycles
     uint32_t algo = kAlgoGeneric;
     SpecialStatic *d_sp = nullptr;
     uint16_t *d_hubs = nullptr;
@@ -458,7 +558,8 @@ struct mr_plan {
     ~mr_plan() {
         for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_rank_inv, (void *)d_src, (void *)d_qb, (void *)d_qd,
                         (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
-                        (void *)d_counter, (void *)d_args})
+                        (void *)d_counter, (void *)d_args, (void *)d_dbg, (void *)d_args_fb, (void *)d_near,
+                        (void *)d_fb})
             if (p) (void)hipFree(p);
         for (auto &e : timed) {
             (void)hipEventDestroy(e.first);
@@ -517,6 +618,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     int per_cu = std::max(1, max_blocks_per_cu(pl->grid_in_lds, pl->algo, bytes));
     uint64_t resident = uint64_t(per_cu) * uint64_t(prop.multiProcessorCount);
     uint64_t blocks = std::min<uint64_t>(std::max<uint32_t>(nsrc, 1), resident);
+    if (hp.hub) blocks = std::min<uint64_t>(blocks, 2ull * prop.multiProcessorCount);  // fallback launches only
     if (!pl->grid_in_lds) {
         const uint64_t slot_bytes = 5ull * V * 4ull;
         const uint64_t budget = 64ull << 30;  // HBM budget for solve slots
@@ -546,6 +648,36 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     ka.early_exit_max = 64;
     ka.grid_in_lds = pl->grid_in_lds ? 1u : 0u;
     ka.algo = pl->algo;
+    ka.dbg = nullptr;
+    ka.near = nullptr;
+    ka.nreg = 0;
+    ka.fb_list = nullptr;
+    ka.fb_mode = 0;
+    ka.fb_all = std::getenv("MR_HUB_FALLBACK_ALL") ? 1u : 0u;  // tests cover the fallback path
+    if (hp.hub) {
+        if (upload(pl->d_near, *hp.near) != MR_OK ||
+            hipMalloc(reinterpret_cast<void **>(&pl->d_fb), std::max<size_t>(nsrc, 1) * 4) != hipSuccess)
+            return bail(fail(MR_ERR_DEVICE, "hub tables"));
+        ka.near = pl->d_near;
+        ka.nreg = hp.nreg;
+        ka.fb_list = pl->d_fb;
+        const uint32_t hb = hub_lds_bytes(NS);
+        const int hper = std::max(1, hub_blocks_per_cu(hb));
+        pl->hub_blocks = uint32_t(std::min<uint64_t>((nsrc + 3) / 4, uint64_t(hper) * prop.multiProcessorCount));
+        if (const char *e = std::getenv("MR_HUB_BLOCKS")) pl->hub_blocks = uint32_t(std::max(1, std::atoi(e)));
+        pl->fb_blocks = pl->blocks;
+        KArgs kf = ka;
+        kf.fb_mode = 1;
+        if (hipMalloc(reinterpret_cast<void **>(&pl->d_args_fb), sizeof(KArgs)) != hipSuccess ||
+            hipMemcpy(pl->d_args_fb, &kf, sizeof(KArgs), hipMemcpyHostToDevice) != hipSuccess)
+            return bail(fail(MR_ERR_DEVICE, "kernel args"));
+    }
+#ifdef MR_STAMPS
+    if (hipMalloc(reinterpret_cast<void **>(&pl->d_dbg), size_t(pl->blocks) * 10 * 8) == hipSuccess) {
+        (void)hipMemset(pl->d_dbg, 0, size_t(pl->blocks) * 10 * 8);
+        ka.dbg = pl->d_dbg;
+    }
+#endif
     if (hipMalloc(reinterpret_cast<void **>(&pl->d_args), sizeof(KArgs)) != hipSuccess ||
         hipMemcpy(pl->d_args, &ka, sizeof(KArgs), hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(MR_ERR_DEVICE, "kernel args"));
@@ -564,8 +696,20 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     if (pl->ka.nsrc == 0) return MR_OK;
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return fail(MR_ERR_DEVICE, "event");
+    // poison the result records: a record the kernels did not write is reported, never returned
+    if (pl->hp.nq && hipMemsetAsync(pl->ka.out_res, 0xFF, size_t(pl->hp.nq) * sizeof(OutResult), s) != hipSuccess)
+        return fail(MR_ERR_DEVICE, "memset results");
     (void)hipEventRecord(e0, s);
-    hipError_t e = launch_solve(pl->d_args, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->blocks, s);
+    hipError_t e;
+    if (pl->hp.hub) {
+        // closed-form hub solve for every source, then the SSSP kernel for the
+        // sources it flagged (usually none; those workgroups exit at once)
+        e = launch_hub(pl->d_args, pl->ka.p.NS, pl->hub_blocks, s);
+        if (e == hipSuccess)
+            e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, s);
+    } else {
+        e = launch_solve(pl->d_args, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->blocks, s);
+    }
     (void)hipEventRecord(e1, s);
     pl->timed.push_back({e0, e1});
     if (e != hipSuccess) return fail(MR_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(e));
@@ -597,6 +741,12 @@ extern "C" int mr_plan_bind_outputs(mr_plan *pl, void *d_results, void *d_comman
     pl->ka.out_cmd = reinterpret_cast<OutCmd *>(d_commands);
     if (hipMemcpy(pl->d_args, &pl->ka, sizeof(KArgs), hipMemcpyHostToDevice) != hipSuccess)
         return fail(MR_ERR_DEVICE, "kernel args");
+    if (pl->d_args_fb) {
+        KArgs kf = pl->ka;
+        kf.fb_mode = 1;
+        if (hipMemcpy(pl->d_args_fb, &kf, sizeof(KArgs), hipMemcpyHostToDevice) != hipSuccess)
+            return fail(MR_ERR_DEVICE, "kernel args");
+    }
     return MR_OK;
 }
 
@@ -643,6 +793,17 @@ static int check_device_errors(mr_plan *pl, uint32_t &flags) {
     uint32_t ctr[4] = {0, 0, 0, 0};
     if (hipMemcpy(ctr, pl->d_counter, 16, hipMemcpyDeviceToHost) != hipSuccess) return fail(MR_ERR_DEVICE, "copy counter");
     flags = ctr[1];
+    if (std::getenv("MR_DEBUG")) {
+        std::fprintf(stderr, "MR_DEBUG hub=%d sources=%u fallback=%u flags=%u hub_blocks=%u\n", int(pl->hp.hub),
+                     pl->ka.nsrc, ctr[2], ctr[1], pl->hub_blocks);
+        if (pl->d_fb && ctr[2] <= pl->ka.nsrc) {
+            std::vector<uint32_t> fb(ctr[2]);
+            (void)hipMemcpy(fb.data(), pl->d_fb, fb.size() * 4, hipMemcpyDeviceToHost);
+            std::fprintf(stderr, "MR_DEBUG fallback sources (vertex):");
+            for (uint32_t s : fb) std::fprintf(stderr, " %u", pl->hp.src_v[s]);
+            std::fprintf(stderr, "\n");
+        }
+    }
     if (flags & (kErrKOverflow | kErrMetricOverflow))
         return fail(MR_ERR_LIMIT, "a label exceeds the engine's 32-bit metric or run-length limits");
     if (flags) return fail(MR_ERR_DEVICE, "internal invariant violated on device (flags " + std::to_string(flags) + ")");
@@ -664,6 +825,10 @@ static int plan_collect(mr_plan *pl, std::vector<OutResult> &res, std::vector<Ou
         if (hipMemcpy(res.data(), pl->ka.out_res, n * sizeof(OutResult), hipMemcpyDeviceToHost) != hipSuccess ||
             hipMemcpy(cmd.data(), pl->ka.out_cmd, size_t(n) * mc * sizeof(OutCmd), hipMemcpyDeviceToHost) != hipSuccess)
             return fail(MR_ERR_DEVICE, "copy outputs");
+        const HostPlan &hp = pl->hp;
+        for (uint32_t k = 0; k < hp.q_id.size(); ++k)
+            if (res[hp.q_id[k]].ncmd_status == 0xFFFFFFFFu)
+                return fail(MR_ERR_DEVICE, "internal: result of query " + std::to_string(hp.q_id[k]) + " not written");
     }
     return MR_OK;
 }
@@ -712,7 +877,23 @@ extern "C" int mr_plan_fetch(mr_plan *pl, mr_result *results, mr_command *pool, 
     return ret;
 }
 
-extern "C" void mr_plan_destroy(mr_plan *pl) { delete pl; }
+extern "C" void mr_plan_destroy(mr_plan *pl) {
+#ifdef MR_STAMPS
+    if (pl && pl->d_dbg) {  // diagnostic summary: phase cycles summed over workgroups (last launch)
+        std::vector<unsigned long long> d(size_t(pl->blocks) * 10);
+        if (hipMemcpy(d.data(), pl->d_dbg, d.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+            unsigned long long acc[9] = {0};
+            for (uint32_t b = 0; b < pl->blocks; ++b)
+                for (int i = 0; i < 9; ++i) acc[i] += d[size_t(b) * 10 + i];
+            std::fprintf(stderr,
+                         "MR_STAMPS blocks=%u sources=%llu cycles: init=%llu fire=%llu specials=%llu next=%llu "
+                         "bar1=%llu claim=%llu bar2=%llu frontier_vertices=%llu\n",
+                         pl->blocks, acc[8], acc[0], acc[1], acc[2], acc[3], acc[4], acc[5], acc[6], acc[7]);
+        }
+    }
+#endif
+    delete pl;
+}
 
 extern "C" int mr_find_path_batch(const mr_grid *g, const mr_params *prm, const mr_query *qs, uint32_t n,
                                   mr_result *results, mr_command *pool, uint64_t pool_cap) {

@@ -58,6 +58,35 @@ struct Shared {
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
+// Diagnostic phase stamps (build with -DMR_STAMPS; never in the product build):
+// thread 0 of each workgroup accumulates shader cycles per phase.
+#ifdef MR_STAMPS
+struct Stamps {
+    unsigned long long last, acc[8];
+    __device__ void start() {
+        last = __builtin_amdgcn_s_memtime();
+        for (int i = 0; i < 8; ++i) acc[i] = 0;
+    }
+    __device__ void mark(int slot) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        acc[slot] += t - last;
+        last = t;
+    }
+};
+#define MR_STAMP(st, slot) \
+    do {                   \
+        if (threadIdx.x == 0) (st).mark(slot); \
+    } while (0)
+#else
+struct Stamps {
+    __device__ void start() {}
+    __device__ void mark(int) {}
+};
+#define MR_STAMP(st, slot) \
+    do {                   \
+    } while (0)
+#endif
+
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -280,14 +309,12 @@ struct Core {
         r.tail[1] = c.t1;
         r.state = 1;
     }
-    // extend the settled label of special s by a non-Standard edge to t
-    // (TotalCost += edge, src/cost.rs:208-315)
-    __device__ __forceinline__ void ext_special(uint32_t s, uint32_t kind, uint32_t payload, uint32_t dm_money,
-                                                uint32_t dm_time, uint32_t t, View &c) const {
-        const Rec &r = R[s];
-        const Cmd last = r.ntail == 2 ? r.tail[1] : r.tail[0];
+    // extend the settled label r of special s (vertex vs) by a non-Standard edge
+    // to the vertex vt (TotalCost += edge, src/cost.rs:208-315)
+    __device__ __forceinline__ void ext_view(const View &r, uint32_t s, uint32_t vs, uint32_t kind, uint32_t payload,
+                                             uint32_t dm_money, uint32_t dm_time, uint32_t vt, View &c) const {
+        const Cmd last = r.ntail == 2 ? r.t1 : r.t0;
         const uint32_t lk = last.kp >> 29;
-        const uint32_t vt = sp[t].v;
         c.t1 = Cmd{0, 0, 0};
         if (lk == kNoMove) {  // the start label: NoMove is replaced, its from kept
             c.m0 = 0;
@@ -298,22 +325,28 @@ struct Core {
             c.ntail = 1;
             c.t0 = Cmd{(kind << 29) | payload, last.from, vt};
         } else if (kind == kCentral && lk == kCentral) {  // CentralMoves merge (ntail is 1)
-            c.m0 = r.m[0];
-            c.m1 = r.m[1];
-            c.m2 = add32(r.m[2], dm_time);
+            c.m0 = r.m0;
+            c.m1 = r.m1;
+            c.m2 = add32(r.m2, dm_time);
             c.len = r.len;
             c.parent = r.parent;
             c.ntail = 1;
             c.t0 = Cmd{last.kp + 1u, last.from, vt};
         } else {
-            c.m0 = r.m[0];
-            c.m1 = add32(r.m[1], dm_money);
-            c.m2 = add32(r.m[2], dm_time);
+            c.m0 = r.m0;
+            c.m1 = add32(r.m1, dm_money);
+            c.m2 = add32(r.m2, dm_time);
             c.len = r.len + 1u;
             c.parent = s;
             c.ntail = 1;
-            c.t0 = Cmd{(kind << 29) | payload, sp[s].v, vt};
+            c.t0 = Cmd{(kind << 29) | payload, vs, vt};
         }
+    }
+    __device__ __forceinline__ void ext_special(uint32_t s, uint32_t kind, uint32_t payload, uint32_t dm_money,
+                                                uint32_t dm_time, uint32_t t, View &c) const {
+        View r;
+        view_rec(s, r);
+        ext_view(r, s, sp[s].v, kind, payload, dm_money, dm_time, sp[t].v, c);
     }
     // the SoE candidate for campfire t from plain vertex u with walk label (b,k)
     __device__ __forceinline__ void soe_from_plain(uint32_t b, uint32_t k, uint32_t u, uint32_t t, View &c) const {
@@ -439,6 +472,135 @@ struct Core {
         }
         return mine;
     }
+    // ---- register-resident exact Dijkstra over the specials of bucket K -------------
+    // (wave 0, NS <= 63): lane t holds the tentative label of special t; the LDS
+    // table R[] stays an exact mirror (every improvement is written back) because
+    // other phases and the list comparator read it.  Per iteration: a 64-lane
+    // lexicographic min over (c1, c2 c3) picks the settle candidate (full
+    // comparator only on exact metric ties), then every lane relaxes the edges
+    // from the settled special into itself — no shared-write races.
+    __device__ __forceinline__ static unsigned long long wave_min_u64(unsigned long long x) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const unsigned long long o = __shfl_xor(x, off, 64);
+            x = o < x ? o : x;
+        }
+        return x;
+    }
+    __device__ __forceinline__ void improve_own(uint32_t t, uint32_t &st, View &my, const View &c) const {
+        if (st == 2) return;
+        if (st == 1) {
+            int cm = cmp_metrics(c.m0, c.m1, c.m2, my.m0, my.m1, my.m2);
+            if (cm > 0) return;
+            if (cm == 0) {
+                if (c.len > my.len) return;
+                if (c.len == my.len && cmp_list(c, kOwn, my, t) >= 0) return;
+            }
+        }
+        my = c;
+        st = 1;
+        Rec &r = R[t];
+        r.m[0] = c.m0;
+        r.m[1] = c.m1;
+        r.m[2] = c.m2;
+        r.len = uint16_t(c.len);
+        r.ntail = uint8_t(c.ntail);
+        r.parent = uint16_t(c.parent);
+        r.tail[0] = c.t0;
+        r.tail[1] = c.t1;
+        r.state = 1;
+    }
+    template <class OnSettle>
+    __device__ __forceinline__ void specials_reg(unsigned long long K, uint32_t par_bits, OnSettle on_settle) const {
+        const DevParams &p = a->p;
+        const uint32_t t = lane_id();
+        const bool mine = t >= 1 && t <= p.NS;
+        const uint32_t q0 = p.perm[0], q1 = p.perm[1], q2 = p.perm[2];
+        View my;
+        uint32_t st = 0;
+        SpecialStatic ss{};
+        if (mine) {
+            st = R[t].state;
+            view_rec(t, my);
+            ss = sp[t];
+        } else {
+            my.m0 = my.m1 = my.m2 = 0;
+        }
+        for (uint32_t it = 0; it <= p.NS; ++it) {
+            const bool tent = mine && st == 1;
+            const unsigned long long key = tent ? key_of(my.m0, my.m1, my.m2) : kInf64;
+            if (tent && key < K) flag(kErrBucket);
+            const bool cand = tent && key == K;
+            const uint32_t a1 = q0 == 0 ? my.m0 : (q0 == 1 ? my.m1 : my.m2);
+            const uint32_t a2 = q1 == 0 ? my.m0 : (q1 == 1 ? my.m1 : my.m2);
+            const uint32_t a3 = q2 == 0 ? my.m0 : (q2 == 1 ? my.m1 : my.m2);
+            const unsigned long long k1 = cand ? (unsigned long long)a1 : kInf64;
+            const unsigned long long min1 = wave_min_u64(k1);
+            if (min1 == kInf64) break;
+            const bool c1 = cand && k1 == min1;
+            const unsigned long long k23 = c1 ? ((unsigned long long)a2 << 32 | a3) : kInf64;
+            const unsigned long long min23 = wave_min_u64(k23);
+            const bool top = c1 && k23 == min23;
+            const unsigned long long bal = __ballot(top);
+            uint32_t s;
+            if (__popcll(bal) == 1) {
+                s = uint32_t(__ffsll((long long)bal) - 1);
+            } else {  // exact metric tie: length, then the command lists
+                uint32_t m = top ? t : kNone32;
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    const uint32_t o = __shfl_xor(m, off, 64);
+                    if (o != kNone32 && (m == kNone32 || cmp_entries(o, m) < 0)) m = o;
+                }
+                s = m;
+            }
+            // settle s
+            View ls;
+            view_rec(s, ls);
+            const Cmd last = ls.ntail == 2 ? ls.t1 : ls.t0;
+            const uint32_t lk = last.kp >> 29;
+            uint32_t seed;
+            bool boundary;
+            if (lk == kNoMove) {  // the source itself
+                seed = 0;
+                boundary = false;
+            } else if (lk == kStandard) {  // continues the walk of its parent boundary
+                seed = (ls.parent << kStBShift) | (last.kp & kStKMask);
+                boundary = false;
+            } else {  // a boundary: walks restart here
+                seed = s << kStBShift;
+                boundary = true;
+            }
+            const SpecialStatic sS = sp[s];
+            if (t == s) st = 2;
+            wave_sync();
+            if (t == 0) {
+                R[s].state = 2;
+                st_state(sS.v, kStSettled | par_bits | seed);
+            }
+            on_settle(s, sS.v, boundary);
+            // relax the CentralMove / caravan / SoE edges s -> t into lane t
+            if (mine && st != 2) {
+                View c;
+                if (((sS.flags & kSpCenter) && (ss.flags & kSpBorder1)) ||
+                    ((sS.flags & kSpBorder1) && (ss.flags & kSpCenter))) {
+                    ext_view(ls, s, sS.v, kCentral, 1, 0, 10, ss.v, c);
+                    improve_own(t, st, my, c);
+                }
+                if (p.use_caravans && (sS.flags & kSpHub) && (ss.flags & kSpHub)) {
+                    const uint32_t d = uint32_t(abs(sS.x - ss.x) + abs(sS.y - ss.y));
+                    const uint32_t coef = ss.coef5 ? 5u : 2u;
+                    ext_view(ls, s, sS.v, kCaravan, (d << 1) | ss.coef5, coef * d, p.rgt * d, ss.v, c);
+                    improve_own(t, st, my, c);
+                }
+                if (p.use_soe && sS.region == t) {
+                    ext_view(ls, s, sS.v, kSoE, 0, p.soe_cost, 0, ss.v, c);
+                    improve_own(t, st, my, c);
+                }
+            }
+            wave_sync();
+        }
+    }
     __device__ __forceinline__ unsigned long long min_special_key() const {
         const DevParams &p = a->p;
         unsigned long long smin = kInf64;
@@ -502,18 +664,10 @@ struct Core {
             try_improve(1, c);
         }
     }
-    __device__ __forceinline__ void write_output(uint32_t w, uint32_t qid) const {
+    // materialise label x as query qid's result record and command slots
+    __device__ __forceinline__ void emit(const View &x, uint32_t qid) const {
         const DevParams &p = a->p;
         OutResult &o = a->out_res[qid];
-        const uint32_t sw = ld_state(w);
-        if (!(sw & kStSettled)) {
-            o = OutResult{0, 0, 0, uint32_t(16 + 1) << 16};  // MR_NOT_FOUND
-            return;
-        }
-        View x;
-        const uint32_t t = special_of(w);
-        if (t != kNone10) view_rec(t, x);
-        else view_walk((sw >> kStBShift) & kNone10, sw & kStKMask, w, x);
         if (x.len > p.max_cmds) {  // MR_ERR_CAPACITY: the host re-runs with more slots
             o = OutResult{x.m0, x.m1, x.m2, (uint32_t(16 - 4) << 16) | (x.len & 0xFFFFu)};
             return;
@@ -537,6 +691,18 @@ struct Core {
         }
         if (pos != -1 || pp != 0) flag(kErrChain);
         o = OutResult{x.m0, x.m1, x.m2, (uint32_t(16) << 16) | (x.len & 0xFFFFu)};
+    }
+    __device__ __forceinline__ void write_output(uint32_t w, uint32_t qid) const {
+        const uint32_t sw = ld_state(w);
+        if (!(sw & kStSettled)) {
+            a->out_res[qid] = OutResult{0, 0, 0, uint32_t(16 + 1) << 16};  // MR_NOT_FOUND
+            return;
+        }
+        View x;
+        const uint32_t t = special_of(w);
+        if (t != kNone10) view_rec(t, x);
+        else view_walk((sw >> kStBShift) & kNone10, sw & kStKMask, w, x);
+        emit(x, qid);
     }
     __device__ __forceinline__ void write_outputs(uint32_t s_idx) const {
         const uint32_t q0 = a->q_begin[s_idx], q1 = a->q_begin[s_idx + 1];
@@ -579,6 +745,8 @@ struct LegsSolver : Core<G> {
     uint32_t *bnd;                 // boundary list (table indices), bnd[0] = 0 (the source)
     unsigned long long *best64;    // per region: (prio << 32 | rank) of the level's best vertex
     uint32_t *fired;
+
+    Stamps *stamps;                // diagnostic builds only
 
     __device__ __forceinline__ IdxT *frontier(uint32_t i) const { return i ? F1 : F0; }
 
@@ -725,23 +893,34 @@ struct LegsSolver : Core<G> {
             this->seed_scrolls();
         }
         __syncthreads();
+        MR_STAMP(*stamps, 0);  // init
         for (uint32_t guard = 0;; ++guard) {
             // ---- specials of level L (wave 0) ----
             if (tid < 64) {
                 const uint32_t L = sh->L;
                 const uint32_t cur = sh->lb;
                 if (p.use_soe) fire_regions();
-                for (uint32_t it = 0; it <= p.NS; ++it) {
-                    const uint32_t s = this->argmin_special(L);
-                    if (s == kNone32) break;
-                    const bool boundary = this->settle_special(s, (L & 1u) ? kStPar : 0u);
+                MR_STAMP(*stamps, 1);  // fire regions
+                const uint32_t par = (L & 1u) ? kStPar : 0u;
+                auto on_settle = [&](uint32_t s, uint32_t vs, bool boundary) {
                     if (lane_id() == 0) {
                         const uint32_t i = sh->cnt[cur]++;
-                        this->st_idx(frontier(cur), i, this->sp[s].v);
+                        this->st_idx(frontier(cur), i, vs);
                         if (boundary) bnd[sh->nbnd++] = s;
                     }
                     wave_sync();
+                };
+                if (p.NS <= 63) {
+                    this->specials_reg(L, par, on_settle);
+                } else {
+                    for (uint32_t it = 0; it <= p.NS; ++it) {
+                        const uint32_t s = this->argmin_special(L);
+                        if (s == kNone32) break;
+                        const bool boundary = this->settle_special(s, par);
+                        on_settle(s, this->sp[s].v, boundary);
+                    }
                 }
+                MR_STAMP(*stamps, 2);  // specials Dijkstra
                 const uint32_t done = this->dsts_done();
                 const uint32_t n = sh->cnt[cur];
                 if (n == 0) {  // empty frontier: jump to the next special level
@@ -764,8 +943,10 @@ struct LegsSolver : Core<G> {
                         sh->cnt[cur ^ 1u] = 0;
                     }
                 }
+                MR_STAMP(*stamps, 3);  // next level / ranking
             }
             __syncthreads();
+            MR_STAMP(*stamps, 4);  // barrier after specials
             if (sh->done) break;
             if (guard > p.V + p.NS + 64u) {
                 this->flag(kErrBucket);
@@ -778,13 +959,18 @@ struct LegsSolver : Core<G> {
                 const IdxT *Fc = frontier(cur);
                 IdxT *Fn = frontier(cur ^ 1u);
                 for (uint32_t i = tid; i < n; i += kBS) claim_from(this->ld_idx(Fc, i), L, Fn, cur ^ 1u);
+#ifdef MR_STAMPS
+                if (tid == 0) stamps->acc[7] += n;  // frontier vertices processed
+#endif
             }
+            MR_STAMP(*stamps, 5);  // own claims
             __syncthreads();
             if (tid == 0) {
                 sh->lb ^= 1u;
                 sh->L += 1;
             }
             __syncthreads();
+            MR_STAMP(*stamps, 6);  // claim barriers
         }
         this->write_outputs(s_idx);
         __syncthreads();
@@ -980,13 +1166,19 @@ struct GenericSolver : Core<G> {
             if (tid < 64) {
                 if (p.use_soe) fire_regions();
                 const unsigned long long B = sh->B;
-                for (uint32_t it = 0; it <= p.NS; ++it) {
-                    const uint32_t s = this->argmin_special(B);
-                    if (s == kNone32) break;
-                    this->settle_special(s, 0u);
-                    const uint32_t vs = this->sp[s].v;
+                auto on_settle = [&](uint32_t, uint32_t vs, bool) {
                     if (lane_id() < 4) mark_dirty(vs, this->nbr(vs, int(lane_id())));
                     wave_sync();
+                };
+                if (p.NS <= 63) {
+                    this->specials_reg(B, 0u, on_settle);
+                } else {
+                    for (uint32_t it = 0; it <= p.NS; ++it) {
+                        const uint32_t s = this->argmin_special(B);
+                        if (s == kNone32) break;
+                        this->settle_special(s, 0u);
+                        on_settle(s, this->sp[s].v, false);
+                    }
                 }
             }
             __syncthreads();
@@ -1007,6 +1199,259 @@ struct GenericSolver : Core<G> {
         __syncthreads();
     }
 };
+
+// ===================================================================================
+// Hub solver (linear StandardMove run time: Fleetfoot level 0 or out of range)
+// ===================================================================================
+// With a linear run time, extending two walk labels by the same StandardMove
+// preserves their order (metrics shift equally, lengths and prefixes are
+// unchanged), so every plain vertex's label is min over boundaries b of
+// walk(b, d_b(v)), d_b = grid distance avoiding the Center (Manhattan, +2 when
+// the straight line crosses it).  One wave per source runs an exact Dijkstra
+// over the specials (lane t owns special t) whose edges are those walks, the
+// CentralMove/caravan/SoE edges, and SoE edges from each region's nearest cell
+// (precomputed table).  The only step that is not order-preserving — extending
+// a boundary special whose label ties a walk candidate on all three metrics
+// (the tie is then decided by length/commands, which a StandardMove can flip) —
+// is detected and such sources are re-solved by the SSSP kernel.  DESIGN.md §3b.
+__device__ __forceinline__ uint32_t walk_dist(int ax, int ay, int bx, int by) {
+    uint32_t d = uint32_t(abs(ax - bx) + abs(ay - by));
+    if ((ay == 0 && by == 0 && ax != 0 && bx != 0 && ((ax < 0) != (bx < 0))) ||
+        (ax == 0 && bx == 0 && ay != 0 && by != 0 && ((ay < 0) != (by < 0))))
+        d += 2;  // both on one axis, on opposite sides of the Center: detour
+    return d;
+}
+
+struct HubSolver : Core<false> {
+    uint32_t *bnd;  // this wave's boundary list (table indices; bnd[0] = 0, the source)
+
+    __device__ __forceinline__ void note_walk(const View &c, uint32_t &bwh, uint32_t &b0, uint32_t &b1,
+                                              uint32_t &b2) const {
+        if (!bwh || cmp_metrics(c.m0, c.m1, c.m2, b0, b1, b2) < 0) {
+            bwh = 1;
+            b0 = c.m0;
+            b1 = c.m1;
+            b2 = c.m2;
+        }
+    }
+    // walks and SoE-region edges from boundary b (at bx, by) into lane t's special
+    __device__ __forceinline__ void relax_boundary(uint32_t b, int bx, int by, uint32_t t, bool mine, uint32_t &st,
+                                                   View &my, const SpecialStatic &ss, uint32_t &bwh, uint32_t &b0,
+                                                   uint32_t &b1, uint32_t &b2) const {
+        const DevParams &p = a->p;
+        if (!mine || st == 2) return;
+        const uint32_t vb = vert_of(b);
+        if (ss.v != p.vc && ss.v != vb) {
+            View c;
+            view_walk(b, walk_dist(bx, by, ss.x, ss.y), ss.v, c);
+            note_walk(c, bwh, b0, b1, b2);
+            improve_own(t, st, my, c);
+        }
+        if (p.use_soe && ss.rid != kNone10) {
+            const uint32_t *e = a->near + 2ull * (unsigned long long)(vb * a->nreg + ss.rid);
+            const uint32_t d = e[0], u = e[1];
+            if (d != kNone32 && (d != 0 || b == 0)) {  // d == 0, b special: its own SoE edge
+                View c;
+                soe_from_plain(b, d, u, t, c);
+                improve_own(t, st, my, c);
+            }
+        }
+    }
+
+    __device__ __forceinline__ void solve(uint32_t s_idx) {
+        const DevParams &p = a->p;
+        const uint32_t t = lane_id();
+        const bool mine = t >= 1 && t <= p.NS;
+        src = a->src_v[s_idx];
+        const int sx = int(src % p.S) - int(p.H), sy = int(src / p.S) - int(p.H);
+        const uint32_t ts = a->sinfo[src] & kNone10;
+        const uint32_t q0 = p.perm[0], q1 = p.perm[1], q2 = p.perm[2];
+        SpecialStatic ss{};
+        if (mine) ss = sp[t];
+        View my, st0;
+        view_start(st0);
+        my = st0;
+        uint32_t st = 0, bwh = 0, b0 = 0, b1 = 0, b2 = 0, tie = 0;
+        if (t == 0) {
+            Rec &r0 = R[0];
+            r0.m[0] = r0.m[1] = r0.m[2] = 0;
+            r0.len = 1;
+            r0.ntail = 1;
+            r0.parent = 0;
+            r0.tail[0] = st0.t0;
+            r0.state = 2;
+            bnd[0] = 0;
+        }
+        if (mine) R[t].state = 0;
+        wave_sync();
+        if (mine) {
+            if (t == ts) improve_own(t, st, my, st0);
+            if (t == p.hq_t) {  // SHQ / SFm: only the source's own edges can be minimal
+                View c = st0;
+                c.m1 = p.shq_cost;
+                c.t0 = Cmd{kSHQ << 29, src, ss.v};
+                improve_own(t, st, my, c);
+            }
+            if (p.use_sfm && t == 1) {
+                View c = st0;
+                c.m1 = p.sfm_cost;
+                c.t0 = Cmd{kSFm << 29, src, p.vc};
+                improve_own(t, st, my, c);
+            }
+        }
+        uint32_t nb = 1;
+        if (src != p.vc) relax_boundary(0, sx, sy, t, mine, st, my, ss, bwh, b0, b1, b2);
+        wave_sync();
+        for (uint32_t it = 0; it <= p.NS; ++it) {
+            const bool tent = mine && st == 1;
+            const uint32_t a1 = q0 == 0 ? my.m0 : (q0 == 1 ? my.m1 : my.m2);
+            const uint32_t a2 = q1 == 0 ? my.m0 : (q1 == 1 ? my.m1 : my.m2);
+            const uint32_t a3 = q2 == 0 ? my.m0 : (q2 == 1 ? my.m1 : my.m2);
+            const unsigned long long k1 = tent ? (unsigned long long)a1 : kInf64;
+            const unsigned long long min1 = wave_min_u64(k1);
+            if (min1 == kInf64) break;
+            const bool c1 = tent && k1 == min1;
+            const unsigned long long k23 = c1 ? ((unsigned long long)a2 << 32 | a3) : kInf64;
+            const unsigned long long min23 = wave_min_u64(k23);
+            const bool top = c1 && k23 == min23;
+            const unsigned long long bal = __ballot(top);
+            uint32_t s;
+            if (__popcll(bal) == 1) {
+                s = uint32_t(__ffsll((long long)bal) - 1);
+            } else {
+                uint32_t m = top ? t : kNone32;
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    const uint32_t o = __shfl_xor(m, off, 64);
+                    if (o != kNone32 && (m == kNone32 || cmp_entries(o, m) < 0)) m = o;
+                }
+                s = m;
+            }
+            View ls;
+            view_rec(s, ls);
+            const SpecialStatic sS = sp[s];
+            const Cmd last = ls.ntail == 2 ? ls.t1 : ls.t0;
+            const uint32_t lk = last.kp >> 29;
+            const bool boundary = lk != kNoMove && lk != kStandard;
+            if (t == s) {
+                st = 2;
+                if (boundary && bwh && b0 == my.m0 && b1 == my.m1 && b2 == my.m2) tie = 1;
+            }
+            wave_sync();
+            if (t == 0) R[s].state = 2;
+            wave_sync();
+            if (mine && st != 2) {  // CentralMove / caravan / SoE edges s -> t
+                View c;
+                if (((sS.flags & kSpCenter) && (ss.flags & kSpBorder1)) ||
+                    ((sS.flags & kSpBorder1) && (ss.flags & kSpCenter))) {
+                    ext_view(ls, s, sS.v, kCentral, 1, 0, 10, ss.v, c);
+                    improve_own(t, st, my, c);
+                }
+                if (p.use_caravans && (sS.flags & kSpHub) && (ss.flags & kSpHub)) {
+                    const uint32_t d = uint32_t(abs(sS.x - ss.x) + abs(sS.y - ss.y));
+                    const uint32_t coef = ss.coef5 ? 5u : 2u;
+                    ext_view(ls, s, sS.v, kCaravan, (d << 1) | ss.coef5, coef * d, p.rgt * d, ss.v, c);
+                    improve_own(t, st, my, c);
+                }
+                if (p.use_soe && sS.region == t) {
+                    ext_view(ls, s, sS.v, kSoE, 0, p.soe_cost, 0, ss.v, c);
+                    improve_own(t, st, my, c);
+                }
+            }
+            if (boundary && sS.v != p.vc) {  // a new walk source
+                relax_boundary(s, sS.x, sS.y, t, mine, st, my, ss, bwh, b0, b1, b2);
+                if (t == 0) bnd[nb] = s;
+                ++nb;
+            }
+            wave_sync();
+        }
+        // An order-sensitive tie hands this source to the SSSP kernel.  No early
+        // return: the wave must stay converged for the next dequeue's broadcast.
+        const bool fallback = __any(tie != 0) || a->fb_all;
+        if (fallback && t == 0) a->fb_list[atomicAdd(a->counter + 2, 1u)] = s_idx;
+        const uint32_t qa = a->q_begin[s_idx], qb = fallback ? qa : a->q_begin[s_idx + 1];
+        for (uint32_t i = qa + t; i < qb; i += 64) {
+            const uint32_t w = a->q_dst[i];
+            View x;
+            if (w == src) {
+                x = st0;
+            } else {
+                const uint32_t tw = a->sinfo[w] & kNone10;
+                if (tw != kNone10) {
+                    view_rec(tw, x);
+                } else {
+                    const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
+                    bool have = false;
+                    for (uint32_t j = 0; j < nb; ++j) {
+                        const uint32_t b = bnd[j];
+                        if (vert_of(b) == p.vc) continue;
+                        const int bx = b == 0 ? sx : sp[b].x, by = b == 0 ? sy : sp[b].y;
+                        View c;
+                        view_walk(b, walk_dist(bx, by, wx, wy), w, c);
+                        if (!have || cmp_view(c, kOwn, x, kOwn) < 0) {
+                            x = c;
+                            have = true;
+                        }
+                    }
+                }
+            }
+            emit(x, a->q_id[i]);
+        }
+        wave_sync();
+    }
+};
+
+__host__ __device__ constexpr uint32_t align16h(uint32_t x) { return (x + 15u) & ~15u; }
+
+struct HubLayout {
+    uint32_t off_sp, off_hubs, off_R, off_bnd, rstride, bstride, total;
+};
+__host__ __device__ inline HubLayout hub_layout(uint32_t NS) {
+    HubLayout L{};
+    const uint32_t T = NS + 1;
+    uint32_t o = 0;
+    L.off_sp = o;
+    o = align16h(o + T * uint32_t(sizeof(SpecialStatic)));
+    L.off_hubs = o;
+    o = align16h(o + T * 2);
+    L.rstride = align16h(T * uint32_t(sizeof(Rec)));
+    L.off_R = o;
+    o += 4 * L.rstride;
+    L.bstride = align16h((T + 1) * 4);
+    L.off_bnd = o;
+    o += 4 * L.bstride;
+    L.total = o;
+    return L;
+}
+
+__global__ __launch_bounds__(kBS) void hub_kernel(const KArgs *__restrict__ a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const uint32_t NS = a->p.NS;
+    const HubLayout L = hub_layout(NS);
+    SpecialStatic *spl = reinterpret_cast<SpecialStatic *>(smem + L.off_sp);
+    uint16_t *hubl = reinterpret_cast<uint16_t *>(smem + L.off_hubs);
+    for (uint32_t t = threadIdx.x; t <= NS; t += kBS) spl[t] = a->sp[t];
+    for (uint32_t h = threadIdx.x; h < a->p.n_hubs; h += kBS) hubl[h] = a->hubs[h];
+    __syncthreads();
+    const uint32_t wv = threadIdx.x >> 6;
+    HubSolver H;
+    H.a = a;
+    H.sh = nullptr;
+    H.R = reinterpret_cast<Rec *>(smem + L.off_R + wv * L.rstride);
+    H.state = nullptr;
+    H.sp = spl;
+    H.hubs = hubl;
+    H.dst = nullptr;
+    H.src = 0;
+    H.bnd = reinterpret_cast<uint32_t *>(smem + L.off_bnd + wv * L.bstride);
+    for (;;) {  // each wave dequeues its own sources
+        uint32_t s = 0;
+        if (lane_id() == 0) s = atomicAdd(a->counter, 1u);
+        s = __shfl(s, 0, 64);
+        if (s >= a->nsrc) break;
+        H.solve(s);
+    }
+}
 
 // ===================================================================================
 // LDS layout and kernels
@@ -1051,6 +1496,18 @@ __host__ __device__ inline LdsLayout lds_layout(uint32_t NS, uint32_t V, bool gr
     }
     L.total = o;
     return L;
+}
+
+// next source index for a workgroup: every source in order, or (fallback launch
+// after the hub solver) the sources it listed
+__device__ __forceinline__ uint32_t next_source(const KArgs *__restrict__ a) {
+    if (a->fb_mode) {
+        const uint32_t n = __hip_atomic_load(a->counter + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t i = atomicAdd(a->counter + 3, 1u);
+        return i < n ? a->fb_list[i] : kNone32;
+    }
+    const uint32_t i = atomicAdd(a->counter, 1u);
+    return i < a->nsrc ? i : kNone32;
 }
 
 template <bool G, class IdxT, uint32_t ALGO>
@@ -1100,14 +1557,27 @@ __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a)
         S.fired = reinterpret_cast<uint32_t *>(smem + L.off_d);
         (void)l2;
         (void)l3;
+        Stamps stamps;
+        stamps.start();
+        S.stamps = &stamps;
+        uint32_t nsolved = 0;
         for (;;) {
-            if (threadIdx.x == 0) sh->sidx = atomicAdd(a->counter, 1u);
+            if (threadIdx.x == 0) sh->sidx = next_source(a);
             __syncthreads();
             const uint32_t s = sh->sidx;
             __syncthreads();
-            if (s >= a->nsrc) break;
+            if (s == kNone32) break;
             S.solve(s);
+            ++nsolved;
         }
+#ifdef MR_STAMPS
+        if (threadIdx.x == 0 && a->dbg) {
+            for (int i = 0; i < 8; ++i) a->dbg[blockIdx.x * 10 + i] = stamps.acc[i];
+            a->dbg[blockIdx.x * 10 + 8] = nsolved;
+        }
+#else
+        (void)nsolved;
+#endif
     } else {
         GenericSolver<G, IdxT> S;
         S.a = a;
@@ -1124,11 +1594,11 @@ __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a)
         S.best = reinterpret_cast<uint32_t *>(smem + L.off_b);
         S.fired = reinterpret_cast<uint32_t *>(smem + L.off_d);
         for (;;) {
-            if (threadIdx.x == 0) sh->sidx = atomicAdd(a->counter, 1u);
+            if (threadIdx.x == 0) sh->sidx = next_source(a);
             __syncthreads();
             const uint32_t s = sh->sidx;
             __syncthreads();
-            if (s >= a->nsrc) break;
+            if (s == kNone32) break;
             S.solve(s);
         }
     }
@@ -1156,6 +1626,22 @@ hipError_t launch_solve(const KArgs *d_args, bool grid_in_lds, uint32_t algo, ui
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
     void *args[] = {const_cast<KArgs **>(&d_args)};
     return hipLaunchKernel(fn, dim3(blocks), dim3(kBS), args, bytes, stream);
+}
+
+uint32_t hub_lds_bytes(uint32_t NS) { return hub_layout(NS).total; }
+
+hipError_t launch_hub(const KArgs *d_args, uint32_t NS, uint32_t blocks, hipStream_t stream) {
+    const uint32_t bytes = hub_lds_bytes(NS);
+    const void *fn = reinterpret_cast<const void *>(&hub_kernel);
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
+    void *args[] = {const_cast<KArgs **>(&d_args)};
+    return hipLaunchKernel(fn, dim3(blocks), dim3(kBS), args, bytes, stream);
+}
+
+int hub_blocks_per_cu(uint32_t bytes) {
+    int n = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, hub_kernel, kBS, bytes);
+    return n;
 }
 
 int max_blocks_per_cu(bool grid_in_lds, uint32_t algo, uint32_t bytes) {

@@ -20,7 +20,8 @@ from .abi import (MR_ERR_CAPACITY, MR_NOT_FOUND, MR_OK, CellIndex, Params, Total
                   mr_cell, mr_cell_index, mr_command, mr_params, mr_query, mr_result, queries_to_c,
                   result_from_c)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmarshrutka_pf.so")
+LIB_PATH = os.environ.get("MR_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                                                          "libmarshrutka_pf.so")
 
 EXPORTED_SYMBOLS = [
     "mr_grid_create", "mr_grid_destroy", "mr_grid_square_size", "mr_params_default", "mr_find_path",

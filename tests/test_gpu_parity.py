@@ -23,16 +23,22 @@ def eng():
     return pathfinder
 
 
-@pytest.fixture(params=["lds-auto", "hbm-auto", "lds-generic", "hbm-generic"])
+@pytest.fixture(params=["auto-lds", "auto-hbm", "fallback-lds", "fallback-hbm", "sssp-lds", "sssp-hbm",
+                        "generic-lds", "generic-hbm"])
 def grid_state(request, monkeypatch):
-    """Both grid-state regimes x both solvers (Legs-first parameters use the
-    level-synchronous solver unless MR_ALGO=generic forces the bucketed one)."""
-    state, algo = request.param.split("-")
+    """Every solver path x both grid-state regimes:
+    auto     — hub solver when the run time is linear, else the SSSP solvers
+    fallback — hub solver handing every source to the SSSP kernel
+    sssp     — no hub solver (level-synchronous solver for Legs-first orders)
+    generic  — the bucketed solver for every order."""
+    algo, state = request.param.split("-")
     monkeypatch.setenv("MR_GRID_STATE", state)
-    if algo == "generic":
-        monkeypatch.setenv("MR_ALGO", "generic")
-    else:
-        monkeypatch.delenv("MR_ALGO", raising=False)
+    monkeypatch.delenv("MR_ALGO", raising=False)
+    monkeypatch.delenv("MR_HUB_FALLBACK_ALL", raising=False)
+    if algo in ("sssp", "generic"):
+        monkeypatch.setenv("MR_ALGO", algo)
+    if algo == "fallback":
+        monkeypatch.setenv("MR_HUB_FALLBACK_ALL", "1")
     return request.param
 
 
