@@ -83,6 +83,32 @@ def cpu_baseline_leg(m, params, queries, gpu_results, budget_s):
             {"checked": n, "mismatches": mism})
 
 
+def algorithmic_bytes(plan, stats, V):
+    """Bytes one launch must move.
+
+    SSSP kernel: V x 20 B per unique source (4 B per-cell record
+    read + 16 B final label write).  Hub solver: it never touches the grid, so
+    its bytes are what it reads and writes per query (destination + query id
+    8 B, destination static word 4 B, result record 16 B, 16 B per command
+    slot written), per source (source vertex + range 8 B, its region row
+    8 B x regions), plus the SSSP figure for every source it hands to the
+    fallback.  Returns (bytes, kernel name, SURVEY-8d-equivalent bytes)."""
+    n_src = stats["num_sources"]
+    survey = float(n_src) * V * BYTES_PER_VERTEX_SOLVE
+    if stats["solver"] != "hub":
+        return survey, "sssp_kernel", survey
+    import numpy as np
+    res, _ = plan.fetch_raw()
+    words = np.frombuffer(res, dtype=np.uint32).reshape(-1, 8)[: plan.n]
+    ok = words[:, 6].view(np.int32) == 0
+    n_cmds = int(words[ok, 4].astype(np.int64).sum())
+    nq = plan.n
+    b = nq * (8 + 4 + 16) + 16 * n_cmds + n_src * (8 + 8 * stats["num_regions"])
+    b += stats["fallback_sources"] * V * BYTES_PER_VERTEX_SOLVE
+    name = "hub_kernel" + (" + sssp_kernel (fallback)" if stats["fallback_sources"] else "")
+    return float(b), name, survey
+
+
 def as_expected(label):
     if label is None:
         return None
@@ -182,9 +208,17 @@ def main():
     total_queries = sum(counts) * args.steps
     value = total_queries / elapsed
     V = wl["size"] ** 2
-    # roofline: SURVEY §8d algorithmic bytes = (unique sources) x V x 20 B per launch,
-    # over the solve kernel's average launch time (HIP events on its stream)
-    alg_bytes = n_src * V * BYTES_PER_VERTEX_SOLVE
+    stats = plan.stats()
+    alg_bytes, kernel_name, survey_bytes = algorithmic_bytes(plan, stats, V)
+    if world > 1:
+        t = torch.tensor([alg_bytes, survey_bytes, stats["fallback_sources"]], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t)
+        alg_bytes, survey_bytes, fb_total = float(t[0]), float(t[1]), int(t[2])
+    else:
+        fb_total = stats["fallback_sources"]
+    # roofline: algorithmic bytes per launch (see algorithmic_bytes) over the solve's
+    # average launch time (HIP events on its stream); with N ranks, the aggregate
+    # bytes over the slowest rank's launch time
     achieved = alg_bytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     traffic = None
     pmc_path = args.pmc or os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
@@ -204,12 +238,20 @@ def main():
         "config": {"workload": wl["desc"], "grid": f"{wl['size']}x{wl['size']}", "queries_per_gpu": qpg,
                    "campfires_per_homeland": wl["campfires"], "unique_sources_per_step": tot_src,
                    "params": "FindPath defaults: sort (Legs,Money), SoE 50, caravans, skills 0, homeland Blue",
+                   "solver": stats["solver"], "fallback_sources_per_step": fb_total,
+                   "specials": stats["num_specials"],
                    "parallelism": f"sources sharded over {world} GPU(s), RCCL gather of results to rank 0"
                                   if world > 1 else "1 GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "sssp_kernel", "kernel_ms": kms, "launches": nl,
-                     "alg_bytes_per_launch": alg_bytes},
+                     "kernel": kernel_name, "kernel_ms": kms, "launches": nl,
+                     "alg_bytes_per_launch": alg_bytes,
+                     "survey_8d_bytes_per_launch": survey_bytes,
+                     "note": ("hub solver: latency-bound per-source wave Dijkstra over the specials; bytes = "
+                              "queries in, results and command slots out, per-source region rows, plus V*20 B "
+                              "per SSSP fallback source (DESIGN.md section 4)")
+                     if stats["solver"] == "hub" else
+                     "SSSP kernel: SURVEY 8d bytes, V*20 B per unique source"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         gpu_res = plan.fetch()

@@ -191,6 +191,25 @@ int mr_plan_device_outputs(mr_plan *plan, void **d_results, uint64_t *results_by
 int mr_plan_bind_outputs(mr_plan *plan, void *d_results, void *d_commands);
 /* Number of unique sources (= single-source solves per pass). */
 uint32_t mr_plan_num_sources(const mr_plan *plan);
+
+/* Which solver a plan runs and how the last pass went (diagnostics, bench). */
+enum {
+    MR_SOLVER_BUCKETED = 0, /* SSSP kernel, bucketed settling (any comparator) */
+    MR_SOLVER_LEVELS = 1,   /* SSSP kernel, level-synchronous (Legs-first comparator) */
+    MR_SOLVER_HUB = 2       /* closed-form hub solver (linear run time) + SSSP fallback */
+};
+typedef struct mr_plan_stats {
+    uint32_t solver;            /* MR_SOLVER_* */
+    uint32_t grid_state_in_lds; /* SSSP kernel: 1 grid state in LDS, 0 in HBM slots */
+    uint32_t num_sources;       /* unique sources per pass */
+    uint32_t fallback_sources;  /* hub solver: sources re-solved by the SSSP kernel in the last pass */
+    uint32_t num_specials;      /* Center, border-1 cells, campfires, HQ */
+    uint32_t num_regions;       /* hub solver: Scroll-of-Escape regions of the homeland */
+    uint32_t hub_workgroups;    /* hub launch size (4 waves each) */
+    uint32_t sssp_workgroups;   /* SSSP launch size */
+} mr_plan_stats;
+/* Fills *out; waits for the plan's stream.  MR_OK or MR_ERR_INVALID_ARG. */
+int mr_plan_get_stats(mr_plan *plan, mr_plan_stats *out);
 /* Average device time (ms) of the main solve kernel over the last
  * mr_plan_run calls since the previous call to this function, measured with
  * HIP events on the stream the kernel is launched on. */

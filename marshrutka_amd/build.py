@@ -29,7 +29,8 @@ def build_diag(verbose: bool = False) -> str:
     lib/diag/; load it with MR_LIB_PATH=<path>.  Never used by the product path."""
     out = os.path.join(LIB_DIR, "diag", "libmarshrutka_pf.so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = [HIPCC, *FLAGS, "-DMR_STAMPS", *[os.path.join(CSRC, s) for s in SOURCES], "-o", out]
+    flag = "-DMR_HUBDUMP" if os.environ.get("MR_DIAG") == "hubdump" else "-DMR_STAMPS"
+    cmd = [HIPCC, *FLAGS, flag, *[os.path.join(CSRC, s) for s in SOURCES], "-o", out]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

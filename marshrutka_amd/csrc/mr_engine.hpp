@@ -37,7 +37,7 @@ enum : uint32_t { kNoMove = 0, kCentral = 1, kStandard = 2, kCaravan = 3, kSoE =
 // Caravan money d*coef orders by the coef bit at equal d).
 struct Cmd {
     uint32_t kp;
-    uint32_t from;  // vertex id (row-major)
+    uint32_t from;  // rank of the cell (position in CellIndex order, src/index.rs:41-46)
     uint32_t to;
 };
 
@@ -62,7 +62,7 @@ struct SpecialStatic {
     uint32_t region;  // table index of this cell's nearest campfire (query homeland), kNone10 if none
     uint32_t coef5;   // 1 if a caravan INTO this special costs 5/distance (else 2)
     uint32_t rid;     // hub solver: region id if this is a query-homeland campfire, else kNone10
-    uint32_t pad;
+    uint32_t rk;      // rank of v (position in CellIndex order): commands name cells by rank
 };
 constexpr uint32_t kSpCenter = 1u, kSpBorder1 = 2u, kSpHub = 4u;
 
@@ -116,12 +116,13 @@ struct KArgs {
     uint32_t algo;               // kAlgoLegs (Legs-first level-synchronous) or kAlgoGeneric
     unsigned long long *dbg;     // diagnostic builds (-DMR_STAMPS): per-workgroup phase cycles
     // hub solver (linear run time): per vertex and region, the nearest region cell by
-    // walk distance avoiding the Center: near[2*(v*nreg + r)] = {distance, cell}
+    // walk distance avoiding the Center: near[2*(v*nreg + r)] = {distance, rank of the cell}
     const uint32_t *near;
     uint32_t nreg;
     uint32_t *fb_list;           // sources the hub solver hands to the SSSP kernel (counter[2] of them)
     uint32_t fb_mode;            // 1: this SSSP launch solves fb_list[counter[3]++] only
     uint32_t fb_all;             // tests: the hub solver hands every source to the SSSP kernel
+    uint32_t dbg_blocks;         // diagnostic builds: SSSP workgroups (hub stamps follow their slots)
 };
 enum : uint32_t { kAlgoGeneric = 0, kAlgoLegs = 1 };
 

@@ -23,9 +23,10 @@ uint32_t lds_bytes(uint32_t NS, uint32_t V, bool grid_in_lds, uint32_t algo);
 hipError_t launch_solve(const KArgs *d_args, bool grid_in_lds, uint32_t algo, uint32_t NS, uint32_t V,
                         uint32_t blocks, hipStream_t stream);
 int max_blocks_per_cu(bool grid_in_lds, uint32_t algo, uint32_t bytes);
-uint32_t hub_lds_bytes(uint32_t NS);
-hipError_t launch_hub(const KArgs *d_args, uint32_t NS, uint32_t blocks, hipStream_t stream);
-int hub_blocks_per_cu(uint32_t bytes);
+uint32_t hub_lds_bytes(uint32_t NS, uint32_t nreg);
+hipError_t launch_hub(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t blocks,
+                      hipStream_t stream);
+int hub_blocks_per_cu(const uint32_t perm[3], uint32_t bytes);
 }  // namespace mr
 
 
@@ -107,7 +108,7 @@ struct mr_grid {
     std::vector<uint32_t> nearest[4];      // nearest campfire vertex per homeland (kNone32)
     // hub solver: per homeland, the regions (campfires of the homeland, CellIndex order) and
     // for every vertex and region the nearest cell of that region by walk distance avoiding
-    // the Center, ties by CellIndex order: near[2*(v*nreg+r)] = {distance, cell}
+    // the Center, ties by CellIndex order: near[2*(v*nreg+r)] = {distance, rank of the cell}
     mutable std::mutex near_mu;
     mutable std::vector<uint32_t> regions[4];
     mutable std::vector<uint32_t> near[4];
@@ -329,7 +330,7 @@ static const std::vector<uint32_t> &region_table(const mr_grid *g, int h, const 
         }
         for (uint32_t v = 0; v < V; ++v) {
             tab[(size_t(v) * nreg + r) * 2] = dist[v];
-            tab[(size_t(v) * nreg + r) * 2 + 1] = dist[v] == kNone32 ? kNone32 : org[v];
+            tab[(size_t(v) * nreg + r) * 2 + 1] = dist[v] == kNone32 ? kNone32 : g->rank[org[v]];
         }
     }
     g->regions[h] = std::move(regs);
@@ -436,6 +437,7 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
         uint32_t v = order[t];
         SpecialStatic &s = hp.sp[t];
         s.v = v;
+        s.rk = g->rank[v];
         s.x = g->gx(v);
         s.y = g->gy(v);
         bool is_cf = g->poi[v] == MR_POI_CAMPFIRE;
@@ -661,8 +663,8 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         ka.near = pl->d_near;
         ka.nreg = hp.nreg;
         ka.fb_list = pl->d_fb;
-        const uint32_t hb = hub_lds_bytes(NS);
-        const int hper = std::max(1, hub_blocks_per_cu(hb));
+        const uint32_t hb = hub_lds_bytes(NS, hp.nreg);
+        const int hper = std::max(1, hub_blocks_per_cu(hp.p.perm, hb));
         pl->hub_blocks = uint32_t(std::min<uint64_t>((nsrc + 3) / 4, uint64_t(hper) * prop.multiProcessorCount));
         if (const char *e = std::getenv("MR_HUB_BLOCKS")) pl->hub_blocks = uint32_t(std::max(1, std::atoi(e)));
         pl->fb_blocks = pl->blocks;
@@ -672,10 +674,19 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
             hipMemcpy(pl->d_args_fb, &kf, sizeof(KArgs), hipMemcpyHostToDevice) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "kernel args"));
     }
+#ifdef MR_HUBDUMP
+    if (const char *e = std::getenv("MR_DEBUG_SRC"))
+        if (hipMalloc(reinterpret_cast<void **>(&pl->d_dbg), 64 * 16 * 4) == hipSuccess) {
+            (void)hipMemset(pl->d_dbg, 0, 64 * 16 * 4);
+            ka.dbg = pl->d_dbg;
+            ka.dbg_blocks = uint32_t(std::atoi(e));
+        }
+#endif
 #ifdef MR_STAMPS
-    if (hipMalloc(reinterpret_cast<void **>(&pl->d_dbg), size_t(pl->blocks) * 10 * 8) == hipSuccess) {
-        (void)hipMemset(pl->d_dbg, 0, size_t(pl->blocks) * 10 * 8);
+    if (hipMalloc(reinterpret_cast<void **>(&pl->d_dbg), (size_t(pl->blocks) * 10 + 16) * 8) == hipSuccess) {
+        (void)hipMemset(pl->d_dbg, 0, (size_t(pl->blocks) * 10 + 16) * 8);
         ka.dbg = pl->d_dbg;
+        ka.dbg_blocks = pl->blocks;
     }
 #endif
     if (hipMalloc(reinterpret_cast<void **>(&pl->d_args), sizeof(KArgs)) != hipSuccess ||
@@ -704,7 +715,7 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     if (pl->hp.hub) {
         // closed-form hub solve for every source, then the SSSP kernel for the
         // sources it flagged (usually none; those workgroups exit at once)
-        e = launch_hub(pl->d_args, pl->ka.p.NS, pl->hub_blocks, s);
+        e = launch_hub(pl->d_args, pl->ka.p.perm, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
         if (e == hipSuccess)
             e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, s);
     } else {
@@ -752,6 +763,24 @@ extern "C" int mr_plan_bind_outputs(mr_plan *pl, void *d_results, void *d_comman
 
 extern "C" uint32_t mr_plan_num_sources(const mr_plan *pl) { return pl ? pl->ka.nsrc : 0; }
 
+extern "C" int mr_plan_get_stats(mr_plan *pl, mr_plan_stats *out) {
+    if (!pl || !out) return fail(MR_ERR_INVALID_ARG, "null argument");
+    std::memset(out, 0, sizeof(*out));
+    uint32_t ctr[4] = {0, 0, 0, 0};
+    if (hipStreamSynchronize(pl->stream) != hipSuccess ||
+        hipMemcpy(ctr, pl->d_counter, 16, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(MR_ERR_DEVICE, "copy counter");
+    out->solver = pl->hp.hub ? MR_SOLVER_HUB : (pl->algo == kAlgoLegs ? MR_SOLVER_LEVELS : MR_SOLVER_BUCKETED);
+    out->grid_state_in_lds = pl->grid_in_lds ? 1u : 0u;
+    out->num_sources = pl->ka.nsrc;
+    out->fallback_sources = pl->hp.hub ? ctr[2] : 0u;
+    out->num_specials = pl->ka.p.NS;
+    out->num_regions = pl->hp.nreg;
+    out->hub_workgroups = pl->hub_blocks;
+    out->sssp_workgroups = pl->blocks;
+    return MR_OK;
+}
+
 extern "C" int mr_plan_device_outputs(mr_plan *pl, void **d_results, uint64_t *rb, void **d_commands, uint64_t *cb) {
     if (!pl) return fail(MR_ERR_INVALID_ARG, "null plan");
     if (d_results) *d_results = pl->ka.out_res;
@@ -785,14 +814,35 @@ static void expand_cmd(const mr_grid *g, const HostPlan &hp, const OutCmd &c, mr
         case kSFm: o.money = p.sfm_cost; break;
         default: break;
     }
-    o.from = g->idx[c.from];
-    o.to = g->idx[c.to];
+    o.from = g->idx[g->rank_inv[c.from]];  // device commands name cells by rank
+    o.to = g->idx[g->rank_inv[c.to]];
 }
 
 static int check_device_errors(mr_plan *pl, uint32_t &flags) {
     uint32_t ctr[4] = {0, 0, 0, 0};
     if (hipMemcpy(ctr, pl->d_counter, 16, hipMemcpyDeviceToHost) != hipSuccess) return fail(MR_ERR_DEVICE, "copy counter");
     flags = ctr[1];
+#ifdef MR_HUBDUMP
+    if (pl->d_dbg) {
+        std::vector<uint32_t> d(64 * 16);
+        (void)hipMemcpy(d.data(), pl->d_dbg, d.size() * 4, hipMemcpyDeviceToHost);
+        for (uint32_t t = 0; t <= pl->ka.p.NS; ++t) {
+            const uint32_t *r = &d[t * 16];
+            const uint32_t v = t ? pl->hp.sp[t].v : pl->ka.dbg_blocks;
+            const mr_cell_index &c = pl->grid->idx[v];
+            std::fprintf(stderr, "T%2u (%u,%u,%u,%u) R.m=(%u,%u,%u) len=%u ntail=%u state=%u par=%u", t, c.kind, c.sub,
+                         c.x, c.y, r[0], r[1], r[2], r[3] & 0xFFFF, (r[3] >> 16) & 0xFF, r[3] >> 24, r[4] & 0xFFFF);
+            for (uint32_t i = 0; i < 2; ++i) {
+                const uint32_t f = r[6 + 3 * i], to = r[7 + 3 * i];
+                const mr_cell_index &cf = pl->grid->idx[pl->grid->rank_inv[f < pl->grid->V ? f : 0]];
+                const mr_cell_index &ct = pl->grid->idx[pl->grid->rank_inv[to < pl->grid->V ? to : 0]];
+                std::fprintf(stderr, " [k%u p%u (%u,%u,%u,%u)->(%u,%u,%u,%u)]", r[5 + 3 * i] >> 29, r[5 + 3 * i] & 0x1FFFFFFF,
+                             cf.kind, cf.sub, cf.x, cf.y, ct.kind, ct.sub, ct.x, ct.y);
+            }
+            std::fprintf(stderr, " st=%u my=(%u,%u,%u) %08x\n", r[11], r[12], r[13], r[14], r[15]);
+        }
+    }
+#endif
     if (std::getenv("MR_DEBUG")) {
         std::fprintf(stderr, "MR_DEBUG hub=%d sources=%u fallback=%u flags=%u hub_blocks=%u\n", int(pl->hp.hub),
                      pl->ka.nsrc, ctr[2], ctr[1], pl->hub_blocks);
@@ -880,7 +930,7 @@ extern "C" int mr_plan_fetch(mr_plan *pl, mr_result *results, mr_command *pool, 
 extern "C" void mr_plan_destroy(mr_plan *pl) {
 #ifdef MR_STAMPS
     if (pl && pl->d_dbg) {  // diagnostic summary: phase cycles summed over workgroups (last launch)
-        std::vector<unsigned long long> d(size_t(pl->blocks) * 10);
+        std::vector<unsigned long long> d(size_t(pl->blocks) * 10 + 16);
         if (hipMemcpy(d.data(), pl->d_dbg, d.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
             unsigned long long acc[9] = {0};
             for (uint32_t b = 0; b < pl->blocks; ++b)
@@ -889,6 +939,12 @@ extern "C" void mr_plan_destroy(mr_plan *pl) {
                          "MR_STAMPS blocks=%u sources=%llu cycles: init=%llu fire=%llu specials=%llu next=%llu "
                          "bar1=%llu claim=%llu bar2=%llu frontier_vertices=%llu\n",
                          pl->blocks, acc[8], acc[0], acc[1], acc[2], acc[3], acc[4], acc[5], acc[6], acc[7]);
+            const unsigned long long *h = &d[size_t(pl->blocks) * 10];
+            if (pl->hp.hub)
+                std::fprintf(stderr,
+                             "MR_STAMPS hub (sum over waves): sources=%llu iterations=%llu boundaries=%llu cycles: "
+                             "init=%llu select=%llu edges=%llu boundary=%llu emit=%llu dequeue=%llu\n",
+                             h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]);
         }
     }
 #endif

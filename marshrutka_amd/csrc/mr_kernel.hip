@@ -93,6 +93,33 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// ---- wave-wide minimum on the DPP network (all 64 lanes active) ----------------------
+// row_shr 1/2/4/8 leave each row's minimum in its lane 15, row_bcast 15/31 carry it
+// to lane 63; rows outside the mask keep the identity, so min() leaves them intact.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_min(uint32_t x) {
+    const uint32_t y = uint32_t(__builtin_amdgcn_update_dpp(-1, int(x), CTRL, ROWS, 0xF, false));
+    return y < x ? y : x;
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+    x = dpp_min<0x111, 0xF>(x);  // row_shr:1
+    x = dpp_min<0x112, 0xF>(x);  // row_shr:2
+    x = dpp_min<0x114, 0xF>(x);  // row_shr:4
+    x = dpp_min<0x118, 0xF>(x);  // row_shr:8
+    x = dpp_min<0x142, 0xA>(x);  // row_bcast:15
+    x = dpp_min<0x143, 0xC>(x);  // row_bcast:31
+    return uint32_t(__builtin_amdgcn_readlane(int(x), 63));
+}
+// keep in c only the lanes whose key is the minimum over the lanes in c
+__device__ __forceinline__ void narrow(bool &c, uint32_t key) {
+    const uint32_t m = wave_min_u32(c ? key : 0xFFFFFFFFu);
+    c = c && key == m;
+}
+// value of x in (uniform) lane l, without LDS
+__device__ __forceinline__ uint32_t bcast(uint32_t x, uint32_t l) {
+    return uint32_t(__builtin_amdgcn_readlane(int(x), int(l)));
+}
+
 // A label viewed for comparison: metrics, length, prefix pointer (table
 // index, 0 = empty prefix) and the last <= 2 commands.  Scalar fields only, so
 // nothing is runtime-indexed (no scratch).
@@ -101,6 +128,19 @@ struct View {
     uint32_t len, parent, ntail;
     Cmd t0, t1;
 };
+__device__ __forceinline__ Cmd bcast(const Cmd &c, uint32_t l) { return Cmd{bcast(c.kp, l), bcast(c.from, l), bcast(c.to, l)}; }
+__device__ __forceinline__ View bcast(const View &x, uint32_t l) {
+    View y;
+    y.m0 = bcast(x.m0, l);
+    y.m1 = bcast(x.m1, l);
+    y.m2 = bcast(x.m2, l);
+    y.len = bcast(x.len, l);
+    y.parent = bcast(x.parent, l);
+    y.ntail = bcast(x.ntail, l);
+    y.t0 = bcast(x.t0, l);
+    y.t1 = bcast(x.t1, l);
+    return y;
+}
 // selected with masks rather than ?: so the optimiser cannot turn it into a
 // load through a selected pointer (which would force the View into scratch)
 __device__ __forceinline__ Cmd tail_at(const View &x, int i) {
@@ -114,10 +154,16 @@ struct Core {
     Shared *sh;
     Rec *R;
     uint32_t *state;
+    // Register copies of the launch constants: wave_sync's fences make the compiler
+    // re-load anything read through `a` after every sync.
+    DevParams P;
+    const uint32_t *rank;     // a->rank
+    const uint32_t *sinfo;    // a->sinfo
+    uint32_t *counter;        // a->counter
     const SpecialStatic *sp;  // LDS copy of a->sp (loaded once per workgroup)
     const uint16_t *hubs;     // LDS copy of a->hubs
     uint32_t *dst;            // LDS: destinations of the current source (<= early_exit_max)
-    uint32_t src;
+    uint32_t src, src_rk;
 
     // ---- memory helpers -----------------------------------------------------
     __device__ __forceinline__ uint32_t ld_state(uint32_t v) const {
@@ -142,10 +188,12 @@ struct Core {
         if constexpr (G) __hip_atomic_store(l + i, IdxT(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else l[i] = IdxT(v);
     }
-    __device__ __forceinline__ void flag(uint32_t e) const { atomicOr(a->counter + 1, e); }
-    __device__ __forceinline__ uint32_t special_of(uint32_t v) const { return a->sinfo[v] & kNone10; }
-    __device__ __forceinline__ uint32_t region_of(uint32_t v) const { return (a->sinfo[v] >> 10) & kNone10; }
+    __device__ __forceinline__ void flag(uint32_t e) const { atomicOr(counter + 1, e); }
+    __device__ __forceinline__ uint32_t special_of(uint32_t v) const { return sinfo[v] & kNone10; }
+    __device__ __forceinline__ uint32_t region_of(uint32_t v) const { return (sinfo[v] >> 10) & kNone10; }
     __device__ __forceinline__ uint32_t vert_of(uint32_t t) const { return t == 0 ? src : sp[t].v; }
+    // commands name cells by CellIndex rank, so comparing them needs no memory access
+    __device__ __forceinline__ uint32_t rk_of(uint32_t t) const { return t == 0 ? src_rk : sp[t].rk; }
 
     // ---- arithmetic (u32 like the reference; overflow is reported, not wrapped)
     __device__ __forceinline__ uint32_t add32(uint32_t x, uint32_t y) const {
@@ -156,14 +204,14 @@ struct Core {
     // AggregatedCost::time of a StandardMove run of k legs: Fleetfoot ceil of
     // 180k seconds (src/cost.rs:122-124, src/skill.rs:21-30)
     __device__ __forceinline__ uint32_t run_time(uint32_t k) const {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         unsigned long long t = 180ull * k;
         if (p.ff_num != p.ff_den) t = (t * p.ff_num + p.ff_den - 1) / p.ff_den;
         if (t > 0xFFFFFFFFull) flag(kErrMetricOverflow);
         return uint32_t(t);
     }
     __device__ __forceinline__ unsigned long long key_of(uint32_t m0, uint32_t m1, uint32_t m2) const {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         switch (p.bucket_mode) {
             case kBucketLegs: return m0;
             case kBucketTime: return m2 / p.W;
@@ -191,11 +239,11 @@ struct Core {
         x.len = 1;
         x.parent = 0;
         x.ntail = 1;
-        x.t0 = Cmd{kNoMove << 29, src, src};
+        x.t0 = Cmd{kNoMove << 29, src_rk, src_rk};
         x.t1 = Cmd{0, 0, 0};
     }
-    // walk label of v: full(b) ++ [StandardMove{k} vert(b) -> v]
-    __device__ __forceinline__ void view_walk(uint32_t b, uint32_t k, uint32_t v, View &x) const {
+    // walk label of v (rank vr): full(b) ++ [StandardMove{k} vert(b) -> v]
+    __device__ __forceinline__ void view_walk(uint32_t b, uint32_t k, uint32_t vr, View &x) const {
         if (b == 0 && k == 0) {
             view_start(x);
             return;
@@ -207,15 +255,43 @@ struct Core {
         x.len = (b == 0 ? 0u : rb.len) + 1u;
         x.parent = b;
         x.ntail = 1;
-        x.t0 = Cmd{(kStandard << 29) | k, vert_of(b), v};
+        x.t0 = Cmd{(kStandard << 29) | k, rk_of(b), vr};
         x.t1 = Cmd{0, 0, 0};
+    }
+
+    // the same, from b's label lb held in registers
+    __device__ __forceinline__ void view_walk_lab(const View &lb, uint32_t b, uint32_t k, uint32_t vr, View &x) const {
+        if (b == 0 && k == 0) {
+            view_start(x);
+            return;
+        }
+        x.m0 = add32(lb.m0, k);
+        x.m1 = lb.m1;
+        x.m2 = add32(lb.m2, run_time(k));
+        x.len = (b == 0 ? 0u : lb.len) + 1u;
+        x.parent = b;
+        x.ntail = 1;
+        x.t0 = Cmd{(kStandard << 29) | k, rk_of(b), vr};
+        x.t1 = Cmd{0, 0, 0};
+    }
+    __device__ __forceinline__ void write_rec(uint32_t t, const View &c, uint32_t state) const {
+        Rec &r = R[t];
+        r.m[0] = c.m0;
+        r.m[1] = c.m1;
+        r.m[2] = c.m2;
+        r.len = uint16_t(c.len);
+        r.ntail = uint8_t(c.ntail);
+        r.parent = uint16_t(c.parent);
+        r.tail[0] = c.t0;
+        r.tail[1] = c.t1;
+        r.state = uint8_t(state);
     }
 
     // ---- comparator: CostComparator::and_then (src/cost.rs:411-426) ------------
     __device__ __forceinline__ int cmp_cmd(const Cmd &x, const Cmd &y) const {
         if (x.kp != y.kp) return x.kp < y.kp ? -1 : 1;
-        if (x.from != y.from) return a->rank[x.from] < a->rank[y.from] ? -1 : 1;
-        if (x.to != y.to) return a->rank[x.to] < a->rank[y.to] ? -1 : 1;
+        if (x.from != y.from) return x.from < y.from ? -1 : 1;  // ranks: CellIndex order
+        if (x.to != y.to) return x.to < y.to ? -1 : 1;
         return 0;
     }
     // command i of table entry t, by value (no pointer into LDS escapes)
@@ -256,7 +332,7 @@ struct Core {
     }
     __device__ __forceinline__ int cmp_metrics(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t y0, uint32_t y1,
                                                uint32_t y2) const {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             const uint32_t pi = p.perm[i];
@@ -309,10 +385,10 @@ struct Core {
         r.tail[1] = c.t1;
         r.state = 1;
     }
-    // extend the settled label r of special s (vertex vs) by a non-Standard edge
-    // to the vertex vt (TotalCost += edge, src/cost.rs:208-315)
-    __device__ __forceinline__ void ext_view(const View &r, uint32_t s, uint32_t vs, uint32_t kind, uint32_t payload,
-                                             uint32_t dm_money, uint32_t dm_time, uint32_t vt, View &c) const {
+    // extend the settled label r of special s (rank rs) by a non-Standard edge
+    // to the cell of rank rt (TotalCost += edge, src/cost.rs:208-315)
+    __device__ __forceinline__ void ext_view(const View &r, uint32_t s, uint32_t rs, uint32_t kind, uint32_t payload,
+                                             uint32_t dm_money, uint32_t dm_time, uint32_t rt, View &c) const {
         const Cmd last = r.ntail == 2 ? r.t1 : r.t0;
         const uint32_t lk = last.kp >> 29;
         c.t1 = Cmd{0, 0, 0};
@@ -323,7 +399,7 @@ struct Core {
             c.len = 1;
             c.parent = 0;
             c.ntail = 1;
-            c.t0 = Cmd{(kind << 29) | payload, last.from, vt};
+            c.t0 = Cmd{(kind << 29) | payload, last.from, rt};
         } else if (kind == kCentral && lk == kCentral) {  // CentralMoves merge (ntail is 1)
             c.m0 = r.m0;
             c.m1 = r.m1;
@@ -331,7 +407,7 @@ struct Core {
             c.len = r.len;
             c.parent = r.parent;
             c.ntail = 1;
-            c.t0 = Cmd{last.kp + 1u, last.from, vt};
+            c.t0 = Cmd{last.kp + 1u, last.from, rt};
         } else {
             c.m0 = r.m0;
             c.m1 = add32(r.m1, dm_money);
@@ -339,19 +415,19 @@ struct Core {
             c.len = r.len + 1u;
             c.parent = s;
             c.ntail = 1;
-            c.t0 = Cmd{(kind << 29) | payload, vs, vt};
+            c.t0 = Cmd{(kind << 29) | payload, rs, rt};
         }
     }
     __device__ __forceinline__ void ext_special(uint32_t s, uint32_t kind, uint32_t payload, uint32_t dm_money,
                                                 uint32_t dm_time, uint32_t t, View &c) const {
         View r;
         view_rec(s, r);
-        ext_view(r, s, sp[s].v, kind, payload, dm_money, dm_time, sp[t].v, c);
+        ext_view(r, s, sp[s].rk, kind, payload, dm_money, dm_time, sp[t].rk, c);
     }
-    // the SoE candidate for campfire t from plain vertex u with walk label (b,k)
-    __device__ __forceinline__ void soe_from_plain(uint32_t b, uint32_t k, uint32_t u, uint32_t t, View &c) const {
-        const DevParams &p = a->p;
-        const uint32_t vt = sp[t].v;
+    // the SoE candidate for campfire t from plain vertex u (rank ur) with walk label (b,k)
+    __device__ __forceinline__ void soe_from_plain(uint32_t b, uint32_t k, uint32_t ur, uint32_t t, View &c) const {
+        const DevParams &p = P;
+        const uint32_t vt = sp[t].rk;
         if (b == 0 && k == 0) {  // u is the source: [SoE src->c]
             c.m0 = 0;
             c.m1 = p.soe_cost;
@@ -359,21 +435,21 @@ struct Core {
             c.len = 1;
             c.parent = 0;
             c.ntail = 1;
-            c.t0 = Cmd{kSoE << 29, src, vt};
+            c.t0 = Cmd{kSoE << 29, src_rk, vt};
             c.t1 = Cmd{0, 0, 0};
         } else {  // full(b) ++ [Std{k} b->u, SoE u->c]
-            view_walk(b, k, u, c);
+            view_walk(b, k, ur, c);
             c.m1 = add32(c.m1, p.soe_cost);
             c.len += 1;
             c.ntail = 2;
-            c.t1 = Cmd{kSoE << 29, u, vt};
+            c.t1 = Cmd{kSoE << 29, ur, vt};
         }
     }
 
     // ---- grid helpers -------------------------------------------------------------
     // geometric neighbour d (0:-x 1:+x 2:-y 3:+y) of v, or kNone32
     __device__ __forceinline__ uint32_t nbr(uint32_t v, int d) const {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         const uint32_t x = v % p.S;
         switch (d) {
             case 0: return x == 0 ? kNone32 : v - 1;
@@ -388,7 +464,7 @@ struct Core {
     // caravan (:140-160, 251-273) and Scroll-of-Escape (:162-170) edges.
     // Returns whether s is a boundary (its label does not end in a StandardMove).
     __device__ __forceinline__ bool settle_special(uint32_t s, uint32_t par_bits) const {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         const uint32_t lane = lane_id();
         const uint32_t vs = sp[s].v;
         Rec &r = R[s];
@@ -455,7 +531,7 @@ struct Core {
 
     // wave argmin (full comparator) over tentative specials whose key == K
     __device__ __forceinline__ uint32_t argmin_special(unsigned long long K) const {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         const uint32_t lane = lane_id();
         uint32_t mine = kNone32;
         for (uint32_t t = 1 + lane; t <= p.NS; t += 64) {
@@ -475,17 +551,31 @@ struct Core {
     // ---- register-resident exact Dijkstra over the specials of bucket K -------------
     // (wave 0, NS <= 63): lane t holds the tentative label of special t; the LDS
     // table R[] stays an exact mirror (every improvement is written back) because
-    // other phases and the list comparator read it.  Per iteration: a 64-lane
-    // lexicographic min over (c1, c2 c3) picks the settle candidate (full
-    // comparator only on exact metric ties), then every lane relaxes the edges
-    // from the settled special into itself — no shared-write races.
-    __device__ __forceinline__ static unsigned long long wave_min_u64(unsigned long long x) {
+    // other phases and the list comparator read it.  Per iteration select_lane picks
+    // the settle candidate, then every lane relaxes the edges from the settled
+    // special into itself — no shared-write races.
+    __device__ __forceinline__ static uint32_t metric(const View &x, uint32_t i) {
+        return i == 0 ? x.m0 : (i == 1 ? x.m1 : x.m2);
+    }
+    // among the lanes with c set, the one holding the smallest table label (lane t holds
+    // entry t, mirrored in `my`): metrics in comparator order, then length on the DPP
+    // network; only exact ties of both reach the command-list compare.  kNone32 if none.
+    __device__ __forceinline__ uint32_t select_lane(bool c, const View &my) const {
+        if (__ballot(c) == 0) return kNone32;
+        const DevParams &p = P;
+        narrow(c, metric(my, p.perm[0]));
+        narrow(c, metric(my, p.perm[1]));
+        narrow(c, metric(my, p.perm[2]));
+        narrow(c, my.len);
+        const unsigned long long bal = __ballot(c);
+        if (__popcll(bal) == 1) return uint32_t(__ffsll((long long)bal) - 1);
+        uint32_t m = c ? lane_id() : kNone32;
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
-            const unsigned long long o = __shfl_xor(x, off, 64);
-            x = o < x ? o : x;
+            const uint32_t o = __shfl_xor(m, off, 64);
+            if (o != kNone32 && (m == kNone32 || cmp_entries(o, m) < 0)) m = o;
         }
-        return x;
+        return m;
     }
     __device__ __forceinline__ void improve_own(uint32_t t, uint32_t &st, View &my, const View &c) const {
         if (st == 2) return;
@@ -512,10 +602,9 @@ struct Core {
     }
     template <class OnSettle>
     __device__ __forceinline__ void specials_reg(unsigned long long K, uint32_t par_bits, OnSettle on_settle) const {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         const uint32_t t = lane_id();
         const bool mine = t >= 1 && t <= p.NS;
-        const uint32_t q0 = p.perm[0], q1 = p.perm[1], q2 = p.perm[2];
         View my;
         uint32_t st = 0;
         SpecialStatic ss{};
@@ -531,29 +620,8 @@ struct Core {
             const unsigned long long key = tent ? key_of(my.m0, my.m1, my.m2) : kInf64;
             if (tent && key < K) flag(kErrBucket);
             const bool cand = tent && key == K;
-            const uint32_t a1 = q0 == 0 ? my.m0 : (q0 == 1 ? my.m1 : my.m2);
-            const uint32_t a2 = q1 == 0 ? my.m0 : (q1 == 1 ? my.m1 : my.m2);
-            const uint32_t a3 = q2 == 0 ? my.m0 : (q2 == 1 ? my.m1 : my.m2);
-            const unsigned long long k1 = cand ? (unsigned long long)a1 : kInf64;
-            const unsigned long long min1 = wave_min_u64(k1);
-            if (min1 == kInf64) break;
-            const bool c1 = cand && k1 == min1;
-            const unsigned long long k23 = c1 ? ((unsigned long long)a2 << 32 | a3) : kInf64;
-            const unsigned long long min23 = wave_min_u64(k23);
-            const bool top = c1 && k23 == min23;
-            const unsigned long long bal = __ballot(top);
-            uint32_t s;
-            if (__popcll(bal) == 1) {
-                s = uint32_t(__ffsll((long long)bal) - 1);
-            } else {  // exact metric tie: length, then the command lists
-                uint32_t m = top ? t : kNone32;
-#pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) {
-                    const uint32_t o = __shfl_xor(m, off, 64);
-                    if (o != kNone32 && (m == kNone32 || cmp_entries(o, m) < 0)) m = o;
-                }
-                s = m;
-            }
+            const uint32_t s = select_lane(cand, my);
+            if (s == kNone32) break;
             // settle s
             View ls;
             view_rec(s, ls);
@@ -584,17 +652,17 @@ struct Core {
                 View c;
                 if (((sS.flags & kSpCenter) && (ss.flags & kSpBorder1)) ||
                     ((sS.flags & kSpBorder1) && (ss.flags & kSpCenter))) {
-                    ext_view(ls, s, sS.v, kCentral, 1, 0, 10, ss.v, c);
+                    ext_view(ls, s, sS.rk, kCentral, 1, 0, 10, ss.rk, c);
                     improve_own(t, st, my, c);
                 }
                 if (p.use_caravans && (sS.flags & kSpHub) && (ss.flags & kSpHub)) {
                     const uint32_t d = uint32_t(abs(sS.x - ss.x) + abs(sS.y - ss.y));
                     const uint32_t coef = ss.coef5 ? 5u : 2u;
-                    ext_view(ls, s, sS.v, kCaravan, (d << 1) | ss.coef5, coef * d, p.rgt * d, ss.v, c);
+                    ext_view(ls, s, sS.rk, kCaravan, (d << 1) | ss.coef5, coef * d, p.rgt * d, ss.rk, c);
                     improve_own(t, st, my, c);
                 }
                 if (p.use_soe && sS.region == t) {
-                    ext_view(ls, s, sS.v, kSoE, 0, p.soe_cost, 0, ss.v, c);
+                    ext_view(ls, s, sS.rk, kSoE, 0, p.soe_cost, 0, ss.rk, c);
                     improve_own(t, st, my, c);
                 }
             }
@@ -602,7 +670,7 @@ struct Core {
         }
     }
     __device__ __forceinline__ unsigned long long min_special_key() const {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         unsigned long long smin = kInf64;
         for (uint32_t t = 1 + lane_id(); t <= p.NS; t += 64)
             if (R[t].state == 1) {
@@ -621,9 +689,10 @@ struct Core {
     // Untouched grid words carry the vertex's static info in their k field
     // (special index | region << 10), so a claim needs no extra global load.
     __device__ __forceinline__ void init_source(uint32_t s_idx) {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         const uint32_t tid = threadIdx.x;
         src = a->src_v[s_idx];
+        src_rk = rank[src];
         if constexpr (G) {
             const uint4 *i4 = reinterpret_cast<const uint4 *>(a->sinfo);
             uint4 *s4 = reinterpret_cast<uint4 *>(state);
@@ -648,25 +717,25 @@ struct Core {
     // SHQ / SFm: only the source's own edges can be minimal (any prefix only adds
     // metrics and length), src/pathfinder.rs:172-178
     __device__ __forceinline__ void seed_scrolls() const {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         if (p.hq_t) {
             View c;
             view_start(c);
             c.m1 = p.shq_cost;
-            c.t0 = Cmd{kSHQ << 29, src, sp[p.hq_t].v};
+            c.t0 = Cmd{kSHQ << 29, src_rk, sp[p.hq_t].rk};
             try_improve(p.hq_t, c);
         }
         if (p.use_sfm) {
             View c;
             view_start(c);
             c.m1 = p.sfm_cost;
-            c.t0 = Cmd{kSFm << 29, src, p.vc};
+            c.t0 = Cmd{kSFm << 29, src_rk, sp[1].rk};  // entry 1 = the Center
             try_improve(1, c);
         }
     }
     // materialise label x as query qid's result record and command slots
     __device__ __forceinline__ void emit(const View &x, uint32_t qid) const {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         OutResult &o = a->out_res[qid];
         if (x.len > p.max_cmds) {  // MR_ERR_CAPACITY: the host re-runs with more slots
             o = OutResult{x.m0, x.m1, x.m2, (uint32_t(16 - 4) << 16) | (x.len & 0xFFFFu)};
@@ -701,7 +770,7 @@ struct Core {
         View x;
         const uint32_t t = special_of(w);
         if (t != kNone10) view_rec(t, x);
-        else view_walk((sw >> kStBShift) & kNone10, sw & kStKMask, w, x);
+        else view_walk((sw >> kStBShift) & kNone10, sw & kStKMask, rank[w], x);
         emit(x, qid);
     }
     __device__ __forceinline__ void write_outputs(uint32_t s_idx) const {
@@ -740,6 +809,10 @@ struct LegsSolver : Core<G> {
     using Core<G>::R;
     using Core<G>::state;
     using Core<G>::src;
+    using Core<G>::P;
+    using Core<G>::rank;
+    using Core<G>::sinfo;
+    using Core<G>::counter;
     IdxT *F0, *F1;                 // frontier ping-pong lists
     uint32_t *prio;                // per boundary rank for the next level
     uint32_t *bnd;                 // boundary list (table indices), bnd[0] = 0 (the source)
@@ -779,7 +852,7 @@ struct LegsSolver : Core<G> {
     }
     // wave 0: SoE candidates from the level-L region argmins
     __device__ __forceinline__ void fire_regions() const {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         for (uint32_t t = 1 + lane_id(); t <= p.NS; t += 64) {
             const unsigned long long key = best64[t];
             if (key == kInf64) continue;
@@ -789,14 +862,14 @@ struct LegsSolver : Core<G> {
             const uint32_t u = a->rank_inv[uint32_t(key)];
             const uint32_t su = this->ld_state(u);
             View c;
-            this->soe_from_plain((su >> kStBShift) & kNone10, su & kStKMask, u, t, c);
+            this->soe_from_plain((su >> kStBShift) & kNone10, su & kStKMask, uint32_t(key), t, c);
             this->try_improve(t, c);
         }
         wave_sync();
     }
     // claim the unsettled StandardMove neighbours of frontier vertex v (level L)
     __device__ __forceinline__ void claim_from(uint32_t v, uint32_t L, IdxT *Fn, uint32_t cn) const {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         if (v == p.vc) return;  // the Center's out-edges are CentralMoves
         const uint32_t parL = (L & 1u) ? kStPar : 0u;
         const uint32_t parN = parL ^ kStPar;
@@ -837,7 +910,7 @@ struct LegsSolver : Core<G> {
             const uint32_t t = sw & kNone10;  // static info of the untouched word
             if (t != kNone10) {  // a special: offer the walk label to the table
                 View c;
-                this->view_walk(bb, bk, w, c);
+                this->view_walk(bb, bk, this->sp[t].rk, c);
                 this->try_improve(t, c);
                 continue;
             }
@@ -846,13 +919,13 @@ struct LegsSolver : Core<G> {
             this->st_idx(Fn, i, w);
             if (p.use_soe) {
                 const uint32_t r = (sw >> 10) & kNone10;
-                if (r != kNone10 && !fired[r]) atomicMin(best64 + r, ((unsigned long long)bp << 32) | a->rank[w]);
+                if (r != kNone10 && !fired[r]) atomicMin(best64 + r, ((unsigned long long)bp << 32) | rank[w]);
             }
         }
     }
 
     __device__ __forceinline__ void solve(uint32_t s_idx) {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         const uint32_t tid = threadIdx.x;
         this->init_source(s_idx);
         for (uint32_t t = tid; t <= p.NS; t += kBS) {
@@ -885,7 +958,7 @@ struct LegsSolver : Core<G> {
                 const uint32_t r = this->region_of(src);
                 if (p.use_soe && r != kNone10) {  // [SoE src -> nearest campfire]
                     View c;
-                    this->soe_from_plain(0, 0, src, r, c);
+                    this->soe_from_plain(0, 0, this->src_rk, r, c);
                     this->try_improve(r, c);
                     fired[r] = 1;
                 }
@@ -987,6 +1060,10 @@ struct GenericSolver : Core<G> {
     using Core<G>::R;
     using Core<G>::state;
     using Core<G>::src;
+    using Core<G>::P;
+    using Core<G>::rank;
+    using Core<G>::sinfo;
+    using Core<G>::counter;
     IdxT *L0b, *dirty;  // the three bucket lists are L0b + i * lstride
     uint32_t lstride;
     uint32_t *best;
@@ -995,7 +1072,7 @@ struct GenericSolver : Core<G> {
     __device__ __forceinline__ IdxT *lbuf(uint32_t i) const { return L0b + i * lstride; }
 
     __device__ __forceinline__ void mark_dirty(uint32_t v, uint32_t n) const {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         if (n == kNone32 || v == p.vc || n == p.vc) return;
         const uint32_t old = this->or_state(n, kStDirty);
         if (old & (kStSettled | kStDirty)) return;
@@ -1008,8 +1085,8 @@ struct GenericSolver : Core<G> {
             if (cur != kNone32) {
                 const uint32_t su = this->ld_state(cur), sv = this->ld_state(v);
                 View xu, xv;
-                this->view_walk((su >> kStBShift) & kNone10, su & kStKMask, cur, xu);
-                this->view_walk((sv >> kStBShift) & kNone10, sv & kStKMask, v, xv);
+                this->view_walk((su >> kStBShift) & kNone10, su & kStKMask, rank[cur], xu);
+                this->view_walk((sv >> kStBShift) & kNone10, sv & kStKMask, rank[v], xv);
                 if (this->cmp_view(xu, kOwn, xv, kOwn) <= 0) return;
             }
             const uint32_t prev = atomicCAS(best + r, cur, v);
@@ -1018,7 +1095,7 @@ struct GenericSolver : Core<G> {
         }
     }
     __device__ __forceinline__ void settle_plain(uint32_t v) const {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         this->or_state(v, kStSettled);
         if (p.use_soe) {
             const uint32_t r = this->region_of(v);
@@ -1028,7 +1105,7 @@ struct GenericSolver : Core<G> {
         for (int d = 0; d < 4; ++d) mark_dirty(v, this->nbr(v, d));
     }
     __device__ __forceinline__ void fire_regions() const {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         for (uint32_t t = 1 + lane_id(); t <= p.NS; t += 64) {
             const uint32_t u = best[t];
             if (u == kNone32) continue;
@@ -1037,13 +1114,13 @@ struct GenericSolver : Core<G> {
             if (R[t].state == 2) continue;
             const uint32_t su = this->ld_state(u);
             View c;
-            this->soe_from_plain((su >> kStBShift) & kNone10, su & kStKMask, u, t, c);
+            this->soe_from_plain((su >> kStBShift) & kNone10, su & kStKMask, rank[u], t, c);
             this->try_improve(t, c);
         }
         wave_sync();
     }
     __device__ __forceinline__ void pull(uint32_t w) const {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         // a vertex marked dirty may have been settled later in the same bucket
         if (this->ld_state(w) & kStSettled) return;
         const uint32_t t = this->special_of(w);
@@ -1066,9 +1143,9 @@ struct GenericSolver : Core<G> {
                 } else if (b == bb) {
                     if (k < bk) bk = k;  // same boundary: fewer legs is smaller in every order
                 } else {
-                    View xc, xb;
-                    this->view_walk(b, k, w, xc);
-                    this->view_walk(bb, bk, w, xb);
+                    View xc, xb;  // same endpoint: its rank cannot decide, any value serves
+                    this->view_walk(b, k, 0, xc);
+                    this->view_walk(bb, bk, 0, xb);
                     if (this->cmp_view(xc, kOwn, xb, kOwn) < 0) {
                         bb = b;
                         bk = k;
@@ -1080,7 +1157,7 @@ struct GenericSolver : Core<G> {
             this->st_state(w, this->ld_state(w) & ~kStDirty);
             if (bb != kNone10) {
                 View c;
-                this->view_walk(bb, bk, w, c);
+                this->view_walk(bb, bk, this->sp[t].rk, c);
                 this->try_improve(t, c);
             }
             return;
@@ -1094,7 +1171,7 @@ struct GenericSolver : Core<G> {
         this->st_state(w, (bb << kStBShift) | bk);
         if (((old >> kStBShift) & kNone10) == kNone10) {  // first touch: list it (its bucket is final)
             View c;
-            this->view_walk(bb, bk, w, c);
+            this->view_walk(bb, bk, 0, c);  // metrics only
             const unsigned long long X = this->key_of(c.m0, c.m1, c.m2), B = sh->B;
             uint32_t j;
             if (X == B + 1) j = 1;
@@ -1126,7 +1203,7 @@ struct GenericSolver : Core<G> {
         }
     }
     __device__ __forceinline__ void solve(uint32_t s_idx) {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         const uint32_t tid = threadIdx.x;
         this->init_source(s_idx);
         for (uint32_t t = tid; t <= p.NS; t += kBS) {
@@ -1223,8 +1300,79 @@ __device__ __forceinline__ uint32_t walk_dist(int ax, int ay, int bx, int by) {
 }
 
 struct HubSolver : Core<false> {
-    uint32_t *bnd;  // this wave's boundary list (table indices; bnd[0] = 0, the source)
+    uint32_t *bnd;          // this wave's boundary list (table indices; bnd[0] = 0, the source)
+    const uint32_t *nearS;  // LDS: region rows {distance, rank} of every special (row t at t*2*nreg)
+    uint32_t *srow;         // LDS: this wave's region row of the current source
+    uint32_t nreg;
+#ifdef MR_STAMPS
+    mutable unsigned long long hs_last = 0, hs[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    __device__ void hmark(int slot) const {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        hs[slot] += t - hs_last;
+        hs_last = t;
+    }
+#define MR_HSTAMP(slot) hmark(slot)
+#define MR_HCOUNT(slot, n) (hs[slot] += (n))
+#else
+#define MR_HSTAMP(slot) \
+    do {                \
+    } while (0)
+#define MR_HCOUNT(slot, n) \
+    do {                   \
+    } while (0)
+#endif
 
+    // tentative labels live only in registers (lane t = special t); the LDS table
+    // receives a label when it settles (command chains and list compares read it)
+    // (the update is a per-field select, not a divergent block assignment)
+    __device__ __forceinline__ void improve_reg(bool active, uint32_t &st, View &my, const View &c) const {
+        bool take = active && st != 2;
+        if (take && st == 1) {
+            const int cm = cmp_metrics(c.m0, c.m1, c.m2, my.m0, my.m1, my.m2);
+            if (cm != 0) take = cm < 0;
+            else if (c.len != my.len) take = c.len < my.len;
+            else take = cmp_list(c, kOwn, my, kOwn) < 0;
+        }
+        my.m0 = take ? c.m0 : my.m0;
+        my.m1 = take ? c.m1 : my.m1;
+        my.m2 = take ? c.m2 : my.m2;
+        my.len = take ? c.len : my.len;
+        my.parent = take ? c.parent : my.parent;
+        my.ntail = take ? c.ntail : my.ntail;
+        my.t0.kp = take ? c.t0.kp : my.t0.kp;
+        my.t0.from = take ? c.t0.from : my.t0.from;
+        my.t0.to = take ? c.t0.to : my.t0.to;
+        my.t1.kp = take ? c.t1.kp : my.t1.kp;
+        my.t1.from = take ? c.t1.from : my.t1.from;
+        my.t1.to = take ? c.t1.to : my.t1.to;
+        st = take ? 1u : st;
+    }
+    // the settle candidate: smallest tentative label, resolved metric by metric on the
+    // DPP network with an exit as soon as one lane is left; exact ties of metrics and
+    // length publish the tied labels to the table and compare command lists
+    __device__ __forceinline__ uint32_t select_reg(bool c, const View &my) const {
+        unsigned long long bal = __ballot(c);
+        if (bal == 0) return kNone32;
+        const DevParams &p = P;
+        const uint32_t keys[4] = {metric(my, p.perm[0]), metric(my, p.perm[1]), metric(my, p.perm[2]), my.len};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (__popcll(bal) == 1) return uint32_t(__ffsll((long long)bal) - 1);
+            narrow(c, keys[i]);
+            bal = __ballot(c);
+        }
+        if (__popcll(bal) == 1) return uint32_t(__ffsll((long long)bal) - 1);
+        const uint32_t t = lane_id();
+        if (c) write_rec(t, my, 1);
+        wave_sync();
+        uint32_t m = c ? t : kNone32;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const uint32_t o = __shfl_xor(m, off, 64);
+            if (o != kNone32 && (m == kNone32 || cmp_entries(o, m) < 0)) m = o;
+        }
+        return m;
+    }
     __device__ __forceinline__ void note_walk(const View &c, uint32_t &bwh, uint32_t &b0, uint32_t &b1,
                                               uint32_t &b2) const {
         if (!bwh || cmp_metrics(c.m0, c.m1, c.m2, b0, b1, b2) < 0) {
@@ -1234,38 +1382,120 @@ struct HubSolver : Core<false> {
             b2 = c.m2;
         }
     }
-    // walks and SoE-region edges from boundary b (at bx, by) into lane t's special
-    __device__ __forceinline__ void relax_boundary(uint32_t b, int bx, int by, uint32_t t, bool mine, uint32_t &st,
-                                                   View &my, const SpecialStatic &ss, uint32_t &bwh, uint32_t &b0,
-                                                   uint32_t &b1, uint32_t &b2) const {
-        const DevParams &p = a->p;
-        if (!mine || st == 2) return;
-        const uint32_t vb = vert_of(b);
-        if (ss.v != p.vc && ss.v != vb) {
+    // walks and SoE-region edges from boundary b (label lb, at bx, by) into lane t's special
+    __device__ __forceinline__ void relax_boundary(const View &lb, uint32_t b, int bx, int by, uint32_t t, bool mine,
+                                                   uint32_t &st, View &my, const SpecialStatic &ss, uint32_t &bwh,
+                                                   uint32_t &b0, uint32_t &b1, uint32_t &b2) const {
+        const DevParams &p = P;
+        const bool live = mine && st != 2;
+        {  // the walk: not into the Center (entry 1) nor b's own cell
+            const bool on = live && t != 1 && t != b && !(b == 0 && ss.v == src);
             View c;
-            view_walk(b, walk_dist(bx, by, ss.x, ss.y), ss.v, c);
-            note_walk(c, bwh, b0, b1, b2);
-            improve_own(t, st, my, c);
+            view_walk_lab(lb, b, walk_dist(bx, by, ss.x, ss.y), ss.rk, c);
+            if (on) note_walk(c, bwh, b0, b1, b2);
+            improve_reg(on, st, my, c);
         }
-        if (p.use_soe && ss.rid != kNone10) {
-            const uint32_t *e = a->near + 2ull * (unsigned long long)(vb * a->nreg + ss.rid);
-            const uint32_t d = e[0], u = e[1];
-            if (d != kNone32 && (d != 0 || b == 0)) {  // d == 0, b special: its own SoE edge
-                View c;
-                soe_from_plain(b, d, u, t, c);
-                improve_own(t, st, my, c);
+        if (p.use_soe) {  // [Std{d} b->u, SoE u->c] from the region cell u nearest to b
+            uint32_t d = kNone32, u = 0;
+            if (live && ss.rid != kNone10) {
+                const uint32_t *e = (b == 0 ? srow : nearS + 2u * b * nreg) + 2u * ss.rid;
+                d = e[0];
+                u = e[1];
             }
+            const bool on = live && d != kNone32 && (d != 0 || b == 0);  // d == 0, b special: its own SoE edge
+            View c;
+            view_walk_lab(lb, b, on ? d : 0u, u, c);
+            if (d == 0) {  // b is the source, standing on the region: [SoE src->c]
+                c.ntail = 1;
+                c.t0 = Cmd{kSoE << 29, src_rk, ss.rk};
+                c.m1 = p.soe_cost;
+            } else {
+                c.m1 = add32(c.m1, p.soe_cost);
+                c.len += 1;
+                c.ntail = 2;
+                c.t1 = Cmd{kSoE << 29, u, ss.rk};
+            }
+            improve_reg(on, st, my, c);
         }
     }
 
+    // Few destinations: one query at a time, lane j evaluating boundary j's walk,
+    // the winner picked on the DPP network (exact metric + length ties: full compare).
+    static constexpr uint32_t kEmitWaveMax = 32;
+    __device__ __forceinline__ void bpos(uint32_t b, int sx, int sy, int &bx, int &by) const {
+        bx = b == 0 ? sx : sp[b].x;
+        by = b == 0 ? sy : sp[b].y;
+    }
+    __device__ __forceinline__ void emit_wave(uint32_t qa, uint32_t qb, uint32_t nb, int sx, int sy,
+                                              const View &st0) const {
+        const DevParams &p = P;
+        const uint32_t t = lane_id();
+        const uint32_t bj = t < nb ? bnd[t] : 0u;
+        const bool usable = t < nb && vert_of(bj) != p.vc;
+        int bx, by;
+        bpos(bj, sx, sy, bx, by);
+        for (uint32_t i = qa; i < qb; ++i) {
+            const uint32_t w = a->q_dst[i];
+            View x;
+            if (w == src) {
+                x = st0;
+            } else {
+                const uint32_t tw = sinfo[w] & kNone10;
+                if (tw != kNone10) {
+                    view_rec(tw, x);
+                } else {
+                    const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
+                    const uint32_t wr = rank[w];
+                    View c;
+                    view_walk(bj, walk_dist(bx, by, wx, wy), wr, c);
+                    bool cand = usable;
+                    narrow(cand, metric(c, p.perm[0]));
+                    narrow(cand, metric(c, p.perm[1]));
+                    narrow(cand, metric(c, p.perm[2]));
+                    narrow(cand, c.len);
+                    const unsigned long long bal = __ballot(cand);
+                    uint32_t win;
+                    if (__popcll(bal) == 1) {
+                        win = uint32_t(__ffsll((long long)bal) - 1);
+                    } else {  // equal metrics and length: compare the command lists
+                        win = cand ? t : kNone32;
+#pragma unroll
+                        for (int off = 32; off >= 1; off >>= 1) {
+                            const uint32_t o = __shfl_xor(win, off, 64);
+                            if (o == kNone32) continue;
+                            if (win == kNone32) {
+                                win = o;
+                                continue;
+                            }
+                            const uint32_t bo = bnd[o], bm = bnd[win];
+                            int ox, oy, mx, my_;
+                            bpos(bo, sx, sy, ox, oy);
+                            bpos(bm, sx, sy, mx, my_);
+                            View co, cm;
+                            view_walk(bo, walk_dist(ox, oy, wx, wy), wr, co);
+                            view_walk(bm, walk_dist(mx, my_, wx, wy), wr, cm);
+                            if (cmp_view(co, kOwn, cm, kOwn) < 0) win = o;
+                        }
+                    }
+                    const uint32_t b = bnd[win];
+                    int wbx, wby;
+                    bpos(b, sx, sy, wbx, wby);
+                    view_walk(b, walk_dist(wbx, wby, wx, wy), wr, x);
+                }
+            }
+            if (t == 0) emit(x, a->q_id[i]);
+        }
+        wave_sync();
+    }
+
     __device__ __forceinline__ void solve(uint32_t s_idx) {
-        const DevParams &p = a->p;
+        const DevParams &p = P;
         const uint32_t t = lane_id();
         const bool mine = t >= 1 && t <= p.NS;
         src = a->src_v[s_idx];
+        src_rk = rank[src];
         const int sx = int(src % p.S) - int(p.H), sy = int(src / p.S) - int(p.H);
-        const uint32_t ts = a->sinfo[src] & kNone10;
-        const uint32_t q0 = p.perm[0], q1 = p.perm[1], q2 = p.perm[2];
+        const uint32_t ts = sinfo[src] & kNone10;
         SpecialStatic ss{};
         if (mine) ss = sp[t];
         View my, st0;
@@ -1282,112 +1512,128 @@ struct HubSolver : Core<false> {
             r0.state = 2;
             bnd[0] = 0;
         }
-        if (mine) R[t].state = 0;
+        if (p.use_soe && t < nreg) {
+            const uint2 e = reinterpret_cast<const uint2 *>(a->near)[(unsigned long long)src * nreg + t];
+            srow[2 * t] = e.x;
+            srow[2 * t + 1] = e.y;
+        }
         wave_sync();
         if (mine) {
-            if (t == ts) improve_own(t, st, my, st0);
+            if (t == ts) improve_reg(true, st, my, st0);
             if (t == p.hq_t) {  // SHQ / SFm: only the source's own edges can be minimal
                 View c = st0;
                 c.m1 = p.shq_cost;
-                c.t0 = Cmd{kSHQ << 29, src, ss.v};
-                improve_own(t, st, my, c);
+                c.t0 = Cmd{kSHQ << 29, src_rk, ss.rk};
+                improve_reg(true, st, my, c);
             }
             if (p.use_sfm && t == 1) {
                 View c = st0;
                 c.m1 = p.sfm_cost;
-                c.t0 = Cmd{kSFm << 29, src, p.vc};
-                improve_own(t, st, my, c);
+                c.t0 = Cmd{kSFm << 29, src_rk, sp[1].rk};
+                improve_reg(true, st, my, c);
             }
         }
         uint32_t nb = 1;
-        if (src != p.vc) relax_boundary(0, sx, sy, t, mine, st, my, ss, bwh, b0, b1, b2);
+        MR_HSTAMP(3);
+        if (src != p.vc) {
+            View l0;
+            view_start(l0);
+            l0.len = 0;  // unused for b = 0 (walks from the source start the list)
+            relax_boundary(l0, 0, sx, sy, t, mine, st, my, ss, bwh, b0, b1, b2);
+        }
         wave_sync();
+        MR_HSTAMP(6);
+        MR_HCOUNT(0, 1);
         for (uint32_t it = 0; it <= p.NS; ++it) {
-            const bool tent = mine && st == 1;
-            const uint32_t a1 = q0 == 0 ? my.m0 : (q0 == 1 ? my.m1 : my.m2);
-            const uint32_t a2 = q1 == 0 ? my.m0 : (q1 == 1 ? my.m1 : my.m2);
-            const uint32_t a3 = q2 == 0 ? my.m0 : (q2 == 1 ? my.m1 : my.m2);
-            const unsigned long long k1 = tent ? (unsigned long long)a1 : kInf64;
-            const unsigned long long min1 = wave_min_u64(k1);
-            if (min1 == kInf64) break;
-            const bool c1 = tent && k1 == min1;
-            const unsigned long long k23 = c1 ? ((unsigned long long)a2 << 32 | a3) : kInf64;
-            const unsigned long long min23 = wave_min_u64(k23);
-            const bool top = c1 && k23 == min23;
-            const unsigned long long bal = __ballot(top);
-            uint32_t s;
-            if (__popcll(bal) == 1) {
-                s = uint32_t(__ffsll((long long)bal) - 1);
-            } else {
-                uint32_t m = top ? t : kNone32;
-#pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) {
-                    const uint32_t o = __shfl_xor(m, off, 64);
-                    if (o != kNone32 && (m == kNone32 || cmp_entries(o, m) < 0)) m = o;
-                }
-                s = m;
-            }
-            View ls;
-            view_rec(s, ls);
-            const SpecialStatic sS = sp[s];
+            const uint32_t s = select_reg(mine && st == 1, my);
+            if (s == kNone32) break;
+            MR_HCOUNT(1, 1);
+            const View ls = bcast(my, s);  // the settled label, from lane s's registers
+            SpecialStatic sS;
+            sS.x = int(bcast(uint32_t(ss.x), s));
+            sS.y = int(bcast(uint32_t(ss.y), s));
+            sS.flags = bcast(ss.flags, s);
+            sS.region = bcast(ss.region, s);
+            sS.rk = bcast(ss.rk, s);
             const Cmd last = ls.ntail == 2 ? ls.t1 : ls.t0;
             const uint32_t lk = last.kp >> 29;
             const bool boundary = lk != kNoMove && lk != kStandard;
             if (t == s) {
                 st = 2;
                 if (boundary && bwh && b0 == my.m0 && b1 == my.m1 && b2 == my.m2) tie = 1;
+                write_rec(s, my, 2);
             }
-            wave_sync();
-            if (t == 0) R[s].state = 2;
-            wave_sync();
-            if (mine && st != 2) {  // CentralMove / caravan / SoE edges s -> t
-                View c;
-                if (((sS.flags & kSpCenter) && (ss.flags & kSpBorder1)) ||
-                    ((sS.flags & kSpBorder1) && (ss.flags & kSpCenter))) {
-                    ext_view(ls, s, sS.v, kCentral, 1, 0, 10, ss.v, c);
-                    improve_own(t, st, my, c);
+            wave_sync();  // R[s] may be read by the list compares below
+            MR_HSTAMP(4);
+            {  // CentralMove / caravan / SoE edges s -> t (uniform tests on s skip whole edge kinds)
+                const bool live = mine && st != 2;
+                if (sS.flags & (kSpCenter | kSpBorder1)) {
+                    View c;
+                    ext_view(ls, s, sS.rk, kCentral, 1, 0, 10, ss.rk, c);
+                    const uint32_t want = (sS.flags & kSpCenter) ? kSpBorder1 : kSpCenter;
+                    improve_reg(live && (ss.flags & want), st, my, c);
                 }
-                if (p.use_caravans && (sS.flags & kSpHub) && (ss.flags & kSpHub)) {
+                if (p.use_caravans && (sS.flags & kSpHub)) {
+                    View c;
                     const uint32_t d = uint32_t(abs(sS.x - ss.x) + abs(sS.y - ss.y));
                     const uint32_t coef = ss.coef5 ? 5u : 2u;
-                    ext_view(ls, s, sS.v, kCaravan, (d << 1) | ss.coef5, coef * d, p.rgt * d, ss.v, c);
-                    improve_own(t, st, my, c);
+                    ext_view(ls, s, sS.rk, kCaravan, (d << 1) | ss.coef5, coef * d, p.rgt * d, ss.rk, c);
+                    improve_reg(live && (ss.flags & kSpHub), st, my, c);
                 }
-                if (p.use_soe && sS.region == t) {
-                    ext_view(ls, s, sS.v, kSoE, 0, p.soe_cost, 0, ss.v, c);
-                    improve_own(t, st, my, c);
+                if (p.use_soe && sS.region != kNone10 && sS.region != s) {
+                    View c;
+                    ext_view(ls, s, sS.rk, kSoE, 0, p.soe_cost, 0, ss.rk, c);
+                    improve_reg(live && sS.region == t, st, my, c);
                 }
             }
-            if (boundary && sS.v != p.vc) {  // a new walk source
-                relax_boundary(s, sS.x, sS.y, t, mine, st, my, ss, bwh, b0, b1, b2);
+            MR_HSTAMP(5);
+            if (boundary && s != 1) {  // a new walk source (entry 1, the Center, has no walks)
+                relax_boundary(ls, s, sS.x, sS.y, t, mine, st, my, ss, bwh, b0, b1, b2);
                 if (t == 0) bnd[nb] = s;
                 ++nb;
+                MR_HCOUNT(2, 1);
             }
             wave_sync();
+            MR_HSTAMP(6);
         }
+#ifdef MR_HUBDUMP
+        if (a->dbg && src == uint32_t(a->dbg_blocks)) {  // diagnostics: settled table of one source
+            unsigned int *d = reinterpret_cast<unsigned int *>(a->dbg);
+            const uint32_t *rw = reinterpret_cast<const uint32_t *>(&R[t]);
+            if (t <= p.NS)
+                for (int i = 0; i < 11; ++i) d[t * 16 + i] = rw[i];
+            d[t * 16 + 11] = st;
+            d[t * 16 + 12] = my.m0;
+            d[t * 16 + 13] = my.m1;
+            d[t * 16 + 14] = my.m2;
+            d[t * 16 + 15] = 0xABCD0000u | nb;
+        }
+#endif
         // An order-sensitive tie hands this source to the SSSP kernel.  No early
         // return: the wave must stay converged for the next dequeue's broadcast.
         const bool fallback = __any(tie != 0) || a->fb_all;
         if (fallback && t == 0) a->fb_list[atomicAdd(a->counter + 2, 1u)] = s_idx;
         const uint32_t qa = a->q_begin[s_idx], qb = fallback ? qa : a->q_begin[s_idx + 1];
-        for (uint32_t i = qa + t; i < qb; i += 64) {
+        if (qb - qa <= kEmitWaveMax) emit_wave(qa, qb, nb, sx, sy, st0);  // (no early return: see above)
+        else for (uint32_t i = qa + t; i < qb; i += 64) {
             const uint32_t w = a->q_dst[i];
             View x;
             if (w == src) {
                 x = st0;
             } else {
-                const uint32_t tw = a->sinfo[w] & kNone10;
+                const uint32_t tw = sinfo[w] & kNone10;
                 if (tw != kNone10) {
                     view_rec(tw, x);
                 } else {
                     const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
+                    const uint32_t wr = rank[w];
                     bool have = false;
                     for (uint32_t j = 0; j < nb; ++j) {
                         const uint32_t b = bnd[j];
                         if (vert_of(b) == p.vc) continue;
                         const int bx = b == 0 ? sx : sp[b].x, by = b == 0 ? sy : sp[b].y;
                         View c;
-                        view_walk(b, walk_dist(bx, by, wx, wy), w, c);
+                        view_walk(b, walk_dist(bx, by, wx, wy), wr, c);
                         if (!have || cmp_view(c, kOwn, x, kOwn) < 0) {
                             x = c;
                             have = true;
@@ -1398,15 +1644,16 @@ struct HubSolver : Core<false> {
             emit(x, a->q_id[i]);
         }
         wave_sync();
+        MR_HSTAMP(7);
     }
 };
 
 __host__ __device__ constexpr uint32_t align16h(uint32_t x) { return (x + 15u) & ~15u; }
 
 struct HubLayout {
-    uint32_t off_sp, off_hubs, off_R, off_bnd, rstride, bstride, total;
+    uint32_t off_sp, off_hubs, off_near, off_srow, off_R, off_bnd, rstride, bstride, sstride, total;
 };
-__host__ __device__ inline HubLayout hub_layout(uint32_t NS) {
+__host__ __device__ inline HubLayout hub_layout(uint32_t NS, uint32_t nreg) {
     HubLayout L{};
     const uint32_t T = NS + 1;
     uint32_t o = 0;
@@ -1414,6 +1661,11 @@ __host__ __device__ inline HubLayout hub_layout(uint32_t NS) {
     o = align16h(o + T * uint32_t(sizeof(SpecialStatic)));
     L.off_hubs = o;
     o = align16h(o + T * 2);
+    L.off_near = o;  // region rows of the specials (row 0 unused)
+    o = align16h(o + T * nreg * 8);
+    L.sstride = align16h(nreg * 8);
+    L.off_srow = o;  // per wave: the current source's region row
+    o += 4 * L.sstride;
     L.rstride = align16h(T * uint32_t(sizeof(Rec)));
     L.off_R = o;
     o += 4 * L.rstride;
@@ -1424,18 +1676,34 @@ __host__ __device__ inline HubLayout hub_layout(uint32_t NS) {
     return L;
 }
 
+// PERM = comparator order c1 c2 c3 as metric indices (9*c1 + 3*c2 + c3): a compile-time
+// constant here, so every metric selection and comparison folds.
+template <uint32_t PERM>
 __global__ __launch_bounds__(kBS) void hub_kernel(const KArgs *__restrict__ a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const uint32_t NS = a->p.NS;
-    const HubLayout L = hub_layout(NS);
+    const uint32_t NS = a->p.NS, nreg = a->nreg;
+    const HubLayout L = hub_layout(NS, nreg);
     SpecialStatic *spl = reinterpret_cast<SpecialStatic *>(smem + L.off_sp);
     uint16_t *hubl = reinterpret_cast<uint16_t *>(smem + L.off_hubs);
+    uint2 *nearl = reinterpret_cast<uint2 *>(smem + L.off_near);
     for (uint32_t t = threadIdx.x; t <= NS; t += kBS) spl[t] = a->sp[t];
     for (uint32_t h = threadIdx.x; h < a->p.n_hubs; h += kBS) hubl[h] = a->hubs[h];
+    for (uint32_t i = threadIdx.x; i < NS * nreg; i += kBS) {
+        const uint32_t t = 1 + i / nreg, r = i % nreg;
+        nearl[t * nreg + r] = reinterpret_cast<const uint2 *>(a->near)[(unsigned long long)a->sp[t].v * nreg + r];
+    }
     __syncthreads();
     const uint32_t wv = threadIdx.x >> 6;
     HubSolver H;
     H.a = a;
+    H.P = a->p;
+    H.P.perm[0] = PERM / 9;
+    H.P.perm[1] = (PERM / 3) % 3;
+    H.P.perm[2] = PERM % 3;
+    H.P.ff_num = H.P.ff_den = 1;  // the hub solver runs only with a linear run time
+    H.rank = a->rank;
+    H.sinfo = a->sinfo;
+    H.counter = a->counter;
     H.sh = nullptr;
     H.R = reinterpret_cast<Rec *>(smem + L.off_R + wv * L.rstride);
     H.state = nullptr;
@@ -1443,14 +1711,30 @@ __global__ __launch_bounds__(kBS) void hub_kernel(const KArgs *__restrict__ a) {
     H.hubs = hubl;
     H.dst = nullptr;
     H.src = 0;
+    H.src_rk = 0;
     H.bnd = reinterpret_cast<uint32_t *>(smem + L.off_bnd + wv * L.bstride);
+    H.nearS = reinterpret_cast<const uint32_t *>(smem + L.off_near);
+    H.srow = reinterpret_cast<uint32_t *>(smem + L.off_srow + wv * L.sstride);
+    H.nreg = nreg;
+#ifdef MR_STAMPS
+    H.hs_last = __builtin_amdgcn_s_memtime();
+#endif
     for (;;) {  // each wave dequeues its own sources
         uint32_t s = 0;
         if (lane_id() == 0) s = atomicAdd(a->counter, 1u);
         s = __shfl(s, 0, 64);
+#ifdef MR_STAMPS
+        H.hmark(8);
+#endif
         if (s >= a->nsrc) break;
         H.solve(s);
     }
+#ifdef MR_STAMPS
+    if (lane_id() == 0 && a->dbg) {
+        unsigned long long *h = a->dbg + (unsigned long long)a->dbg_blocks * 10;
+        for (int i = 0; i < 9; ++i) atomicAdd(h + i, H.hs[i]);
+    }
+#endif
 }
 
 // ===================================================================================
@@ -1513,6 +1797,8 @@ __device__ __forceinline__ uint32_t next_source(const KArgs *__restrict__ a) {
 template <bool G, class IdxT, uint32_t ALGO>
 __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    // fallback launch after the hub solver: nothing to do unless it listed sources
+    if (a->fb_mode && __hip_atomic_load(a->counter + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
     const uint32_t V = a->p.V, NS = a->p.NS;
     const LdsLayout L = lds_layout(NS, V, !G, ALGO);
     Shared *sh = reinterpret_cast<Shared *>(smem);
@@ -1542,6 +1828,10 @@ __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a)
     if constexpr (ALGO == kAlgoLegs) {
         LegsSolver<G, IdxT> S;
         S.a = a;
+        S.P = a->p;
+        S.rank = a->rank;
+        S.sinfo = a->sinfo;
+        S.counter = a->counter;
         S.sh = sh;
         S.R = R;
         S.state = state;
@@ -1549,6 +1839,7 @@ __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a)
         S.hubs = hubl;
         S.dst = dstl;
         S.src = 0;
+        S.src_rk = 0;
         S.F0 = l0;
         S.F1 = l1;
         S.best64 = reinterpret_cast<unsigned long long *>(smem + L.off_a);
@@ -1581,6 +1872,10 @@ __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a)
     } else {
         GenericSolver<G, IdxT> S;
         S.a = a;
+        S.P = a->p;
+        S.rank = a->rank;
+        S.sinfo = a->sinfo;
+        S.counter = a->counter;
         S.sh = sh;
         S.R = R;
         S.state = state;
@@ -1588,6 +1883,7 @@ __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a)
         S.hubs = hubl;
         S.dst = dstl;
         S.src = 0;
+        S.src_rk = 0;
         S.L0b = l0;
         S.lstride = uint32_t(l1 - l0);
         S.dirty = l3;
@@ -1628,19 +1924,34 @@ hipError_t launch_solve(const KArgs *d_args, bool grid_in_lds, uint32_t algo, ui
     return hipLaunchKernel(fn, dim3(blocks), dim3(kBS), args, bytes, stream);
 }
 
-uint32_t hub_lds_bytes(uint32_t NS) { return hub_layout(NS).total; }
+uint32_t hub_lds_bytes(uint32_t NS, uint32_t nreg) { return hub_layout(NS, nreg).total; }
 
-hipError_t launch_hub(const KArgs *d_args, uint32_t NS, uint32_t blocks, hipStream_t stream) {
-    const uint32_t bytes = hub_lds_bytes(NS);
-    const void *fn = reinterpret_cast<const void *>(&hub_kernel);
+static const void *hub_fn(const uint32_t perm[3]) {
+    switch (perm[0] * 9 + perm[1] * 3 + perm[2]) {
+        case 5: return reinterpret_cast<const void *>(&hub_kernel<5>);    // legs money time
+        case 7: return reinterpret_cast<const void *>(&hub_kernel<7>);    // legs time money
+        case 11: return reinterpret_cast<const void *>(&hub_kernel<11>);  // money legs time
+        case 15: return reinterpret_cast<const void *>(&hub_kernel<15>);  // money time legs
+        case 19: return reinterpret_cast<const void *>(&hub_kernel<19>);  // time legs money
+        case 21: return reinterpret_cast<const void *>(&hub_kernel<21>);  // time money legs
+        default: return nullptr;
+    }
+}
+
+hipError_t launch_hub(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t blocks,
+                      hipStream_t stream) {
+    const uint32_t bytes = hub_lds_bytes(NS, nreg);
+    const void *fn = hub_fn(perm);
+    if (!fn) return hipErrorInvalidValue;
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
     void *args[] = {const_cast<KArgs **>(&d_args)};
     return hipLaunchKernel(fn, dim3(blocks), dim3(kBS), args, bytes, stream);
 }
 
-int hub_blocks_per_cu(uint32_t bytes) {
+int hub_blocks_per_cu(const uint32_t perm[3], uint32_t bytes) {
     int n = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, hub_kernel, kBS, bytes);
+    const void *fn = hub_fn(perm);
+    if (fn) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kBS, bytes);
     return n;
 }
 

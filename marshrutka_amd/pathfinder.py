@@ -17,7 +17,7 @@ from typing import List, Optional, Sequence, Tuple
 
 from . import abi
 from .abi import (MR_ERR_CAPACITY, MR_NOT_FOUND, MR_OK, CellIndex, Params, TotalCost, cells_to_c,
-                  mr_cell, mr_cell_index, mr_command, mr_params, mr_query, mr_result, queries_to_c,
+                  mr_cell, mr_cell_index, mr_command, mr_params, mr_plan_stats, mr_query, mr_result, queries_to_c,
                   result_from_c)
 
 LIB_PATH = os.environ.get("MR_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
@@ -26,7 +26,7 @@ LIB_PATH = os.environ.get("MR_LIB_PATH") or os.path.join(os.path.dirname(os.path
 EXPORTED_SYMBOLS = [
     "mr_grid_create", "mr_grid_destroy", "mr_grid_square_size", "mr_params_default", "mr_find_path",
     "mr_find_path_batch", "mr_plan_create", "mr_plan_run", "mr_plan_fetch", "mr_plan_device_outputs",
-    "mr_plan_num_sources", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_plan_bind_outputs", "mr_abi_version", "mr_last_error",
+    "mr_plan_num_sources", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_plan_bind_outputs", "mr_abi_version", "mr_last_error",
     "mr_device_available",
 ]
 
@@ -73,6 +73,8 @@ def lib():
         L.mr_plan_bind_outputs.restype = C.c_int
         L.mr_plan_num_sources.argtypes = [vp]
         L.mr_plan_num_sources.restype = C.c_uint32
+        L.mr_plan_get_stats.argtypes = [vp, C.POINTER(mr_plan_stats)]
+        L.mr_plan_get_stats.restype = C.c_int
         L.mr_plan_kernel_ms.argtypes = [vp, C.POINTER(C.c_uint32)]
         L.mr_plan_kernel_ms.restype = C.c_double
         L.mr_plan_destroy.argtypes = [vp]
@@ -216,6 +218,15 @@ class Plan:
         if st != MR_OK:
             raise EngineError(st, last_error())
 
+    def stats(self) -> dict:
+        st = mr_plan_stats()
+        rc = lib().mr_plan_get_stats(self.handle, C.byref(st))
+        if rc != MR_OK:
+            raise EngineError(rc, last_error())
+        d = {f: getattr(st, f) for f, _ in mr_plan_stats._fields_}
+        d["solver"] = {0: "bucketed", 1: "levels", 2: "hub"}.get(st.solver, str(st.solver))
+        return d
+
     def kernel_ms(self) -> Tuple[float, int]:
         n = C.c_uint32()
         ms = lib().mr_plan_kernel_ms(self.handle, C.byref(n))
@@ -232,6 +243,16 @@ class Plan:
         st = lib().mr_plan_bind_outputs(self.handle, C.c_void_p(d_results), C.c_void_p(d_commands))
         if st != MR_OK:
             raise EngineError(st, last_error())
+
+    def fetch_raw(self):
+        """(results, command pool) as ctypes arrays, no Python label objects."""
+        res = (mr_result * max(self.n, 1))()
+        cap = max(1, self.n * 16)
+        pool = (mr_command * cap)()
+        st = lib().mr_plan_fetch(self.handle, res, pool, cap)
+        if st < 0 and st not in (abi.MR_ERR_INVALID_INDEX, MR_ERR_CAPACITY):
+            raise EngineError(st, last_error())
+        return res, pool
 
     def fetch(self) -> List[Optional[TotalCost]]:
         res = (mr_result * max(self.n, 1))()

@@ -130,6 +130,19 @@ def test_edge_cases(eng, oracle_lib):
         check(eng, oracle_lib, m, params, qs, f"edges {params}")
 
 
+@pytest.mark.parametrize("n_dst", [1, 31, 33, 225])
+def test_destinations_per_source(eng, oracle_lib, grid_state, n_dst):
+    """The hub solver reads destinations off one query at a time (few per source)
+    or one lane per query (many per source); both against the oracle."""
+    m = SyntheticMap(15, campfires_per_homeland=3, seed=11, clustered=True)
+    cells = m.all_indices()
+    rng = random.Random(n_dst)
+    srcs = rng.sample(cells, 6)
+    qs = [(a, b) for a in srcs for b in (cells if n_dst >= len(cells) else rng.sample(cells, n_dst))]
+    for params in (Params(), Params(sort_by=(SORT_TIME, SORT_LEGS)), Params(sort_by=(SORT_MONEY, SORT_TIME))):
+        check(eng, oracle_lib, m, params, qs, f"n_dst={n_dst} {params}")
+
+
 def test_invalid_queries_report_errors(eng):
     from marshrutka_amd.abi import MR_ERR_INVALID_INDEX, MR_OK
     m = SyntheticMap(7, campfires_per_homeland=1, seed=3)
