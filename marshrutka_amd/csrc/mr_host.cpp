@@ -23,10 +23,10 @@ uint32_t lds_bytes(uint32_t NS, uint32_t V, bool grid_in_lds, uint32_t algo);
 hipError_t launch_solve(const KArgs *d_args, bool grid_in_lds, uint32_t algo, uint32_t NS, uint32_t V,
                         uint32_t blocks, hipStream_t stream);
 int max_blocks_per_cu(bool grid_in_lds, uint32_t algo, uint32_t bytes);
-uint32_t hub_lds_bytes(uint32_t NS, uint32_t nreg);
-hipError_t launch_hub(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t blocks,
-                      hipStream_t stream);
-int hub_blocks_per_cu(const uint32_t perm[3], uint32_t bytes);
+uint32_t hub_lds_bytes(uint32_t NS, uint32_t nreg, uint32_t spw);
+hipError_t launch_hub(const KArgs *d_args, const uint32_t perm[3], uint32_t spw, uint32_t NS, uint32_t nreg,
+                      uint32_t blocks, hipStream_t stream);
+int hub_blocks_per_cu(const uint32_t perm[3], uint32_t spw, uint32_t bytes);
 }  // namespace mr
 
 
@@ -545,7 +545,7 @@ struct mr_plan {
     KArgs *d_args = nullptr;
     KArgs *d_args_fb = nullptr;           // SSSP launch over the hub solver's fallback list
     uint32_t *d_near = nullptr, *d_fb = nullptr;
-    uint32_t hub_blocks = 0, fb_blocks = 0;
+    uint32_t hub_blocks = 0, fb_blocks = 0, spw = 1;
     unsigned long long *d_dbg = nullptr;  // diagnostic builds: per-workgroup phase cycles
     uint32_t algo = kAlgoGeneric;
     SpecialStatic *d_sp = nullptr;
@@ -663,9 +663,15 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         ka.near = pl->d_near;
         ka.nreg = hp.nreg;
         ka.fb_list = pl->d_fb;
-        const uint32_t hb = hub_lds_bytes(NS, hp.nreg);
-        const int hper = std::max(1, hub_blocks_per_cu(hp.p.perm, hb));
-        pl->hub_blocks = uint32_t(std::min<uint64_t>((nsrc + 3) / 4, uint64_t(hper) * prop.multiProcessorCount));
+        // two sources per wave when the specials fit 32 lanes (MR_HUB_SPW=1 forces one)
+        pl->spw = NS + 1 <= 32 ? 2u : 1u;
+        if (const char *e = std::getenv("MR_HUB_SPW"))
+            if (std::atoi(e) == 1) pl->spw = 1;
+        const uint32_t hb = hub_lds_bytes(NS, hp.nreg, pl->spw);
+        const int hper = std::max(1, hub_blocks_per_cu(hp.p.perm, pl->spw, hb));
+        const uint64_t per_block = 4ull * pl->spw;
+        pl->hub_blocks = uint32_t(std::min<uint64_t>((nsrc + per_block - 1) / per_block,
+                                                     uint64_t(hper) * prop.multiProcessorCount));
         if (const char *e = std::getenv("MR_HUB_BLOCKS")) pl->hub_blocks = uint32_t(std::max(1, std::atoi(e)));
         pl->fb_blocks = pl->blocks;
         KArgs kf = ka;
@@ -715,7 +721,7 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     if (pl->hp.hub) {
         // closed-form hub solve for every source, then the SSSP kernel for the
         // sources it flagged (usually none; those workgroups exit at once)
-        e = launch_hub(pl->d_args, pl->ka.p.perm, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
+        e = launch_hub(pl->d_args, pl->ka.p.perm, pl->spw, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
         if (e == hipSuccess)
             e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, s);
     } else {

@@ -1299,10 +1299,46 @@ __device__ __forceinline__ uint32_t walk_dist(int ax, int ay, int bx, int by) {
     return d;
 }
 
+// Lanes are split into SPW segments of LPS = 64 / SPW lanes; segment h solves its
+// own source with lane t (within the segment) owning special t.  Per-source values
+// (source, settled special, boundary count) are segment-uniform per-lane values.
+template <uint32_t LPS>
+__device__ __forceinline__ uint32_t seg_min_u32(uint32_t x) {
+    x = dpp_min<0x111, 0xF>(x);  // row_shr:1
+    x = dpp_min<0x112, 0xF>(x);  // row_shr:2
+    x = dpp_min<0x114, 0xF>(x);  // row_shr:4
+    x = dpp_min<0x118, 0xF>(x);  // row_shr:8
+    x = dpp_min<0x142, 0xA>(x);  // row_bcast:15: lanes 31 and 63 hold the two 32-lane minima
+    if constexpr (LPS == 64) {
+        x = dpp_min<0x143, 0xC>(x);  // row_bcast:31
+        return bcast(x, 63);
+    } else {
+        const uint32_t lo = bcast(x, 31), hi = bcast(x, 63);
+        return lane_id() >= 32 ? hi : lo;
+    }
+}
+template <uint32_t LPS>
+__device__ __forceinline__ void narrow_seg(bool &c, uint32_t key) {
+    const uint32_t m = seg_min_u32<LPS>(c ? key : 0xFFFFFFFFu);
+    c = c && key == m;
+}
+// this lane's segment of a wave ballot
+template <uint32_t LPS>
+__device__ __forceinline__ unsigned long long seg_bits(unsigned long long bal) {
+    if constexpr (LPS == 64) return bal;
+    else return lane_id() >= 32 ? (bal >> 32) : (bal & 0xFFFFFFFFull);
+}
+template <uint32_t LPS>
+__device__ __forceinline__ uint32_t seg_max_u32(uint32_t x) {
+    return ~seg_min_u32<LPS>(~x);
+}
+
+template <uint32_t SPW>
 struct HubSolver : Core<false> {
-    uint32_t *bnd;          // this wave's boundary list (table indices; bnd[0] = 0, the source)
+    static constexpr uint32_t LPS = 64 / SPW;
+    uint32_t *bnd;          // LDS: this segment's boundary list (table indices; bnd[0] = 0, the source)
     const uint32_t *nearS;  // LDS: region rows {distance, rank} of every special (row t at t*2*nreg)
-    uint32_t *srow;         // LDS: this wave's region row of the current source
+    uint32_t *srow;         // LDS: this segment's region row of its source
     uint32_t nreg;
 #ifdef MR_STAMPS
     mutable unsigned long long hs_last = 0, hs[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1321,10 +1357,12 @@ struct HubSolver : Core<false> {
     do {                   \
     } while (0)
 #endif
+    __device__ __forceinline__ static uint32_t seg_lane() { return lane_id() % LPS; }
 
     // tentative labels live only in registers (lane t = special t); the LDS table
-    // receives a label when it settles (command chains and list compares read it)
-    // (the update is a per-field select, not a divergent block assignment)
+    // receives a label when it settles (command chains and list compares read it).
+    // The update is a per-field select under an explicit mask, never a divergent
+    // block assignment.
     __device__ __forceinline__ void improve_reg(bool active, uint32_t &st, View &my, const View &c) const {
         bool take = active && st != 2;
         if (take && st == 1) {
@@ -1347,52 +1385,55 @@ struct HubSolver : Core<false> {
         my.t1.to = take ? c.t1.to : my.t1.to;
         st = take ? 1u : st;
     }
-    // the settle candidate: smallest tentative label, resolved metric by metric on the
-    // DPP network with an exit as soon as one lane is left; exact ties of metrics and
-    // length publish the tied labels to the table and compare command lists
+    // Per segment, the settle candidate: the smallest tentative label, resolved
+    // metric by metric on the DPP network (exit once every segment has at most one
+    // lane left).  Exact ties of metrics and length publish the tied labels to the
+    // table and compare command lists.  Returns the segment lane, or kNone32.
     __device__ __forceinline__ uint32_t select_reg(bool c, const View &my) const {
-        unsigned long long bal = __ballot(c);
-        if (bal == 0) return kNone32;
         const DevParams &p = P;
+        unsigned long long m = seg_bits<LPS>(__ballot(c));
         const uint32_t keys[4] = {metric(my, p.perm[0]), metric(my, p.perm[1]), metric(my, p.perm[2]), my.len};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            if (__popcll(bal) == 1) return uint32_t(__ffsll((long long)bal) - 1);
-            narrow(c, keys[i]);
-            bal = __ballot(c);
+            if (__all(__popcll(m) <= 1)) break;
+            narrow_seg<LPS>(c, keys[i]);
+            m = seg_bits<LPS>(__ballot(c));
         }
-        if (__popcll(bal) == 1) return uint32_t(__ffsll((long long)bal) - 1);
-        const uint32_t t = lane_id();
-        if (c) write_rec(t, my, 1);
-        wave_sync();
-        uint32_t m = c ? t : kNone32;
+        uint32_t win = __popcll(m) == 1 ? uint32_t(__ffsll((long long)m) - 1) : kNone32;
+        if (__any(__popcll(m) > 1)) {
+            const bool tied = __popcll(m) > 1;
+            const uint32_t t = seg_lane();
+            if (tied && c) write_rec(t, my, 1);
+            wave_sync();
+            uint32_t mm = (tied && c) ? t : kNone32;
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const uint32_t o = __shfl_xor(m, off, 64);
-            if (o != kNone32 && (m == kNone32 || cmp_entries(o, m) < 0)) m = o;
+            for (int off = LPS / 2; off >= 1; off >>= 1) {
+                const uint32_t o = __shfl_xor(mm, off, 64);
+                if (o != kNone32 && (mm == kNone32 || cmp_entries(o, mm) < 0)) mm = o;
+            }
+            if (tied) win = mm;
         }
-        return m;
+        return win;
     }
-    __device__ __forceinline__ void note_walk(const View &c, uint32_t &bwh, uint32_t &b0, uint32_t &b1,
+    __device__ __forceinline__ void note_walk(bool on, const View &c, uint32_t &bwh, uint32_t &b0, uint32_t &b1,
                                               uint32_t &b2) const {
-        if (!bwh || cmp_metrics(c.m0, c.m1, c.m2, b0, b1, b2) < 0) {
-            bwh = 1;
-            b0 = c.m0;
-            b1 = c.m1;
-            b2 = c.m2;
-        }
+        const bool take = on && (!bwh || cmp_metrics(c.m0, c.m1, c.m2, b0, b1, b2) < 0);
+        bwh = take ? 1u : bwh;
+        b0 = take ? c.m0 : b0;
+        b1 = take ? c.m1 : b1;
+        b2 = take ? c.m2 : b2;
     }
     // walks and SoE-region edges from boundary b (label lb, at bx, by) into lane t's special
-    __device__ __forceinline__ void relax_boundary(const View &lb, uint32_t b, int bx, int by, uint32_t t, bool mine,
+    __device__ __forceinline__ void relax_boundary(bool live, const View &lb, uint32_t b, int bx, int by, uint32_t t,
                                                    uint32_t &st, View &my, const SpecialStatic &ss, uint32_t &bwh,
                                                    uint32_t &b0, uint32_t &b1, uint32_t &b2) const {
         const DevParams &p = P;
-        const bool live = mine && st != 2;
+        live = live && st != 2;
         {  // the walk: not into the Center (entry 1) nor b's own cell
             const bool on = live && t != 1 && t != b && !(b == 0 && ss.v == src);
             View c;
             view_walk_lab(lb, b, walk_dist(bx, by, ss.x, ss.y), ss.rk, c);
-            if (on) note_walk(c, bwh, b0, b1, b2);
+            note_walk(on, c, bwh, b0, b1, b2);
             improve_reg(on, st, my, c);
         }
         if (p.use_soe) {  // [Std{d} b->u, SoE u->c] from the region cell u nearest to b
@@ -1419,97 +1460,121 @@ struct HubSolver : Core<false> {
         }
     }
 
-    // Few destinations: one query at a time, lane j evaluating boundary j's walk,
-    // the winner picked on the DPP network (exact metric + length ties: full compare).
-    static constexpr uint32_t kEmitWaveMax = 32;
     __device__ __forceinline__ void bpos(uint32_t b, int sx, int sy, int &bx, int &by) const {
         bx = b == 0 ? sx : sp[b].x;
         by = b == 0 ? sy : sp[b].y;
     }
-    __device__ __forceinline__ void emit_wave(uint32_t qa, uint32_t qb, uint32_t nb, int sx, int sy,
-                                              const View &st0) const {
+    // the walk label of plain w from boundary b
+    __device__ __forceinline__ void walk_to(uint32_t b, int sx, int sy, int wx, int wy, uint32_t wr, View &x) const {
+        int bx, by;
+        bpos(b, sx, sy, bx, by);
+        view_walk(b, walk_dist(bx, by, wx, wy), wr, x);
+    }
+    // label of destination w (not the source, not a special) by a serial scan of the boundaries
+    __device__ __forceinline__ void plain_label_serial(uint32_t w, uint32_t nb, int sx, int sy, View &x) const {
         const DevParams &p = P;
-        const uint32_t t = lane_id();
+        const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
+        const uint32_t wr = rank[w];
+        bool have = false;
+        for (uint32_t j = 0; j < nb; ++j) {
+            const uint32_t b = bnd[j];
+            if (vert_of(b) == p.vc) continue;
+            View c;
+            walk_to(b, sx, sy, wx, wy, wr, c);
+            if (!have || cmp_view(c, kOwn, x, kOwn) < 0) {
+                x = c;
+                have = true;
+            }
+        }
+    }
+
+    // Destinations.  A segment with few (<= kEmitWaveMax) takes them one at a time,
+    // lane j evaluating boundary j's walk and the winner picked on the DPP network
+    // (exact metric + length ties: full compare); one with many gives each lane a query.
+    static constexpr uint32_t kEmitWaveMax = 32;
+    __device__ __forceinline__ void emit_all(uint32_t qa, uint32_t qb, uint32_t nb, int sx, int sy,
+                                             const View &st0) const {
+        const DevParams &p = P;
+        const uint32_t t = seg_lane();
+        const uint32_t nq = qb - qa;
+        const bool few = nq <= kEmitWaveMax;
+        const uint32_t trip = seg_max_u32<64>(few ? nq : 0u);  // wave-uniform trip count
         const uint32_t bj = t < nb ? bnd[t] : 0u;
         const bool usable = t < nb && vert_of(bj) != p.vc;
         int bx, by;
         bpos(bj, sx, sy, bx, by);
-        for (uint32_t i = qa; i < qb; ++i) {
+        for (uint32_t i = 0; i < trip; ++i) {
+            const bool qon = few && i < nq;
+            const uint32_t qi = qa + (qon ? i : 0u);
+            const uint32_t w = qon ? a->q_dst[qi] : src;
+            const uint32_t tw = sinfo[w] & kNone10;
+            const bool plain = qon && w != src && tw == kNone10;
+            const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
+            const uint32_t wr = rank[w];
+            View c;
+            view_walk(bj, walk_dist(bx, by, wx, wy), wr, c);
+            bool cand = usable && plain;
+            narrow_seg<LPS>(cand, metric(c, p.perm[0]));
+            narrow_seg<LPS>(cand, metric(c, p.perm[1]));
+            narrow_seg<LPS>(cand, metric(c, p.perm[2]));
+            narrow_seg<LPS>(cand, c.len);
+            const unsigned long long m = seg_bits<LPS>(__ballot(cand));
+            uint32_t win = __popcll(m) >= 1 ? uint32_t(__ffsll((long long)m) - 1) : 0u;
+            if (__any(__popcll(m) > 1)) {  // equal metrics and length: compare the command lists
+                const bool tied = __popcll(m) > 1;
+                uint32_t mm = (tied && cand) ? t : kNone32;
+#pragma unroll
+                for (int off = LPS / 2; off >= 1; off >>= 1) {
+                    const uint32_t o = __shfl_xor(mm, off, 64);
+                    if (o == kNone32) continue;
+                    if (mm == kNone32) {
+                        mm = o;
+                        continue;
+                    }
+                    View co, cm;
+                    walk_to(bnd[o], sx, sy, wx, wy, wr, co);
+                    walk_to(bnd[mm], sx, sy, wx, wy, wr, cm);
+                    if (cmp_view(co, kOwn, cm, kOwn) < 0) mm = o;
+                }
+                if (tied) win = mm;
+            }
+            View x;
+            if (plain) walk_to(bnd[win], sx, sy, wx, wy, wr, x);
+            else if (w == src) x = st0;
+            else view_rec(tw, x);
+            if (qon && t == 0) emit(x, a->q_id[qi]);
+        }
+        for (uint32_t i = qa + t; !few && i < qb; i += LPS) {
             const uint32_t w = a->q_dst[i];
             View x;
-            if (w == src) {
-                x = st0;
-            } else {
-                const uint32_t tw = sinfo[w] & kNone10;
-                if (tw != kNone10) {
-                    view_rec(tw, x);
-                } else {
-                    const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
-                    const uint32_t wr = rank[w];
-                    View c;
-                    view_walk(bj, walk_dist(bx, by, wx, wy), wr, c);
-                    bool cand = usable;
-                    narrow(cand, metric(c, p.perm[0]));
-                    narrow(cand, metric(c, p.perm[1]));
-                    narrow(cand, metric(c, p.perm[2]));
-                    narrow(cand, c.len);
-                    const unsigned long long bal = __ballot(cand);
-                    uint32_t win;
-                    if (__popcll(bal) == 1) {
-                        win = uint32_t(__ffsll((long long)bal) - 1);
-                    } else {  // equal metrics and length: compare the command lists
-                        win = cand ? t : kNone32;
-#pragma unroll
-                        for (int off = 32; off >= 1; off >>= 1) {
-                            const uint32_t o = __shfl_xor(win, off, 64);
-                            if (o == kNone32) continue;
-                            if (win == kNone32) {
-                                win = o;
-                                continue;
-                            }
-                            const uint32_t bo = bnd[o], bm = bnd[win];
-                            int ox, oy, mx, my_;
-                            bpos(bo, sx, sy, ox, oy);
-                            bpos(bm, sx, sy, mx, my_);
-                            View co, cm;
-                            view_walk(bo, walk_dist(ox, oy, wx, wy), wr, co);
-                            view_walk(bm, walk_dist(mx, my_, wx, wy), wr, cm);
-                            if (cmp_view(co, kOwn, cm, kOwn) < 0) win = o;
-                        }
-                    }
-                    const uint32_t b = bnd[win];
-                    int wbx, wby;
-                    bpos(b, sx, sy, wbx, wby);
-                    view_walk(b, walk_dist(wbx, wby, wx, wy), wr, x);
-                }
-            }
-            if (t == 0) emit(x, a->q_id[i]);
+            const uint32_t tw = sinfo[w] & kNone10;
+            if (w == src) x = st0;
+            else if (tw != kNone10) view_rec(tw, x);
+            else plain_label_serial(w, nb, sx, sy, x);
+            emit(x, a->q_id[i]);
         }
         wave_sync();
     }
 
-    __device__ __forceinline__ void solve(uint32_t s_idx) {
+    // Segment h solves source base + h (none past the end).
+    __device__ __forceinline__ void solve(uint32_t base) {
         const DevParams &p = P;
-        const uint32_t t = lane_id();
-        const bool mine = t >= 1 && t <= p.NS;
-        src = a->src_v[s_idx];
+        const uint32_t t = seg_lane();
+        const uint32_t s_idx = base + lane_id() / LPS;
+        const bool have = s_idx < a->nsrc;
+        const uint32_t si = have ? s_idx : base;
+        const bool mine = have && t >= 1 && t <= p.NS;
+        src = a->src_v[si];
         src_rk = rank[src];
         const int sx = int(src % p.S) - int(p.H), sy = int(src / p.S) - int(p.H);
         const uint32_t ts = sinfo[src] & kNone10;
-        SpecialStatic ss{};
-        if (mine) ss = sp[t];
+        const SpecialStatic ss = sp[t <= p.NS ? t : 0u];
         View my, st0;
         view_start(st0);
         my = st0;
         uint32_t st = 0, bwh = 0, b0 = 0, b1 = 0, b2 = 0, tie = 0;
         if (t == 0) {
-            Rec &r0 = R[0];
-            r0.m[0] = r0.m[1] = r0.m[2] = 0;
-            r0.len = 1;
-            r0.ntail = 1;
-            r0.parent = 0;
-            r0.tail[0] = st0.t0;
-            r0.state = 2;
+            write_rec(0, st0, 2);
             bnd[0] = 0;
         }
         if (p.use_soe && t < nreg) {
@@ -1518,86 +1583,83 @@ struct HubSolver : Core<false> {
             srow[2 * t + 1] = e.y;
         }
         wave_sync();
-        if (mine) {
-            if (t == ts) improve_reg(true, st, my, st0);
-            if (t == p.hq_t) {  // SHQ / SFm: only the source's own edges can be minimal
-                View c = st0;
-                c.m1 = p.shq_cost;
-                c.t0 = Cmd{kSHQ << 29, src_rk, ss.rk};
-                improve_reg(true, st, my, c);
-            }
-            if (p.use_sfm && t == 1) {
-                View c = st0;
-                c.m1 = p.sfm_cost;
-                c.t0 = Cmd{kSFm << 29, src_rk, sp[1].rk};
-                improve_reg(true, st, my, c);
-            }
+        improve_reg(mine && t == ts, st, my, st0);
+        {  // SHQ / SFm: only the source's own edges can be minimal
+            View c = st0;
+            c.m1 = p.shq_cost;
+            c.t0 = Cmd{kSHQ << 29, src_rk, ss.rk};
+            improve_reg(mine && t == p.hq_t, st, my, c);
+            c.m1 = p.sfm_cost;
+            c.t0 = Cmd{kSFm << 29, src_rk, sp[1].rk};
+            improve_reg(mine && p.use_sfm && t == 1, st, my, c);
         }
         uint32_t nb = 1;
         MR_HSTAMP(3);
-        if (src != p.vc) {
+        {
             View l0;
             view_start(l0);
             l0.len = 0;  // unused for b = 0 (walks from the source start the list)
-            relax_boundary(l0, 0, sx, sy, t, mine, st, my, ss, bwh, b0, b1, b2);
+            relax_boundary(mine && src != p.vc, l0, 0, sx, sy, t, st, my, ss, bwh, b0, b1, b2);
         }
         wave_sync();
         MR_HSTAMP(6);
         MR_HCOUNT(0, 1);
         for (uint32_t it = 0; it <= p.NS; ++it) {
             const uint32_t s = select_reg(mine && st == 1, my);
-            if (s == kNone32) break;
+            if (__all(s == kNone32)) break;
             MR_HCOUNT(1, 1);
-            const View ls = bcast(my, s);  // the settled label, from lane s's registers
-            SpecialStatic sS;
-            sS.x = int(bcast(uint32_t(ss.x), s));
-            sS.y = int(bcast(uint32_t(ss.y), s));
-            sS.flags = bcast(ss.flags, s);
-            sS.region = bcast(ss.region, s);
-            sS.rk = bcast(ss.rk, s);
-            const Cmd last = ls.ntail == 2 ? ls.t1 : ls.t0;
-            const uint32_t lk = last.kp >> 29;
-            const bool boundary = lk != kNoMove && lk != kStandard;
-            if (t == s) {
+            const bool act = s != kNone32;  // this segment settles a special
+            const uint32_t sc = act ? s : 0u;
+            if (act && t == s) {
                 st = 2;
-                if (boundary && bwh && b0 == my.m0 && b1 == my.m1 && b2 == my.m2) tie = 1;
                 write_rec(s, my, 2);
             }
-            wave_sync();  // R[s] may be read by the list compares below
+            wave_sync();
+            View ls;  // the settled label, from the table
+            view_rec(sc, ls);
+            const SpecialStatic sS = sp[sc];
+            const Cmd last = ls.ntail == 2 ? ls.t1 : ls.t0;
+            const uint32_t lk = last.kp >> 29;
+            const bool boundary = act && lk != kNoMove && lk != kStandard;
+            if (act && t == s && boundary && bwh && b0 == my.m0 && b1 == my.m1 && b2 == my.m2) tie = 1;
             MR_HSTAMP(4);
-            {  // CentralMove / caravan / SoE edges s -> t (uniform tests on s skip whole edge kinds)
-                const bool live = mine && st != 2;
-                if (sS.flags & (kSpCenter | kSpBorder1)) {
+            {  // CentralMove / caravan / SoE edges s -> t (skipped when no segment needs an edge kind)
+                const bool live = mine && act && st != 2;
+                const bool central_s = act && (sS.flags & (kSpCenter | kSpBorder1));
+                if (__any(central_s)) {
                     View c;
-                    ext_view(ls, s, sS.rk, kCentral, 1, 0, 10, ss.rk, c);
+                    ext_view(ls, sc, sS.rk, kCentral, 1, 0, 10, ss.rk, c);
                     const uint32_t want = (sS.flags & kSpCenter) ? kSpBorder1 : kSpCenter;
-                    improve_reg(live && (ss.flags & want), st, my, c);
+                    improve_reg(live && central_s && (ss.flags & want), st, my, c);
                 }
-                if (p.use_caravans && (sS.flags & kSpHub)) {
+                const bool hub_s = act && p.use_caravans && (sS.flags & kSpHub);
+                if (__any(hub_s)) {
                     View c;
                     const uint32_t d = uint32_t(abs(sS.x - ss.x) + abs(sS.y - ss.y));
                     const uint32_t coef = ss.coef5 ? 5u : 2u;
-                    ext_view(ls, s, sS.rk, kCaravan, (d << 1) | ss.coef5, coef * d, p.rgt * d, ss.rk, c);
-                    improve_reg(live && (ss.flags & kSpHub), st, my, c);
+                    ext_view(ls, sc, sS.rk, kCaravan, (d << 1) | ss.coef5, coef * d, p.rgt * d, ss.rk, c);
+                    improve_reg(live && hub_s && (ss.flags & kSpHub), st, my, c);
                 }
-                if (p.use_soe && sS.region != kNone10 && sS.region != s) {
+                const bool soe_s = act && p.use_soe && sS.region != kNone10 && sS.region != sc;
+                if (__any(soe_s)) {
                     View c;
-                    ext_view(ls, s, sS.rk, kSoE, 0, p.soe_cost, 0, ss.rk, c);
-                    improve_reg(live && sS.region == t, st, my, c);
+                    ext_view(ls, sc, sS.rk, kSoE, 0, p.soe_cost, 0, ss.rk, c);
+                    improve_reg(live && soe_s && sS.region == t, st, my, c);
                 }
             }
             MR_HSTAMP(5);
-            if (boundary && s != 1) {  // a new walk source (entry 1, the Center, has no walks)
-                relax_boundary(ls, s, sS.x, sS.y, t, mine, st, my, ss, bwh, b0, b1, b2);
-                if (t == 0) bnd[nb] = s;
-                ++nb;
+            const bool walks = boundary && sc != 1;  // a new walk source (entry 1, the Center, has none)
+            if (__any(walks)) {
+                relax_boundary(mine && walks, ls, sc, sS.x, sS.y, t, st, my, ss, bwh, b0, b1, b2);
+                if (walks && t == 0) bnd[nb] = sc;
+                nb += walks ? 1u : 0u;
                 MR_HCOUNT(2, 1);
             }
             wave_sync();
             MR_HSTAMP(6);
         }
 #ifdef MR_HUBDUMP
-        if (a->dbg && src == uint32_t(a->dbg_blocks)) {  // diagnostics: settled table of one source
+        if (a->dbg && have && src == uint32_t(a->dbg_blocks)) {  // diagnostics: settled table of one source
             unsigned int *d = reinterpret_cast<unsigned int *>(a->dbg);
             const uint32_t *rw = reinterpret_cast<const uint32_t *>(&R[t]);
             if (t <= p.NS)
@@ -1609,53 +1671,25 @@ struct HubSolver : Core<false> {
             d[t * 16 + 15] = 0xABCD0000u | nb;
         }
 #endif
-        // An order-sensitive tie hands this source to the SSSP kernel.  No early
+        // An order-sensitive tie hands the source to the SSSP kernel.  No early
         // return: the wave must stay converged for the next dequeue's broadcast.
-        const bool fallback = __any(tie != 0) || a->fb_all;
-        if (fallback && t == 0) a->fb_list[atomicAdd(a->counter + 2, 1u)] = s_idx;
-        const uint32_t qa = a->q_begin[s_idx], qb = fallback ? qa : a->q_begin[s_idx + 1];
-        if (qb - qa <= kEmitWaveMax) emit_wave(qa, qb, nb, sx, sy, st0);  // (no early return: see above)
-        else for (uint32_t i = qa + t; i < qb; i += 64) {
-            const uint32_t w = a->q_dst[i];
-            View x;
-            if (w == src) {
-                x = st0;
-            } else {
-                const uint32_t tw = sinfo[w] & kNone10;
-                if (tw != kNone10) {
-                    view_rec(tw, x);
-                } else {
-                    const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
-                    const uint32_t wr = rank[w];
-                    bool have = false;
-                    for (uint32_t j = 0; j < nb; ++j) {
-                        const uint32_t b = bnd[j];
-                        if (vert_of(b) == p.vc) continue;
-                        const int bx = b == 0 ? sx : sp[b].x, by = b == 0 ? sy : sp[b].y;
-                        View c;
-                        view_walk(b, walk_dist(bx, by, wx, wy), wr, c);
-                        if (!have || cmp_view(c, kOwn, x, kOwn) < 0) {
-                            x = c;
-                            have = true;
-                        }
-                    }
-                }
-            }
-            emit(x, a->q_id[i]);
-        }
-        wave_sync();
+        const bool fallback = have && (seg_bits<LPS>(__ballot(tie != 0)) != 0 || a->fb_all);
+        if (fallback && t == 0) a->fb_list[atomicAdd(counter + 2, 1u)] = s_idx;
+        const uint32_t qa = a->q_begin[si], qb = (!have || fallback) ? qa : a->q_begin[si + 1];
+        emit_all(qa, qb, nb, sx, sy, st0);
         MR_HSTAMP(7);
     }
 };
 
 __host__ __device__ constexpr uint32_t align16h(uint32_t x) { return (x + 15u) & ~15u; }
 
+// per-source LDS slots: 4 waves x SPW segments
 struct HubLayout {
     uint32_t off_sp, off_hubs, off_near, off_srow, off_R, off_bnd, rstride, bstride, sstride, total;
 };
-__host__ __device__ inline HubLayout hub_layout(uint32_t NS, uint32_t nreg) {
+__host__ __device__ inline HubLayout hub_layout(uint32_t NS, uint32_t nreg, uint32_t spw) {
     HubLayout L{};
-    const uint32_t T = NS + 1;
+    const uint32_t T = NS + 1, slots = 4 * spw;
     uint32_t o = 0;
     L.off_sp = o;
     o = align16h(o + T * uint32_t(sizeof(SpecialStatic)));
@@ -1664,25 +1698,25 @@ __host__ __device__ inline HubLayout hub_layout(uint32_t NS, uint32_t nreg) {
     L.off_near = o;  // region rows of the specials (row 0 unused)
     o = align16h(o + T * nreg * 8);
     L.sstride = align16h(nreg * 8);
-    L.off_srow = o;  // per wave: the current source's region row
-    o += 4 * L.sstride;
+    L.off_srow = o;  // per slot: its source's region row
+    o += slots * L.sstride;
     L.rstride = align16h(T * uint32_t(sizeof(Rec)));
     L.off_R = o;
-    o += 4 * L.rstride;
+    o += slots * L.rstride;
     L.bstride = align16h((T + 1) * 4);
     L.off_bnd = o;
-    o += 4 * L.bstride;
+    o += slots * L.bstride;
     L.total = o;
     return L;
 }
 
 // PERM = comparator order c1 c2 c3 as metric indices (9*c1 + 3*c2 + c3): a compile-time
-// constant here, so every metric selection and comparison folds.
-template <uint32_t PERM>
-__global__ __launch_bounds__(kBS) void hub_kernel(const KArgs *__restrict__ a) {
+// constant here, so every metric selection and comparison folds.  SPW = sources per wave.
+template <uint32_t PERM, uint32_t SPW>
+__global__ __launch_bounds__(kBS, 5) void hub_kernel(const KArgs *__restrict__ a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint32_t NS = a->p.NS, nreg = a->nreg;
-    const HubLayout L = hub_layout(NS, nreg);
+    const HubLayout L = hub_layout(NS, nreg, SPW);
     SpecialStatic *spl = reinterpret_cast<SpecialStatic *>(smem + L.off_sp);
     uint16_t *hubl = reinterpret_cast<uint16_t *>(smem + L.off_hubs);
     uint2 *nearl = reinterpret_cast<uint2 *>(smem + L.off_near);
@@ -1693,8 +1727,8 @@ __global__ __launch_bounds__(kBS) void hub_kernel(const KArgs *__restrict__ a) {
         nearl[t * nreg + r] = reinterpret_cast<const uint2 *>(a->near)[(unsigned long long)a->sp[t].v * nreg + r];
     }
     __syncthreads();
-    const uint32_t wv = threadIdx.x >> 6;
-    HubSolver H;
+    const uint32_t slot = (threadIdx.x >> 6) * SPW + lane_id() / (64 / SPW);
+    HubSolver<SPW> H;
     H.a = a;
     H.P = a->p;
     H.P.perm[0] = PERM / 9;
@@ -1705,29 +1739,29 @@ __global__ __launch_bounds__(kBS) void hub_kernel(const KArgs *__restrict__ a) {
     H.sinfo = a->sinfo;
     H.counter = a->counter;
     H.sh = nullptr;
-    H.R = reinterpret_cast<Rec *>(smem + L.off_R + wv * L.rstride);
+    H.R = reinterpret_cast<Rec *>(smem + L.off_R + slot * L.rstride);
     H.state = nullptr;
     H.sp = spl;
     H.hubs = hubl;
     H.dst = nullptr;
     H.src = 0;
     H.src_rk = 0;
-    H.bnd = reinterpret_cast<uint32_t *>(smem + L.off_bnd + wv * L.bstride);
+    H.bnd = reinterpret_cast<uint32_t *>(smem + L.off_bnd + slot * L.bstride);
     H.nearS = reinterpret_cast<const uint32_t *>(smem + L.off_near);
-    H.srow = reinterpret_cast<uint32_t *>(smem + L.off_srow + wv * L.sstride);
+    H.srow = reinterpret_cast<uint32_t *>(smem + L.off_srow + slot * L.sstride);
     H.nreg = nreg;
 #ifdef MR_STAMPS
     H.hs_last = __builtin_amdgcn_s_memtime();
 #endif
-    for (;;) {  // each wave dequeues its own sources
-        uint32_t s = 0;
-        if (lane_id() == 0) s = atomicAdd(a->counter, 1u);
-        s = __shfl(s, 0, 64);
+    for (;;) {  // each wave dequeues SPW sources at a time
+        uint32_t base = 0;
+        if (lane_id() == 0) base = atomicAdd(a->counter, SPW);
+        base = __shfl(base, 0, 64);
 #ifdef MR_STAMPS
         H.hmark(8);
 #endif
-        if (s >= a->nsrc) break;
-        H.solve(s);
+        if (base >= a->nsrc) break;
+        H.solve(base);
     }
 #ifdef MR_STAMPS
     if (lane_id() == 0 && a->dbg) {
@@ -1924,33 +1958,38 @@ hipError_t launch_solve(const KArgs *d_args, bool grid_in_lds, uint32_t algo, ui
     return hipLaunchKernel(fn, dim3(blocks), dim3(kBS), args, bytes, stream);
 }
 
-uint32_t hub_lds_bytes(uint32_t NS, uint32_t nreg) { return hub_layout(NS, nreg).total; }
+uint32_t hub_lds_bytes(uint32_t NS, uint32_t nreg, uint32_t spw) { return hub_layout(NS, nreg, spw).total; }
 
-static const void *hub_fn(const uint32_t perm[3]) {
-    switch (perm[0] * 9 + perm[1] * 3 + perm[2]) {
-        case 5: return reinterpret_cast<const void *>(&hub_kernel<5>);    // legs money time
-        case 7: return reinterpret_cast<const void *>(&hub_kernel<7>);    // legs time money
-        case 11: return reinterpret_cast<const void *>(&hub_kernel<11>);  // money legs time
-        case 15: return reinterpret_cast<const void *>(&hub_kernel<15>);  // money time legs
-        case 19: return reinterpret_cast<const void *>(&hub_kernel<19>);  // time legs money
-        case 21: return reinterpret_cast<const void *>(&hub_kernel<21>);  // time money legs
+template <uint32_t SPW>
+static const void *hub_fn_spw(uint32_t perm) {
+    switch (perm) {
+        case 5: return reinterpret_cast<const void *>(&hub_kernel<5, SPW>);    // legs money time
+        case 7: return reinterpret_cast<const void *>(&hub_kernel<7, SPW>);    // legs time money
+        case 11: return reinterpret_cast<const void *>(&hub_kernel<11, SPW>);  // money legs time
+        case 15: return reinterpret_cast<const void *>(&hub_kernel<15, SPW>);  // money time legs
+        case 19: return reinterpret_cast<const void *>(&hub_kernel<19, SPW>);  // time legs money
+        case 21: return reinterpret_cast<const void *>(&hub_kernel<21, SPW>);  // time money legs
         default: return nullptr;
     }
 }
+static const void *hub_fn(const uint32_t perm[3], uint32_t spw) {
+    const uint32_t k = perm[0] * 9 + perm[1] * 3 + perm[2];
+    return spw == 2 ? hub_fn_spw<2>(k) : hub_fn_spw<1>(k);
+}
 
-hipError_t launch_hub(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t blocks,
-                      hipStream_t stream) {
-    const uint32_t bytes = hub_lds_bytes(NS, nreg);
-    const void *fn = hub_fn(perm);
+hipError_t launch_hub(const KArgs *d_args, const uint32_t perm[3], uint32_t spw, uint32_t NS, uint32_t nreg,
+                      uint32_t blocks, hipStream_t stream) {
+    const uint32_t bytes = hub_lds_bytes(NS, nreg, spw);
+    const void *fn = hub_fn(perm, spw);
     if (!fn) return hipErrorInvalidValue;
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
     void *args[] = {const_cast<KArgs **>(&d_args)};
     return hipLaunchKernel(fn, dim3(blocks), dim3(kBS), args, bytes, stream);
 }
 
-int hub_blocks_per_cu(const uint32_t perm[3], uint32_t bytes) {
+int hub_blocks_per_cu(const uint32_t perm[3], uint32_t spw, uint32_t bytes) {
     int n = 0;
-    const void *fn = hub_fn(perm);
+    const void *fn = hub_fn(perm, spw);
     if (fn) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kBS, bytes);
     return n;
 }

@@ -23,11 +23,13 @@ def eng():
     return pathfinder
 
 
-@pytest.fixture(params=["auto-lds", "auto-hbm", "fallback-lds", "fallback-hbm", "sssp-lds", "sssp-hbm",
+@pytest.fixture(params=["auto-lds", "auto-hbm", "hub1-lds", "fallback-lds", "fallback-hbm", "sssp-lds", "sssp-hbm",
                         "generic-lds", "generic-hbm"])
 def grid_state(request, monkeypatch):
     """Every solver path x both grid-state regimes:
-    auto     — hub solver when the run time is linear, else the SSSP solvers
+    auto     — hub solver when the run time is linear (two sources per wave when
+               the specials fit 32 lanes), else the SSSP solvers
+    hub1     — hub solver with one source per wave
     fallback — hub solver handing every source to the SSSP kernel
     sssp     — no hub solver (level-synchronous solver for Legs-first orders)
     generic  — the bucketed solver for every order."""
@@ -35,6 +37,9 @@ def grid_state(request, monkeypatch):
     monkeypatch.setenv("MR_GRID_STATE", state)
     monkeypatch.delenv("MR_ALGO", raising=False)
     monkeypatch.delenv("MR_HUB_FALLBACK_ALL", raising=False)
+    monkeypatch.delenv("MR_HUB_SPW", raising=False)
+    if algo == "hub1":
+        monkeypatch.setenv("MR_HUB_SPW", "1")
     if algo in ("sssp", "generic"):
         monkeypatch.setenv("MR_ALGO", algo)
     if algo == "fallback":
