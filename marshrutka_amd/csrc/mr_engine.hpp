@@ -109,7 +109,7 @@ struct KArgs {
     OutResult *out_res;          // per query id
     OutCmd *out_cmd;             // per query id * max_cmds
     uint32_t *ws;                // grid-in-HBM mode: per-workgroup slots of 5*V words
-    uint32_t *counter;           // [0] source dequeue, [1] error flags, [2] fallback count, [3] fallback dequeue
+    uint32_t *counter;           // kCtr* words (below)
     uint32_t nsrc;
     uint32_t early_exit_max;     // early exit if a source has <= this many destinations (<= 64)
     uint32_t grid_in_lds;        // 1: grid state in LDS, 0: per-workgroup HBM slots
@@ -123,6 +123,20 @@ struct KArgs {
     uint32_t fb_mode;            // 1: this SSSP launch solves fb_list[counter[3]++] only
     uint32_t fb_all;             // tests: the hub solver hands every source to the SSSP kernel
     uint32_t dbg_blocks;         // diagnostic builds: SSSP workgroups (hub stamps follow their slots)
+    uint32_t last_launch;        // 1: the pass's last kernel; its last workgroup resets the counters
+};
+// counter words: the pass's last workgroup copies the fallback and written counts
+// to their "last" slots and zeroes the rest, so no memset precedes a pass
+enum : uint32_t {
+    kCtrDequeue = 0,      // SSSP source dequeue
+    kCtrFlags = 1,        // error flags (sticky until the host collects them)
+    kCtrFbCount = 2,      // sources the hub solver handed to the SSSP kernel
+    kCtrFbDequeue = 3,    // fallback dequeue
+    kCtrLastFb = 4,       // kCtrFbCount of the last completed pass
+    kCtrDone = 5,         // workgroups of the last kernel that finished
+    kCtrWritten = 6,      // result records written
+    kCtrLastWritten = 7,  // kCtrWritten of the last completed pass
+    kCtrWords = 8
 };
 enum : uint32_t { kAlgoGeneric = 0, kAlgoLegs = 1 };
 

@@ -544,6 +544,9 @@ struct mr_plan {
              *d_qd = nullptr, *d_qi = nullptr;
     KArgs *d_args = nullptr;
     KArgs *d_args_fb = nullptr;           // SSSP launch over the hub solver's fallback list
+    KArgs *d_args_hub_last = nullptr;     // hub launch that ends the pass (fallback known to be empty)
+    bool fb_none = false;                 // a completed pass of this plan had no fallback sources
+    uint32_t runs = 0;
     uint32_t *d_near = nullptr, *d_fb = nullptr;
     uint32_t hub_blocks = 0, fb_blocks = 0, spw = 1;
     unsigned long long *d_dbg = nullptr;  // diagnostic builds: per-workgroup phase cycles
@@ -561,7 +564,7 @@ struct mr_plan {
         for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_rank_inv, (void *)d_src, (void *)d_qb, (void *)d_qd,
                         (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
                         (void *)d_counter, (void *)d_args, (void *)d_dbg, (void *)d_args_fb, (void *)d_near,
-                        (void *)d_fb})
+                        (void *)d_fb, (void *)d_args_hub_last})
             if (p) (void)hipFree(p);
         for (auto &e : timed) {
             (void)hipEventDestroy(e.first);
@@ -570,6 +573,22 @@ struct mr_plan {
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
+
+// Kernel-argument blocks of a plan: the main launch, and for hub plans the fallback
+// launch and the hub launch that ends a pass on its own (last_launch marks the
+// kernel whose last workgroup resets the per-pass counters).
+static int upload_args(mr_plan *pl) {
+    KArgs k = pl->ka;
+    k.last_launch = pl->hp.hub ? 0u : 1u;
+    if (hipMemcpy(pl->d_args, &k, sizeof(KArgs), hipMemcpyHostToDevice) != hipSuccess) return MR_ERR_DEVICE;
+    if (pl->hp.hub) {
+        k.last_launch = 1;
+        if (hipMemcpy(pl->d_args_hub_last, &k, sizeof(KArgs), hipMemcpyHostToDevice) != hipSuccess) return MR_ERR_DEVICE;
+        k.fb_mode = 1;
+        if (hipMemcpy(pl->d_args_fb, &k, sizeof(KArgs), hipMemcpyHostToDevice) != hipSuccess) return MR_ERR_DEVICE;
+    }
+    return MR_OK;
+}
 
 static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *qs, uint32_t n, uint32_t max_cmds,
                        mr_plan **out) {
@@ -597,7 +616,8 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     size_t nres = std::max<uint32_t>(n, 1);
     if (hipMalloc(reinterpret_cast<void **>(&pl->d_res), nres * sizeof(OutResult)) != hipSuccess ||
         hipMalloc(reinterpret_cast<void **>(&pl->d_cmd), nres * size_t(max_cmds) * sizeof(OutCmd)) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void **>(&pl->d_counter), 16) != hipSuccess)
+        hipMalloc(reinterpret_cast<void **>(&pl->d_counter), kCtrWords * 4) != hipSuccess ||
+        hipMemset(pl->d_counter, 0, kCtrWords * 4) != hipSuccess)
         return bail(fail(MR_ERR_DEVICE, "hipMalloc outputs"));
     // algorithm: level-synchronous when the comparator leads with Legs (MR_ALGO=generic forces the
     // bucketed solver, used by the tests to cover both); grid state in LDS when it fits 3
@@ -674,10 +694,8 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
                                                      uint64_t(hper) * prop.multiProcessorCount));
         if (const char *e = std::getenv("MR_HUB_BLOCKS")) pl->hub_blocks = uint32_t(std::max(1, std::atoi(e)));
         pl->fb_blocks = pl->blocks;
-        KArgs kf = ka;
-        kf.fb_mode = 1;
         if (hipMalloc(reinterpret_cast<void **>(&pl->d_args_fb), sizeof(KArgs)) != hipSuccess ||
-            hipMemcpy(pl->d_args_fb, &kf, sizeof(KArgs), hipMemcpyHostToDevice) != hipSuccess)
+            hipMalloc(reinterpret_cast<void **>(&pl->d_args_hub_last), sizeof(KArgs)) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "kernel args"));
     }
 #ifdef MR_HUBDUMP
@@ -695,8 +713,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         ka.dbg_blocks = pl->blocks;
     }
 #endif
-    if (hipMalloc(reinterpret_cast<void **>(&pl->d_args), sizeof(KArgs)) != hipSuccess ||
-        hipMemcpy(pl->d_args, &ka, sizeof(KArgs), hipMemcpyHostToDevice) != hipSuccess)
+    if (hipMalloc(reinterpret_cast<void **>(&pl->d_args), sizeof(KArgs)) != hipSuccess || upload_args(pl) != MR_OK)
         return bail(fail(MR_ERR_DEVICE, "kernel args"));
     *out = pl;
     return MR_OK;
@@ -709,16 +726,17 @@ extern "C" int mr_plan_create(const mr_grid *g, const mr_params *prm, const mr_q
 extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     if (!pl) return fail(MR_ERR_INVALID_ARG, "null plan");
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : pl->stream;
-    if (hipMemsetAsync(pl->d_counter, 0, 16, s) != hipSuccess) return fail(MR_ERR_DEVICE, "memset");
     if (pl->ka.nsrc == 0) return MR_OK;
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return fail(MR_ERR_DEVICE, "event");
-    // poison the result records: a record the kernels did not write is reported, never returned
-    if (pl->hp.nq && hipMemsetAsync(pl->ka.out_res, 0xFF, size_t(pl->hp.nq) * sizeof(OutResult), s) != hipSuccess)
-        return fail(MR_ERR_DEVICE, "memset results");
     (void)hipEventRecord(e0, s);
     hipError_t e;
-    if (pl->hp.hub) {
+    ++pl->runs;
+    if (pl->hp.hub && pl->fb_none) {
+        // a pass of this plan (same inputs, deterministic result) had no fallback
+        // sources: the hub launch ends the pass on its own
+        e = launch_hub(pl->d_args_hub_last, pl->ka.p.perm, pl->spw, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
+    } else if (pl->hp.hub) {
         // closed-form hub solve for every source, then the SSSP kernel for the
         // sources it flagged (usually none; those workgroups exit at once)
         e = launch_hub(pl->d_args, pl->ka.p.perm, pl->spw, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
@@ -730,6 +748,15 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     (void)hipEventRecord(e1, s);
     pl->timed.push_back({e0, e1});
     if (e != hipSuccess) return fail(MR_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(e));
+    return MR_OK;
+}
+
+// counters after the plan's stream has drained; notes a pass without fallback sources
+static int read_counters(mr_plan *pl, uint32_t ctr[kCtrWords]) {
+    if (hipStreamSynchronize(pl->stream) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(ctr, pl->d_counter, kCtrWords * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(MR_ERR_DEVICE, "copy counter");
+    if (pl->hp.hub && pl->runs && !pl->ka.fb_all && ctr[kCtrLastFb] == 0) pl->fb_none = true;
     return MR_OK;
 }
 
@@ -748,6 +775,8 @@ extern "C" double mr_plan_kernel_ms(mr_plan *pl, uint32_t *n_launches) {
         (void)hipEventDestroy(e.second);
     }
     pl->timed.clear();
+    uint32_t ctr[kCtrWords];
+    (void)read_counters(pl, ctr);
     if (n_launches) *n_launches = k;
     return k ? tot / k : 0.0;
 }
@@ -756,14 +785,7 @@ extern "C" int mr_plan_bind_outputs(mr_plan *pl, void *d_results, void *d_comman
     if (!pl || !d_results || !d_commands) return fail(MR_ERR_INVALID_ARG, "null argument");
     pl->ka.out_res = reinterpret_cast<OutResult *>(d_results);
     pl->ka.out_cmd = reinterpret_cast<OutCmd *>(d_commands);
-    if (hipMemcpy(pl->d_args, &pl->ka, sizeof(KArgs), hipMemcpyHostToDevice) != hipSuccess)
-        return fail(MR_ERR_DEVICE, "kernel args");
-    if (pl->d_args_fb) {
-        KArgs kf = pl->ka;
-        kf.fb_mode = 1;
-        if (hipMemcpy(pl->d_args_fb, &kf, sizeof(KArgs), hipMemcpyHostToDevice) != hipSuccess)
-            return fail(MR_ERR_DEVICE, "kernel args");
-    }
+    if (hipDeviceSynchronize() != hipSuccess || upload_args(pl) != MR_OK) return fail(MR_ERR_DEVICE, "kernel args");
     return MR_OK;
 }
 
@@ -772,14 +794,12 @@ extern "C" uint32_t mr_plan_num_sources(const mr_plan *pl) { return pl ? pl->ka.
 extern "C" int mr_plan_get_stats(mr_plan *pl, mr_plan_stats *out) {
     if (!pl || !out) return fail(MR_ERR_INVALID_ARG, "null argument");
     std::memset(out, 0, sizeof(*out));
-    uint32_t ctr[4] = {0, 0, 0, 0};
-    if (hipStreamSynchronize(pl->stream) != hipSuccess ||
-        hipMemcpy(ctr, pl->d_counter, 16, hipMemcpyDeviceToHost) != hipSuccess)
-        return fail(MR_ERR_DEVICE, "copy counter");
+    uint32_t ctr[kCtrWords];
+    if (int st = read_counters(pl, ctr)) return st;
     out->solver = pl->hp.hub ? MR_SOLVER_HUB : (pl->algo == kAlgoLegs ? MR_SOLVER_LEVELS : MR_SOLVER_BUCKETED);
     out->grid_state_in_lds = pl->grid_in_lds ? 1u : 0u;
     out->num_sources = pl->ka.nsrc;
-    out->fallback_sources = pl->hp.hub ? ctr[2] : 0u;
+    out->fallback_sources = pl->hp.hub ? ctr[kCtrLastFb] : 0u;
     out->num_specials = pl->ka.p.NS;
     out->num_regions = pl->hp.nreg;
     out->hub_workgroups = pl->hub_blocks;
@@ -825,9 +845,10 @@ static void expand_cmd(const mr_grid *g, const HostPlan &hp, const OutCmd &c, mr
 }
 
 static int check_device_errors(mr_plan *pl, uint32_t &flags) {
-    uint32_t ctr[4] = {0, 0, 0, 0};
-    if (hipMemcpy(ctr, pl->d_counter, 16, hipMemcpyDeviceToHost) != hipSuccess) return fail(MR_ERR_DEVICE, "copy counter");
-    flags = ctr[1];
+    uint32_t ctr[kCtrWords];
+    if (int st = read_counters(pl, ctr)) return st;
+    flags = ctr[kCtrFlags];
+    if (flags) (void)hipMemset(pl->d_counter + kCtrFlags, 0, 4);  // collected
 #ifdef MR_HUBDUMP
     if (pl->d_dbg) {
         std::vector<uint32_t> d(64 * 16);
@@ -851,9 +872,9 @@ static int check_device_errors(mr_plan *pl, uint32_t &flags) {
 #endif
     if (std::getenv("MR_DEBUG")) {
         std::fprintf(stderr, "MR_DEBUG hub=%d sources=%u fallback=%u flags=%u hub_blocks=%u\n", int(pl->hp.hub),
-                     pl->ka.nsrc, ctr[2], ctr[1], pl->hub_blocks);
-        if (pl->d_fb && ctr[2] <= pl->ka.nsrc) {
-            std::vector<uint32_t> fb(ctr[2]);
+                     pl->ka.nsrc, ctr[kCtrLastFb], ctr[kCtrFlags], pl->hub_blocks);
+        if (pl->d_fb && ctr[kCtrLastFb] <= pl->ka.nsrc) {
+            std::vector<uint32_t> fb(ctr[kCtrLastFb]);
             (void)hipMemcpy(fb.data(), pl->d_fb, fb.size() * 4, hipMemcpyDeviceToHost);
             std::fprintf(stderr, "MR_DEBUG fallback sources (vertex):");
             for (uint32_t s : fb) std::fprintf(stderr, " %u", pl->hp.src_v[s]);
@@ -863,6 +884,9 @@ static int check_device_errors(mr_plan *pl, uint32_t &flags) {
     if (flags & (kErrKOverflow | kErrMetricOverflow))
         return fail(MR_ERR_LIMIT, "a label exceeds the engine's 32-bit metric or run-length limits");
     if (flags) return fail(MR_ERR_DEVICE, "internal invariant violated on device (flags " + std::to_string(flags) + ")");
+    if (pl->runs && ctr[kCtrLastWritten] != pl->hp.q_id.size())
+        return fail(MR_ERR_DEVICE, "internal: " + std::to_string(ctr[kCtrLastWritten]) + " of " +
+                                       std::to_string(pl->hp.q_id.size()) + " result records written");
     return MR_OK;
 }
 
@@ -881,10 +905,6 @@ static int plan_collect(mr_plan *pl, std::vector<OutResult> &res, std::vector<Ou
         if (hipMemcpy(res.data(), pl->ka.out_res, n * sizeof(OutResult), hipMemcpyDeviceToHost) != hipSuccess ||
             hipMemcpy(cmd.data(), pl->ka.out_cmd, size_t(n) * mc * sizeof(OutCmd), hipMemcpyDeviceToHost) != hipSuccess)
             return fail(MR_ERR_DEVICE, "copy outputs");
-        const HostPlan &hp = pl->hp;
-        for (uint32_t k = 0; k < hp.q_id.size(); ++k)
-            if (res[hp.q_id[k]].ncmd_status == 0xFFFFFFFFu)
-                return fail(MR_ERR_DEVICE, "internal: result of query " + std::to_string(hp.q_id[k]) + " not written");
     }
     return MR_OK;
 }

@@ -188,7 +188,7 @@ struct Core {
         if constexpr (G) __hip_atomic_store(l + i, IdxT(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else l[i] = IdxT(v);
     }
-    __device__ __forceinline__ void flag(uint32_t e) const { atomicOr(counter + 1, e); }
+    __device__ __forceinline__ void flag(uint32_t e) const { atomicOr(counter + kCtrFlags, e); }
     __device__ __forceinline__ uint32_t special_of(uint32_t v) const { return sinfo[v] & kNone10; }
     __device__ __forceinline__ uint32_t region_of(uint32_t v) const { return (sinfo[v] >> 10) & kNone10; }
     __device__ __forceinline__ uint32_t vert_of(uint32_t t) const { return t == 0 ? src : sp[t].v; }
@@ -1277,6 +1277,28 @@ struct GenericSolver : Core<G> {
     }
 };
 
+// End of a workgroup (thread 0, after a barrier): add its written records; in the
+// pass's last kernel the last workgroup to finish publishes the pass's counts and
+// zeroes the per-pass counters for the next pass.
+__device__ __forceinline__ void finish_launch(const KArgs *__restrict__ a, uint32_t written) {
+    uint32_t *c = a->counter;
+    if (written) atomicAdd(c + kCtrWritten, written);
+    if (!a->last_launch) return;
+    __threadfence();
+    if (atomicAdd(c + kCtrDone, 1u) == gridDim.x - 1) {
+        __threadfence();
+        const uint32_t fb = atomicAdd(c + kCtrFbCount, 0u), wr = atomicAdd(c + kCtrWritten, 0u);
+        c[kCtrLastFb] = fb;
+        c[kCtrLastWritten] = wr;
+        c[kCtrDequeue] = 0;
+        c[kCtrFbCount] = 0;
+        c[kCtrFbDequeue] = 0;
+        c[kCtrWritten] = 0;
+        c[kCtrDone] = 0;
+        __threadfence();
+    }
+}
+
 // ===================================================================================
 // Hub solver (linear StandardMove run time: Fleetfoot level 0 or out of range)
 // ===================================================================================
@@ -1340,6 +1362,7 @@ struct HubSolver : Core<false> {
     const uint32_t *nearS;  // LDS: region rows {distance, rank} of every special (row t at t*2*nreg)
     uint32_t *srow;         // LDS: this segment's region row of its source
     uint32_t nreg;
+    uint32_t written = 0;   // result records this lane emitted for (segment lane 0)
 #ifdef MR_STAMPS
     mutable unsigned long long hs_last = 0, hs[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     __device__ void hmark(int slot) const {
@@ -1674,8 +1697,9 @@ struct HubSolver : Core<false> {
         // An order-sensitive tie hands the source to the SSSP kernel.  No early
         // return: the wave must stay converged for the next dequeue's broadcast.
         const bool fallback = have && (seg_bits<LPS>(__ballot(tie != 0)) != 0 || a->fb_all);
-        if (fallback && t == 0) a->fb_list[atomicAdd(counter + 2, 1u)] = s_idx;
+        if (fallback && t == 0) a->fb_list[atomicAdd(counter + kCtrFbCount, 1u)] = s_idx;
         const uint32_t qa = a->q_begin[si], qb = (!have || fallback) ? qa : a->q_begin[si + 1];
+        if (t == 0) written += qb - qa;
         emit_all(qa, qb, nb, sx, sy, st0);
         MR_HSTAMP(7);
     }
@@ -1753,16 +1777,23 @@ __global__ __launch_bounds__(kBS, 5) void hub_kernel(const KArgs *__restrict__ a
 #ifdef MR_STAMPS
     H.hs_last = __builtin_amdgcn_s_memtime();
 #endif
-    for (;;) {  // each wave dequeues SPW sources at a time
-        uint32_t base = 0;
-        if (lane_id() == 0) base = atomicAdd(a->counter, SPW);
-        base = __shfl(base, 0, 64);
+    // sources are strided over the launch's waves (no dequeue atomics: one word
+    // would saturate at ~88 dequeues/us, MI355X_MICROARCH.md)
+    const uint32_t waves = gridDim.x * (kBS / 64), wid = blockIdx.x * (kBS / 64) + (threadIdx.x >> 6);
+    for (uint32_t k = 0;; ++k) {
+        const unsigned long long base = ((unsigned long long)k * waves + wid) * SPW;
 #ifdef MR_STAMPS
         H.hmark(8);
 #endif
         if (base >= a->nsrc) break;
-        H.solve(base);
+        H.solve(uint32_t(base));
     }
+    __shared__ uint32_t wsum;
+    if (threadIdx.x == 0) wsum = 0;
+    __syncthreads();
+    if (H.written) atomicAdd(&wsum, H.written);
+    __syncthreads();
+    if (threadIdx.x == 0) finish_launch(a, wsum);
 #ifdef MR_STAMPS
     if (lane_id() == 0 && a->dbg) {
         unsigned long long *h = a->dbg + (unsigned long long)a->dbg_blocks * 10;
@@ -1820,11 +1851,11 @@ __host__ __device__ inline LdsLayout lds_layout(uint32_t NS, uint32_t V, bool gr
 // after the hub solver) the sources it listed
 __device__ __forceinline__ uint32_t next_source(const KArgs *__restrict__ a) {
     if (a->fb_mode) {
-        const uint32_t n = __hip_atomic_load(a->counter + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t i = atomicAdd(a->counter + 3, 1u);
+        const uint32_t n = __hip_atomic_load(a->counter + kCtrFbCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t i = atomicAdd(a->counter + kCtrFbDequeue, 1u);
         return i < n ? a->fb_list[i] : kNone32;
     }
-    const uint32_t i = atomicAdd(a->counter, 1u);
+    const uint32_t i = atomicAdd(a->counter + kCtrDequeue, 1u);
     return i < a->nsrc ? i : kNone32;
 }
 
@@ -1832,7 +1863,10 @@ template <bool G, class IdxT, uint32_t ALGO>
 __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // fallback launch after the hub solver: nothing to do unless it listed sources
-    if (a->fb_mode && __hip_atomic_load(a->counter + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+    if (a->fb_mode && __hip_atomic_load(a->counter + kCtrFbCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        if (threadIdx.x == 0) finish_launch(a, 0);
+        return;
+    }
     const uint32_t V = a->p.V, NS = a->p.NS;
     const LdsLayout L = lds_layout(NS, V, !G, ALGO);
     Shared *sh = reinterpret_cast<Shared *>(smem);
@@ -1859,6 +1893,7 @@ __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a)
     for (uint32_t t = threadIdx.x; t <= NS; t += kBS) spl[t] = a->sp[t];
     for (uint32_t h = threadIdx.x; h < a->p.n_hubs; h += kBS) hubl[h] = a->hubs[h];
     __syncthreads();
+    uint32_t written = 0;  // result records of this workgroup's sources (thread 0 reports them)
     if constexpr (ALGO == kAlgoLegs) {
         LegsSolver<G, IdxT> S;
         S.a = a;
@@ -1893,6 +1928,7 @@ __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a)
             __syncthreads();
             if (s == kNone32) break;
             S.solve(s);
+            written += a->q_begin[s + 1] - a->q_begin[s];
             ++nsolved;
         }
 #ifdef MR_STAMPS
@@ -1930,8 +1966,11 @@ __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a)
             __syncthreads();
             if (s == kNone32) break;
             S.solve(s);
+            written += a->q_begin[s + 1] - a->q_begin[s];
         }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) finish_launch(a, written);
 }
 
 // ---- host-side launch helpers (called from mr_host.cpp) ------------------------------

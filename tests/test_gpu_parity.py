@@ -173,3 +173,23 @@ def test_plan_rerun_is_identical(eng):
     assert a == b
     ms, n = plan.kernel_ms()
     assert n == 3 and ms > 0
+
+
+def test_plan_rerun_with_fallback_sources(eng, oracle_lib):
+    """A hub plan whose sources partly fall back (clustered map, Time first) keeps
+    both launches on every pass; a plan without any skips the empty fallback launch
+    once a pass has shown it empty.  Results stay identical and exact either way."""
+    m = SyntheticMap(21, campfires_per_homeland=6, seed=5, clustered=True)
+    g = eng.MapGrid(m.cells())
+    og = oracle_lib.OracleGrid(m.cells())
+    for params in (Params(sort_by=(SORT_TIME, SORT_MONEY)), Params()):
+        qs = random_queries(m, 300, 13)
+        exp = [as_expected(e) for e in og.find_path_batch(params, qs, threads=0)]
+        plan = eng.Plan(g, params, qs)
+        for _ in range(3):
+            plan.run()
+            assert [as_expected(r) for r in plan.fetch()] == exp
+        st = plan.stats()
+        assert st["solver"] == "hub"
+        if params.sort_by[0] == SORT_TIME:
+            assert st["fallback_sources"] > 0
