@@ -89,6 +89,17 @@ typedef struct mr_grid mr_grid; /* opaque, immutable */
  * (src/pathfinder.rs:24-138) is not the geometric 4-neighbourhood. */
 int mr_grid_create(const mr_cell *cells, uint32_t n_cells, mr_grid **out);
 void mr_grid_destroy(mr_grid *grid);
+
+/* MapGrid::parse (src/grid.rs:47-133): the reference's HTML map format
+ * (class "map-grid" > "map-cell" children with corner texts and a centre emoji)
+ * into row-major cells.  *n_cells receives the cell count; MR_ERR_CAPACITY if cap
+ * is smaller (nothing written).  MR_ERR_INVALID_GRID for the reference's parse
+ * errors: no map-grid, not square, a bad background-color, an unindexable cell,
+ * Center missing or not at (0,0) (mr_parse_error() names it).  Host only. */
+int mr_parse_map_html(const char *html, uint64_t len, mr_cell *cells, uint32_t cap, uint32_t *n_cells);
+const char *mr_parse_error(void);
+/* mr_parse_map_html + mr_grid_create. */
+int mr_grid_from_html(const char *html, uint64_t len, mr_grid **out);
 /* MapGrid::square_size / homeland_size (src/grid.rs:280-282) */
 uint32_t mr_grid_square_size(const mr_grid *grid);
 

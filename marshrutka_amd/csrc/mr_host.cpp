@@ -62,6 +62,14 @@ static mr_cell_index build_border(int b, int s) {
     if (s == 0) return ci_make(MR_CELL_CENTER, 0, 0, 0);
     return ci_make(MR_CELL_BORDER, uint8_t(b), uint16_t(s), 0);
 }
+// CellIndexBuilder::build on a raw (homeland, x, y) / (border, shift) index
+namespace mr {
+mr_cell_index build_index(const mr_cell_index &c) {
+    if (c.kind == MR_CELL_HOMELAND && c.sub < 4) return build_homeland(c.sub, c.x, c.y);
+    if (c.kind == MR_CELL_BORDER && c.sub < 4 && c.y == 0) return build_border(c.sub, c.x);
+    return c;
+}
+}  // namespace mr
 static bool canonical(const mr_cell_index &c) {
     if (c.reserved) return false;
     if (c.kind == MR_CELL_CENTER) return c.sub == 0 && c.x == 0 && c.y == 0;
@@ -144,8 +152,7 @@ extern "C" int mr_grid_create(const mr_cell *cells, uint32_t n, mr_grid **out) {
     for (uint32_t i = 0; i < n; ++i) {
         mr_cell_index c = cells[i].index;
         // MapGrid::parse builds every index canonically (src/index.rs:419-431)
-        if (c.kind == MR_CELL_HOMELAND && c.sub < 4) c = build_homeland(c.sub, c.x, c.y);
-        else if (c.kind == MR_CELL_BORDER && c.sub < 4 && c.y == 0) c = build_border(c.sub, c.x);
+        c = build_index(c);
         if (!canonical(c) || cells[i].poi > MR_POI_FORUM || cells[i].index.reserved) {
             delete g;
             return fail(MR_ERR_INVALID_GRID, "invalid cell index or poi at cell " + std::to_string(i));

@@ -27,7 +27,7 @@ EXPORTED_SYMBOLS = [
     "mr_grid_create", "mr_grid_destroy", "mr_grid_square_size", "mr_params_default", "mr_find_path",
     "mr_find_path_batch", "mr_plan_create", "mr_plan_run", "mr_plan_fetch", "mr_plan_device_outputs",
     "mr_plan_num_sources", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_plan_bind_outputs", "mr_abi_version", "mr_last_error",
-    "mr_device_available",
+    "mr_device_available", "mr_parse_map_html", "mr_parse_error", "mr_grid_from_html",
 ]
 
 
@@ -81,6 +81,11 @@ def lib():
         L.mr_abi_version.restype = C.c_uint32
         L.mr_last_error.restype = C.c_char_p
         L.mr_device_available.restype = C.c_int
+        L.mr_parse_map_html.argtypes = [C.c_char_p, C.c_uint64, C.POINTER(mr_cell), C.c_uint32, C.POINTER(C.c_uint32)]
+        L.mr_parse_map_html.restype = C.c_int
+        L.mr_parse_error.restype = C.c_char_p
+        L.mr_grid_from_html.argtypes = [C.c_char_p, C.c_uint64, C.POINTER(vp)]
+        L.mr_grid_from_html.restype = C.c_int
         _lib = L
     return _lib
 
@@ -93,8 +98,29 @@ def device_available() -> bool:
     return bool(lib().mr_device_available())
 
 
+def parse_map_html(html: str) -> List[Tuple[CellIndex, int]]:
+    """MapGrid::parse (src/grid.rs:47-133) on the host: the reference's HTML map
+    format -> [(CellIndex, poi)] in row-major order.  Raises EngineError
+    (MR_ERR_INVALID_GRID) on the reference's parse errors."""
+    data = html.encode("utf-8")
+    n = C.c_uint32()
+    st = lib().mr_parse_map_html(data, len(data), None, 0, C.byref(n))
+    if st not in (MR_OK, MR_ERR_CAPACITY):
+        raise EngineError(st, (lib().mr_parse_error() or b"").decode())
+    cells = (mr_cell * max(n.value, 1))()
+    st = lib().mr_parse_map_html(data, len(data), cells, n.value, C.byref(n))
+    if st != MR_OK:
+        raise EngineError(st, (lib().mr_parse_error() or b"").decode())
+    return [(CellIndex(c.index.kind, c.index.sub, c.index.x, c.index.y), c.poi) for c in cells[: n.value]]
+
+
 class MapGrid:
     """The immutable grid handle (MapGrid, src/grid.rs:31-38)."""
+
+    @classmethod
+    def from_html(cls, html: str) -> "MapGrid":
+        """MapGrid::parse + the engine's grid (canonical indices, nearest campfires)."""
+        return cls(parse_map_html(html))
 
     def __init__(self, cells: Sequence[Tuple[CellIndex, int]]):
         self._cells = cells_to_c(cells)
