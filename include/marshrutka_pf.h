@@ -234,6 +234,21 @@ const char *mr_last_error(void);
 /* 1 if a gfx950 device is visible to this process. */
 int mr_device_available(void);
 
+/* ---- the app's command table for a path (src/app.rs:481-561) ----------- */
+/* AggregatedCost::time of one command (src/cost.rs:118-150): a StandardMove's
+ * raw run time with Fleetfoot's ceil applied for levels 1..3. */
+int64_t mr_command_time(const mr_command *cmd);
+/* time 0.3 Duration Display ("1h3m10s", "0s"; src/pathfinder.rs:279-285). */
+int mr_duration_display(int64_t seconds, char *buf, uint64_t cap);
+/* One line per command (NoMove skipped), tab-separated:
+ *   "<bot command>\t<duration>\t<running total>\t<start hh:mm:ss>\n"
+ * e.g. "/go_direct_b_2_2", "/car_0_0", "/use_soe".  The total adds pause_s per
+ * command; starts are back-scheduled from arrive_at_s (seconds after midnight,
+ * < 86400), wrapping at midnight.  *len = text length; MR_ERR_CAPACITY if
+ * cap <= *len (then nothing is written). */
+int mr_render_schedule(const mr_command *cmds, uint32_t n, uint32_t arrive_at_s, uint32_t pause_s, char *buf,
+                       uint64_t cap, uint64_t *len);
+
 #ifdef __cplusplus
 }
 #endif

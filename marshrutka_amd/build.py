@@ -10,7 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libmarshrutka_pf.so")
-SOURCES = ["mr_kernel.hip", "mr_host.cpp", "mr_html.cpp"]
+SOURCES = ["mr_kernel.hip", "mr_host.cpp", "mr_html.cpp", "mr_render.cpp"]
 HEADERS = ["mr_engine.hpp", os.path.join("..", "..", "include", "marshrutka_pf.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",

@@ -28,6 +28,7 @@ EXPORTED_SYMBOLS = [
     "mr_find_path_batch", "mr_plan_create", "mr_plan_run", "mr_plan_fetch", "mr_plan_device_outputs",
     "mr_plan_num_sources", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_plan_bind_outputs", "mr_abi_version", "mr_last_error",
     "mr_device_available", "mr_parse_map_html", "mr_parse_error", "mr_grid_from_html",
+    "mr_command_time", "mr_duration_display", "mr_render_schedule",
 ]
 
 
@@ -86,6 +87,13 @@ def lib():
         L.mr_parse_error.restype = C.c_char_p
         L.mr_grid_from_html.argtypes = [C.c_char_p, C.c_uint64, C.POINTER(vp)]
         L.mr_grid_from_html.restype = C.c_int
+        L.mr_command_time.argtypes = [C.POINTER(mr_command)]
+        L.mr_command_time.restype = C.c_int64
+        L.mr_duration_display.argtypes = [C.c_int64, C.c_char_p, C.c_uint64]
+        L.mr_duration_display.restype = C.c_int
+        L.mr_render_schedule.argtypes = [C.POINTER(mr_command), C.c_uint32, C.c_uint32, C.c_uint32, C.c_char_p,
+                                         C.c_uint64, C.POINTER(C.c_uint64)]
+        L.mr_render_schedule.restype = C.c_int
         _lib = L
     return _lib
 
@@ -96,6 +104,26 @@ def last_error() -> str:
 
 def device_available() -> bool:
     return bool(lib().mr_device_available())
+
+
+def render_schedule(label: TotalCost, arrive_at_s: int, pause_s: int = 0) -> List[Tuple[str, str, str, str]]:
+    """The app's command table for a path (src/app.rs:481-561): rows of
+    (bot command, duration, running total, back-scheduled start hh:mm:ss)."""
+    cmds = (mr_command * max(len(label.commands), 1))()
+    for i, c in enumerate(label.commands):
+        cmds[i].kind, cmds[i].time_s, cmds[i].legs = c.kind, c.time_s, c.legs
+        cmds[i].money, cmds[i].fleetfoot = c.money, c.fleetfoot
+        for dst, ci in ((cmds[i].from_, c.from_), (cmds[i].to, c.to)):
+            dst.kind, dst.sub, dst.x, dst.y = ci.kind, ci.sub, ci.x, ci.y
+    n = C.c_uint64()
+    st = lib().mr_render_schedule(cmds, len(label.commands), arrive_at_s, pause_s, None, 0, C.byref(n))
+    if st not in (MR_OK, MR_ERR_CAPACITY):
+        raise EngineError(st, "render_schedule")
+    buf = C.create_string_buffer(n.value + 1)
+    st = lib().mr_render_schedule(cmds, len(label.commands), arrive_at_s, pause_s, buf, n.value + 1, C.byref(n))
+    if st != MR_OK:
+        raise EngineError(st, "render_schedule")
+    return [tuple(line.split("\t")) for line in buf.value.decode().splitlines()]
 
 
 def parse_map_html(html: str) -> List[Tuple[CellIndex, int]]:

@@ -276,3 +276,62 @@ def label_to_json(label) -> Optional[dict]:
         c["to"] = list(to)
         out.append(c)
     return {"legs": legs, "money": money, "time_s": time, "commands": out}
+
+
+# ---- the app's command table (src/app.rs:481-561) — test-side restatement --------
+FF_LEVEL_RATIO = {1: (50, 53), 2: (100, 109), 3: (25, 28)}   # src/skill.rs:65-71
+
+
+def command_time(c: dict) -> int:
+    """AggregatedCost::time (src/cost.rs:118-150) on a label_to_json command."""
+    if c["kind"] in (CENTRAL, CARAVAN):
+        return c["time_s"]
+    if c["kind"] == STANDARD:
+        r = FF_LEVEL_RATIO.get(c["fleetfoot"])
+        return c["time_s"] if r is None else -(-c["time_s"] * r[0] // r[1])
+    return 0
+
+
+def duration_str(s: int) -> str:
+    """time 0.3 Duration Display (src/pathfinder.rs:279-285 pins "1h3m10s")."""
+    if s == 0:
+        return "0s"
+    a, out = abs(s), ("-" if s < 0 else "")
+    for v, u in ((a // 86400, "d"), (a // 3600 % 24, "h"), (a // 60 % 60, "m"), (a % 60, "s")):
+        if v:
+            out += f"{v}{u}"
+    return out
+
+
+def command_suffix(ci) -> str:
+    """CellIndexCommandSuffix (src/index.rs:378-390) on a (kind, sub, x, y) tuple."""
+    kind, sub, x, y = ci
+    if kind == 0:
+        return "0_0"
+    if kind == 1:
+        return f"{'brgy'[sub]}_{x}_{y}"
+    return f"{['br', 'rg', 'gy', 'yb'][sub]}_{x}"
+
+
+def render_schedule(label_json: dict, arrive_at_s: int, pause_s: int):
+    """Rows (command, duration, total, start) of the app's table (src/app.rs:481-561)."""
+    cmds = [c for c in label_json["commands"] if c["kind"] != NOMOVE]
+    times, acc = [], arrive_at_s
+    for c in reversed(cmds):
+        acc -= command_time(c) + pause_s
+        times.append(acc)
+    times.reverse()
+    rows, total = [], 0
+    names = {SOE: "/use_soe", SHQ: "/use_shq", SFM: "/use_sfm"}
+    for c, at in zip(cmds, times):
+        if c["kind"] in (CENTRAL, STANDARD):
+            cmd = "/go_direct_" + command_suffix(tuple(c["to"]))
+        elif c["kind"] == CARAVAN:
+            cmd = "/car_" + command_suffix(tuple(c["to"]))
+        else:
+            cmd = names[c["kind"]]
+        t = command_time(c)
+        total += t + pause_s
+        tod = at % 86400
+        rows.append((cmd, duration_str(t), duration_str(total), f"{tod // 3600:02d}:{tod // 60 % 60:02d}:{tod % 60:02d}"))
+    return rows
