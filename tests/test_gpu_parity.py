@@ -193,3 +193,27 @@ def test_plan_rerun_with_fallback_sources(eng, oracle_lib):
         assert st["solver"] == "hub"
         if params.sort_by[0] == SORT_TIME:
             assert st["fallback_sources"] > 0
+
+
+def _sweep():
+    """Every FindPath dimension over its whole range, one at a time:
+    the 9 sort_by inputs (src/cost.rs:387-405), Fleetfoot 0..3 and out of range,
+    RouteGuru 0..5 and out of range, each scroll/caravan toggle, zero and odd costs."""
+    sorts = [(a, b) for a in (SORT_LEGS, SORT_TIME, SORT_MONEY) for b in (SORT_LEGS, SORT_TIME, SORT_MONEY)]
+    out = [Params(sort_by=s) for s in sorts]
+    out += [Params(fleetfoot=f, sort_by=(SORT_TIME, SORT_LEGS)) for f in range(6)]
+    out += [Params(route_guru=r, sort_by=(SORT_TIME, SORT_MONEY)) for r in range(8)]
+    out += [Params(use_soe=False), Params(use_caravans=False), Params(use_sfm=True),
+            Params(use_sfm=True, scroll_of_escape_forum_cost=0),
+            Params(scroll_of_escape_cost=0), Params(scroll_of_escape_cost=7, sort_by=(SORT_MONEY, SORT_TIME))]
+    return out
+
+
+@pytest.mark.parametrize("params", _sweep(), ids=lambda p: f"sort{p.sort_by}-ff{p.fleetfoot}-rg{p.route_guru}-"
+                         f"soe{int(p.use_soe)}{p.scroll_of_escape_cost}-sfm{int(p.use_sfm)}-car{int(p.use_caravans)}")
+def test_parameter_sweep(eng, oracle_lib, params):
+    for size, k, clustered, seed in ((15, 3, False, 21), (21, 5, True, 22)):
+        m = SyntheticMap(size, campfires_per_homeland=k, seed=seed, clustered=clustered)
+        hq = m.campfires()[-1]
+        for p in (params, Params(**{**params.__dict__, "hq_position": hq})):
+            check(eng, oracle_lib, m, p, random_queries(m, 150, seed + 1), f"S={size} {p}")
