@@ -227,6 +227,25 @@ int mr_plan_get_stats(mr_plan *plan, mr_plan_stats *out);
 double mr_plan_kernel_ms(mr_plan *plan, uint32_t *n_launches);
 void mr_plan_destroy(mr_plan *plan);
 
+/* ---- all destinations (single source -> every cell) ------- */
+/* One record per (source, cell): the label's metrics and how to rebuild it. */
+typedef struct mr_label_record {
+    uint32_t legs, money, time_s;
+    uint32_t via; /* internal: boundary / special table entry; 0xFFFFFFFF = the source */
+} mr_label_record;
+/* A plan answering every destination of each source: mr_plan_run computes
+ * n_sources x V records on the device; mr_plan_kernel_ms / mr_plan_get_stats /
+ * mr_plan_destroy apply.  Sources may repeat (they share a solve). */
+int mr_sssp_plan_create(const mr_grid *grid, const mr_params *params, const mr_cell_index *sources,
+                        uint32_t n_sources, mr_plan **out);
+/* The V records of the caller's source i, in row-major cell order (waits for the plan). */
+int mr_sssp_records(mr_plan *plan, uint32_t i, mr_label_record *out);
+/* Device pointer to all records ([plan source][cell], 16 B each) and their size. */
+int mr_sssp_device_records(mr_plan *plan, void **d_records, uint64_t *bytes);
+/* The full label (FindPath::eval(sources[i], dst)) rebuilt from its record:
+ * MR_OK, MR_ERR_CAPACITY (out->n_commands > cap) or an error. */
+int mr_sssp_label(mr_plan *plan, uint32_t i, mr_cell_index dst, mr_result *out, mr_command *cmds, uint32_t cap);
+
 /* ---- misc ---------------------------------------------------------------- */
 uint32_t mr_abi_version(void);
 /* Human-readable description of the last error on this thread. */

@@ -93,6 +93,14 @@ struct OutResult {
 struct OutCmd {
     uint32_t kp, from, to, pad;
 };
+// all-destinations output: one record per source and cell.  via =
+// the table index b of the boundary whose walk ends here (the label is the table
+// chain of b ++ [StandardMove{d_b(v)} b -> v]), kViaSpecial | t for special t (its
+// own table label), kViaSource for the source (the start label).
+struct VRecord {
+    uint32_t m0, m1, m2, via;
+};
+constexpr uint32_t kViaSpecial = 0x80000000u, kViaSource = 0xFFFFFFFFu;
 
 // kernel arguments (one solve launch)
 struct KArgs {
@@ -124,6 +132,13 @@ struct KArgs {
     uint32_t fb_all;             // tests: the hub solver hands every source to the SSSP kernel
     uint32_t dbg_blocks;         // diagnostic builds: SSSP workgroups (hub stamps follow their slots)
     uint32_t last_launch;        // 1: the pass's last kernel; its last workgroup resets the counters
+    // all-destinations mode: no per-query outputs; per source, a record per cell, the
+    // label table (NS+1 entries), the boundaries' lexicographic ranks and how it was solved
+    uint32_t all_mode;
+    VRecord *out_rec;            // nsrc * V
+    Rec *out_tab;                // nsrc * (NS+1)
+    uint32_t *out_lex;           // nsrc * (NS+1): rank of boundary t by (length, command list), else kNone32
+    uint32_t *src_state;         // nsrc: 1 hub solved (records by the fill kernel), 2 SSSP kernel
 };
 // counter words: the pass's last workgroup copies the fallback and written counts
 // to their "last" slots and zeroes the rest, so no memset precedes a pass

@@ -26,6 +26,7 @@ int max_blocks_per_cu(bool grid_in_lds, uint32_t algo, uint32_t bytes);
 uint32_t hub_lds_bytes(uint32_t NS, uint32_t nreg, uint32_t spw);
 hipError_t launch_hub(const KArgs *d_args, const uint32_t perm[3], uint32_t spw, uint32_t NS, uint32_t nreg,
                       uint32_t blocks, hipStream_t stream);
+hipError_t launch_fill(const KArgs *d_args, const uint32_t perm[3], uint32_t gx, uint32_t gy, hipStream_t stream);
 int hub_blocks_per_cu(const uint32_t perm[3], uint32_t spw, uint32_t bytes);
 }  // namespace mr
 
@@ -552,6 +553,12 @@ struct mr_plan {
     KArgs *d_args = nullptr;
     KArgs *d_args_fb = nullptr;           // SSSP launch over the hub solver's fallback list
     KArgs *d_args_hub_last = nullptr;     // hub launch that ends the pass (fallback known to be empty)
+    KArgs *d_args_fill = nullptr;         // all-destinations mode: the fill launch (ends the pass)
+    bool all_mode = false;
+    VRecord *d_rec = nullptr;             // all-destinations outputs (KArgs::out_rec ...)
+    Rec *d_tab = nullptr;
+    uint32_t *d_lex = nullptr, *d_sstate = nullptr;
+    std::vector<uint32_t> src_of_input;   // caller's source i -> plan source index
     bool fb_none = false;                 // a completed pass of this plan had no fallback sources
     uint32_t runs = 0;
     uint32_t *d_near = nullptr, *d_fb = nullptr;
@@ -571,7 +578,8 @@ struct mr_plan {
         for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_rank_inv, (void *)d_src, (void *)d_qb, (void *)d_qd,
                         (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
                         (void *)d_counter, (void *)d_args, (void *)d_dbg, (void *)d_args_fb, (void *)d_near,
-                        (void *)d_fb, (void *)d_args_hub_last})
+                        (void *)d_fb, (void *)d_args_hub_last, (void *)d_args_fill, (void *)d_rec, (void *)d_tab,
+                        (void *)d_lex, (void *)d_sstate})
             if (p) (void)hipFree(p);
         for (auto &e : timed) {
             (void)hipEventDestroy(e.first);
@@ -585,20 +593,27 @@ struct mr_plan {
 // launch and the hub launch that ends a pass on its own (last_launch marks the
 // kernel whose last workgroup resets the per-pass counters).
 static int upload_args(mr_plan *pl) {
+    auto put = [](KArgs *d, const KArgs &k) { return hipMemcpy(d, &k, sizeof(KArgs), hipMemcpyHostToDevice) == hipSuccess; };
     KArgs k = pl->ka;
-    k.last_launch = pl->hp.hub ? 0u : 1u;
-    if (hipMemcpy(pl->d_args, &k, sizeof(KArgs), hipMemcpyHostToDevice) != hipSuccess) return MR_ERR_DEVICE;
-    if (pl->hp.hub) {
-        k.last_launch = 1;
-        if (hipMemcpy(pl->d_args_hub_last, &k, sizeof(KArgs), hipMemcpyHostToDevice) != hipSuccess) return MR_ERR_DEVICE;
-        k.fb_mode = 1;
-        if (hipMemcpy(pl->d_args_fb, &k, sizeof(KArgs), hipMemcpyHostToDevice) != hipSuccess) return MR_ERR_DEVICE;
+    const bool hub = pl->hp.hub;
+    // the pass ends with: the SSSP kernel (no hub), the fill kernel (all-destinations
+    // hub plans), else the fallback launch or a lone hub launch
+    k.last_launch = hub ? 0u : 1u;
+    if (!put(pl->d_args, k)) return MR_ERR_DEVICE;
+    if (hub) {
+        KArgs f = k;
+        f.fb_mode = 1;
+        f.last_launch = pl->all_mode ? 0u : 1u;
+        if (!put(pl->d_args_fb, f)) return MR_ERR_DEVICE;
+        KArgs l = k;
+        l.last_launch = 1;
+        if (!put(pl->all_mode ? pl->d_args_fill : pl->d_args_hub_last, l)) return MR_ERR_DEVICE;
     }
     return MR_OK;
 }
 
 static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *qs, uint32_t n, uint32_t max_cmds,
-                       mr_plan **out) {
+                       mr_plan **out, bool all_mode = false) {
     if (!out || (n && !qs)) return fail(MR_ERR_INVALID_ARG, "null argument");
     *out = nullptr;
     if (!mr_device_available()) return fail(MR_ERR_NO_DEVICE, "no gfx950 device visible (no CPU fallback)");
@@ -683,6 +698,24 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     ka.fb_list = nullptr;
     ka.fb_mode = 0;
     ka.fb_all = std::getenv("MR_HUB_FALLBACK_ALL") ? 1u : 0u;  // tests cover the fallback path
+    pl->all_mode = all_mode;
+    if (all_mode) {  // per source: a record per cell, the label table, the boundary ranks
+        const size_t T = size_t(NS) + 1;
+        if (hipMalloc(reinterpret_cast<void **>(&pl->d_rec), std::max<size_t>(nsrc, 1) * V * sizeof(VRecord)) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&pl->d_tab), std::max<size_t>(nsrc, 1) * T * sizeof(Rec)) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&pl->d_lex), std::max<size_t>(nsrc, 1) * T * 4) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&pl->d_sstate), std::max<size_t>(nsrc, 1) * 4) != hipSuccess)
+            return bail(fail(MR_ERR_DEVICE, "hipMalloc all-destinations outputs"));
+        ka.all_mode = 1;
+        ka.out_rec = pl->d_rec;
+        ka.out_tab = pl->d_tab;
+        ka.out_lex = pl->d_lex;
+        ka.src_state = pl->d_sstate;
+        ka.early_exit_max = 0;  // every cell must settle
+        pl->src_of_input.assign(n, kNone32);
+        for (uint32_t si = 0; si < nsrc; ++si)
+            for (uint32_t k = hp.q_begin[si]; k < hp.q_begin[si + 1]; ++k) pl->src_of_input[hp.q_id[k]] = si;
+    }
     if (hp.hub) {
         if (upload(pl->d_near, *hp.near) != MR_OK ||
             hipMalloc(reinterpret_cast<void **>(&pl->d_fb), std::max<size_t>(nsrc, 1) * 4) != hipSuccess)
@@ -702,7 +735,8 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         if (const char *e = std::getenv("MR_HUB_BLOCKS")) pl->hub_blocks = uint32_t(std::max(1, std::atoi(e)));
         pl->fb_blocks = pl->blocks;
         if (hipMalloc(reinterpret_cast<void **>(&pl->d_args_fb), sizeof(KArgs)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&pl->d_args_hub_last), sizeof(KArgs)) != hipSuccess)
+            hipMalloc(reinterpret_cast<void **>(&pl->d_args_hub_last), sizeof(KArgs)) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&pl->d_args_fill), sizeof(KArgs)) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "kernel args"));
     }
 #ifdef MR_HUBDUMP
@@ -730,6 +764,8 @@ extern "C" int mr_plan_create(const mr_grid *g, const mr_params *prm, const mr_q
     return plan_create(g, prm, qs, n, 16, out);
 }
 
+
+
 extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     if (!pl) return fail(MR_ERR_INVALID_ARG, "null plan");
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : pl->stream;
@@ -739,7 +775,16 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     (void)hipEventRecord(e0, s);
     hipError_t e;
     ++pl->runs;
-    if (pl->hp.hub && pl->fb_none) {
+    if (pl->hp.hub && pl->all_mode) {
+        // hub solve + table export, the SSSP kernel for flagged sources, then the fill
+        const uint32_t gy = std::min<uint32_t>(pl->ka.nsrc, 65535u);
+        const uint32_t gx = std::max<uint32_t>(1u, std::min<uint32_t>((pl->ka.p.V + 1023) / 1024,
+                                                                      std::max<uint32_t>(1u, 262144u / gy)));
+        e = launch_hub(pl->d_args, pl->ka.p.perm, pl->spw, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
+        if (e == hipSuccess && !pl->fb_none)
+            e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, s);
+        if (e == hipSuccess) e = launch_fill(pl->d_args_fill, pl->ka.p.perm, gx, gy, s);
+    } else if (pl->hp.hub && pl->fb_none) {
         // a pass of this plan (same inputs, deterministic result) had no fallback
         // sources: the hub launch ends the pass on its own
         e = launch_hub(pl->d_args_hub_last, pl->ka.p.perm, pl->spw, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
@@ -1025,5 +1070,105 @@ extern "C" int mr_find_path(const mr_grid *g, const mr_params *prm, mr_cell_inde
         return MR_ERR_CAPACITY;
     }
     if (cmds) std::memcpy(cmds, pool.data(), out->n_commands * sizeof(mr_command));
+    return MR_OK;
+}
+
+// ------------------------------------------------------------ all destinations
+extern "C" int mr_sssp_plan_create(const mr_grid *g, const mr_params *prm, const mr_cell_index *sources, uint32_t n,
+                                   mr_plan **out) {
+    if (!g || !prm || !out || (n && !sources)) return fail(MR_ERR_INVALID_ARG, "null argument");
+    std::vector<mr_query> qs(n);
+    for (uint32_t i = 0; i < n; ++i) qs[i].from = qs[i].to = sources[i];
+    const int st = plan_create(g, prm, qs.data(), n, 16, out, true);
+    if (st == MR_OK) {
+        for (uint32_t i = 0; i < n; ++i)
+            if ((*out)->hp.q_status[i] != MR_OK) {
+                mr_plan_destroy(*out);
+                *out = nullptr;
+                return fail(MR_ERR_INVALID_INDEX, "source " + std::to_string(i) + " is not a grid cell");
+            }
+    }
+    return st;
+}
+
+static int sssp_source(mr_plan *pl, uint32_t i, uint32_t &si) {
+    if (!pl || !pl->all_mode) return fail(MR_ERR_INVALID_ARG, "not an all-destinations plan");
+    if (i >= pl->src_of_input.size() || pl->src_of_input[i] == kNone32) return fail(MR_ERR_INVALID_ARG, "source index");
+    si = pl->src_of_input[i];
+    uint32_t flags = 0;
+    return check_device_errors(pl, flags);
+}
+
+extern "C" int mr_sssp_records(mr_plan *pl, uint32_t i, mr_label_record *out) {
+    uint32_t si = 0;
+    if (int st = sssp_source(pl, i, si)) return st;
+    if (!out) return fail(MR_ERR_INVALID_ARG, "null output");
+    static_assert(sizeof(mr_label_record) == sizeof(VRecord), "record layout");
+    if (hipMemcpy(out, pl->d_rec + size_t(si) * pl->ka.p.V, size_t(pl->ka.p.V) * sizeof(VRecord),
+                  hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(MR_ERR_DEVICE, "copy records");
+    return MR_OK;
+}
+
+extern "C" int mr_sssp_device_records(mr_plan *pl, void **d_records, uint64_t *bytes) {
+    if (!pl || !pl->all_mode) return fail(MR_ERR_INVALID_ARG, "not an all-destinations plan");
+    if (d_records) *d_records = pl->d_rec;
+    if (bytes) *bytes = uint64_t(pl->ka.nsrc) * pl->ka.p.V * sizeof(VRecord);
+    return MR_OK;
+}
+
+// The full label of destination dst from source i: the record's boundary chain in
+// the source's label table, plus the final walk (its length is the boundary's
+// grid distance to dst).
+extern "C" int mr_sssp_label(mr_plan *pl, uint32_t i, mr_cell_index dst, mr_result *res, mr_command *cmds, uint32_t cap) {
+    uint32_t si = 0;
+    if (int st = sssp_source(pl, i, si)) return st;
+    if (!res) return fail(MR_ERR_INVALID_ARG, "null result");
+    const mr_grid *g = pl->grid;
+    uint32_t w;
+    if (!g->find(dst, w)) return fail(MR_ERR_INVALID_INDEX, "destination is not a grid cell");
+    const uint32_t T = pl->ka.p.NS + 1;
+    VRecord rec;
+    std::vector<Rec> tab(T);
+    if (hipMemcpy(&rec, pl->d_rec + size_t(si) * pl->ka.p.V + w, sizeof(rec), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(tab.data(), pl->d_tab + size_t(si) * T, T * sizeof(Rec), hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(MR_ERR_DEVICE, "copy label");
+    const uint32_t src = pl->hp.src_v[si];
+    std::vector<OutCmd> seq;
+    auto chain = [&](uint32_t t) {  // commands of table label t (parent 0 ends the chain)
+        std::vector<uint32_t> path;
+        for (uint32_t e = t, guard = 0; e != 0 && guard <= T; e = tab[e].parent, ++guard) path.push_back(e);
+        for (size_t j = path.size(); j-- > 0;)
+            for (uint32_t c = 0; c < tab[path[j]].ntail; ++c)
+                seq.push_back(OutCmd{tab[path[j]].tail[c].kp, tab[path[j]].tail[c].from, tab[path[j]].tail[c].to, 0});
+    };
+    if (rec.via == kViaSource) {
+        seq.push_back(OutCmd{kNoMove << 29, g->rank[src], g->rank[src], 0});
+    } else if (rec.via & kViaSpecial) {
+        const uint32_t t = rec.via & kNone10;
+        if (t >= T) return fail(MR_ERR_DEVICE, "record names no table entry");
+        chain(t);
+    } else {
+        const uint32_t b = rec.via;
+        if (b >= T) return fail(MR_ERR_DEVICE, "record names no boundary");
+        const uint32_t vb = b == 0 ? src : pl->hp.sp[b].v;
+        chain(b);
+        int32_t ax = g->gx(vb), ay = g->gy(vb), bx = g->gx(w), by = g->gy(w);
+        uint32_t k = uint32_t(std::abs(ax - bx) + std::abs(ay - by));
+        if ((ay == 0 && by == 0 && ax != 0 && bx != 0 && ((ax < 0) != (bx < 0))) ||
+            (ax == 0 && bx == 0 && ay != 0 && by != 0 && ((ay < 0) != (by < 0))))
+            k += 2;  // the walk goes round the Center
+        seq.push_back(OutCmd{(kStandard << 29) | k, g->rank[vb], g->rank[w], 0});
+    }
+    std::memset(res, 0, sizeof(*res));
+    res->legs = rec.m0;
+    res->money = rec.m1;
+    res->time_s = int64_t(rec.m2);
+    res->n_commands = uint32_t(seq.size());
+    if (seq.size() > cap || (!cmds && !seq.empty())) {
+        res->status = MR_ERR_CAPACITY;
+        return MR_ERR_CAPACITY;
+    }
+    for (size_t j = 0; j < seq.size(); ++j) expand_cmd(g, pl->hp, seq[j], cmds[j]);
     return MR_OK;
 }

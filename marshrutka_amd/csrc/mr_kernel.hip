@@ -774,8 +774,40 @@ struct Core {
         emit(x, qid);
     }
     __device__ __forceinline__ void write_outputs(uint32_t s_idx) const {
+        if (a->all_mode) {
+            write_all(s_idx);
+            return;
+        }
         const uint32_t q0 = a->q_begin[s_idx], q1 = a->q_begin[s_idx + 1];
         for (uint32_t i = q0 + threadIdx.x; i < q1; i += kBS) write_output(a->q_dst[i], a->q_id[i]);
+    }
+    // all-destinations mode: the label table and a record for every cell (VRecord)
+    __device__ __forceinline__ void write_all(uint32_t s_idx) const {
+        const DevParams &p = P;
+        const unsigned long long tb = (unsigned long long)s_idx * (p.NS + 1);
+        for (uint32_t t = threadIdx.x; t <= p.NS; t += kBS) {
+            a->out_tab[tb + t] = R[t];
+            a->out_lex[tb + t] = kNone32;
+        }
+        VRecord *out = a->out_rec + (unsigned long long)s_idx * p.V;
+        for (uint32_t v = threadIdx.x; v < p.V; v += kBS) {
+            VRecord r{0, 0, 0, kViaSource};
+            const uint32_t sw = ld_state(v);
+            const uint32_t t = special_of(v);
+            if (v == src) {
+            } else if (t != kNone10) {
+                r = VRecord{R[t].m[0], R[t].m[1], R[t].m[2], kViaSpecial | t};
+            } else if (sw & kStSettled) {
+                View x;
+                const uint32_t b = (sw >> kStBShift) & kNone10;
+                view_walk(b, sw & kStKMask, 0, x);
+                r = VRecord{x.m0, x.m1, x.m2, b};
+            } else {
+                flag(kErrBucket);  // every cell of the connected grid settles
+            }
+            out[v] = r;
+        }
+        if (threadIdx.x == 0) a->src_state[s_idx] = 2;
     }
     // 1 if every destination of this source (when <= early_exit_max) is settled
     __device__ __forceinline__ uint32_t dsts_done() const {
@@ -1285,7 +1317,7 @@ __device__ __forceinline__ void finish_launch(const KArgs *__restrict__ a, uint3
     if (written) atomicAdd(c + kCtrWritten, written);
     if (!a->last_launch) return;
     __threadfence();
-    if (atomicAdd(c + kCtrDone, 1u) == gridDim.x - 1) {
+    if (atomicAdd(c + kCtrDone, 1u) == gridDim.x * gridDim.y * gridDim.z - 1) {  // the grid's last workgroup
         __threadfence();
         const uint32_t fb = atomicAdd(c + kCtrFbCount, 0u), wr = atomicAdd(c + kCtrWritten, 0u);
         c[kCtrLastFb] = fb;
@@ -1359,6 +1391,7 @@ template <uint32_t SPW>
 struct HubSolver : Core<false> {
     static constexpr uint32_t LPS = 64 / SPW;
     uint32_t *bnd;          // LDS: this segment's boundary list (table indices; bnd[0] = 0, the source)
+    uint32_t *lexs;         // LDS: all-destinations mode, rank of each table entry among the boundaries
     const uint32_t *nearS;  // LDS: region rows {distance, rank} of every special (row t at t*2*nreg)
     uint32_t *srow;         // LDS: this segment's region row of its source
     uint32_t nreg;
@@ -1579,6 +1612,46 @@ struct HubSolver : Core<false> {
         wave_sync();
     }
 
+    // All-destinations mode: publish the label table and rank the boundaries by
+    // (length, command list) — the order in which their walks tie-break at any cell
+    // (equal metrics and lengths leave the lists to decide, and two walks' lists
+    // first differ inside the boundaries' own labels).  The source (b = 0) ranks first.
+    __device__ __forceinline__ void export_table(bool ok, bool have, bool fallback, uint32_t s_idx, uint32_t nb) const {
+        const DevParams &p = P;
+        const uint32_t t = seg_lane();
+        if (t <= p.NS) lexs[t] = kNone32;
+        wave_sync();
+        if (ok && t < nb) {
+            const uint32_t bj = bnd[t];
+            uint32_t r = 0;
+            for (uint32_t i = 0; i < nb; ++i) {
+                const uint32_t bi = bnd[i];
+                if (bi == bj) continue;
+                bool less;
+                if (bi == 0 || bj == 0) {
+                    less = bi == 0;
+                } else if (R[bi].len != R[bj].len) {
+                    less = R[bi].len < R[bj].len;
+                } else {
+                    View xi, xj;
+                    view_rec(bi, xi);
+                    view_rec(bj, xj);
+                    less = cmp_list(xi, bi, xj, bj) < 0;
+                }
+                r += less ? 1u : 0u;
+            }
+            lexs[bj] = r;
+        }
+        wave_sync();
+        const unsigned long long tb = (unsigned long long)s_idx * (p.NS + 1);
+        if (ok && t <= p.NS) {
+            a->out_tab[tb + t] = R[t];
+            a->out_lex[tb + t] = lexs[t];
+        }
+        if (have && t == 0) a->src_state[s_idx] = fallback ? 2u : 1u;
+        wave_sync();
+    }
+
     // Segment h solves source base + h (none past the end).
     __device__ __forceinline__ void solve(uint32_t base) {
         const DevParams &p = P;
@@ -1700,7 +1773,8 @@ struct HubSolver : Core<false> {
         if (fallback && t == 0) a->fb_list[atomicAdd(counter + kCtrFbCount, 1u)] = s_idx;
         const uint32_t qa = a->q_begin[si], qb = (!have || fallback) ? qa : a->q_begin[si + 1];
         if (t == 0) written += qb - qa;
-        emit_all(qa, qb, nb, sx, sy, st0);
+        if (a->all_mode) export_table(have && !fallback, have, fallback, s_idx, nb);
+        else emit_all(qa, qb, nb, sx, sy, st0);
         MR_HSTAMP(7);
     }
 };
@@ -1709,7 +1783,7 @@ __host__ __device__ constexpr uint32_t align16h(uint32_t x) { return (x + 15u) &
 
 // per-source LDS slots: 4 waves x SPW segments
 struct HubLayout {
-    uint32_t off_sp, off_hubs, off_near, off_srow, off_R, off_bnd, rstride, bstride, sstride, total;
+    uint32_t off_sp, off_hubs, off_near, off_srow, off_R, off_bnd, off_lex, rstride, bstride, sstride, total;
 };
 __host__ __device__ inline HubLayout hub_layout(uint32_t NS, uint32_t nreg, uint32_t spw) {
     HubLayout L{};
@@ -1729,6 +1803,8 @@ __host__ __device__ inline HubLayout hub_layout(uint32_t NS, uint32_t nreg, uint
     o += slots * L.rstride;
     L.bstride = align16h((T + 1) * 4);
     L.off_bnd = o;
+    o += slots * L.bstride;
+    L.off_lex = o;  // per slot: all-destinations mode, the boundaries' ranks (bstride words)
     o += slots * L.bstride;
     L.total = o;
     return L;
@@ -1771,6 +1847,7 @@ __global__ __launch_bounds__(kBS, 5) void hub_kernel(const KArgs *__restrict__ a
     H.src = 0;
     H.src_rk = 0;
     H.bnd = reinterpret_cast<uint32_t *>(smem + L.off_bnd + slot * L.bstride);
+    H.lexs = reinterpret_cast<uint32_t *>(smem + L.off_lex + slot * L.bstride);
     H.nearS = reinterpret_cast<const uint32_t *>(smem + L.off_near);
     H.srow = reinterpret_cast<uint32_t *>(smem + L.off_srow + slot * L.sstride);
     H.nreg = nreg;
@@ -1800,6 +1877,72 @@ __global__ __launch_bounds__(kBS, 5) void hub_kernel(const KArgs *__restrict__ a
         for (int i = 0; i < 9; ++i) atomicAdd(h + i, H.hs[i]);
     }
 #endif
+}
+
+// ===================================================================================
+// All-destinations fill: the record of every cell of every
+// hub-solved source is the best walk from its boundaries — metrics in comparator
+// order, then the boundary's rank (precomputed by the hub kernel).  One grid row
+// of workgroups per source, a strided sweep over the cells, one 16-byte store each.
+// =====================================================================================
+template <uint32_t PERM>
+__global__ __launch_bounds__(kBS) void fill_kernel(const KArgs *__restrict__ a) {
+    constexpr uint32_t q0 = PERM / 9, q1 = (PERM / 3) % 3, q2 = PERM % 3;
+    __shared__ int bx[64], by[64];
+    __shared__ uint32_t bm0[64], bm1[64], bm2[64], bt[64];
+    __shared__ uint32_t nbs;
+    const uint32_t NS = a->p.NS, T = NS + 1, V = a->p.V, S = a->p.S;
+    const int H = int(a->p.H);
+    const uint32_t *sinfo = a->sinfo;
+    for (uint32_t s = blockIdx.y; s < a->nsrc; s += gridDim.y) {
+        __syncthreads();
+        if (a->src_state[s] != 1) continue;  // uniform: solved by the SSSP kernel
+        const unsigned long long tb = (unsigned long long)s * T;
+        const uint32_t src = a->src_v[s];
+        if (threadIdx.x == 0) nbs = 0;
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < T; t += kBS) {
+            const uint32_t r = a->out_lex[tb + t];
+            if (r == kNone32) continue;
+            const Rec &e = a->out_tab[tb + t];
+            bx[r] = t == 0 ? int(src % S) - H : a->sp[t].x;
+            by[r] = t == 0 ? int(src / S) - H : a->sp[t].y;
+            bm0[r] = e.m[0];
+            bm1[r] = e.m[1];
+            bm2[r] = e.m[2];
+            bt[r] = t;
+            atomicAdd(&nbs, 1u);
+        }
+        __syncthreads();
+        const uint32_t nb = nbs;
+        VRecord *out = a->out_rec + (unsigned long long)s * V;
+        for (uint32_t v = blockIdx.x * kBS + threadIdx.x; v < V; v += gridDim.x * kBS) {
+            VRecord rec{0, 0, 0, kViaSource};
+            const uint32_t t = sinfo[v] & kNone10;
+            if (v == src) {
+            } else if (t != kNone10) {
+                const Rec &e = a->out_tab[tb + t];
+                rec = VRecord{e.m[0], e.m[1], e.m[2], kViaSpecial | t};
+            } else {
+                const int wx = int(v % S) - H, wy = int(v / S) - H;
+                uint32_t k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu, k3 = 0xFFFFFFFFu;
+                for (uint32_t r = 0; r < nb; ++r) {  // rank order: the first of equal metrics wins
+                    const uint32_t d = walk_dist(bx[r], by[r], wx, wy);
+                    const uint32_t m[3] = {bm0[r] + d, bm1[r], bm2[r] + 180u * d};
+                    const uint32_t c1 = m[q0], c2 = m[q1], c3 = m[q2];
+                    if (c1 < k1 || (c1 == k1 && (c2 < k2 || (c2 == k2 && c3 < k3)))) {
+                        k1 = c1;
+                        k2 = c2;
+                        k3 = c3;
+                        rec = VRecord{m[0], m[1], m[2], bt[r]};
+                    }
+                }
+            }
+            out[v] = rec;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) finish_launch(a, 0);
 }
 
 // ===================================================================================
@@ -2024,6 +2167,21 @@ hipError_t launch_hub(const KArgs *d_args, const uint32_t perm[3], uint32_t spw,
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
     void *args[] = {const_cast<KArgs **>(&d_args)};
     return hipLaunchKernel(fn, dim3(blocks), dim3(kBS), args, bytes, stream);
+}
+
+hipError_t launch_fill(const KArgs *d_args, const uint32_t perm[3], uint32_t gx, uint32_t gy, hipStream_t stream) {
+    const void *fn = nullptr;
+    switch (perm[0] * 9 + perm[1] * 3 + perm[2]) {
+        case 5: fn = reinterpret_cast<const void *>(&fill_kernel<5>); break;
+        case 7: fn = reinterpret_cast<const void *>(&fill_kernel<7>); break;
+        case 11: fn = reinterpret_cast<const void *>(&fill_kernel<11>); break;
+        case 15: fn = reinterpret_cast<const void *>(&fill_kernel<15>); break;
+        case 19: fn = reinterpret_cast<const void *>(&fill_kernel<19>); break;
+        case 21: fn = reinterpret_cast<const void *>(&fill_kernel<21>); break;
+        default: return hipErrorInvalidValue;
+    }
+    void *args[] = {const_cast<KArgs **>(&d_args)};
+    return hipLaunchKernel(fn, dim3(gx, gy), dim3(kBS), args, 0, stream);
 }
 
 int hub_blocks_per_cu(const uint32_t perm[3], uint32_t spw, uint32_t bytes) {

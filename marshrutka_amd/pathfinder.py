@@ -29,6 +29,7 @@ EXPORTED_SYMBOLS = [
     "mr_plan_num_sources", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_plan_bind_outputs", "mr_abi_version", "mr_last_error",
     "mr_device_available", "mr_parse_map_html", "mr_parse_error", "mr_grid_from_html",
     "mr_command_time", "mr_duration_display", "mr_render_schedule",
+    "mr_sssp_plan_create", "mr_sssp_records", "mr_sssp_device_records", "mr_sssp_label",
 ]
 
 
@@ -94,6 +95,16 @@ def lib():
         L.mr_render_schedule.argtypes = [C.POINTER(mr_command), C.c_uint32, C.c_uint32, C.c_uint32, C.c_char_p,
                                          C.c_uint64, C.POINTER(C.c_uint64)]
         L.mr_render_schedule.restype = C.c_int
+        L.mr_sssp_plan_create.argtypes = [vp, C.POINTER(mr_params), C.POINTER(mr_cell_index), C.c_uint32,
+                                          C.POINTER(vp)]
+        L.mr_sssp_plan_create.restype = C.c_int
+        L.mr_sssp_records.argtypes = [vp, C.c_uint32, vp]
+        L.mr_sssp_records.restype = C.c_int
+        L.mr_sssp_device_records.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_uint64)]
+        L.mr_sssp_device_records.restype = C.c_int
+        L.mr_sssp_label.argtypes = [vp, C.c_uint32, mr_cell_index, C.POINTER(mr_result), C.POINTER(mr_command),
+                                    C.c_uint32]
+        L.mr_sssp_label.restype = C.c_int
         _lib = L
     return _lib
 
@@ -322,3 +333,57 @@ class Plan:
         if h and _lib is not None:
             _lib.mr_plan_destroy(h)
             self.handle = None
+
+
+class SSSPPlan(Plan):
+    """All destinations of each source: run() computes a record for
+    every (source, cell) on the device; label(i, dst) rebuilds the full TotalCost."""
+
+    def __init__(self, grid: MapGrid, params: Params, sources: Sequence[CellIndex]):
+        self.grid = grid
+        self.n = len(sources)
+        self.sources = list(sources)
+        arr = (mr_cell_index * max(self.n, 1))()
+        for i, c in enumerate(sources):
+            arr[i].kind, arr[i].sub, arr[i].x, arr[i].y = c.kind, c.sub, c.x, c.y
+        self._p = params.to_c()
+        h = C.c_void_p()
+        st = lib().mr_sssp_plan_create(grid.handle, C.byref(self._p), arr, self.n, C.byref(h))
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+        self.handle = h
+
+    def records(self, i: int):
+        """(V, 4) uint32 array: legs, money, time, via — row-major cells."""
+        import numpy as np
+        V = self.grid.square_size ** 2
+        out = np.empty((V, 4), dtype=np.uint32)
+        st = lib().mr_sssp_records(self.handle, i, out.ctypes.data)
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+        return out
+
+    def device_records(self):
+        ptr, n = C.c_void_p(), C.c_uint64()
+        st = lib().mr_sssp_device_records(self.handle, C.byref(ptr), C.byref(n))
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+        return ptr.value, n.value
+
+    def label(self, i: int, dst: CellIndex) -> TotalCost:
+        res = mr_result()
+        cap = 64
+        while True:
+            cmds = (mr_command * cap)()
+            st = lib().mr_sssp_label(self.handle, i, dst.to_c(), C.byref(res), cmds, cap)
+            if st == MR_ERR_CAPACITY and res.n_commands > cap:
+                cap = res.n_commands
+                continue
+            break
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+        res.command_offset = 0
+        return result_from_c(res, cmds)
+
+    def fetch(self):
+        raise NotImplementedError("all-destinations plans: use records() / label()")

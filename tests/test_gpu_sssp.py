@@ -1,0 +1,95 @@
+"""All destinations of a source through the C ABI: every cell's
+label rebuilt from its device record must equal the oracle's FindPath::eval,
+for the hub path (fill kernel), sources handed to the SSSP kernel, and the SSSP
+kernel alone (non-linear run times)."""
+import random
+
+import pytest
+
+from golden_util import as_expected
+from marshrutka_amd.abi import SORT_LEGS, SORT_MONEY, SORT_TIME, CellIndex, Params
+from marshrutka_amd.mapgen import SyntheticMap
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from marshrutka_amd import build, pathfinder
+    build.build()
+    if not pathfinder.device_available():
+        pytest.fail("no gfx950 device visible to the GPU tests")
+    return pathfinder
+
+
+@pytest.fixture(params=["auto", "fallback", "sssp"])
+def mode(request, monkeypatch):
+    monkeypatch.delenv("MR_ALGO", raising=False)
+    monkeypatch.delenv("MR_HUB_FALLBACK_ALL", raising=False)
+    if request.param == "fallback":
+        monkeypatch.setenv("MR_HUB_FALLBACK_ALL", "1")
+    if request.param == "sssp":
+        monkeypatch.setenv("MR_ALGO", "sssp")
+    return request.param
+
+
+PARAMS = [Params(), Params(sort_by=(SORT_TIME, SORT_MONEY)), Params(sort_by=(SORT_MONEY, SORT_LEGS), use_sfm=True),
+          Params(fleetfoot=2, sort_by=(SORT_TIME, SORT_LEGS)), Params(route_guru=3, use_soe=False)]
+
+
+def all_labels_match(eng, oracle_lib, m, params, sources):
+    g = eng.MapGrid(m.cells())
+    og = oracle_lib.OracleGrid(m.cells())
+    cells = m.all_indices()
+    plan = eng.SSSPPlan(g, params, sources)
+    plan.run()
+    for i, s in enumerate(sources):
+        exp = og.find_path_batch(params, [(s, d) for d in cells], threads=0)
+        rec = plan.records(i)
+        pos = {c: j for j, (c, _) in enumerate(m.cells())}
+        for d, e in zip(cells, exp):
+            got = plan.label(i, d)
+            assert as_expected(got) == as_expected(e), (params, s, d)
+            r = rec[pos[d]]
+            assert (int(r[0]), int(r[1]), int(r[2])) == (e.legs, e.money, e.time_s)
+
+
+@pytest.mark.parametrize("size,k,clustered", [(9, 2, False), (21, 5, True), (33, 4, False)])
+@pytest.mark.parametrize("pi", range(len(PARAMS)))
+def test_every_cell_matches_oracle(eng, oracle_lib, mode, size, k, clustered, pi):
+    m = SyntheticMap(size, campfires_per_homeland=k, seed=size + pi, clustered=clustered)
+    rng = random.Random(size * 10 + pi)
+    cells = m.all_indices()
+    sources = [CellIndex.center(), m.campfires()[0]] + rng.sample(cells, 2)
+    all_labels_match(eng, oracle_lib, m, PARAMS[pi], sources)
+
+
+def test_repeated_sources_and_reruns(eng, oracle_lib):
+    m = SyntheticMap(15, campfires_per_homeland=3, seed=4)
+    s = m.all_indices()[7]
+    g = eng.MapGrid(m.cells())
+    plan = eng.SSSPPlan(g, Params(), [s, s, m.campfires()[1]])
+    plan.run()
+    a = plan.records(0).copy()
+    plan.run()
+    plan.run()
+    assert (plan.records(1) == a).all() and (plan.records(0) == a).all()
+    assert plan.stats()["num_sources"] == 2
+
+
+def test_c3_sample_1025(eng, oracle_lib):
+    """configs[2]/c3: S = 1025, single source -> all 1 050 625 cells; a sample of
+    destinations against the oracle (one CPU Dijkstra over 1M cells each)."""
+    m = SyntheticMap(1025, campfires_per_homeland=4, seed=4096)
+    g = eng.MapGrid(m.cells())
+    og = oracle_lib.OracleGrid(m.cells())
+    cells = m.all_indices()
+    rng = random.Random(3)
+    sources = rng.sample(cells, 2)
+    plan = eng.SSSPPlan(g, Params(), sources)
+    plan.run()
+    for i, s in enumerate(sources):
+        dsts = rng.sample(cells, 24) + m.campfires()[:2]
+        exp = og.find_path_batch(Params(), [(s, d) for d in dsts], threads=0)
+        for d, e in zip(dsts, exp):
+            assert as_expected(plan.label(i, d)) == as_expected(e), (s, d)
