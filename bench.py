@@ -12,6 +12,8 @@ before the timed region starts.
 Workloads (BASELINE.json configs; odd sides per SURVEY.md §8a A14):
   c2 (default) 10k uniform (src,dst) queries per GPU on a 65x65 synthetic map
                (configs[1]: "10k random (src,dst) batch on 64x64")
+  c3           64 sources per GPU, every destination of each on 1025x1025
+               (configs[2]: single-source -> all-destinations; V queries per source)
   c4           the 1025x1025 map with 1M/8 = 125k queries per GPU
                (configs[3] shard; weak scaling up to the 1M batch at N=8)
 
@@ -38,6 +40,9 @@ WORKLOADS = {
     "c2": dict(size=65, queries_per_gpu=10_000, campfires=4, seed=2024,
                desc="configs[1]: 10k uniform (src,dst) per GPU on a 65x65 synthetic map (64x64 -> odd 65), "
                     "default FindPath params"),
+    "c3": dict(size=1025, queries_per_gpu=64, campfires=4, seed=4096, all_destinations=True,
+               desc="configs[2]: single source -> all 1 050 625 cells of the 1025x1025 synthetic map, 64 sources "
+                    "per GPU; a step answers V queries per source (SURVEY 8d c3)"),
     "c4": dict(size=1025, queries_per_gpu=125_000, campfires=4, seed=4096,
                desc="configs[3] shard: 125k uniform (src,dst) per GPU on a 1025x1025 synthetic map "
                     "(1024 -> odd 1025), default FindPath params; N=8 is the 1M batch"),
@@ -80,6 +85,44 @@ def cpu_baseline_leg(m, params, queries, gpu_results, budget_s):
              "sample": f"first {n} queries of the rank-0 batch, oracle/mr_oracle.cpp (binary heap of full "
                        f"labels + hash map, as the reference) on {threads} host threads, {wall:.2f} s wall; "
                        f"cpu model: {cpu_model()}; nproc {os.cpu_count()}"},
+            {"checked": n, "mismatches": mism})
+
+
+def cpu_baseline_all(m, params, plan, sources, budget_s):
+    """Oracle single-source solves to the cell farthest from each source (a full
+    Dijkstra over the grid, as the reference would need for every destination), on
+    host threads; value = cells answered per second.  The sampled labels are also
+    checked against the GPU's records."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_lib
+    oracle_lib.build()
+    og = oracle_lib.OracleGrid(m.cells())
+    threads = max(1, min(16, os.cpu_count() or 1))
+    H = m.size // 2
+    V = m.size * m.size
+
+    cells = m.all_indices()
+    pos = {c: (j % m.size - H, j // m.size - H) for j, c in enumerate(cells)}
+
+    def far(s):
+        # the opposite corner of the map from the source's quadrant
+        x, y = pos[s]
+        tx, ty = (-H if x >= 0 else H), (-H if y >= 0 else H)
+        return cells[(ty + H) * m.size + (tx + H)]
+
+    t0 = time.perf_counter()
+    og.find_path_batch_raw(params, [(sources[0], far(sources[0]))], threads=1)
+    per = max(time.perf_counter() - t0, 1e-3)
+    n = int(max(1, min(len(sources), threads * max(1, budget_s / per / threads))))
+    sample = [(s, far(s)) for s in sources[:n]]
+    t0 = time.perf_counter()
+    labels = og.find_path_batch(params, sample, threads=threads)
+    wall = time.perf_counter() - t0
+    mism = sum(1 for i, ((s, d), e) in enumerate(zip(sample, labels)) if as_expected(plan.label(i, d)) != as_expected(e))
+    return ({"value": n * V / wall, "unit": "queries/s", "cores": threads, "kind": "port",
+             "sample": f"{n} single-source solves to the farthest cell (~all {V} cells settled each), "
+                       f"oracle/mr_oracle.cpp on {threads} host threads, {wall:.2f} s wall, cells/s; "
+                       f"cpu model: {cpu_model()}"},
             {"checked": n, "mismatches": mism})
 
 
@@ -156,17 +199,27 @@ def main():
     qpg = args.queries or wl["queries_per_gpu"]
     m = SyntheticMap(wl["size"], campfires_per_homeland=wl["campfires"], seed=wl["seed"])
     params = Params()  # the app's defaults (src/app.rs:782-811)
-    all_q = random_queries(m, qpg * world, wl["seed"] + 17)
-    keys = [(a.kind << 40) | (a.sub << 32) | (a.x << 16) | a.y for a, _ in all_q]
-    shards = shard_by_source(keys, world)
-    mine = [all_q[i] for i in shards[rank]]
-    counts = [len(s) for s in shards]
-
+    all_dst = bool(wl.get("all_destinations"))
     grid = pathfinder.MapGrid(m.cells())
-    plan = pathfinder.Plan(grid, params, mine)
-    n_src = plan.num_sources
-    _, rbytes, _, cbytes = plan.device_outputs()
-    if world > 1:
+    if all_dst:
+        # distinct sources, a contiguous block per rank; no cross-rank data path
+        cells = m.all_indices()
+        pick = random_queries(m, 4 * qpg * world, wl["seed"] + 17)
+        srcs = list(dict.fromkeys(a for a, _ in pick))[: qpg * world]
+        mine = srcs[rank * qpg:(rank + 1) * qpg]
+        counts = [qpg * len(cells)] * world  # V queries answered per source
+        plan = pathfinder.SSSPPlan(grid, params, mine)
+        n_src = plan.num_sources
+    else:
+        all_q = random_queries(m, qpg * world, wl["seed"] + 17)
+        keys = [(a.kind << 40) | (a.sub << 32) | (a.x << 16) | a.y for a, _ in all_q]
+        shards = shard_by_source(keys, world)
+        mine = [all_q[i] for i in shards[rank]]
+        counts = [len(s) for s in shards]
+        plan = pathfinder.Plan(grid, params, mine)
+        n_src = plan.num_sources
+        _, rbytes, _, cbytes = plan.device_outputs()
+    if world > 1 and not all_dst:
         # compact result records and command slots in torch-owned device buffers,
         # padded to the largest shard so the gather moves equal-sized rows
         rows, nq = max(counts), max(1, len(mine))
@@ -176,7 +229,7 @@ def main():
 
     def step():
         plan.run(stream.cuda_stream)
-        if world > 1:
+        if world > 1 and not all_dst:
             gather_rows_to_root(res_t, counts, rank, world)
             gather_rows_to_root(cmd_t, counts, rank, world)
 
@@ -209,7 +262,12 @@ def main():
     value = total_queries / elapsed
     V = wl["size"] ** 2
     stats = plan.stats()
-    alg_bytes, kernel_name, survey_bytes = algorithmic_bytes(plan, stats, V)
+    if all_dst:
+        # V x 20 B per solve (the 4 B per-cell word read, the 16 B record written)
+        alg_bytes = survey_bytes = float(n_src) * V * BYTES_PER_VERTEX_SOLVE
+        kernel_name = "hub_kernel + fill_kernel" if stats["solver"] == "hub" else "sssp_kernel"
+    else:
+        alg_bytes, kernel_name, survey_bytes = algorithmic_bytes(plan, stats, V)
     if world > 1:
         t = torch.tensor([alg_bytes, survey_bytes, stats["fallback_sources"]], dtype=torch.float64, device="cuda")
         dist.all_reduce(t)
@@ -253,7 +311,11 @@ def main():
                      if stats["solver"] == "hub" else
                      "SSSP kernel: SURVEY 8d bytes, V*20 B per unique source"},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and all_dst:
+        cb, parity = cpu_baseline_all(m, params, plan, mine, args.cpu_seconds)
+        out["cpu_baseline"] = cb
+        out["parity"] = parity
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline:
         gpu_res = plan.fetch()
         cb, parity = cpu_baseline_leg(m, params, mine, gpu_res, args.cpu_seconds)
         out["cpu_baseline"] = cb
