@@ -139,6 +139,7 @@ struct KArgs {
     Rec *out_tab;                // nsrc * (NS+1)
     uint32_t *out_lex;           // nsrc * (NS+1): rank of boundary t by (length, command list), else kNone32
     uint32_t *src_state;         // nsrc: 1 hub solved (records by the fill kernel), 2 SSSP kernel
+    uint32_t dbg_flags;          // experiments (MR_DBG_FLAGS); 0 in normal runs
 };
 // counter words: the pass's last workgroup copies the fallback and written counts
 // to their "last" slots and zeroes the rest, so no memset precedes a pass

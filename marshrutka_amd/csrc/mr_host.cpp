@@ -562,7 +562,7 @@ struct mr_plan {
     bool fb_none = false;                 // a completed pass of this plan had no fallback sources
     uint32_t runs = 0;
     uint32_t *d_near = nullptr, *d_fb = nullptr;
-    uint32_t hub_blocks = 0, fb_blocks = 0, spw = 1;
+    uint32_t hub_blocks = 0, fb_blocks = 0, spw = 1, cus = 256;
     unsigned long long *d_dbg = nullptr;  // diagnostic builds: per-workgroup phase cycles
     uint32_t algo = kAlgoGeneric;
     SpecialStatic *d_sp = nullptr;
@@ -659,6 +659,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     if (bytes > 160 * 1024) return bail(fail(MR_ERR_LIMIT, "special table exceeds LDS"));
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, pl->device) != hipSuccess) return bail(fail(MR_ERR_DEVICE, "props"));
+    pl->cus = uint32_t(prop.multiProcessorCount);
     int per_cu = std::max(1, max_blocks_per_cu(pl->grid_in_lds, pl->algo, bytes));
     uint64_t resident = uint64_t(per_cu) * uint64_t(prop.multiProcessorCount);
     uint64_t blocks = std::min<uint64_t>(std::max<uint32_t>(nsrc, 1), resident);
@@ -698,6 +699,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     ka.fb_list = nullptr;
     ka.fb_mode = 0;
     ka.fb_all = std::getenv("MR_HUB_FALLBACK_ALL") ? 1u : 0u;  // tests cover the fallback path
+    if (const char *e = std::getenv("MR_DBG_FLAGS")) ka.dbg_flags = uint32_t(std::atoi(e));
     pl->all_mode = all_mode;
     if (all_mode) {  // per source: a record per cell, the label table, the boundary ranks
         const size_t T = size_t(NS) + 1;
@@ -777,9 +779,11 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     ++pl->runs;
     if (pl->hp.hub && pl->all_mode) {
         // hub solve + table export, the SSSP kernel for flagged sources, then the fill
-        const uint32_t gy = std::min<uint32_t>(pl->ka.nsrc, 65535u);
-        const uint32_t gx = std::max<uint32_t>(1u, std::min<uint32_t>((pl->ka.p.V + 1023) / 1024,
-                                                                      std::max<uint32_t>(1u, 262144u / gy)));
+        // (source, 32x32 tile) items over a resident-sized grid
+        const uint64_t items = uint64_t(pl->ka.nsrc) * ((pl->ka.p.S + 31) / 32) * ((pl->ka.p.S + 31) / 32);
+        uint32_t gx = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(items, 8ull * pl->cus)));
+        if (const char *e = std::getenv("MR_FILL_GX")) gx = uint32_t(std::max(1, std::atoi(e)));
+        const uint32_t gy = 1;
         e = launch_hub(pl->d_args, pl->ka.p.perm, pl->spw, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
         if (e == hipSuccess && !pl->fb_none)
             e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, s);

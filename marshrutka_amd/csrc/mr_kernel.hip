@@ -1888,20 +1888,38 @@ __global__ __launch_bounds__(kBS, 5) void hub_kernel(const KArgs *__restrict__ a
 template <uint32_t PERM>
 __global__ __launch_bounds__(kBS) void fill_kernel(const KArgs *__restrict__ a) {
     constexpr uint32_t q0 = PERM / 9, q1 = (PERM / 3) % 3, q2 = PERM % 3;
+    // the leading metric of a walk is base + slope * distance (legs 1, money 0, time 180 s)
+    constexpr uint64_t slope1 = q0 == 0 ? 1u : (q0 == 1 ? 0u : 180u);
+    constexpr int kTile = 32;  // 32 x 32 cells per workgroup pass, 4 per thread
     __shared__ int bx[64], by[64];
     __shared__ uint32_t bm0[64], bm1[64], bm2[64], bt[64];
     __shared__ uint32_t nbs;
+    __shared__ unsigned long long minhi, live;
     const uint32_t NS = a->p.NS, T = NS + 1, V = a->p.V, S = a->p.S;
     const int H = int(a->p.H);
     const uint32_t *sinfo = a->sinfo;
-    for (uint32_t s = blockIdx.y; s < a->nsrc; s += gridDim.y) {
+    const uint32_t tps = (S + kTile - 1) / kTile, ntile = tps * tps;
+    const uint32_t tid = threadIdx.x;
+    // each workgroup takes a contiguous run of (source, tile) items, so the boundary
+    // table is reloaded only when its source changes (and the grid stays small: every
+    // workgroup ends with one atomic on the pass's done counter)
+    const unsigned long long total = (unsigned long long)a->nsrc * ntile;
+    const unsigned long long chunk = (total + gridDim.x - 1) / gridDim.x;
+    const unsigned long long w0 = (unsigned long long)blockIdx.x * chunk;
+    const unsigned long long w1 = w0 + chunk < total ? w0 + chunk : total;
+    for (unsigned long long w = w0; w < w1;) {
+        const uint32_t s = uint32_t(w / ntile);
+        const unsigned long long wend = (unsigned long long)(s + 1) * ntile < w1 ? (unsigned long long)(s + 1) * ntile : w1;
         __syncthreads();
-        if (a->src_state[s] != 1) continue;  // uniform: solved by the SSSP kernel
+        if (a->src_state[s] != 1) {  // uniform: solved by the SSSP kernel
+            w = wend;
+            continue;
+        }
         const unsigned long long tb = (unsigned long long)s * T;
         const uint32_t src = a->src_v[s];
-        if (threadIdx.x == 0) nbs = 0;
+        if (tid == 0) nbs = 0;
         __syncthreads();
-        for (uint32_t t = threadIdx.x; t < T; t += kBS) {
+        for (uint32_t t = tid; t < T; t += kBS) {
             const uint32_t r = a->out_lex[tb + t];
             if (r == kNone32) continue;
             const Rec &e = a->out_tab[tb + t];
@@ -1916,29 +1934,64 @@ __global__ __launch_bounds__(kBS) void fill_kernel(const KArgs *__restrict__ a) 
         __syncthreads();
         const uint32_t nb = nbs;
         VRecord *out = a->out_rec + (unsigned long long)s * V;
-        for (uint32_t v = blockIdx.x * kBS + threadIdx.x; v < V; v += gridDim.x * kBS) {
-            VRecord rec{0, 0, 0, kViaSource};
-            const uint32_t t = sinfo[v] & kNone10;
-            if (v == src) {
-            } else if (t != kNone10) {
-                const Rec &e = a->out_tab[tb + t];
-                rec = VRecord{e.m[0], e.m[1], e.m[2], kViaSpecial | t};
-            } else {
-                const int wx = int(v % S) - H, wy = int(v / S) - H;
-                uint32_t k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu, k3 = 0xFFFFFFFFu;
-                for (uint32_t r = 0; r < nb; ++r) {  // rank order: the first of equal metrics wins
-                    const uint32_t d = walk_dist(bx[r], by[r], wx, wy);
-                    const uint32_t m[3] = {bm0[r] + d, bm1[r], bm2[r] + 180u * d};
-                    const uint32_t c1 = m[q0], c2 = m[q1], c3 = m[q2];
-                    if (c1 < k1 || (c1 == k1 && (c2 < k2 || (c2 == k2 && c3 < k3)))) {
-                        k1 = c1;
-                        k2 = c2;
-                        k3 = c3;
-                        rec = VRecord{m[0], m[1], m[2], bt[r]};
+        for (; w < wend; ++w) {
+            const uint32_t tile = uint32_t(w % ntile);
+            const int tx0 = int(tile % tps) * kTile, ty0 = int(tile / tps) * kTile;
+            const int x0 = tx0 - H, y0 = ty0 - H;
+            const int x1 = min(tx0 + kTile - 1, int(S) - 1) - H, y1 = min(ty0 + kTile - 1, int(S) - 1) - H;
+            if (tid == 0) {
+                minhi = ~0ull;
+                live = 0;
+            }
+            __syncthreads();
+            // Prune the boundaries whose leading metric is beaten everywhere in the tile:
+            // lo_b > min over b' of hi_b' (walks are at least the L1 distance to the tile
+            // and at most the farthest corner's plus the 2-cell detour round the Center).
+            unsigned long long lo = 0;
+            if (tid < nb) {
+                const int bxx = bx[tid], byy = by[tid];
+                const int dx = bxx < x0 ? x0 - bxx : (bxx > x1 ? bxx - x1 : 0);
+                const int dy = byy < y0 ? y0 - byy : (byy > y1 ? byy - y1 : 0);
+                const int fx = max(abs(bxx - x0), abs(bxx - x1)), fy = max(abs(byy - y0), abs(byy - y1));
+                const uint32_t base = q0 == 0 ? bm0[tid] : (q0 == 1 ? bm1[tid] : bm2[tid]);
+                lo = base + slope1 * uint64_t(dx + dy);
+                atomicMin(&minhi, base + slope1 * uint64_t(fx + fy + 2));
+            }
+            __syncthreads();
+            if (tid < nb && (lo <= minhi || (a->dbg_flags & 1u))) atomicOr(&live, 1ull << tid);
+            __syncthreads();
+            const unsigned long long lv = live;
+#pragma unroll
+            for (int part = 0; part < kTile * kTile / kBS; ++part) {
+            const int cx = tx0 + int(tid % kTile), cy = ty0 + int(tid / kTile) + part * (kBS / kTile);
+            if (cx < int(S) && cy < int(S)) {
+                const uint32_t v = uint32_t(cy) * S + uint32_t(cx);
+                VRecord rec{0, 0, 0, kViaSource};
+                const uint32_t t = sinfo[v] & kNone10;
+                if (v == src) {
+                } else if (t != kNone10) {
+                    const Rec &e = a->out_tab[tb + t];
+                    rec = VRecord{e.m[0], e.m[1], e.m[2], kViaSpecial | t};
+                } else {
+                    const int wx = cx - H, wy = cy - H;
+                    uint32_t k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu, k3 = 0xFFFFFFFFu;
+                    for (unsigned long long m = lv; m; m &= m - 1) {  // rank order: the first of equal metrics wins
+                        const uint32_t r = uint32_t(__ffsll((long long)m) - 1);
+                        const uint32_t d = walk_dist(bx[r], by[r], wx, wy);
+                        const uint32_t mm[3] = {bm0[r] + d, bm1[r], bm2[r] + 180u * d};
+                        const uint32_t c1 = mm[q0], c2 = mm[q1], c3 = mm[q2];
+                        if (c1 < k1 || (c1 == k1 && (c2 < k2 || (c2 == k2 && c3 < k3)))) {
+                            k1 = c1;
+                            k2 = c2;
+                            k3 = c3;
+                            rec = VRecord{mm[0], mm[1], mm[2], bt[r]};
+                        }
                     }
                 }
+                out[v] = rec;
             }
-            out[v] = rec;
+            }
+            __syncthreads();
         }
     }
     __syncthreads();
