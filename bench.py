@@ -263,9 +263,14 @@ def main():
     V = wl["size"] ** 2
     stats = plan.stats()
     if all_dst:
-        # V x 20 B per solve (the 4 B per-cell word read, the 16 B record written)
+        # V x 20 B per solve (the 4 B per-cell word read, the 16 B record written),
+        # over the dominant kernel: the fill launch (hub plans) or the whole SSSP pass
         alg_bytes = survey_bytes = float(n_src) * V * BYTES_PER_VERTEX_SOLVE
-        kernel_name = "hub_kernel + fill_kernel" if stats["solver"] == "hub" else "sssp_kernel"
+        fms = plan.fill_ms()
+        if stats["solver"] == "hub" and fms > 0:
+            kernel_name, pass_ms, kms = "fill_kernel", kms, fms
+        else:
+            kernel_name, pass_ms = "sssp_kernel", kms
     else:
         alg_bytes, kernel_name, survey_bytes = algorithmic_bytes(plan, stats, V)
     if world > 1:
@@ -303,9 +308,12 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": kernel_name, "kernel_ms": kms, "launches": nl,
+                     "pass_ms": pass_ms if all_dst else kms,
                      "alg_bytes_per_launch": alg_bytes,
                      "survey_8d_bytes_per_launch": survey_bytes,
-                     "note": ("hub solver: latency-bound per-source wave Dijkstra over the specials; bytes = "
+                     "note": ("all destinations: fill kernel, SURVEY 8d V x 20 B per source (16 B record written, "
+                              "4 B cell word read); pass_ms adds the specials' solve" if all_dst else
+                              "hub solver: latency-bound per-source wave Dijkstra over the specials; bytes = "
                               "queries in, results and command slots out, per-source region rows, plus V*20 B "
                               "per SSSP fallback source (DESIGN.md section 4)")
                      if stats["solver"] == "hub" else

@@ -238,6 +238,9 @@ typedef struct mr_label_record {
  * mr_plan_destroy apply.  Sources may repeat (they share a solve). */
 int mr_sssp_plan_create(const mr_grid *grid, const mr_params *params, const mr_cell_index *sources,
                         uint32_t n_sources, mr_plan **out);
+/* All-destinations plans: the fill launch's average time (ms) over the window the
+ * last mr_plan_kernel_ms call closed (HIP events on the plan's stream). */
+double mr_plan_fill_ms(const mr_plan *plan);
 /* The V records of the caller's source i, in row-major cell order (waits for the plan). */
 int mr_sssp_records(mr_plan *plan, uint32_t i, mr_label_record *out);
 /* Device pointer to all records ([plan source][cell], 16 B each) and their size. */

@@ -561,6 +561,7 @@ struct mr_plan {
     std::vector<uint32_t> src_of_input;   // caller's source i -> plan source index
     bool fb_none = false;                 // a completed pass of this plan had no fallback sources
     uint32_t runs = 0;
+    double fill_ms = 0.0;                 // all-destinations: average fill launch of the last window
     uint32_t *d_near = nullptr, *d_fb = nullptr;
     uint32_t hub_blocks = 0, fb_blocks = 0, spw = 1, cus = 256;
     unsigned long long *d_dbg = nullptr;  // diagnostic builds: per-workgroup phase cycles
@@ -573,6 +574,7 @@ struct mr_plan {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;  // pending event pairs
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> timed_fill;  // all-destinations: fill launches
     int device = 0;
     ~mr_plan() {
         for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_rank_inv, (void *)d_src, (void *)d_qb, (void *)d_qd,
@@ -581,10 +583,11 @@ struct mr_plan {
                         (void *)d_fb, (void *)d_args_hub_last, (void *)d_args_fill, (void *)d_rec, (void *)d_tab,
                         (void *)d_lex, (void *)d_sstate})
             if (p) (void)hipFree(p);
-        for (auto &e : timed) {
-            (void)hipEventDestroy(e.first);
-            (void)hipEventDestroy(e.second);
-        }
+        for (auto *v : {&timed, &timed_fill})
+            for (auto &e : *v) {
+                (void)hipEventDestroy(e.first);
+                (void)hipEventDestroy(e.second);
+            }
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -787,7 +790,10 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         e = launch_hub(pl->d_args, pl->ka.p.perm, pl->spw, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
         if (e == hipSuccess && !pl->fb_none)
             e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, s);
+        hipEvent_t f0 = nullptr;
+        if (e == hipSuccess && hipEventCreate(&f0) == hipSuccess) (void)hipEventRecord(f0, s);
         if (e == hipSuccess) e = launch_fill(pl->d_args_fill, pl->ka.p.perm, gx, gy, s);
+        if (f0) pl->timed_fill.push_back({f0, nullptr});
     } else if (pl->hp.hub && pl->fb_none) {
         // a pass of this plan (same inputs, deterministic result) had no fallback
         // sources: the hub launch ends the pass on its own
@@ -803,6 +809,7 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     }
     (void)hipEventRecord(e1, s);
     pl->timed.push_back({e0, e1});
+    if (!pl->timed_fill.empty() && !pl->timed_fill.back().second) pl->timed_fill.back().second = e1;
     if (e != hipSuccess) return fail(MR_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(e));
     return MR_OK;
 }
@@ -818,6 +825,20 @@ static int read_counters(mr_plan *pl, uint32_t ctr[kCtrWords]) {
 
 extern "C" double mr_plan_kernel_ms(mr_plan *pl, uint32_t *n_launches) {
     if (!pl) return 0.0;
+    // all-destinations passes: the fill launch's own time (its end event is the pass's)
+    double ftot = 0.0;
+    uint32_t kf = 0;
+    for (auto &f : pl->timed_fill) {
+        (void)hipEventSynchronize(f.second);
+        float ms = 0.f;
+        if (f.second && hipEventElapsedTime(&ms, f.first, f.second) == hipSuccess) {
+            ftot += ms;
+            ++kf;
+        }
+        (void)hipEventDestroy(f.first);
+    }
+    pl->timed_fill.clear();
+    pl->fill_ms = kf ? ftot / kf : 0.0;
     double tot = 0.0;
     uint32_t k = 0;
     for (auto &e : pl->timed) {
@@ -846,6 +867,8 @@ extern "C" int mr_plan_bind_outputs(mr_plan *pl, void *d_results, void *d_comman
 }
 
 extern "C" uint32_t mr_plan_num_sources(const mr_plan *pl) { return pl ? pl->ka.nsrc : 0; }
+
+extern "C" double mr_plan_fill_ms(const mr_plan *pl) { return pl ? pl->fill_ms : 0.0; }
 
 extern "C" int mr_plan_get_stats(mr_plan *pl, mr_plan_stats *out) {
     if (!pl || !out) return fail(MR_ERR_INVALID_ARG, "null argument");

@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = [
     "mr_plan_num_sources", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_plan_bind_outputs", "mr_abi_version", "mr_last_error",
     "mr_device_available", "mr_parse_map_html", "mr_parse_error", "mr_grid_from_html",
     "mr_command_time", "mr_duration_display", "mr_render_schedule",
-    "mr_sssp_plan_create", "mr_sssp_records", "mr_sssp_device_records", "mr_sssp_label",
+    "mr_sssp_plan_create", "mr_sssp_records", "mr_sssp_device_records", "mr_sssp_label", "mr_plan_fill_ms",
 ]
 
 
@@ -105,6 +105,8 @@ def lib():
         L.mr_sssp_label.argtypes = [vp, C.c_uint32, mr_cell_index, C.POINTER(mr_result), C.POINTER(mr_command),
                                     C.c_uint32]
         L.mr_sssp_label.restype = C.c_int
+        L.mr_plan_fill_ms.argtypes = [vp]
+        L.mr_plan_fill_ms.restype = C.c_double
         _lib = L
     return _lib
 
@@ -384,6 +386,10 @@ class SSSPPlan(Plan):
             raise EngineError(st, last_error())
         res.command_offset = 0
         return result_from_c(res, cmds)
+
+    def fill_ms(self) -> float:
+        """Average fill-kernel time of the window the last kernel_ms() closed."""
+        return lib().mr_plan_fill_ms(self.handle)
 
     def fetch(self):
         raise NotImplementedError("all-destinations plans: use records() / label()")

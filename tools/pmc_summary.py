@@ -22,7 +22,7 @@ import json
 import os
 from collections import defaultdict
 
-SOLVE_KERNELS = ("hub_kernel", "solve_kernel")
+SOLVE_KERNELS = ("hub_kernel", "solve_kernel", "fill_kernel")
 
 
 def per_dispatch(path: str, counter: str):
@@ -49,9 +49,11 @@ def main():
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--kernels", default="", help="comma-separated kernels the roofline prices (default: all solve kernels)")
     a = ap.parse_args()
-    fe = per_dispatch(a.fetch, "FETCH_SIZE")
-    wr = per_dispatch(a.write, "WRITE_SIZE")
+    keep = set(a.kernels.split(",")) if a.kernels else set(SOLVE_KERNELS)
+    fe = {k: v for k, v in per_dispatch(a.fetch, "FETCH_SIZE").items() if k in keep}
+    wr = {k: v for k, v in per_dispatch(a.write, "WRITE_SIZE").items() if k in keep}
     read_b = sum(2.0 * kb * 1024.0 for kb, _ in fe.values())   # gfx950: FETCH_SIZE = 1/2 of the bytes
     write_b = sum(kb * 1024.0 for kb, _ in wr.values())
     out = {
