@@ -1812,8 +1812,11 @@ __host__ __device__ inline HubLayout hub_layout(uint32_t NS, uint32_t nreg, uint
 
 // PERM = comparator order c1 c2 c3 as metric indices (9*c1 + 3*c2 + c3): a compile-time
 // constant here, so every metric selection and comparison folds.  SPW = sources per wave.
+#ifndef MR_HUB_WAVES
+#define MR_HUB_WAVES 5  // waves per SIMD the register budget is cut for (measured best)
+#endif
 template <uint32_t PERM, uint32_t SPW>
-__global__ __launch_bounds__(kBS, 5) void hub_kernel(const KArgs *__restrict__ a) {
+__global__ __launch_bounds__(kBS, MR_HUB_WAVES) void hub_kernel(const KArgs *__restrict__ a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint32_t NS = a->p.NS, nreg = a->nreg;
     const HubLayout L = hub_layout(NS, nreg, SPW);
