@@ -217,3 +217,14 @@ def test_parameter_sweep(eng, oracle_lib, params):
         hq = m.campfires()[-1]
         for p in (params, Params(**{**params.__dict__, "hq_position": hq})):
             check(eng, oracle_lib, m, p, random_queries(m, 150, seed + 1), f"S={size} {p}")
+
+
+@pytest.mark.parametrize("k,clustered", [(16, False), (40, True), (64, True)])
+def test_many_campfires(eng, oracle_lib, grid_state, k, clustered):
+    """More than 63 specials (SURVEY c5 has 64 clustered campfires per homeland): the
+    hub solver steps aside and the SSSP kernel settles the specials through its LDS
+    argmin; Time- and Money-first orders as c5 prescribes."""
+    m = SyntheticMap(41, campfires_per_homeland=k, seed=k, clustered=clustered)
+    for params in (Params(), Params(sort_by=(SORT_TIME, SORT_LEGS)), Params(sort_by=(SORT_MONEY, SORT_TIME)),
+                   Params(sort_by=(SORT_TIME, SORT_MONEY), fleetfoot=2, route_guru=4)):
+        check(eng, oracle_lib, m, params, random_queries(m, 150, k + 1), f"k={k} {params}")
