@@ -16,6 +16,9 @@ Workloads (BASELINE.json configs; odd sides per SURVEY.md §8a A14):
                (configs[2]: single-source -> all-destinations; V queries per source)
   c4           the 1025x1025 map with 1M/8 = 125k queries per GPU
                (configs[3] shard; weak scaling up to the 1M batch at N=8)
+  c5           10k uniform queries per GPU on a 4097x4097 map with 64 clustered
+               campfires per homeland (261 specials), Time first (configs[4],
+               SURVEY 8d c5 option a)
 
 N>1 is launched by the driver as
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -46,6 +49,10 @@ WORKLOADS = {
     "c4": dict(size=1025, queries_per_gpu=125_000, campfires=4, seed=4096,
                desc="configs[3] shard: 125k uniform (src,dst) per GPU on a 1025x1025 synthetic map "
                     "(1024 -> odd 1025), default FindPath params; N=8 is the 1M batch"),
+    "c5": dict(size=4097, queries_per_gpu=10_000, campfires=64, clustered=True, seed=4097, sort=(1, 2),
+               desc="configs[4]: 10k uniform (src,dst) per GPU on a 4097x4097 synthetic map (4096 -> odd 4097) "
+                    "with 64 clustered campfires per homeland (261 specials); sort_by (Time, Money), so caravan "
+                    "edges span 102 s .. 240 s x 2S (SURVEY 8d c5 option a)"),
 }
 
 
@@ -68,14 +75,17 @@ def cpu_baseline_leg(m, params, queries, gpu_results, budget_s):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_lib
     oracle_lib.build()
-    og = oracle_lib.OracleGrid(m.cells())
+    og = oracle_lib.OracleGrid.from_array(m.cells_array())
     threads = max(1, min(16, os.cpu_count() or 1))
-    # calibrate on a small single-threaded sample, then size the run to ~budget CPU-seconds
-    cal = queries[:64]
+    # calibrate single-threaded (up to 64 queries or ~2 s), then size the run to
+    # ~budget CPU-seconds (at least one query per thread)
     t0 = time.perf_counter()
-    og.find_path_batch_raw(params, cal, threads=1)
-    per_q = max((time.perf_counter() - t0) / len(cal), 1e-6)
-    n = int(min(len(queries), max(256, budget_s / per_q)))
+    done = 0
+    while done < min(64, len(queries)) and (done == 0 or time.perf_counter() - t0 < 2.0):
+        og.find_path_batch_raw(params, queries[done:done + 1], threads=1)
+        done += 1
+    per_q = max((time.perf_counter() - t0) / done, 1e-6)
+    n = int(min(len(queries), max(min(256, 16 * threads) if per_q < 0.05 else threads, budget_s / per_q)))
     sample = queries[:n]
     t0 = time.perf_counter()
     labels = og.find_path_batch(params, sample, threads=threads)
@@ -96,7 +106,7 @@ def cpu_baseline_all(m, params, plan, sources, budget_s):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_lib
     oracle_lib.build()
-    og = oracle_lib.OracleGrid(m.cells())
+    og = oracle_lib.OracleGrid.from_array(m.cells_array())
     threads = max(1, min(16, os.cpu_count() or 1))
     H = m.size // 2
     V = m.size * m.size
@@ -138,7 +148,7 @@ def algorithmic_bytes(plan, stats, V):
     fallback.  Returns (bytes, kernel name, SURVEY-8d-equivalent bytes)."""
     n_src = stats["num_sources"]
     survey = float(n_src) * V * BYTES_PER_VERTEX_SOLVE
-    if stats["solver"] != "hub":
+    if stats["solver"] not in ("hub", "hub_wide"):
         return survey, "sssp_kernel", survey
     import numpy as np
     res, _ = plan.fetch_raw()
@@ -147,8 +157,10 @@ def algorithmic_bytes(plan, stats, V):
     n_cmds = int(words[ok, 4].astype(np.int64).sum())
     nq = plan.n
     b = nq * (8 + 4 + 16) + 16 * n_cmds + n_src * (8 + 8 * stats["num_regions"])
+    b += 8 * stats["region_boundary_cells"]  # wide solver: the regions' boundary cells, read once (L2-resident)
     b += stats["fallback_sources"] * V * BYTES_PER_VERTEX_SOLVE
-    name = "hub_kernel" + (" + sssp_kernel (fallback)" if stats["fallback_sources"] else "")
+    kern = "hub_wide_kernel" if stats["solver"] == "hub_wide" else "hub_kernel"
+    name = kern + (" + sssp_kernel (fallback)" if stats["fallback_sources"] else "")
     return float(b), name, survey
 
 
@@ -177,7 +189,7 @@ def main():
     from marshrutka_amd import build, pathfinder
     from marshrutka_amd.abi import Params
     from marshrutka_amd.mapgen import SyntheticMap, random_queries
-    from marshrutka_amd.shard import gather_rows_to_root, shard_by_source
+    from marshrutka_amd.shard import PipelinedGather, shard_by_source
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -197,10 +209,12 @@ def main():
 
     wl = dict(WORKLOADS[args.workload])
     qpg = args.queries or wl["queries_per_gpu"]
-    m = SyntheticMap(wl["size"], campfires_per_homeland=wl["campfires"], seed=wl["seed"])
-    params = Params()  # the app's defaults (src/app.rs:782-811)
+    m = SyntheticMap(wl["size"], campfires_per_homeland=wl["campfires"], seed=wl["seed"],
+                     clustered=bool(wl.get("clustered")))
+    # the app's defaults (src/app.rs:782-811), with the workload's sort order
+    params = Params(sort_by=wl["sort"]) if "sort" in wl else Params()
     all_dst = bool(wl.get("all_destinations"))
-    grid = pathfinder.MapGrid(m.cells())
+    grid = pathfinder.MapGrid.from_array(m.cells_array())
     if all_dst:
         # distinct sources, a contiguous block per rank; no cross-rank data path
         cells = m.all_indices()
@@ -216,38 +230,58 @@ def main():
         shards = shard_by_source(keys, world)
         mine = [all_q[i] for i in shards[rank]]
         counts = [len(s) for s in shards]
-        plan = pathfinder.Plan(grid, params, mine)
+        # N > 1: two plans over the same shard, so the result gather of one batch
+        # overlaps the solve of the next (double buffering, shard.PipelinedGather)
+        depth = 2 if world > 1 else 1
+        plans = [pathfinder.Plan(grid, params, mine) for _ in range(depth)]
+        plan = plans[0]
         n_src = plan.num_sources
         _, rbytes, _, cbytes = plan.device_outputs()
+    pipe = None
     if world > 1 and not all_dst:
-        # compact result records and command slots in torch-owned device buffers,
-        # padded to the largest shard so the gather moves equal-sized rows
+        # result records then command slots in one flat torch-owned device buffer
+        # per plan, padded to the largest shard: one RCCL gather per batch
         rows, nq = max(counts), max(1, len(mine))
-        res_t = torch.zeros((rows, rbytes // nq // 4), dtype=torch.int32, device="cuda")
-        cmd_t = torch.zeros((rows, cbytes // nq // 4), dtype=torch.int32, device="cuda")
-        plan.bind_outputs(res_t.data_ptr(), cmd_t.data_ptr())
+        rw, cw = rbytes // nq // 4, cbytes // nq // 4
+        bufs = [torch.zeros(rows * (rw + cw), dtype=torch.int32, device="cuda") for _ in plans]
+        for p_, b in zip(plans, bufs):
+            p_.bind_outputs(b.data_ptr(), b.data_ptr() + rows * rw * 4)
+        pipe = PipelinedGather(bufs, rank, world)
+    elif all_dst:
+        plans = [plan]
+    it = [0]
 
     def step():
-        plan.run(stream.cuda_stream)
-        if world > 1 and not all_dst:
-            gather_rows_to_root(res_t, counts, rank, world)
-            gather_rows_to_root(cmd_t, counts, rank, world)
+        k = it[0] % len(plans)
+        it[0] += 1
+        if pipe is not None:
+            pipe.reuse(k)  # the stream waits until batch k-2's gather has read this buffer
+        plans[k].run(stream.cuda_stream)
+        if pipe is not None:
+            pipe.issue(k)
 
     for _ in range(args.warmup):
         step()
+    if pipe is not None:
+        pipe.drain()
     torch.cuda.synchronize()
-    plan.kernel_ms()  # reset the per-launch event window to the timed region
+    for p_ in plans:
+        p_.kernel_ms()  # reset the per-launch event window to the timed region
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    if pipe is not None:
+        pipe.drain()  # every batch's results are at rank 0 inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kms, nl = plan.kernel_ms()
+    kn = [p_.kernel_ms() for p_ in plans]
+    nl = sum(n for _, n in kn)
+    kms = sum(ms * n for ms, n in kn) / nl if nl else 0.0
     if world > 1:
         t = torch.tensor([elapsed, kms], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -300,10 +334,12 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
         "config": {"workload": wl["desc"], "grid": f"{wl['size']}x{wl['size']}", "queries_per_gpu": qpg,
                    "campfires_per_homeland": wl["campfires"], "unique_sources_per_step": tot_src,
-                   "params": "FindPath defaults: sort (Legs,Money), SoE 50, caravans, skills 0, homeland Blue",
+                   "params": "FindPath defaults: sort " + ("(Time,Money)" if wl.get("sort") == (1, 2) else
+                                                           "(Legs,Money)") + ", SoE 50, caravans, skills 0, homeland Blue",
                    "solver": stats["solver"], "fallback_sources_per_step": fb_total,
                    "specials": stats["num_specials"],
-                   "parallelism": f"sources sharded over {world} GPU(s), RCCL gather of results to rank 0"
+                   "parallelism": f"sources sharded over {world} GPU(s), RCCL gather of results to rank 0 "
+                                  "(double-buffered: overlaps the next batch's solve)"
                                   if world > 1 else "1 GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -316,7 +352,7 @@ def main():
                               "hub solver: latency-bound per-source wave Dijkstra over the specials; bytes = "
                               "queries in, results and command slots out, per-source region rows, plus V*20 B "
                               "per SSSP fallback source (DESIGN.md section 4)")
-                     if stats["solver"] == "hub" else
+                     if stats["solver"] in ("hub", "hub_wide") else
                      "SSSP kernel: SURVEY 8d bytes, V*20 B per unique source"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and all_dst:

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MR_ABI_VERSION 1u
+#define MR_ABI_VERSION 2u
 
 /* ---- status codes ------------------------------------------------------ */
 typedef enum mr_status {
@@ -186,13 +186,21 @@ typedef struct mr_plan mr_plan;
  * queries by source.  Inputs stay resident in HBM across mr_plan_run calls. */
 int mr_plan_create(const mr_grid *grid, const mr_params *params, const mr_query *queries,
                    uint32_t n, mr_plan **out);
+/* The same with `max_cmds` (1..4096) command slots per query in the compact
+ * device output (mr_plan_create: 16).  A label with more commands goes to the
+ * plan's overflow pool (8 commands per query) and mr_plan_fetch returns it in
+ * full; only when that pool is exhausted does it report MR_ERR_CAPACITY. */
+int mr_plan_create_ex(const mr_grid *grid, const mr_params *params, const mr_query *queries,
+                      uint32_t n, uint32_t max_cmds, mr_plan **out);
 /* Enqueues one full pass of the hot path on `stream` (a hipStream_t, or NULL
  * for the plan's own stream).  Asynchronous. */
 int mr_plan_run(mr_plan *plan, void *stream);
 /* Waits for the plan's work and copies results/commands to host buffers. */
 int mr_plan_fetch(mr_plan *plan, mr_result *results, mr_command *pool, uint64_t pool_cap);
 /* Device pointers of the compact per-query output records (for an RCCL
- * gather): n * 16 B result records and n * max_cmds * 16 B command slots. */
+ * gather): n * 16 B result records and n * max_cmds * 16 B command slots.
+ * A label longer than max_cmds keeps {0xFFFFFFFF, offset, count} in its first
+ * slot and its commands in the plan's own overflow pool. */
 int mr_plan_device_outputs(mr_plan *plan, void **d_results, uint64_t *results_bytes,
                            void **d_commands, uint64_t *commands_bytes);
 /* Makes subsequent mr_plan_run calls write their compact outputs into caller
@@ -207,7 +215,8 @@ uint32_t mr_plan_num_sources(const mr_plan *plan);
 enum {
     MR_SOLVER_BUCKETED = 0, /* SSSP kernel, bucketed settling (any comparator) */
     MR_SOLVER_LEVELS = 1,   /* SSSP kernel, level-synchronous (Legs-first comparator) */
-    MR_SOLVER_HUB = 2       /* closed-form hub solver (linear run time) + SSSP fallback */
+    MR_SOLVER_HUB = 2,      /* closed-form hub solver (linear run time) + SSSP fallback */
+    MR_SOLVER_HUB_WIDE = 3  /* the same for 64..511 specials or no vertex x region table */
 };
 typedef struct mr_plan_stats {
     uint32_t solver;            /* MR_SOLVER_* */
@@ -218,6 +227,8 @@ typedef struct mr_plan_stats {
     uint32_t num_regions;       /* hub solver: Scroll-of-Escape regions of the homeland */
     uint32_t hub_workgroups;    /* hub launch size (4 waves each) */
     uint32_t sssp_workgroups;   /* SSSP launch size */
+    uint32_t specials_per_lane; /* hub solver: table entries each lane owns (1 = one per lane) */
+    uint32_t region_boundary_cells; /* MR_SOLVER_HUB_WIDE: cells scanned for each source's region row */
 } mr_plan_stats;
 /* Fills *out; waits for the plan's stream.  MR_OK or MR_ERR_INVALID_ARG. */
 int mr_plan_get_stats(mr_plan *plan, mr_plan_stats *out);

@@ -140,6 +140,15 @@ struct KArgs {
     uint32_t *out_lex;           // nsrc * (NS+1): rank of boundary t by (length, command list), else kNone32
     uint32_t *src_state;         // nsrc: 1 hub solved (records by the fill kernel), 2 SSSP kernel
     uint32_t dbg_flags;          // experiments (MR_DBG_FLAGS); 0 in normal runs
+    // wide hub solver (hub_wide_kernel): the specials' region rows ((NS+1) x nreg x
+    // {distance, rank}) and each region's boundary cells, {x | y << 16 (int16), rank},
+    // region r at rb_cell[rb_off[r] .. rb_off[r+1])
+    const uint32_t *near_sp;
+    const uint32_t *rb_off;
+    const uint32_t *rb_cell;
+    // labels longer than max_cmds: their commands in this pool (bump-allocated per pass)
+    OutCmd *ovf;
+    uint32_t ovf_cap;
 };
 // counter words: the pass's last workgroup copies the fallback and written counts
 // to their "last" slots and zeroes the rest, so no memset precedes a pass
@@ -152,8 +161,13 @@ enum : uint32_t {
     kCtrDone = 5,         // workgroups of the last kernel that finished
     kCtrWritten = 6,      // result records written
     kCtrLastWritten = 7,  // kCtrWritten of the last completed pass
-    kCtrWords = 8
+    kCtrOvf = 8,          // command-overflow pool: commands allocated in this pass
+    kCtrLastOvf = 9,      // kCtrOvf of the last completed pass
+    kCtrWords = 10
 };
+// result status (OutResult high half - 16) of a label whose commands went to the
+// overflow pool: its first command slot holds {kOvfTag, offset, count}
+constexpr uint32_t kStatusOverflow = 64u, kOvfTag = 0xFFFFFFFFu;
 enum : uint32_t { kAlgoGeneric = 0, kAlgoLegs = 1 };
 
 constexpr uint32_t kErrKOverflow = 1u, kErrMetricOverflow = 2u, kErrBucket = 4u, kErrChain = 8u;

@@ -28,6 +28,11 @@ hipError_t launch_hub(const KArgs *d_args, const uint32_t perm[3], uint32_t spw,
                       uint32_t blocks, hipStream_t stream);
 hipError_t launch_fill(const KArgs *d_args, const uint32_t perm[3], uint32_t gx, uint32_t gy, hipStream_t stream);
 int hub_blocks_per_cu(const uint32_t perm[3], uint32_t spw, uint32_t bytes);
+uint32_t hub_wide_lds_bytes(uint32_t NS, uint32_t nreg);
+uint32_t hub_wide_spl(uint32_t NS);
+hipError_t launch_hub_wide(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t blocks,
+                           hipStream_t stream);
+int hub_wide_blocks_per_cu(const uint32_t perm[3], uint32_t NS, uint32_t bytes);
 }  // namespace mr
 
 
@@ -122,6 +127,10 @@ struct mr_grid {
     mutable std::vector<uint32_t> regions[4];
     mutable std::vector<uint32_t> near[4];
     mutable bool near_built[4] = {false, false, false, false};
+    // wide hub solver: per homeland, each region's boundary cells (cells of the region
+    // with a neighbour outside it, the Center excluded), {x | y << 16, rank}, by region
+    mutable std::vector<uint32_t> rb_off[4], rb_cell[4];
+    mutable bool rb_built[4] = {false, false, false, false};
     int32_t gx(uint32_t v) const { return int32_t(v % S) - int32_t(H); }
     int32_t gy(uint32_t v) const { return int32_t(v / S) - int32_t(H); }
     bool find(const mr_cell_index &c, uint32_t &v) const {
@@ -348,6 +357,61 @@ static const std::vector<uint32_t> &region_table(const mr_grid *g, int h, const 
     return g->near[h];
 }
 
+// Boundary cells of the regions (wide hub solver).  Seen from outside a region, its
+// nearest cell (walk distance avoiding the Center, ties by rank) is a boundary cell:
+// the last step of a shortest walk enters it from a non-Center cell outside.
+static uint32_t host_walk_dist(int ax, int ay, int bx, int by) {
+    uint32_t d = uint32_t(std::abs(ax - bx) + std::abs(ay - by));
+    if ((ay == 0 && by == 0 && ax != 0 && bx != 0 && ((ax < 0) != (bx < 0))) ||
+        (ax == 0 && bx == 0 && ay != 0 && by != 0 && ((ay < 0) != (by < 0))))
+        d += 2;
+    return d;
+}
+static void region_bounds(const mr_grid *g, int h, std::vector<uint32_t> &regs, const std::vector<uint32_t> *&off,
+                          const std::vector<uint32_t> *&cell) {
+    std::lock_guard<std::mutex> lk(g->near_mu);
+    regs.clear();
+    for (uint32_t v : g->campfires) {
+        const mr_cell_index &c = g->idx[v];
+        if (c.kind == MR_CELL_HOMELAND && c.sub == h) regs.push_back(v);  // CellIndex order
+    }
+    off = &g->rb_off[h];
+    cell = &g->rb_cell[h];
+    if (g->rb_built[h]) return;
+    const uint32_t V = g->V, S = g->S, nreg = uint32_t(regs.size());
+    std::unordered_map<uint32_t, uint32_t> rid;
+    for (uint32_t r = 0; r < nreg; ++r) rid[regs[r]] = r;
+    const std::vector<uint32_t> &near = g->nearest[h];
+    std::vector<uint32_t> cnt(nreg + 1, 0), which;
+    std::vector<uint32_t> list;
+    for (uint32_t v = 0; v < V; ++v) {
+        if (v == g->vc || near[v] == kNone32) continue;
+        const uint32_t x = v % S, y = v / S;
+        const uint32_t nb[4] = {x > 0 ? v - 1 : kNone32, x + 1 < S ? v + 1 : kNone32, y > 0 ? v - S : kNone32,
+                                y + 1 < S ? v + S : kNone32};
+        bool edge = false;
+        for (uint32_t w : nb)
+            if (w != kNone32 && w != g->vc && near[w] != near[v]) edge = true;
+        if (!edge) continue;
+        auto it = rid.find(near[v]);
+        if (it == rid.end()) continue;
+        list.push_back(v);
+        which.push_back(it->second);
+        ++cnt[it->second + 1];
+    }
+    std::vector<uint32_t> o(nreg + 1, 0);
+    for (uint32_t r = 0; r < nreg; ++r) o[r + 1] = o[r] + cnt[r + 1];
+    std::vector<uint32_t> cells(size_t(o[nreg]) * 2), pos(o.begin(), o.end() - 1);
+    for (size_t i = 0; i < list.size(); ++i) {
+        const uint32_t v = list[i], k = pos[which[i]]++;
+        cells[2 * k] = (uint32_t(uint16_t(int16_t(g->gx(v))))) | (uint32_t(uint16_t(int16_t(g->gy(v)))) << 16);
+        cells[2 * k + 1] = g->rank[v];
+    }
+    g->rb_off[h] = std::move(o);
+    g->rb_cell[h] = std::move(cells);
+    g->rb_built[h] = true;
+}
+
 // ------------------------------------------------------------------ planning
 namespace {
 
@@ -363,6 +427,9 @@ struct HostPlan {
     bool hub = false;                       // hub solver applicable (linear run time, small tables)
     const std::vector<uint32_t> *near = nullptr;
     uint32_t nreg = 0;
+    bool wide = false;                      // hub_wide_kernel (NS > 63 or no V x regions table)
+    std::vector<uint32_t> near_sp;          // wide: (NS+1) x nreg x {distance, rank} rows of the specials
+    const std::vector<uint32_t> *rb_off = nullptr, *rb_cell = nullptr;
 };
 
 // (c1, c2) -> (c1, c2', c3): CostComparator::eval_next (src/cost.rs:387-405)
@@ -461,24 +528,62 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     // hub solver: exact when the StandardMove run time is linear (Fleetfoot level 0 or out
     // of range) — see DESIGN.md §3b; the one non-isotone case is detected per source
     // and re-solved by the SSSP kernel.  MR_ALGO=sssp|generic disables it.
-    hp.hub = (p.ff_num == p.ff_den) && NS <= 63;
+    // hub solver: exact when the StandardMove run time is linear (Fleetfoot level 0 or out
+    // of range) — see DESIGN.md §3b; the one non-isotone case is detected per source
+    // and re-solved by the SSSP kernel.  MR_ALGO=sssp|generic disables it.  Up to 63
+    // specials and a V x regions table of <= 2 GB: one special per lane (hub_kernel);
+    // otherwise up to 511 specials with boundary-scanned region rows (hub_wide_kernel,
+    // forced by MR_HUB_WIDE=1 for the tests).
+    bool linear = p.ff_num == p.ff_den;
     if (const char *e = std::getenv("MR_ALGO"))
-        if (!std::strcmp(e, "sssp") || !std::strcmp(e, "generic")) hp.hub = false;
-    if (hp.hub) {
-        size_t nregs = 0;
-        for (uint32_t v : g->campfires)
-            if (g->idx[v].kind == MR_CELL_HOMELAND && g->idx[v].sub == prm->homeland) ++nregs;
-        if (nregs > 63 || size_t(V) * nregs * 8 > (size_t(2) << 30)) hp.hub = false;  // table budget
-    }
-    if (hp.hub) {
+        if (!std::strcmp(e, "sssp") || !std::strcmp(e, "generic")) linear = false;
+    size_t nregs = 0;
+    for (uint32_t v : g->campfires)
+        if (g->idx[v].kind == MR_CELL_HOMELAND && g->idx[v].sub == prm->homeland) ++nregs;
+    const char *fw = std::getenv("MR_HUB_WIDE");
+    const bool force_wide = fw && !std::strcmp(fw, "1");
+    const bool narrow_ok = NS <= 63 && nregs <= 63 && size_t(V) * nregs * 8 <= (size_t(2) << 30);
+    hp.hub = hp.wide = false;
+    if (linear && narrow_ok && !force_wide) {
         const std::vector<uint32_t> *regs = nullptr;
         const std::vector<uint32_t> &tab = region_table(g, prm->homeland, regs);
+        hp.hub = true;
         hp.nreg = uint32_t(regs->size());
-        if (hp.nreg > 63) {
-            hp.hub = false;
-        } else {
-            hp.near = &tab;
-            for (uint32_t r = 0; r < hp.nreg; ++r) hp.sp[tix[(*regs)[r]]].rid = r;
+        hp.near = &tab;
+        for (uint32_t r = 0; r < hp.nreg; ++r) hp.sp[tix[(*regs)[r]]].rid = r;
+    } else if (linear && hub_wide_spl(NS) != 0 && nregs <= 256) {
+        std::vector<uint32_t> regs;
+        region_bounds(g, prm->homeland, regs, hp.rb_off, hp.rb_cell);
+        hp.hub = hp.wide = true;
+        hp.nreg = uint32_t(regs.size());
+        for (uint32_t r = 0; r < hp.nreg; ++r) hp.sp[tix[regs[r]]].rid = r;
+        // the specials' rows (row 0, the source, is computed per source on the device)
+        const uint32_t nr = hp.nreg;
+        hp.near_sp.assign(size_t(NS + 1) * nr * 2, kNone32);
+        const std::vector<uint32_t> &nearh = g->nearest[prm->homeland];
+        const std::vector<uint32_t> &off = *hp.rb_off, &cell = *hp.rb_cell;
+        for (uint32_t t = 1; t <= NS; ++t) {
+            const uint32_t v = order[t];
+            if (v == g->vc) continue;
+            const int vx = g->gx(v), vy = g->gy(v);
+            for (uint32_t r = 0; r < nr; ++r) {
+                uint32_t bd = kNone32, br = kNone32;
+                if (nearh[v] == regs[r]) {
+                    bd = 0;
+                    br = g->rank[v];
+                } else {
+                    for (uint32_t i = off[r]; i < off[r + 1]; ++i) {
+                        const int ux = int16_t(cell[2 * i] & 0xFFFFu), uy = int16_t(cell[2 * i] >> 16);
+                        const uint32_t d = host_walk_dist(vx, vy, ux, uy), rk = cell[2 * i + 1];
+                        if (d < bd || (d == bd && rk < br)) {
+                            bd = d;
+                            br = rk;
+                        }
+                    }
+                }
+                hp.near_sp[(size_t(t) * nr + r) * 2] = bd;
+                hp.near_sp[(size_t(t) * nr + r) * 2 + 1] = br;
+            }
         }
     }
     hp.sinfo.resize(V);
@@ -563,6 +668,8 @@ struct mr_plan {
     uint32_t runs = 0;
     double fill_ms = 0.0;                 // all-destinations: average fill launch of the last window
     uint32_t *d_near = nullptr, *d_fb = nullptr;
+    uint32_t *d_near_sp = nullptr, *d_rb_off = nullptr, *d_rb_cell = nullptr;  // wide hub tables
+    OutCmd *d_ovf = nullptr;              // command-overflow pool (labels longer than max_cmds)
     uint32_t hub_blocks = 0, fb_blocks = 0, spw = 1, cus = 256;
     unsigned long long *d_dbg = nullptr;  // diagnostic builds: per-workgroup phase cycles
     uint32_t algo = kAlgoGeneric;
@@ -581,7 +688,7 @@ struct mr_plan {
                         (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
                         (void *)d_counter, (void *)d_args, (void *)d_dbg, (void *)d_args_fb, (void *)d_near,
                         (void *)d_fb, (void *)d_args_hub_last, (void *)d_args_fill, (void *)d_rec, (void *)d_tab,
-                        (void *)d_lex, (void *)d_sstate})
+                        (void *)d_lex, (void *)d_sstate, (void *)d_near_sp, (void *)d_rb_off, (void *)d_rb_cell, (void *)d_ovf})
             if (p) (void)hipFree(p);
         for (auto *v : {&timed, &timed_fill})
             for (auto &e : *v) {
@@ -628,6 +735,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         return st;
     }
     HostPlan &hp = pl->hp;
+    if (all_mode && hp.wide) hp.hub = hp.wide = false;  // all destinations: hub_kernel + fill only
     auto bail = [&](int code) {
         delete pl;
         return code;
@@ -641,6 +749,8 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     size_t nres = std::max<uint32_t>(n, 1);
     if (hipMalloc(reinterpret_cast<void **>(&pl->d_res), nres * sizeof(OutResult)) != hipSuccess ||
         hipMalloc(reinterpret_cast<void **>(&pl->d_cmd), nres * size_t(max_cmds) * sizeof(OutCmd)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&pl->d_ovf), std::max<size_t>(4096, size_t(n) * 8) * sizeof(OutCmd)) !=
+            hipSuccess ||
         hipMalloc(reinterpret_cast<void **>(&pl->d_counter), kCtrWords * 4) != hipSuccess ||
         hipMemset(pl->d_counter, 0, kCtrWords * 4) != hipSuccess)
         return bail(fail(MR_ERR_DEVICE, "hipMalloc outputs"));
@@ -669,7 +779,8 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     if (hp.hub) blocks = std::min<uint64_t>(blocks, 2ull * prop.multiProcessorCount);  // fallback launches only
     if (!pl->grid_in_lds) {
         const uint64_t slot_bytes = 5ull * V * 4ull;
-        const uint64_t budget = 64ull << 30;  // HBM budget for solve slots
+        // HBM budget for solve slots; hub plans only solve the (few) fallback sources
+        const uint64_t budget = (hp.hub ? 8ull : 64ull) << 30;
         blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, budget / slot_bytes));
         if (hipMalloc(reinterpret_cast<void **>(&pl->d_ws), blocks * slot_bytes) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "hipMalloc workspace"));
@@ -692,6 +803,8 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     ka.out_cmd = pl->d_cmd;
     ka.ws = pl->d_ws;
     ka.counter = pl->d_counter;
+    ka.ovf = pl->d_ovf;
+    ka.ovf_cap = uint32_t(std::min<size_t>(std::max<size_t>(4096, size_t(n) * 8), 0xFFFFFFFFu));
     ka.nsrc = nsrc;
     ka.early_exit_max = 64;
     ka.grid_in_lds = pl->grid_in_lds ? 1u : 0u;
@@ -722,18 +835,32 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
             for (uint32_t k = hp.q_begin[si]; k < hp.q_begin[si + 1]; ++k) pl->src_of_input[hp.q_id[k]] = si;
     }
     if (hp.hub) {
-        if (upload(pl->d_near, *hp.near) != MR_OK ||
-            hipMalloc(reinterpret_cast<void **>(&pl->d_fb), std::max<size_t>(nsrc, 1) * 4) != hipSuccess)
+        if (hipMalloc(reinterpret_cast<void **>(&pl->d_fb), std::max<size_t>(nsrc, 1) * 4) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "hub tables"));
-        ka.near = pl->d_near;
+        if (hp.wide) {
+            std::vector<uint32_t> off(hp.rb_off->begin(), hp.rb_off->end());
+            if (off.empty()) off.push_back(0);
+            if (upload(pl->d_near_sp, hp.near_sp) != MR_OK || upload(pl->d_rb_off, off) != MR_OK ||
+                upload(pl->d_rb_cell, *hp.rb_cell) != MR_OK)
+                return bail(fail(MR_ERR_DEVICE, "wide hub tables"));
+            ka.near_sp = pl->d_near_sp;
+            ka.rb_off = pl->d_rb_off;
+            ka.rb_cell = pl->d_rb_cell;
+        } else {
+            if (upload(pl->d_near, *hp.near) != MR_OK) return bail(fail(MR_ERR_DEVICE, "hub tables"));
+            ka.near = pl->d_near;
+        }
         ka.nreg = hp.nreg;
         ka.fb_list = pl->d_fb;
-        // two sources per wave when the specials fit 32 lanes (MR_HUB_SPW=1 forces one)
-        pl->spw = NS + 1 <= 32 ? 2u : 1u;
+        // two sources per wave when the specials fit 32 lanes (MR_HUB_SPW=1 forces one);
+        // the wide kernel runs one source per wave
+        pl->spw = !hp.wide && NS + 1 <= 32 ? 2u : 1u;
         if (const char *e = std::getenv("MR_HUB_SPW"))
             if (std::atoi(e) == 1) pl->spw = 1;
-        const uint32_t hb = hub_lds_bytes(NS, hp.nreg, pl->spw);
-        const int hper = std::max(1, hub_blocks_per_cu(hp.p.perm, pl->spw, hb));
+        const uint32_t hb = hp.wide ? hub_wide_lds_bytes(NS, hp.nreg) : hub_lds_bytes(NS, hp.nreg, pl->spw);
+        if (hb > 160 * 1024) return bail(fail(MR_ERR_LIMIT, "hub tables exceed LDS"));
+        const int hper = std::max(1, hp.wide ? hub_wide_blocks_per_cu(hp.p.perm, NS, hb)
+                                             : hub_blocks_per_cu(hp.p.perm, pl->spw, hb));
         const uint64_t per_block = 4ull * pl->spw;
         pl->hub_blocks = uint32_t(std::min<uint64_t>((nsrc + per_block - 1) / per_block,
                                                      uint64_t(hper) * prop.multiProcessorCount));
@@ -769,7 +896,18 @@ extern "C" int mr_plan_create(const mr_grid *g, const mr_params *prm, const mr_q
     return plan_create(g, prm, qs, n, 16, out);
 }
 
+extern "C" int mr_plan_create_ex(const mr_grid *g, const mr_params *prm, const mr_query *qs, uint32_t n,
+                                 uint32_t max_cmds, mr_plan **out) {
+    if (max_cmds == 0 || max_cmds > 4096) return fail(MR_ERR_INVALID_ARG, "max_cmds must be 1..4096");
+    return plan_create(g, prm, qs, n, max_cmds, out);
+}
 
+
+
+static hipError_t launch_hub_plan(const mr_plan *pl, const KArgs *d_args, hipStream_t s) {
+    if (pl->hp.wide) return launch_hub_wide(d_args, pl->ka.p.perm, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
+    return launch_hub(d_args, pl->ka.p.perm, pl->spw, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
+}
 
 extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     if (!pl) return fail(MR_ERR_INVALID_ARG, "null plan");
@@ -787,7 +925,7 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         uint32_t gx = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(items, 8ull * pl->cus)));
         if (const char *e = std::getenv("MR_FILL_GX")) gx = uint32_t(std::max(1, std::atoi(e)));
         const uint32_t gy = 1;
-        e = launch_hub(pl->d_args, pl->ka.p.perm, pl->spw, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
+        e = launch_hub_plan(pl, pl->d_args, s);
         if (e == hipSuccess && !pl->fb_none)
             e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, s);
         hipEvent_t f0 = nullptr;
@@ -797,11 +935,11 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     } else if (pl->hp.hub && pl->fb_none) {
         // a pass of this plan (same inputs, deterministic result) had no fallback
         // sources: the hub launch ends the pass on its own
-        e = launch_hub(pl->d_args_hub_last, pl->ka.p.perm, pl->spw, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
+        e = launch_hub_plan(pl, pl->d_args_hub_last, s);
     } else if (pl->hp.hub) {
         // closed-form hub solve for every source, then the SSSP kernel for the
         // sources it flagged (usually none; those workgroups exit at once)
-        e = launch_hub(pl->d_args, pl->ka.p.perm, pl->spw, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
+        e = launch_hub_plan(pl, pl->d_args, s);
         if (e == hipSuccess)
             e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, s);
     } else {
@@ -875,7 +1013,8 @@ extern "C" int mr_plan_get_stats(mr_plan *pl, mr_plan_stats *out) {
     std::memset(out, 0, sizeof(*out));
     uint32_t ctr[kCtrWords];
     if (int st = read_counters(pl, ctr)) return st;
-    out->solver = pl->hp.hub ? MR_SOLVER_HUB : (pl->algo == kAlgoLegs ? MR_SOLVER_LEVELS : MR_SOLVER_BUCKETED);
+    out->solver = pl->hp.hub ? (pl->hp.wide ? MR_SOLVER_HUB_WIDE : MR_SOLVER_HUB)
+                             : (pl->algo == kAlgoLegs ? MR_SOLVER_LEVELS : MR_SOLVER_BUCKETED);
     out->grid_state_in_lds = pl->grid_in_lds ? 1u : 0u;
     out->num_sources = pl->ka.nsrc;
     out->fallback_sources = pl->hp.hub ? ctr[kCtrLastFb] : 0u;
@@ -883,6 +1022,8 @@ extern "C" int mr_plan_get_stats(mr_plan *pl, mr_plan_stats *out) {
     out->num_regions = pl->hp.nreg;
     out->hub_workgroups = pl->hub_blocks;
     out->sssp_workgroups = pl->blocks;
+    out->specials_per_lane = !pl->hp.hub ? 0u : (pl->hp.wide ? hub_wide_spl(pl->ka.p.NS) : 1u);
+    out->region_boundary_cells = pl->hp.wide && pl->hp.rb_off && !pl->hp.rb_off->empty() ? pl->hp.rb_off->back() : 0u;
     return MR_OK;
 }
 
@@ -971,12 +1112,19 @@ static int check_device_errors(mr_plan *pl, uint32_t &flags) {
 
 // Copies the compact outputs and expands them.  Queries whose label needs more
 // than max_cmds commands come back with status MR_ERR_CAPACITY in *over.
-static int plan_collect(mr_plan *pl, std::vector<OutResult> &res, std::vector<OutCmd> &cmd) {
+static int plan_collect(mr_plan *pl, std::vector<OutResult> &res, std::vector<OutCmd> &cmd,
+                        std::vector<OutCmd> &ovf) {
     if (hipStreamSynchronize(pl->stream) != hipSuccess) return fail(MR_ERR_DEVICE, "sync");
     if (hipDeviceSynchronize() != hipSuccess) return fail(MR_ERR_DEVICE, "device sync");
     uint32_t flags = 0;
     int st = check_device_errors(pl, flags);
     if (st != MR_OK) return st;
+    uint32_t ctr[kCtrWords];
+    if ((st = read_counters(pl, ctr))) return st;
+    const uint32_t nov = std::min(ctr[kCtrLastOvf], pl->ka.ovf_cap);
+    ovf.resize(nov);
+    if (nov && hipMemcpy(ovf.data(), pl->d_ovf, size_t(nov) * sizeof(OutCmd), hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(MR_ERR_DEVICE, "copy overflow pool");
     const uint32_t n = pl->hp.nq, mc = pl->hp.p.max_cmds;
     res.resize(n);
     cmd.resize(size_t(n) * mc);
@@ -991,8 +1139,8 @@ static int plan_collect(mr_plan *pl, std::vector<OutResult> &res, std::vector<Ou
 extern "C" int mr_plan_fetch(mr_plan *pl, mr_result *results, mr_command *pool, uint64_t pool_cap) {
     if (!pl || (pl->hp.nq && !results)) return fail(MR_ERR_INVALID_ARG, "null argument");
     std::vector<OutResult> res;
-    std::vector<OutCmd> cmd;
-    int st = plan_collect(pl, res, cmd);
+    std::vector<OutCmd> cmd, ovf;
+    int st = plan_collect(pl, res, cmd, ovf);
     if (st != MR_OK) return st;
     const HostPlan &hp = pl->hp;
     const uint32_t mc = hp.p.max_cmds;
@@ -1018,12 +1166,22 @@ extern "C" int mr_plan_fetch(mr_plan *pl, mr_result *results, mr_command *pool, 
             r.n_commands = 0;
             continue;
         }
+        // a long label: its commands are in the overflow pool at {offset, count}
+        const OutCmd *src = mc ? &cmd[size_t(i) * mc] : nullptr;
+        if (status == int(kStatusOverflow)) {
+            const OutCmd &tag = cmd[size_t(i) * mc];
+            if (tag.kp != kOvfTag || tag.to != r.n_commands || uint64_t(tag.from) + tag.to > ovf.size())
+                return fail(MR_ERR_DEVICE, "overflow pool record");
+            src = &ovf[tag.from];
+            status = MR_OK;
+            r.status = MR_OK;
+        }
         if (status != MR_OK) {
             if (ret == MR_OK) ret = status;
             continue;
         }
         if (off + r.n_commands <= pool_cap && pool) {
-            for (uint32_t j = 0; j < r.n_commands; ++j) expand_cmd(pl->grid, hp, cmd[size_t(i) * mc + j], pool[off + j]);
+            for (uint32_t j = 0; j < r.n_commands; ++j) expand_cmd(pl->grid, hp, src[j], pool[off + j]);
         } else {
             ret = MR_ERR_CAPACITY;
         }

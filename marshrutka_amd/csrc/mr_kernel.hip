@@ -737,11 +737,18 @@ struct Core {
     __device__ __forceinline__ void emit(const View &x, uint32_t qid) const {
         const DevParams &p = P;
         OutResult &o = a->out_res[qid];
-        if (x.len > p.max_cmds) {  // MR_ERR_CAPACITY: the host re-runs with more slots
-            o = OutResult{x.m0, x.m1, x.m2, (uint32_t(16 - 4) << 16) | (x.len & 0xFFFFu)};
-            return;
-        }
         OutCmd *oc = a->out_cmd + (unsigned long long)qid * p.max_cmds;
+        uint32_t status = 16;
+        if (x.len > p.max_cmds) {  // the overflow pool, else MR_ERR_CAPACITY (the host re-runs with more slots)
+            const uint32_t off = atomicAdd(a->counter + kCtrOvf, x.len);
+            if (p.max_cmds == 0 || off + x.len > a->ovf_cap || off + x.len < off) {
+                o = OutResult{x.m0, x.m1, x.m2, (uint32_t(16 - 4) << 16) | (x.len & 0xFFFFu)};
+                return;
+            }
+            oc[0] = OutCmd{kOvfTag, off, x.len, 0};
+            oc = a->ovf + off;
+            status = 16 + kStatusOverflow;
+        }
         int pos = int(x.len) - 1;
         if (x.ntail == 2 && pos >= 0) {
             oc[pos] = OutCmd{x.t1.kp, x.t1.from, x.t1.to, 0};
@@ -759,7 +766,7 @@ struct Core {
             pp = r.parent;
         }
         if (pos != -1 || pp != 0) flag(kErrChain);
-        o = OutResult{x.m0, x.m1, x.m2, (uint32_t(16) << 16) | (x.len & 0xFFFFu)};
+        o = OutResult{x.m0, x.m1, x.m2, (status << 16) | (x.len & 0xFFFFu)};
     }
     __device__ __forceinline__ void write_output(uint32_t w, uint32_t qid) const {
         const uint32_t sw = ld_state(w);
@@ -1319,9 +1326,12 @@ __device__ __forceinline__ void finish_launch(const KArgs *__restrict__ a, uint3
     __threadfence();
     if (atomicAdd(c + kCtrDone, 1u) == gridDim.x * gridDim.y * gridDim.z - 1) {  // the grid's last workgroup
         __threadfence();
-        const uint32_t fb = atomicAdd(c + kCtrFbCount, 0u), wr = atomicAdd(c + kCtrWritten, 0u);
+        const uint32_t fb = atomicAdd(c + kCtrFbCount, 0u), wr = atomicAdd(c + kCtrWritten, 0u),
+                       ov = atomicAdd(c + kCtrOvf, 0u);
         c[kCtrLastFb] = fb;
         c[kCtrLastWritten] = wr;
+        c[kCtrLastOvf] = ov;
+        c[kCtrOvf] = 0;
         c[kCtrDequeue] = 0;
         c[kCtrFbCount] = 0;
         c[kCtrFbDequeue] = 0;
@@ -1394,6 +1404,7 @@ struct HubSolver : Core<false> {
     uint32_t *lexs;         // LDS: all-destinations mode, rank of each table entry among the boundaries
     const uint32_t *nearS;  // LDS: region rows {distance, rank} of every special (row t at t*2*nreg)
     uint32_t *srow;         // LDS: this segment's region row of its source
+    uint32_t *blk;          // LDS: this segment's blocking specials (see avail)
     uint32_t nreg;
     uint32_t written = 0;   // result records this lane emitted for (segment lane 0)
 #ifdef MR_STAMPS
@@ -1516,6 +1527,47 @@ struct HubSolver : Core<false> {
         }
     }
 
+    // A boundary special s whose label tied a walk candidate on all three metrics and
+    // won on length/commands is a blocker: past s that walk's extension can win (the
+    // run merges, so its length stops growing), yet Dijkstra never offers it through
+    // s.  walk(b, d_b(v)) is therefore only certain when some shortest walk from b to
+    // v avoids the blockers.  A strict metric loss needs no care: the winner at s
+    // stays ahead along every extension, so such a b is never the closed-form minimum
+    // there.  Returns false when it cannot rule the blockers out: several of them in
+    // the b-v rectangle, the Center in it too, a Center detour near one, or a
+    // one-cell-wide rectangle through one.  (One blocker inside a rectangle at least
+    // two cells wide leaves a monotone walk around it.)
+    __device__ __forceinline__ bool avail(uint32_t nbk, uint32_t b, int bx, int by, int vx, int vy) const {
+        if (nbk == 0) return true;
+        const int x0 = min(bx, vx), x1 = max(bx, vx), y0 = min(by, vy), y1 = max(by, vy);
+        const bool detour = walk_dist(bx, by, vx, vy) != uint32_t(x1 - x0 + y1 - y0);
+        uint32_t inside = 0;
+        for (uint32_t i = 0; i < nbk; ++i) {
+            const uint32_t k = blk[i];
+            if (k == b) continue;
+            const int kx = sp[k].x, ky = sp[k].y;
+            if (kx >= x0 && kx <= x1 && ky >= y0 && ky <= y1) inside += 1;
+            else if (detour && kx >= x0 - 1 && kx <= x1 + 1 && ky >= y0 - 1 && ky <= y1 + 1) inside += 2;
+        }
+        if (inside == 0) return true;
+        if (inside > 1 || detour) return false;
+        if (x0 <= 0 && 0 <= x1 && y0 <= 0 && 0 <= y1) return false;  // the Center in the rectangle too
+        return x0 != x1 && y0 != y1;
+    }
+    // the settled label x of special (tx, ty): its walk, or the walk to the cell its
+    // Scroll of Escape is read from, must be certain (labels of other kinds extend
+    // settled labels and are exact)
+    __device__ __forceinline__ bool label_avail(const View &x, uint32_t nbk, int tx, int ty, int sx, int sy) const {
+        if (nbk == 0) return true;
+        const uint32_t k0 = x.t0.kp >> 29;
+        if (k0 != kStandard) return true;
+        int bx, by;
+        bpos(x.parent, sx, sy, bx, by);
+        if (x.ntail == 1) return avail(nbk, x.parent, bx, by, tx, ty);
+        const uint32_t u = a->rank_inv[x.t0.to];
+        return avail(nbk, x.parent, bx, by, int(u % P.S) - int(P.H), int(u / P.S) - int(P.H));
+    }
+
     __device__ __forceinline__ void bpos(uint32_t b, int sx, int sy, int &bx, int &by) const {
         bx = b == 0 ? sx : sp[b].x;
         by = b == 0 ? sy : sp[b].y;
@@ -1527,11 +1579,12 @@ struct HubSolver : Core<false> {
         view_walk(b, walk_dist(bx, by, wx, wy), wr, x);
     }
     // label of destination w (not the source, not a special) by a serial scan of the boundaries
-    __device__ __forceinline__ void plain_label_serial(uint32_t w, uint32_t nb, int sx, int sy, View &x) const {
+    __device__ __forceinline__ uint32_t plain_label_serial(uint32_t w, uint32_t nb, int sx, int sy, View &x) const {
         const DevParams &p = P;
         const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
         const uint32_t wr = rank[w];
         bool have = false;
+        uint32_t win = 0;
         for (uint32_t j = 0; j < nb; ++j) {
             const uint32_t b = bnd[j];
             if (vert_of(b) == p.vc) continue;
@@ -1539,17 +1592,27 @@ struct HubSolver : Core<false> {
             walk_to(b, sx, sy, wx, wy, wr, c);
             if (!have || cmp_view(c, kOwn, x, kOwn) < 0) {
                 x = c;
+                win = b;
                 have = true;
             }
         }
+        return win;
+    }
+    // is the closed-form label of plain w (walk from boundary b) certain?
+    __device__ __forceinline__ bool dest_avail(uint32_t nbk, uint32_t b, uint32_t w, int sx, int sy) const {
+        if (nbk == 0) return true;
+        int bx, by;
+        bpos(b, sx, sy, bx, by);
+        return avail(nbk, b, bx, by, int(w % P.S) - int(P.H), int(w / P.S) - int(P.H));
     }
 
     // Destinations.  A segment with few (<= kEmitWaveMax) takes them one at a time,
     // lane j evaluating boundary j's walk and the winner picked on the DPP network
     // (exact metric + length ties: full compare); one with many gives each lane a query.
     static constexpr uint32_t kEmitWaveMax = 32;
-    __device__ __forceinline__ void emit_all(uint32_t qa, uint32_t qb, uint32_t nb, int sx, int sy,
+    __device__ __forceinline__ bool emit_all(uint32_t qa, uint32_t qb, uint32_t nb, uint32_t nbk, int sx, int sy,
                                              const View &st0) const {
+        bool unc = false;
         const DevParams &p = P;
         const uint32_t t = seg_lane();
         const uint32_t nq = qb - qa;
@@ -1598,18 +1661,27 @@ struct HubSolver : Core<false> {
             if (plain) walk_to(bnd[win], sx, sy, wx, wy, wr, x);
             else if (w == src) x = st0;
             else view_rec(tw, x);
-            if (qon && t == 0) emit(x, a->q_id[qi]);
+            if (qon && t == 0) {
+                emit(x, a->q_id[qi]);
+                if (plain && !dest_avail(nbk, bnd[win], w, sx, sy)) unc = true;
+            }
         }
         for (uint32_t i = qa + t; !few && i < qb; i += LPS) {
             const uint32_t w = a->q_dst[i];
             View x;
             const uint32_t tw = sinfo[w] & kNone10;
-            if (w == src) x = st0;
-            else if (tw != kNone10) view_rec(tw, x);
-            else plain_label_serial(w, nb, sx, sy, x);
+            if (w == src) {
+                x = st0;
+            } else if (tw != kNone10) {
+                view_rec(tw, x);
+            } else {
+                const uint32_t b = plain_label_serial(w, nb, sx, sy, x);
+                if (!dest_avail(nbk, b, w, sx, sy)) unc = true;
+            }
             emit(x, a->q_id[i]);
         }
         wave_sync();
+        return unc;
     }
 
     // All-destinations mode: publish the label table and rank the boundaries by
@@ -1668,7 +1740,7 @@ struct HubSolver : Core<false> {
         View my, st0;
         view_start(st0);
         my = st0;
-        uint32_t st = 0, bwh = 0, b0 = 0, b1 = 0, b2 = 0, tie = 0;
+        uint32_t st = 0, bwh = 0, b0 = 0, b1 = 0, b2 = 0, unc = 0, nbk = 0;
         if (t == 0) {
             write_rec(0, st0, 2);
             bnd[0] = 0;
@@ -1717,7 +1789,10 @@ struct HubSolver : Core<false> {
             const Cmd last = ls.ntail == 2 ? ls.t1 : ls.t0;
             const uint32_t lk = last.kp >> 29;
             const bool boundary = act && lk != kNoMove && lk != kStandard;
-            if (act && t == s && boundary && bwh && b0 == my.m0 && b1 == my.m1 && b2 == my.m2) tie = 1;
+            // a boundary that tied a walk becomes a blocker
+            const bool tie = act && t == s && boundary && bwh && b0 == my.m0 && b1 == my.m1 && b2 == my.m2;
+            if (tie) blk[nbk] = s;
+            nbk += seg_bits<LPS>(__ballot(tie)) != 0 ? 1u : 0u;
             MR_HSTAMP(4);
             {  // CentralMove / caravan / SoE edges s -> t (skipped when no segment needs an edge kind)
                 const bool live = mine && act && st != 2;
@@ -1767,14 +1842,27 @@ struct HubSolver : Core<false> {
             d[t * 16 + 15] = 0xABCD0000u | nb;
         }
 #endif
-        // An order-sensitive tie hands the source to the SSSP kernel.  No early
-        // return: the wave must stay converged for the next dequeue's broadcast.
-        const bool fallback = have && (seg_bits<LPS>(__ballot(tie != 0)) != 0 || a->fb_all);
+        // Every settled label must be certain.  Checked after the loop against all the
+        // blockers (one settled after t cannot lie on t's shortest walk, its label being
+        // larger, so the extra ones only make the check more careful).  A label that may
+        // miss a blocker hands the source to the SSSP kernel (in all-destinations mode
+        // any blocker does: the fill kernel cannot check cells).  No early return: the
+        // wave must stay converged.
+        wave_sync();
+        if (__any(nbk != 0) && mine && st == 2 && !label_avail(my, nbk, ss.x, ss.y, sx, sy)) unc = 1;
+        const bool unc_sp = seg_bits<LPS>(__ballot(unc != 0)) != 0;
+        const uint32_t qa = a->q_begin[si];
+        bool fallback = have && (unc_sp || a->fb_all || (a->all_mode && nbk != 0));
+        if (a->all_mode) {
+            if (t == 0 && have && !fallback) written += a->q_begin[si + 1] - qa;
+            export_table(have && !fallback, have, fallback, s_idx, nb);
+        } else {
+            const uint32_t qb = (!have || fallback) ? qa : a->q_begin[si + 1];
+            const bool unc_q = emit_all(qa, qb, nb, nbk, sx, sy, st0);
+            fallback = fallback || (have && seg_bits<LPS>(__ballot(unc_q)) != 0);
+            if (t == 0 && have && !fallback) written += qb - qa;
+        }
         if (fallback && t == 0) a->fb_list[atomicAdd(counter + kCtrFbCount, 1u)] = s_idx;
-        const uint32_t qa = a->q_begin[si], qb = (!have || fallback) ? qa : a->q_begin[si + 1];
-        if (t == 0) written += qb - qa;
-        if (a->all_mode) export_table(have && !fallback, have, fallback, s_idx, nb);
-        else emit_all(qa, qb, nb, sx, sy, st0);
         MR_HSTAMP(7);
     }
 };
@@ -1783,7 +1871,7 @@ __host__ __device__ constexpr uint32_t align16h(uint32_t x) { return (x + 15u) &
 
 // per-source LDS slots: 4 waves x SPW segments
 struct HubLayout {
-    uint32_t off_sp, off_hubs, off_near, off_srow, off_R, off_bnd, off_lex, rstride, bstride, sstride, total;
+    uint32_t off_sp, off_hubs, off_near, off_srow, off_R, off_bnd, off_lex, off_blk, rstride, bstride, sstride, total;
 };
 __host__ __device__ inline HubLayout hub_layout(uint32_t NS, uint32_t nreg, uint32_t spw) {
     HubLayout L{};
@@ -1805,6 +1893,8 @@ __host__ __device__ inline HubLayout hub_layout(uint32_t NS, uint32_t nreg, uint
     L.off_bnd = o;
     o += slots * L.bstride;
     L.off_lex = o;  // per slot: all-destinations mode, the boundaries' ranks (bstride words)
+    o += slots * L.bstride;
+    L.off_blk = o;  // per slot: blocking specials (bstride words)
     o += slots * L.bstride;
     L.total = o;
     return L;
@@ -1851,6 +1941,7 @@ __global__ __launch_bounds__(kBS, MR_HUB_WAVES) void hub_kernel(const KArgs *__r
     H.src_rk = 0;
     H.bnd = reinterpret_cast<uint32_t *>(smem + L.off_bnd + slot * L.bstride);
     H.lexs = reinterpret_cast<uint32_t *>(smem + L.off_lex + slot * L.bstride);
+    H.blk = reinterpret_cast<uint32_t *>(smem + L.off_blk + slot * L.bstride);
     H.nearS = reinterpret_cast<const uint32_t *>(smem + L.off_near);
     H.srow = reinterpret_cast<uint32_t *>(smem + L.off_srow + slot * L.sstride);
     H.nreg = nreg;
@@ -1880,6 +1971,397 @@ __global__ __launch_bounds__(kBS, MR_HUB_WAVES) void hub_kernel(const KArgs *__r
         for (int i = 0; i < 9; ++i) atomicAdd(h + i, H.hs[i]);
     }
 #endif
+}
+
+// ===================================================================================
+// Wide hub solver: more specials than one wave has lanes (NS + 1 up to 64 * SPL;
+// c5 has 262 with 64 campfires per homeland), or a grid whose V x regions table
+// would not fit.  One source per wave; lane j owns specials j, j + 64, ... with
+// their tentative labels in registers.  A settle picks each lane's best owned
+// label (full comparator) and then the wave's best on the DPP network, exactly
+// as the one-lane-per-special kernel does; the relaxations are the same per
+// special.  The source's region row {distance, rank} is computed in the kernel
+// from the per-region boundary cells (the nearest cell of a region seen from
+// outside it lies on its boundary), the specials' rows come from a per-plan table.
+// =====================================================================================
+__device__ __forceinline__ void sel_view(bool take, View &d, const View &s) {
+    d.m0 = take ? s.m0 : d.m0;
+    d.m1 = take ? s.m1 : d.m1;
+    d.m2 = take ? s.m2 : d.m2;
+    d.len = take ? s.len : d.len;
+    d.parent = take ? s.parent : d.parent;
+    d.ntail = take ? s.ntail : d.ntail;
+    d.t0.kp = take ? s.t0.kp : d.t0.kp;
+    d.t0.from = take ? s.t0.from : d.t0.from;
+    d.t0.to = take ? s.t0.to : d.t0.to;
+    d.t1.kp = take ? s.t1.kp : d.t1.kp;
+    d.t1.from = take ? s.t1.from : d.t1.from;
+    d.t1.to = take ? s.t1.to : d.t1.to;
+}
+
+template <uint32_t SPL>
+struct HubWide : HubSolver<1> {
+    using B = HubSolver<1>;
+    using B::a;
+    using B::P;
+    using B::rank;
+    using B::sinfo;
+    using B::counter;
+    using B::sp;
+    using B::src;
+    using B::src_rk;
+    using B::bnd;
+    using B::srow;
+    using B::nreg;
+    using B::written;
+
+    // srow[2r], srow[2r+1] = distance and rank of the region-r cell nearest to the
+    // source (walks avoid the Center; ties by rank), as the host BFS table defines it
+    __device__ __forceinline__ void near_rows(int sx, int sy) const {
+        const DevParams &p = P;
+        const uint32_t lane = lane_id();
+        const uint32_t rs = region_of(src);  // table index of the source's nearest campfire
+        const uint32_t rid_src = rs != kNone10 ? sp[rs].rid : kNone10;
+        const uint2 *cells = reinterpret_cast<const uint2 *>(a->rb_cell);
+        for (uint32_t r = 0; r < nreg; ++r) {
+            uint32_t bd = kNone32, br = kNone32;
+            if (src != p.vc) {
+                const uint32_t e = a->rb_off[r + 1];
+                for (uint32_t i = a->rb_off[r] + lane; i < e; i += 64) {
+                    const uint2 c = cells[i];
+                    const int ux = int(int16_t(c.x & 0xFFFFu)), uy = int(int16_t(c.x >> 16));
+                    const uint32_t d = walk_dist(sx, sy, ux, uy);
+                    const bool take = d < bd || (d == bd && c.y < br);
+                    bd = take ? d : bd;
+                    br = take ? c.y : br;
+                }
+            }
+            const uint32_t md = wave_min_u32(bd);
+            const uint32_t mr = wave_min_u32(bd == md ? br : kNone32);
+            if (lane == 0) {
+                const bool inside = src != p.vc && rid_src == r;
+                srow[2 * r] = inside ? 0u : md;
+                srow[2 * r + 1] = inside ? src_rk : mr;
+            }
+        }
+    }
+
+    // the wave's best tentative label over every lane's owned specials; returns its
+    // table index (wave-uniform) or kNone32
+    __device__ __forceinline__ uint32_t select_wide(const bool (&c)[SPL], const View (&my)[SPL]) const {
+        const DevParams &p = P;
+        const uint32_t j = lane_id();
+        bool any = false;
+        View bv = my[0];
+        uint32_t bt = kNone32;
+#pragma unroll
+        for (uint32_t i = 0; i < SPL; ++i) {
+            const bool take = c[i] && (!any || cmp_view(my[i], kOwn, bv, kOwn) < 0);
+            sel_view(take, bv, my[i]);
+            bt = take ? j + 64u * i : bt;
+            any = any || c[i];
+        }
+        bool cand = any;
+        unsigned long long m = __ballot(cand);
+        if (m == 0) return kNone32;
+        const uint32_t keys[4] = {metric(bv, p.perm[0]), metric(bv, p.perm[1]), metric(bv, p.perm[2]), bv.len};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (__popcll(m) <= 1) break;
+            narrow(cand, keys[i]);
+            m = __ballot(cand);
+        }
+        if (__popcll(m) == 1) return bcast(bt, uint32_t(__ffsll((long long)m) - 1));
+        // equal metrics and length in several lanes: compare the command lists
+        if (cand) write_rec(bt, bv, 1);
+        wave_sync();
+        uint32_t mm = cand ? bt : kNone32;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const uint32_t o = __shfl_xor(mm, off, 64);
+            if (o != kNone32 && (mm == kNone32 || cmp_entries(o, mm) < 0)) mm = o;
+        }
+        return mm;
+    }
+
+    // destinations of the source: with few, each query at a time over all lanes
+    // (lane j scans boundaries j, j + 64, ...); with many, a query per lane
+    __device__ __forceinline__ bool emit_wide(uint32_t qa, uint32_t qb, uint32_t nb, uint32_t nbk, int sx, int sy,
+                                              const View &st0) const {
+        const DevParams &p = P;
+        bool unc = false;
+        const uint32_t j = lane_id();
+        const uint32_t nq = qb - qa;
+        if (nq <= B::kEmitWaveMax) {
+            for (uint32_t i = 0; i < nq; ++i) {
+                const uint32_t qi = qa + i;
+                const uint32_t w = a->q_dst[qi];
+                const uint32_t tw = sinfo[w] & kNone10;
+                const bool plain = w != src && tw == kNone10;
+                View x;
+                if (plain) {
+                    const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
+                    const uint32_t wr = rank[w];
+                    bool any = false;
+                    View bv;
+                    view_start(bv);
+                    uint32_t bp = kNone32;
+                    for (uint32_t k = j; k < nb; k += 64) {
+                        const uint32_t b = bnd[k];
+                        if (vert_of(b) == p.vc) continue;
+                        View c;
+                        walk_to(b, sx, sy, wx, wy, wr, c);
+                        const bool take = !any || cmp_view(c, kOwn, bv, kOwn) < 0;
+                        sel_view(take, bv, c);
+                        bp = take ? k : bp;
+                        any = true;
+                    }
+                    bool cand = any;
+                    narrow(cand, metric(bv, p.perm[0]));
+                    narrow(cand, metric(bv, p.perm[1]));
+                    narrow(cand, metric(bv, p.perm[2]));
+                    narrow(cand, bv.len);
+                    const unsigned long long m = __ballot(cand);
+                    uint32_t win = kNone32;
+                    if (__popcll(m) == 1) {
+                        win = bcast(bp, uint32_t(__ffsll((long long)m) - 1));
+                    } else {
+                        uint32_t mm = cand ? bp : kNone32;
+#pragma unroll
+                        for (int off = 32; off >= 1; off >>= 1) {
+                            const uint32_t o = __shfl_xor(mm, off, 64);
+                            if (o == kNone32) continue;
+                            if (mm == kNone32) {
+                                mm = o;
+                                continue;
+                            }
+                            View co, cm;
+                            walk_to(bnd[o], sx, sy, wx, wy, wr, co);
+                            walk_to(bnd[mm], sx, sy, wx, wy, wr, cm);
+                            if (cmp_view(co, kOwn, cm, kOwn) < 0) mm = o;
+                        }
+                        win = mm;
+                    }
+                    walk_to(bnd[win], sx, sy, wx, wy, wr, x);
+                    if (j == 0 && !B::dest_avail(nbk, bnd[win], w, sx, sy)) unc = true;
+                } else if (w == src) {
+                    x = st0;
+                } else {
+                    view_rec(tw, x);
+                }
+                if (j == 0) emit(x, a->q_id[qi]);
+            }
+        } else {
+            for (uint32_t i = qa + j; i < qb; i += 64) {
+                const uint32_t w = a->q_dst[i];
+                View x;
+                const uint32_t tw = sinfo[w] & kNone10;
+                if (w == src) {
+                    x = st0;
+                } else if (tw != kNone10) {
+                    view_rec(tw, x);
+                } else {
+                    const uint32_t b = B::plain_label_serial(w, nb, sx, sy, x);
+                    if (!B::dest_avail(nbk, b, w, sx, sy)) unc = true;
+                }
+                emit(x, a->q_id[i]);
+            }
+        }
+        wave_sync();
+        return unc;
+    }
+
+    __device__ __forceinline__ void solve(uint32_t s_idx) {
+        const DevParams &p = P;
+        const uint32_t j = lane_id();
+        src = a->src_v[s_idx];
+        src_rk = rank[src];
+        const int sx = int(src % p.S) - int(p.H), sy = int(src / p.S) - int(p.H);
+        const uint32_t ts = sinfo[src] & kNone10;
+        View st0;
+        view_start(st0);
+        View my[SPL];
+        uint32_t st[SPL], bwh[SPL], b0[SPL], b1[SPL], b2[SPL];
+        bool mine[SPL];
+        uint32_t unc = 0, nbk = 0;
+        if (j == 0) {
+            write_rec(0, st0, 2);
+            bnd[0] = 0;
+        }
+        if (p.use_soe) near_rows(sx, sy);
+        wave_sync();
+        View l0;
+        view_start(l0);
+        l0.len = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < SPL; ++i) {
+            const uint32_t t = j + 64u * i;
+            mine[i] = t >= 1 && t <= p.NS;
+            const SpecialStatic ss = sp[mine[i] ? t : 0u];
+            my[i] = st0;
+            st[i] = bwh[i] = b0[i] = b1[i] = b2[i] = 0;
+            improve_reg(mine[i] && t == ts, st[i], my[i], st0);
+            View c = st0;
+            c.m1 = p.shq_cost;
+            c.t0 = Cmd{kSHQ << 29, src_rk, ss.rk};
+            improve_reg(mine[i] && t == p.hq_t, st[i], my[i], c);
+            c.m1 = p.sfm_cost;
+            c.t0 = Cmd{kSFm << 29, src_rk, sp[1].rk};
+            improve_reg(mine[i] && p.use_sfm && t == 1, st[i], my[i], c);
+            relax_boundary(mine[i] && src != p.vc, l0, 0, sx, sy, t, st[i], my[i], ss, bwh[i], b0[i], b1[i], b2[i]);
+        }
+        wave_sync();
+        uint32_t nb = 1;
+        for (uint32_t it = 0; it <= p.NS; ++it) {
+            bool c[SPL];
+#pragma unroll
+            for (uint32_t i = 0; i < SPL; ++i) c[i] = mine[i] && st[i] == 1;
+            const uint32_t s = select_wide(c, my);
+            if (s == kNone32) break;
+            const uint32_t so = s & 63u, si = s >> 6;
+#pragma unroll
+            for (uint32_t i = 0; i < SPL; ++i)
+                if (j == so && i == si) {
+                    st[i] = 2;
+                    write_rec(s, my[i], 2);
+                }
+            wave_sync();
+            View ls;
+            view_rec(s, ls);
+            const SpecialStatic sS = sp[s];
+            const Cmd last = ls.ntail == 2 ? ls.t1 : ls.t0;
+            const uint32_t lk = last.kp >> 29;
+            const bool boundary = lk != kNoMove && lk != kStandard;
+            // a boundary that tied a walk becomes a blocker
+            bool tie = false;
+#pragma unroll
+            for (uint32_t i = 0; i < SPL; ++i)
+                if (j == so && i == si)
+                    tie = boundary && bwh[i] && b0[i] == my[i].m0 && b1[i] == my[i].m1 && b2[i] == my[i].m2;
+            if (tie) B::blk[nbk] = s;
+            nbk += __ballot(tie) != 0 ? 1u : 0u;
+            const bool central_s = (sS.flags & (kSpCenter | kSpBorder1)) != 0;
+            const bool hub_s = p.use_caravans && (sS.flags & kSpHub);
+            const bool soe_s = p.use_soe && sS.region != kNone10 && sS.region != s;
+            const bool walks = boundary && s != 1;
+            View cc;
+            if (central_s) ext_view(ls, s, sS.rk, kCentral, 1, 0, 10, 0, cc);
+            const uint32_t want = (sS.flags & kSpCenter) ? kSpBorder1 : kSpCenter;
+#pragma unroll
+            for (uint32_t i = 0; i < SPL; ++i) {
+                const uint32_t t = j + 64u * i;
+                const SpecialStatic ss = sp[mine[i] ? t : 0u];
+                const bool live = mine[i] && st[i] != 2;
+                if (central_s) {
+                    View c = cc;
+                    c.t0.to = ss.rk;
+                    improve_reg(live && (ss.flags & want), st[i], my[i], c);
+                }
+                if (hub_s) {
+                    View c;
+                    const uint32_t d = uint32_t(abs(sS.x - ss.x) + abs(sS.y - ss.y));
+                    const uint32_t coef = ss.coef5 ? 5u : 2u;
+                    ext_view(ls, s, sS.rk, kCaravan, (d << 1) | ss.coef5, coef * d, p.rgt * d, ss.rk, c);
+                    improve_reg(live && (ss.flags & kSpHub), st[i], my[i], c);
+                }
+                if (soe_s) {
+                    View c;
+                    ext_view(ls, s, sS.rk, kSoE, 0, p.soe_cost, 0, ss.rk, c);
+                    improve_reg(live && sS.region == t, st[i], my[i], c);
+                }
+                if (walks)
+                    relax_boundary(mine[i], ls, s, sS.x, sS.y, t, st[i], my[i], ss, bwh[i], b0[i], b1[i], b2[i]);
+            }
+            if (walks && j == 0) bnd[nb] = s;
+            nb += walks ? 1u : 0u;
+            wave_sync();
+        }
+        wave_sync();
+        if (nbk != 0) {  // every settled label must be certain (as in HubSolver::solve)
+#pragma unroll
+            for (uint32_t i = 0; i < SPL; ++i) {
+                const SpecialStatic ss = sp[mine[i] ? j + 64u * i : 0u];
+                if (mine[i] && st[i] == 2 && !B::label_avail(my[i], nbk, ss.x, ss.y, sx, sy)) unc = 1;
+            }
+        }
+        bool fallback = __ballot(unc != 0) != 0 || a->fb_all;
+        const uint32_t qa = a->q_begin[s_idx], qb = fallback ? qa : a->q_begin[s_idx + 1];
+        fallback = __ballot(emit_wide(qa, qb, nb, nbk, sx, sy, st0)) != 0 || fallback;
+        if (j == 0 && !fallback) written += qb - qa;
+        if (fallback && j == 0) a->fb_list[atomicAdd(counter + kCtrFbCount, 1u)] = s_idx;
+    }
+};
+
+// per-wave LDS slots of the wide kernel (4 waves, one source each)
+struct WideLayout {
+    uint32_t off_sp, off_hubs, off_srow, off_R, off_bnd, off_blk, rstride, bstride, sstride, total;
+};
+__host__ __device__ inline WideLayout wide_layout(uint32_t NS, uint32_t nreg) {
+    WideLayout L{};
+    const uint32_t T = NS + 1;
+    uint32_t o = 0;
+    L.off_sp = o;
+    o = align16h(o + T * uint32_t(sizeof(SpecialStatic)));
+    L.off_hubs = o;
+    o = align16h(o + T * 2);
+    L.sstride = align16h(nreg * 8 + 8);
+    L.off_srow = o;
+    o += 4 * L.sstride;
+    L.rstride = align16h(T * uint32_t(sizeof(Rec)));
+    L.off_R = o;
+    o += 4 * L.rstride;
+    L.bstride = align16h((T + 1) * 4);
+    L.off_bnd = o;
+    o += 4 * L.bstride;
+    L.off_blk = o;
+    o += 4 * L.bstride;
+    L.total = o;
+    return L;
+}
+
+template <uint32_t PERM, uint32_t SPL>
+__global__ __launch_bounds__(kBS) void hub_wide_kernel(const KArgs *__restrict__ a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const uint32_t NS = a->p.NS, nreg = a->nreg;
+    const WideLayout L = wide_layout(NS, nreg);
+    SpecialStatic *spl = reinterpret_cast<SpecialStatic *>(smem + L.off_sp);
+    uint16_t *hubl = reinterpret_cast<uint16_t *>(smem + L.off_hubs);
+    for (uint32_t t = threadIdx.x; t <= NS; t += kBS) spl[t] = a->sp[t];
+    for (uint32_t h = threadIdx.x; h < a->p.n_hubs; h += kBS) hubl[h] = a->hubs[h];
+    __syncthreads();
+    const uint32_t slot = threadIdx.x >> 6;
+    HubWide<SPL> H;
+    H.a = a;
+    H.P = a->p;
+    H.P.perm[0] = PERM / 9;
+    H.P.perm[1] = (PERM / 3) % 3;
+    H.P.perm[2] = PERM % 3;
+    H.P.ff_num = H.P.ff_den = 1;
+    H.rank = a->rank;
+    H.sinfo = a->sinfo;
+    H.counter = a->counter;
+    H.sh = nullptr;
+    H.R = reinterpret_cast<Rec *>(smem + L.off_R + slot * L.rstride);
+    H.state = nullptr;
+    H.sp = spl;
+    H.hubs = hubl;
+    H.dst = nullptr;
+    H.src = 0;
+    H.src_rk = 0;
+    H.bnd = reinterpret_cast<uint32_t *>(smem + L.off_bnd + slot * L.bstride);
+    H.lexs = nullptr;
+    H.blk = reinterpret_cast<uint32_t *>(smem + L.off_blk + slot * L.bstride);
+    H.nearS = a->near_sp;  // specials' region rows (global, (NS+1) x nreg x 2 words)
+    H.srow = reinterpret_cast<uint32_t *>(smem + L.off_srow + slot * L.sstride);
+    H.nreg = nreg;
+    const uint32_t waves = gridDim.x * (kBS / 64), wid = blockIdx.x * (kBS / 64) + slot;
+    for (uint32_t s = wid; s < a->nsrc; s += waves) H.solve(s);
+    __shared__ uint32_t wsum;
+    if (threadIdx.x == 0) wsum = 0;
+    __syncthreads();
+    if (H.written) atomicAdd(&wsum, H.written);
+    __syncthreads();
+    if (threadIdx.x == 0) finish_launch(a, wsum);
 }
 
 // ===================================================================================
@@ -2223,6 +2705,50 @@ hipError_t launch_hub(const KArgs *d_args, const uint32_t perm[3], uint32_t spw,
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
     void *args[] = {const_cast<KArgs **>(&d_args)};
     return hipLaunchKernel(fn, dim3(blocks), dim3(kBS), args, bytes, stream);
+}
+
+uint32_t hub_wide_lds_bytes(uint32_t NS, uint32_t nreg) { return wide_layout(NS, nreg).total; }
+
+template <uint32_t SPL>
+static const void *wide_fn_spl(uint32_t perm) {
+    switch (perm) {
+        case 5: return reinterpret_cast<const void *>(&hub_wide_kernel<5, SPL>);
+        case 7: return reinterpret_cast<const void *>(&hub_wide_kernel<7, SPL>);
+        case 11: return reinterpret_cast<const void *>(&hub_wide_kernel<11, SPL>);
+        case 15: return reinterpret_cast<const void *>(&hub_wide_kernel<15, SPL>);
+        case 19: return reinterpret_cast<const void *>(&hub_wide_kernel<19, SPL>);
+        case 21: return reinterpret_cast<const void *>(&hub_wide_kernel<21, SPL>);
+        default: return nullptr;
+    }
+}
+// specials per lane for a table of NS + 1 entries: 2, 5 or 8 (0 if too many)
+uint32_t hub_wide_spl(uint32_t NS) {
+    const uint32_t T = NS + 1;
+    return T <= 128 ? 2u : (T <= 320 ? 5u : (T <= 512 ? 8u : 0u));
+}
+static const void *wide_fn(const uint32_t perm[3], uint32_t NS) {
+    const uint32_t k = perm[0] * 9 + perm[1] * 3 + perm[2];
+    switch (hub_wide_spl(NS)) {
+        case 2: return wide_fn_spl<2>(k);
+        case 5: return wide_fn_spl<5>(k);
+        case 8: return wide_fn_spl<8>(k);
+        default: return nullptr;
+    }
+}
+hipError_t launch_hub_wide(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t blocks,
+                           hipStream_t stream) {
+    const uint32_t bytes = hub_wide_lds_bytes(NS, nreg);
+    const void *fn = wide_fn(perm, NS);
+    if (!fn) return hipErrorInvalidValue;
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
+    void *args[] = {const_cast<KArgs **>(&d_args)};
+    return hipLaunchKernel(fn, dim3(blocks), dim3(kBS), args, bytes, stream);
+}
+int hub_wide_blocks_per_cu(const uint32_t perm[3], uint32_t NS, uint32_t bytes) {
+    int n = 0;
+    const void *fn = wide_fn(perm, NS);
+    if (fn) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kBS, bytes);
+    return n;
 }
 
 hipError_t launch_fill(const KArgs *d_args, const uint32_t perm[3], uint32_t gx, uint32_t gy, hipStream_t stream) {

@@ -126,6 +126,36 @@ class SyntheticMap:
     def all_indices(self) -> List[CellIndex]:
         return [ci for ci, _ in self.cells()]
 
+    def index_at(self, i: int) -> CellIndex:
+        """CellIndex of row-major cell i (no list of all cells)."""
+        return geo_to_index(i % self.size - self.h, i // self.size - self.h)
+
+    def cells_array(self):
+        """The cells as a numpy record array with mr_cell's layout (16 B per cell),
+        vectorised for large maps (S = 4097: 16.8 M cells); same content as cells()."""
+        import numpy as np
+        S, H = self.size, self.h
+        dt = np.dtype([("kind", "u1"), ("sub", "u1"), ("x", "<u2"), ("y", "<u2"), ("res", "<u2"),
+                       ("poi", "u1"), ("pad", "u1", (7,))])
+        out = np.zeros(S * S, dtype=dt)
+        x = (np.arange(S, dtype=np.int32) - H)[None, :].repeat(S, 0).ravel()
+        y = (np.arange(S, dtype=np.int32) - H)[:, None].repeat(S, 1).ravel()
+        kind = np.full(S * S, CELL_HOMELAND, np.uint8)
+        sub = np.where(x < 0, np.where(y < 0, BLUE, RED), np.where(y > 0, GREEN, YELLOW)).astype(np.uint8)
+        ix, iy = np.abs(x), np.abs(y)
+        on_y0, on_x0 = (y == 0) & (x != 0), (x == 0) & (y != 0)
+        kind[on_y0 | on_x0] = CELL_BORDER
+        sub[on_y0] = np.where(x[on_y0] < 0, BR, GY)
+        sub[on_x0] = np.where(y[on_x0] > 0, RG, YB)
+        bx = np.where(on_y0, ix, np.where(on_x0, iy, ix))
+        by = np.where(on_y0 | on_x0, 0, iy)
+        c = (x == 0) & (y == 0)
+        kind[c], sub[c], bx[c], by[c] = CELL_CENTER, 0, 0, 0
+        out["kind"], out["sub"], out["x"], out["y"] = kind, sub, bx, by
+        for (px, py), p in self.poi.items():
+            out["poi"][(py + H) * S + (px + H)] = p
+        return out
+
     def campfires(self) -> List[CellIndex]:
         return sorted(geo_to_index(x, y) for (x, y), p in self.poi.items() if p == POI_CAMPFIRE)
 
@@ -170,9 +200,8 @@ def to_html(m: SyntheticMap) -> str:
 
 def random_queries(m: SyntheticMap, n: int, seed: int) -> List[Tuple[CellIndex, CellIndex]]:
     rng = SplitMix64(seed ^ 0x5DEECE66D)
-    idx = m.all_indices()
-    V = len(idx)
-    return [(idx[rng.below(V)], idx[rng.below(V)]) for _ in range(n)]
+    V = m.size * m.size
+    return [(m.index_at(rng.below(V)), m.index_at(rng.below(V))) for _ in range(n)]
 
 
 def random_sources_queries(m: SyntheticMap, n: int, n_sources: int, seed: int):

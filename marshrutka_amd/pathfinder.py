@@ -25,7 +25,7 @@ LIB_PATH = os.environ.get("MR_LIB_PATH") or os.path.join(os.path.dirname(os.path
 
 EXPORTED_SYMBOLS = [
     "mr_grid_create", "mr_grid_destroy", "mr_grid_square_size", "mr_params_default", "mr_find_path",
-    "mr_find_path_batch", "mr_plan_create", "mr_plan_run", "mr_plan_fetch", "mr_plan_device_outputs",
+    "mr_find_path_batch", "mr_plan_create", "mr_plan_create_ex", "mr_plan_run", "mr_plan_fetch", "mr_plan_device_outputs",
     "mr_plan_num_sources", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_plan_bind_outputs", "mr_abi_version", "mr_last_error",
     "mr_device_available", "mr_parse_map_html", "mr_parse_error", "mr_grid_from_html",
     "mr_command_time", "mr_duration_display", "mr_render_schedule",
@@ -71,6 +71,9 @@ def lib():
         L.mr_plan_device_outputs.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_uint64), C.POINTER(vp),
                                              C.POINTER(C.c_uint64)]
         L.mr_plan_device_outputs.restype = C.c_int
+        L.mr_plan_create_ex.argtypes = [vp, C.POINTER(mr_params), C.POINTER(mr_query), C.c_uint32, C.c_uint32,
+                                        C.POINTER(vp)]
+        L.mr_plan_create_ex.restype = C.c_int
         L.mr_plan_bind_outputs.argtypes = [vp, vp, vp]
         L.mr_plan_bind_outputs.restype = C.c_int
         L.mr_plan_num_sources.argtypes = [vp]
@@ -163,10 +166,23 @@ class MapGrid:
         """MapGrid::parse + the engine's grid (canonical indices, nearest campfires)."""
         return cls(parse_map_html(html))
 
+    @classmethod
+    def from_array(cls, arr) -> "MapGrid":
+        """From a numpy record array with mr_cell's 16-byte layout (mapgen.cells_array)."""
+        g = cls.__new__(cls)
+        g._cells = arr
+        if arr.dtype.itemsize != C.sizeof(mr_cell) or not arr.flags["C_CONTIGUOUS"]:
+            raise EngineError(abi.MR_ERR_INVALID_ARG, "cell array must be contiguous mr_cell records")
+        g._create(C.cast(arr.ctypes.data, C.POINTER(mr_cell)), len(arr))
+        return g
+
     def __init__(self, cells: Sequence[Tuple[CellIndex, int]]):
         self._cells = cells_to_c(cells)
+        self._create(self._cells, len(cells))
+
+    def _create(self, ptr, n: int) -> None:
         h = C.c_void_p()
-        st = lib().mr_grid_create(self._cells, len(cells), C.byref(h))
+        st = lib().mr_grid_create(ptr, n, C.byref(h))
         if st != MR_OK:
             raise EngineError(st, last_error())
         self.handle = h
@@ -265,13 +281,20 @@ class FindPath:
 class Plan:
     """Device-resident batch: inputs uploaded once, `run()` enqueues one pass."""
 
-    def __init__(self, grid: MapGrid, params: Params, pairs: Sequence[Tuple[CellIndex, CellIndex]]):
+    def __init__(self, grid: MapGrid, params: Params, pairs: Sequence[Tuple[CellIndex, CellIndex]],
+                 max_cmds: int = 0):
+        """max_cmds: command slots per query in the device output (0 = the C default, 16);
+        longer labels go through the plan's overflow pool."""
         self.grid = grid
         self.n = len(pairs)
+        self.max_cmds = max_cmds or 16
         self._qs = queries_to_c(pairs)
         self._p = params.to_c()
         h = C.c_void_p()
-        st = lib().mr_plan_create(grid.handle, C.byref(self._p), self._qs, self.n, C.byref(h))
+        if max_cmds:
+            st = lib().mr_plan_create_ex(grid.handle, C.byref(self._p), self._qs, self.n, max_cmds, C.byref(h))
+        else:
+            st = lib().mr_plan_create(grid.handle, C.byref(self._p), self._qs, self.n, C.byref(h))
         if st != MR_OK:
             raise EngineError(st, last_error())
         self.handle = h
@@ -291,7 +314,7 @@ class Plan:
         if rc != MR_OK:
             raise EngineError(rc, last_error())
         d = {f: getattr(st, f) for f, _ in mr_plan_stats._fields_}
-        d["solver"] = {0: "bucketed", 1: "levels", 2: "hub"}.get(st.solver, str(st.solver))
+        d["solver"] = {0: "bucketed", 1: "levels", 2: "hub", 3: "hub_wide"}.get(st.solver, str(st.solver))
         return d
 
     def kernel_ms(self) -> Tuple[float, int]:
@@ -314,7 +337,7 @@ class Plan:
     def fetch_raw(self):
         """(results, command pool) as ctypes arrays, no Python label objects."""
         res = (mr_result * max(self.n, 1))()
-        cap = max(1, self.n * 16)
+        cap = self.n * self.max_cmds + max(4096, self.n * 8)  # slots + overflow pool
         pool = (mr_command * cap)()
         st = lib().mr_plan_fetch(self.handle, res, pool, cap)
         if st < 0 and st not in (abi.MR_ERR_INVALID_INDEX, MR_ERR_CAPACITY):
@@ -323,7 +346,7 @@ class Plan:
 
     def fetch(self) -> List[Optional[TotalCost]]:
         res = (mr_result * max(self.n, 1))()
-        cap = max(1, self.n * 16)
+        cap = self.n * self.max_cmds + max(4096, self.n * 8)  # slots + overflow pool
         pool = (mr_command * cap)()
         st = lib().mr_plan_fetch(self.handle, res, pool, cap)
         if st < 0 and st != abi.MR_ERR_INVALID_INDEX:

@@ -44,3 +44,40 @@ def gather_rows_to_root(local, counts: Sequence[int], rank: int, world: int, gro
         return torch.cat([b[: counts[r]] for r, b in enumerate(bufs)], dim=0)
     dist.gather(local, dst=0, group=group)
     return None
+
+
+class PipelinedGather:
+    """Double-buffered result gather for a stream of batches (bench.py at N > 1).
+
+    Each rank owns `depth` flat device buffers (result records followed by command
+    slots, padded to the largest shard).  `issue(k)` starts an asynchronous gather
+    of buffer k to rank 0 — on RCCL the collective runs on the process group's
+    own stream, ordered after the kernels already enqueued on the caller's stream
+    — so the gather of batch i overlaps the solve of batch i+1.  `reuse(k)` makes
+    the caller's stream wait for the previous gather of buffer k before a new
+    solve overwrites it; `drain()` waits for every gather still in flight."""
+
+    def __init__(self, bufs, rank: int, world: int, group=None):
+        import torch
+        self.bufs, self.rank, self.world, self.group = list(bufs), rank, world, group
+        self.pending = [None] * len(self.bufs)
+        self.out = ([[torch.empty_like(b) for _ in range(world)] for b in self.bufs] if rank == 0 else None)
+
+    def issue(self, k: int) -> None:
+        import torch.distributed as dist
+        self.pending[k] = dist.gather(self.bufs[k], gather_list=self.out[k] if self.rank == 0 else None, dst=0,
+                                      group=self.group, async_op=True)
+
+    def reuse(self, k: int) -> None:
+        w, self.pending[k] = self.pending[k], None
+        if w is not None:
+            w.wait()
+
+    def drain(self) -> None:
+        for k in range(len(self.pending)):
+            self.reuse(k)
+
+    def rows(self, k: int, counts: Sequence[int], row_words: int):
+        """Rank 0: the gathered rows of buffer k, per rank, as views [counts[r], row_words]
+        of the region that starts the buffer (the caller's layout)."""
+        return [b[: counts[r] * row_words].view(counts[r], row_words) for r, b in enumerate(self.out[k])]

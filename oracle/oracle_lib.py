@@ -57,9 +57,20 @@ def lib():
 class OracleGrid:
     def __init__(self, cells: Sequence[Tuple[CellIndex, int]]):
         self._cells = cells_to_c(cells)
-        self.n = len(cells)
+        self._create(self._cells, len(cells))
+
+    @classmethod
+    def from_array(cls, arr) -> "OracleGrid":
+        """From a numpy record array with mr_cell's layout (mapgen.SyntheticMap.cells_array)."""
+        g = cls.__new__(cls)
+        g._cells = arr
+        g._create(C.cast(arr.ctypes.data, C.POINTER(mr_cell)), len(arr))
+        return g
+
+    def _create(self, ptr, n: int) -> None:
+        self.n = n
         h = C.c_void_p()
-        st = lib().mro_grid_create(self._cells, self.n, C.byref(h))
+        st = lib().mro_grid_create(ptr, n, C.byref(h))
         if st != MR_OK:
             raise ValueError(f"oracle grid create failed: {st}")
         self.h = h

@@ -23,13 +23,15 @@ def eng():
     return pathfinder
 
 
-@pytest.fixture(params=["auto-lds", "auto-hbm", "hub1-lds", "fallback-lds", "fallback-hbm", "sssp-lds", "sssp-hbm",
-                        "generic-lds", "generic-hbm"])
+@pytest.fixture(params=["auto-lds", "auto-hbm", "hub1-lds", "wide-lds", "fallback-lds", "fallback-hbm", "sssp-lds",
+                        "sssp-hbm", "generic-lds", "generic-hbm"])
 def grid_state(request, monkeypatch):
     """Every solver path x both grid-state regimes:
     auto     — hub solver when the run time is linear (two sources per wave when
                the specials fit 32 lanes), else the SSSP solvers
     hub1     — hub solver with one source per wave
+    wide     — the wide hub solver (several specials per lane, region rows scanned
+               from the regions' boundary cells) even where the narrow one applies
     fallback — hub solver handing every source to the SSSP kernel
     sssp     — no hub solver (level-synchronous solver for Legs-first orders)
     generic  — the bucketed solver for every order."""
@@ -38,6 +40,9 @@ def grid_state(request, monkeypatch):
     monkeypatch.delenv("MR_ALGO", raising=False)
     monkeypatch.delenv("MR_HUB_FALLBACK_ALL", raising=False)
     monkeypatch.delenv("MR_HUB_SPW", raising=False)
+    monkeypatch.delenv("MR_HUB_WIDE", raising=False)
+    if algo == "wide":
+        monkeypatch.setenv("MR_HUB_WIDE", "1")
     if algo == "hub1":
         monkeypatch.setenv("MR_HUB_SPW", "1")
     if algo in ("sssp", "generic"):
@@ -222,9 +227,61 @@ def test_parameter_sweep(eng, oracle_lib, params):
 @pytest.mark.parametrize("k,clustered", [(16, False), (40, True), (64, True)])
 def test_many_campfires(eng, oracle_lib, grid_state, k, clustered):
     """More than 63 specials (SURVEY c5 has 64 clustered campfires per homeland): the
-    hub solver steps aside and the SSSP kernel settles the specials through its LDS
-    argmin; Time- and Money-first orders as c5 prescribes."""
+    wide hub solver (2 or 5 specials per lane) with linear run times, the SSSP kernel
+    (LDS argmin over the specials) otherwise; Time- and Money-first orders as c5
+    prescribes."""
     m = SyntheticMap(41, campfires_per_homeland=k, seed=k, clustered=clustered)
     for params in (Params(), Params(sort_by=(SORT_TIME, SORT_LEGS)), Params(sort_by=(SORT_MONEY, SORT_TIME)),
                    Params(sort_by=(SORT_TIME, SORT_MONEY), fleetfoot=2, route_guru=4)):
         check(eng, oracle_lib, m, params, random_queries(m, 150, k + 1), f"k={k} {params}")
+    if grid_state.startswith("auto"):
+        st = eng.Plan(eng.MapGrid(m.cells()), Params(), random_queries(m, 10, 1)).stats()
+        assert st["solver"] == "hub_wide" and st["specials_per_lane"] == (2 if k == 16 else 5)
+
+
+def test_c5_full_scale_sample(eng, oracle_lib):
+    """configs[4]/c5 at full size: S = 4097 (16.8 M cells), 64 clustered campfires per
+    homeland (NS = 261), Time first (SURVEY 8d option a) and Money first (option b).
+    The wide hub solver answers a 2000-query batch; a sample is checked against the
+    oracle (one CPU Dijkstra over the 16.8 M-cell grid per query), and the whole
+    batch against properties that hold at any size: every label is a valid command
+    chain from its source to its destination with the reported metrics."""
+    m = SyntheticMap(4097, campfires_per_homeland=64, seed=4097, clustered=True)
+    arr = m.cells_array()
+    g = eng.MapGrid.from_array(arr)
+    og = oracle_lib.OracleGrid.from_array(arr)
+    qs = random_queries(m, 2000, 45)
+    for params in (Params(sort_by=(SORT_TIME, SORT_MONEY)), Params(sort_by=(SORT_MONEY, SORT_LEGS))):
+        plan = eng.Plan(g, params, qs)
+        plan.run()
+        got = plan.fetch()
+        assert plan.stats()["solver"] == "hub_wide"
+        sample = list(range(0, 2000, 250))
+        exp = og.find_path_batch(params, [qs[i] for i in sample], threads=0)
+        for i, e in zip(sample, exp):
+            assert as_expected(got[i]) == as_expected(e), (params, qs[i])
+        for (a, b), r in zip(qs, got):
+            assert r is not None
+            cmds = r.commands
+            assert cmds[0].from_ == a and cmds[-1].to == b
+            assert all(x.to == y.from_ for x, y in zip(cmds, cmds[1:]))
+            assert (r.legs, r.money, r.time_s) == (sum(c.legs for c in cmds), sum(c.money for c in cmds),
+                                                   sum(c.time_s for c in cmds))
+
+
+@pytest.mark.parametrize("max_cmds", [1, 2, 3])
+def test_overflow_pool(eng, oracle_lib, grid_state, max_cmds):
+    """Labels longer than the plan's command slots go through the overflow pool
+    (mr_plan_create_ex); with 1-3 slots most labels do, and every one must still
+    come back whole.  Reruns reuse the pool (its allocator resets per pass)."""
+    m = SyntheticMap(25, campfires_per_homeland=6, seed=9, clustered=True)
+    g = eng.MapGrid(m.cells())
+    og = oracle_lib.OracleGrid(m.cells())
+    for params in (Params(), Params(sort_by=(SORT_TIME, SORT_MONEY))):
+        qs = random_queries(m, 200, 3 + max_cmds)
+        exp = [as_expected(e) for e in og.find_path_batch(params, qs, threads=0)]
+        plan = eng.Plan(g, params, qs, max_cmds=max_cmds)
+        for _ in range(2):
+            plan.run()
+            assert [as_expected(r) for r in plan.fetch()] == exp
+        assert any(len(e[3]) > max_cmds for e in exp)

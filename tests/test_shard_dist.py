@@ -67,3 +67,54 @@ def test_gather_rows_to_root_gloo_world2():
     assert len(out) == 8
     assert out[0] == [0, 1, 2, 3] and out[3] == [100, 101, 102, 103]
     assert out[-1] == [116, 117, 118, 119]
+
+
+def _pipe_worker(rank, world, port, ret):
+    import torch
+    import torch.distributed as dist
+    from marshrutka_amd.shard import PipelinedGather
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        counts, rw = [2, 3], 4
+        bufs = [torch.full((3 * rw + 6,), -1, dtype=torch.int32) for _ in range(2)]
+        pg = PipelinedGather(bufs, rank, world)
+        seen = []
+        for step in range(5):
+            k = step % 2
+            pg.reuse(k)
+            if rank == 0 and step >= 2:
+                seen.append([r.tolist() for r in pg.rows(k, counts, rw)])
+            b = bufs[k]
+            b.fill_(-1)
+            b[: counts[rank] * rw] = torch.arange(counts[rank] * rw, dtype=torch.int32) + 1000 * step + 100 * rank
+            pg.issue(k)
+        pg.drain()
+        if rank == 0:
+            seen.append([r.tolist() for r in pg.rows(1, counts, rw)])
+            seen.append([r.tolist() for r in pg.rows(0, counts, rw)])
+            ret.put(seen)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipelined_gather_gloo_world2():
+    """Double-buffered gathers: every batch's rows arrive intact at rank 0 even
+    though a buffer is rewritten two steps later."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    ret = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, 2, port, ret)) for r in range(2)]
+    for p in procs:
+        p.start()
+    seen = ret.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    # batches 0, 1, 2 read back before reuse, then 3 and 4 after the drain
+    for step, got in zip([0, 1, 2, 3, 4], seen):
+        assert got[0] == [[1000 * step + j * 4 + c for c in range(4)] for j in range(2)]
+        assert got[1] == [[1000 * step + 100 + j * 4 + c for c in range(4)] for j in range(3)]

@@ -13,7 +13,8 @@ export TMPDIR=/tmp
 cd /tmp
 for W in $WLS; do
   K=""
-  if [ "$W" = c2 ]; then Q=10000; ST=20; elif [ "$W" = c3 ]; then Q=64; ST=10; K="--kernels fill_kernel"; else Q=125000; ST=5; fi
+  if [ "$W" = c2 ]; then Q=10000; ST=20; elif [ "$W" = c3 ]; then Q=64; ST=10; K="--kernels fill_kernel";
+  elif [ "$W" = c5 ]; then Q=10000; ST=3; else Q=125000; ST=5; fi
   timeout -k 10 400 python3 "$R/bench.py" --workload "$W" --steps "$ST" --warmup 2 > "$O/bench_$W.json" 2> "$O/bench_$W.err"
   echo "bench $W done"
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/trace_$W" -o run --output-format csv -- \
