@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -131,6 +132,13 @@ struct mr_grid {
     // with a neighbour outside it, the Center excluded), {x | y << 16, rank}, by region
     mutable std::vector<uint32_t> rb_off[4], rb_cell[4];
     mutable bool rb_built[4] = {false, false, false, false};
+    // device copies of the region tables, uploaded on first use and shared by the
+    // grid's plans (the grid outlives its plans)
+    mutable uint32_t *d_near[4] = {nullptr, nullptr, nullptr, nullptr};
+    ~mr_grid() {
+        for (uint32_t *p : d_near)
+            if (p) (void)hipFree(p);
+    }
     int32_t gx(uint32_t v) const { return int32_t(v % S) - int32_t(H); }
     int32_t gy(uint32_t v) const { return int32_t(v / S) - int32_t(H); }
     bool find(const mr_cell_index &c, uint32_t &v) const {
@@ -316,8 +324,11 @@ static const std::vector<uint32_t> &region_table(const mr_grid *g, int h, const 
     std::vector<uint32_t> rid(V, kNone32);
     for (uint32_t r = 0; r < nreg; ++r) rid[regs[r]] = r;
     std::vector<uint32_t> tab(size_t(V) * nreg * 2, kNone32);
+    // one BFS per region, spread over host threads (c5: 64 regions x 16.8 M cells)
+    std::atomic<uint32_t> next{0};
+    auto worker = [&]() {
     std::vector<uint32_t> dist(V), org(V), cur, nxt;
-    for (uint32_t r = 0; r < nreg; ++r) {
+    for (uint32_t r = next++; r < nreg; r = next++) {
         std::fill(dist.begin(), dist.end(), kNone32);
         cur.clear();
         for (uint32_t v = 0; v < V; ++v) {
@@ -350,11 +361,34 @@ static const std::vector<uint32_t> &region_table(const mr_grid *g, int h, const 
             tab[(size_t(v) * nreg + r) * 2 + 1] = dist[v] == kNone32 ? kNone32 : g->rank[org[v]];
         }
     }
+    };
+    const uint32_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const uint32_t nt = std::min<uint32_t>(hw, std::max<uint32_t>(1, nreg));
+    std::vector<std::thread> pool;
+    for (uint32_t i = 1; i < nt; ++i) pool.emplace_back(worker);
+    worker();
+    for (auto &t : pool) t.join();
     g->regions[h] = std::move(regs);
     g->near[h] = std::move(tab);
     g->near_built[h] = true;
     (void)rid;
     return g->near[h];
+}
+
+// The region table of homeland h on the current device (uploaded once per grid).
+static const uint32_t *region_table_device(const mr_grid *g, int h, const std::vector<uint32_t> &tab) {
+    std::lock_guard<std::mutex> lk(g->near_mu);
+    if (!g->d_near[h]) {
+        uint32_t *d = nullptr;
+        const size_t bytes = std::max<size_t>(tab.size(), 1) * 4;
+        if (hipMalloc(reinterpret_cast<void **>(&d), bytes) != hipSuccess) return nullptr;
+        if (!tab.empty() && hipMemcpy(d, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(d);
+            return nullptr;
+        }
+        g->d_near[h] = d;
+    }
+    return g->d_near[h];
 }
 
 // Boundary cells of the regions (wide hub solver).  Seen from outside a region, its
@@ -541,8 +575,12 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     for (uint32_t v : g->campfires)
         if (g->idx[v].kind == MR_CELL_HOMELAND && g->idx[v].sub == prm->homeland) ++nregs;
     const char *fw = std::getenv("MR_HUB_WIDE");
-    const bool force_wide = fw && !std::strcmp(fw, "1");
-    const bool narrow_ok = NS <= 63 && nregs <= 63 && size_t(V) * nregs * 8 <= (size_t(2) << 30);
+    const bool force_wide = fw && (!std::strcmp(fw, "1") || !std::strcmp(fw, "scan"));
+    // the V x regions table (grid preprocessing, shared by the grid's plans) up to
+    // 16 GB of HBM (c5: 8.6 GB); beyond it the wide kernel scans boundary cells
+    const bool table_ok = nregs <= 256 && size_t(V) * nregs * 8 <= (size_t(16) << 30) &&
+                          !(fw && !std::strcmp(fw, "scan"));
+    const bool narrow_ok = NS <= 63 && nregs <= 63 && table_ok;
     hp.hub = hp.wide = false;
     if (linear && narrow_ok && !force_wide) {
         const std::vector<uint32_t> *regs = nullptr;
@@ -554,6 +592,10 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     } else if (linear && hub_wide_spl(NS) != 0 && nregs <= 256) {
         std::vector<uint32_t> regs;
         region_bounds(g, prm->homeland, regs, hp.rb_off, hp.rb_cell);
+        if (table_ok) {  // the source's row read from the table instead of scanned
+            const std::vector<uint32_t> *tregs = nullptr;
+            hp.near = &region_table(g, prm->homeland, tregs);
+        }
         hp.hub = hp.wide = true;
         hp.nreg = uint32_t(regs.size());
         for (uint32_t r = 0; r < hp.nreg; ++r) hp.sp[tix[regs[r]]].rid = r;
@@ -837,6 +879,10 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     if (hp.hub) {
         if (hipMalloc(reinterpret_cast<void **>(&pl->d_fb), std::max<size_t>(nsrc, 1) * 4) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "hub tables"));
+        if (hp.near) {
+            ka.near = region_table_device(g, prm->homeland, *hp.near);
+            if (!ka.near) return bail(fail(MR_ERR_DEVICE, "region table upload"));
+        }
         if (hp.wide) {
             std::vector<uint32_t> off(hp.rb_off->begin(), hp.rb_off->end());
             if (off.empty()) off.push_back(0);
@@ -846,9 +892,6 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
             ka.near_sp = pl->d_near_sp;
             ka.rb_off = pl->d_rb_off;
             ka.rb_cell = pl->d_rb_cell;
-        } else {
-            if (upload(pl->d_near, *hp.near) != MR_OK) return bail(fail(MR_ERR_DEVICE, "hub tables"));
-            ka.near = pl->d_near;
         }
         ka.nreg = hp.nreg;
         ka.fb_list = pl->d_fb;

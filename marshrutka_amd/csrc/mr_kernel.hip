@@ -1496,13 +1496,7 @@ struct HubSolver : Core<false> {
                                                    uint32_t &b0, uint32_t &b1, uint32_t &b2) const {
         const DevParams &p = P;
         live = live && st != 2;
-        {  // the walk: not into the Center (entry 1) nor b's own cell
-            const bool on = live && t != 1 && t != b && !(b == 0 && ss.v == src);
-            View c;
-            view_walk_lab(lb, b, walk_dist(bx, by, ss.x, ss.y), ss.rk, c);
-            note_walk(on, c, bwh, b0, b1, b2);
-            improve_reg(on, st, my, c);
-        }
+        relax_walk(live, lb, b, bx, by, t, st, my, ss, bwh, b0, b1, b2);
         if (p.use_soe) {  // [Std{d} b->u, SoE u->c] from the region cell u nearest to b
             uint32_t d = kNone32, u = 0;
             if (live && ss.rid != kNone10) {
@@ -1510,7 +1504,28 @@ struct HubSolver : Core<false> {
                 d = e[0];
                 u = e[1];
             }
-            const bool on = live && d != kNone32 && (d != 0 || b == 0);  // d == 0, b special: its own SoE edge
+            relax_soe(live, lb, b, t, st, my, ss, d, u);
+        }
+    }
+    // the walk from boundary b into lane t's special: not into the Center (entry 1)
+    // nor b's own cell
+    __device__ __forceinline__ void relax_walk(bool live, const View &lb, uint32_t b, int bx, int by, uint32_t t,
+                                               uint32_t &st, View &my, const SpecialStatic &ss, uint32_t &bwh,
+                                               uint32_t &b0, uint32_t &b1, uint32_t &b2) const {
+        const bool on = live && st != 2 && t != 1 && t != b && !(b == 0 && ss.v == src);
+        View c;
+        view_walk_lab(lb, b, walk_dist(bx, by, ss.x, ss.y), ss.rk, c);
+        note_walk(on, c, bwh, b0, b1, b2);
+        improve_reg(on, st, my, c);
+    }
+    // the SoE-region edge from boundary b into lane t's special, with b's region row
+    // entry {d, u} for t's region already read
+    __device__ __forceinline__ void relax_soe(bool live, const View &lb, uint32_t b, uint32_t t, uint32_t &st, View &my,
+                                              const SpecialStatic &ss, uint32_t d, uint32_t u) const {
+        const DevParams &p = P;
+        (void)t;
+        {
+            const bool on = live && st != 2 && d != kNone32 && (d != 0 || b == 0);  // d == 0, b special: its own SoE edge
             View c;
             view_walk_lab(lb, b, on ? d : 0u, u, c);
             if (d == 0) {  // b is the source, standing on the region: [SoE src->c]
@@ -2020,6 +2035,15 @@ struct HubWide : HubSolver<1> {
     __device__ __forceinline__ void near_rows(int sx, int sy) const {
         const DevParams &p = P;
         const uint32_t lane = lane_id();
+        if (a->near) {  // the grid's V x regions table
+            const uint2 *row = reinterpret_cast<const uint2 *>(a->near) + (unsigned long long)src * nreg;
+            for (uint32_t r = lane; r < nreg; r += 64) {
+                const uint2 e = row[r];
+                srow[2 * r] = e.x;
+                srow[2 * r + 1] = e.y;
+            }
+            return;
+        }
         const uint32_t rs = region_of(src);  // table index of the source's nearest campfire
         const uint32_t rid_src = rs != kNone10 ? sp[rs].rid : kNone10;
         const uint2 *cells = reinterpret_cast<const uint2 *>(a->rb_cell);
@@ -2184,6 +2208,17 @@ struct HubWide : HubSolver<1> {
         uint32_t st[SPL], bwh[SPL], b0[SPL], b1[SPL], b2[SPL];
         bool mine[SPL];
         uint32_t unc = 0, nbk = 0;
+        // the owned specials' static records: in registers up to 5 per lane (LDS
+        // occupancy, not registers, bounds this kernel), else re-read from LDS
+        constexpr bool kRegStatic = SPL <= 5;
+        SpecialStatic ssr[kRegStatic ? SPL : 1];
+#pragma unroll
+        for (uint32_t i = 0; i < SPL; ++i)
+            if constexpr (kRegStatic) ssr[i] = sp[j + 64u * i <= p.NS ? j + 64u * i : 0u];
+        auto SS = [&](uint32_t i) -> SpecialStatic {
+            if constexpr (kRegStatic) return ssr[i];
+            else return sp[j + 64u * i <= p.NS ? j + 64u * i : 0u];
+        };
         if (j == 0) {
             write_rec(0, st0, 2);
             bnd[0] = 0;
@@ -2197,7 +2232,7 @@ struct HubWide : HubSolver<1> {
         for (uint32_t i = 0; i < SPL; ++i) {
             const uint32_t t = j + 64u * i;
             mine[i] = t >= 1 && t <= p.NS;
-            const SpecialStatic ss = sp[mine[i] ? t : 0u];
+            const SpecialStatic ss = SS(i);
             my[i] = st0;
             st[i] = bwh[i] = b0[i] = b1[i] = b2[i] = 0;
             improve_reg(mine[i] && t == ts, st[i], my[i], st0);
@@ -2219,6 +2254,20 @@ struct HubWide : HubSolver<1> {
             const uint32_t s = select_wide(c, my);
             if (s == kNone32) break;
             const uint32_t so = s & 63u, si = s >> 6;
+            // s's region-row entries for the owned specials' regions, read before the
+            // settle so their latency overlaps it (used if s turns out a boundary)
+            uint32_t ed[SPL], eu[SPL];
+#pragma unroll
+            for (uint32_t i = 0; i < SPL; ++i) {
+                const uint32_t rid = SS(i).rid;
+                ed[i] = kNone32;
+                eu[i] = 0;
+                if (p.use_soe && mine[i] && st[i] == 1 && rid != kNone10) {
+                    const uint2 e = reinterpret_cast<const uint2 *>(B::nearS)[s * nreg + rid];
+                    ed[i] = e.x;
+                    eu[i] = e.y;
+                }
+            }
 #pragma unroll
             for (uint32_t i = 0; i < SPL; ++i)
                 if (j == so && i == si) {
@@ -2250,8 +2299,9 @@ struct HubWide : HubSolver<1> {
 #pragma unroll
             for (uint32_t i = 0; i < SPL; ++i) {
                 const uint32_t t = j + 64u * i;
-                const SpecialStatic ss = sp[mine[i] ? t : 0u];
                 const bool live = mine[i] && st[i] != 2;
+                if (!__any(live)) continue;  // a row whose specials all settled
+                const SpecialStatic ss = SS(i);
                 if (central_s) {
                     View c = cc;
                     c.t0.to = ss.rk;
@@ -2269,8 +2319,10 @@ struct HubWide : HubSolver<1> {
                     ext_view(ls, s, sS.rk, kSoE, 0, p.soe_cost, 0, ss.rk, c);
                     improve_reg(live && sS.region == t, st[i], my[i], c);
                 }
-                if (walks)
-                    relax_boundary(mine[i], ls, s, sS.x, sS.y, t, st[i], my[i], ss, bwh[i], b0[i], b1[i], b2[i]);
+                if (walks) {
+                    B::relax_walk(live, ls, s, sS.x, sS.y, t, st[i], my[i], ss, bwh[i], b0[i], b1[i], b2[i]);
+                    if (p.use_soe) B::relax_soe(live, ls, s, t, st[i], my[i], ss, ed[i], eu[i]);
+                }
             }
             if (walks && j == 0) bnd[nb] = s;
             nb += walks ? 1u : 0u;
@@ -2280,7 +2332,7 @@ struct HubWide : HubSolver<1> {
         if (nbk != 0) {  // every settled label must be certain (as in HubSolver::solve)
 #pragma unroll
             for (uint32_t i = 0; i < SPL; ++i) {
-                const SpecialStatic ss = sp[mine[i] ? j + 64u * i : 0u];
+                const SpecialStatic ss = SS(i);
                 if (mine[i] && st[i] == 2 && !B::label_avail(my[i], nbk, ss.x, ss.y, sx, sy)) unc = 1;
             }
         }

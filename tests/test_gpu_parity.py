@@ -23,15 +23,17 @@ def eng():
     return pathfinder
 
 
-@pytest.fixture(params=["auto-lds", "auto-hbm", "hub1-lds", "wide-lds", "fallback-lds", "fallback-hbm", "sssp-lds",
-                        "sssp-hbm", "generic-lds", "generic-hbm"])
+@pytest.fixture(params=["auto-lds", "auto-hbm", "hub1-lds", "wide-lds", "widescan-lds", "fallback-lds", "fallback-hbm",
+                        "sssp-lds", "sssp-hbm", "generic-lds", "generic-hbm"])
 def grid_state(request, monkeypatch):
     """Every solver path x both grid-state regimes:
     auto     — hub solver when the run time is linear (two sources per wave when
                the specials fit 32 lanes), else the SSSP solvers
     hub1     — hub solver with one source per wave
-    wide     — the wide hub solver (several specials per lane, region rows scanned
-               from the regions' boundary cells) even where the narrow one applies
+    wide     — the wide hub solver (several specials per lane) even where the
+               narrow one applies
+    widescan — the same with each source's region row scanned from the regions'
+               boundary cells instead of read from the grid's region table
     fallback — hub solver handing every source to the SSSP kernel
     sssp     — no hub solver (level-synchronous solver for Legs-first orders)
     generic  — the bucketed solver for every order."""
@@ -43,6 +45,8 @@ def grid_state(request, monkeypatch):
     monkeypatch.delenv("MR_HUB_WIDE", raising=False)
     if algo == "wide":
         monkeypatch.setenv("MR_HUB_WIDE", "1")
+    if algo == "widescan":
+        monkeypatch.setenv("MR_HUB_WIDE", "scan")
     if algo == "hub1":
         monkeypatch.setenv("MR_HUB_SPW", "1")
     if algo in ("sssp", "generic"):
