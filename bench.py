@@ -196,13 +196,20 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
+    # MR_BENCH_BACKEND=gloo: a rehearsal of the N>1 path with every rank on the one
+    # visible GPU and the gather staged through host memory (RCCL needs a GPU per rank)
+    backend = os.environ.get("MR_BENCH_BACKEND", "nccl")
+    device = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
+    torch.cuda.set_device(device)
     # a dedicated stream: the solve kernel and the RCCL gather are ordered on it
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+        if backend == "gloo":
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", device))
     build.build()
     if not pathfinder.device_available():
         raise SystemExit("no gfx950 device visible: the engine has no CPU fallback")
@@ -246,7 +253,7 @@ def main():
         bufs = [torch.zeros(rows * (rw + cw), dtype=torch.int32, device="cuda") for _ in plans]
         for p_, b in zip(plans, bufs):
             p_.bind_outputs(b.data_ptr(), b.data_ptr() + rows * rw * 4)
-        pipe = PipelinedGather(bufs, rank, world)
+        pipe = PipelinedGather(bufs, rank, world, host_staging=backend == "gloo")
     elif all_dst:
         plans = [plan]
     it = [0]
@@ -279,14 +286,24 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    gather_check = None
+    if pipe is not None and rank == 0:
+        # every gathered result record of the last batch: status OK (16), not found (17)
+        # or in the rank's overflow pool (16 + 64), per mr_engine.hpp OutResult
+        k_last = (it[0] - 1) % len(plans)
+        rows_all = pipe.rows(k_last, counts, rw)
+        st = torch.cat([r[:, 3] for r in rows_all]).to("cpu").numpy().astype("uint32") >> 16
+        bad = int(((st != 16) & (st != 17) & (st != 80)).sum())
+        gather_check = {"rows": int(st.size), "bad_status": bad}
     kn = [p_.kernel_ms() for p_ in plans]
     nl = sum(n for _, n in kn)
     kms = sum(ms * n for ms, n in kn) / nl if nl else 0.0
     if world > 1:
-        t = torch.tensor([elapsed, kms], dtype=torch.float64, device="cuda")
+        rdev = "cpu" if backend == "gloo" else "cuda"
+        t = torch.tensor([elapsed, kms], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kms = float(t[0]), float(t[1])
-        tot_src = torch.tensor([n_src], dtype=torch.int64, device="cuda")
+        tot_src = torch.tensor([n_src], dtype=torch.int64, device=rdev)
         dist.all_reduce(tot_src)
         tot_src = int(tot_src)
     else:
@@ -308,7 +325,8 @@ def main():
     else:
         alg_bytes, kernel_name, survey_bytes = algorithmic_bytes(plan, stats, V)
     if world > 1:
-        t = torch.tensor([alg_bytes, survey_bytes, stats["fallback_sources"]], dtype=torch.float64, device="cuda")
+        t = torch.tensor([alg_bytes, survey_bytes, stats["fallback_sources"]], dtype=torch.float64,
+                         device="cpu" if backend == "gloo" else "cuda")
         dist.all_reduce(t)
         alg_bytes, survey_bytes, fb_total = float(t[0]), float(t[1]), int(t[2])
     else:
@@ -324,7 +342,11 @@ def main():
             with open(pmc_path) as f:
                 pm = json.load(f)
             if pm.get("workload") == args.workload and pm.get("queries_per_gpu") == qpg:
+                # one rank's PMC bytes per launch (profiled at N=1); the aggregate over
+                # the N ranks, like alg_bytes
                 traffic = pm.get("hbm_bytes_per_launch")
+                if traffic is not None:
+                    traffic *= world
         except (OSError, ValueError):
             traffic = None
 
@@ -355,6 +377,8 @@ def main():
                      if stats["solver"] in ("hub", "hub_wide") else
                      "SSSP kernel: SURVEY 8d bytes, V*20 B per unique source"},
     }
+    if gather_check is not None:
+        out["gather_check"] = gather_check
     if rank == 0 and world == 1 and not args.no_cpu_baseline and all_dst:
         cb, parity = cpu_baseline_all(m, params, plan, mine, args.cpu_seconds)
         out["cpu_baseline"] = cb

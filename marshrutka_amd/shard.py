@@ -57,15 +57,20 @@ class PipelinedGather:
     the caller's stream wait for the previous gather of buffer k before a new
     solve overwrites it; `drain()` waits for every gather still in flight."""
 
-    def __init__(self, bufs, rank: int, world: int, group=None):
+    def __init__(self, bufs, rank: int, world: int, group=None, host_staging: bool = False):
+        """host_staging: gather host copies (a gloo rehearsal of the RCCL path on one GPU)."""
         import torch
         self.bufs, self.rank, self.world, self.group = list(bufs), rank, world, group
+        self.host = host_staging
         self.pending = [None] * len(self.bufs)
-        self.out = ([[torch.empty_like(b) for _ in range(world)] for b in self.bufs] if rank == 0 else None)
+        dev = "cpu" if host_staging else None
+        self.out = ([[torch.empty_like(b, device=dev) for _ in range(world)] for b in self.bufs]
+                    if rank == 0 else None)
 
     def issue(self, k: int) -> None:
         import torch.distributed as dist
-        self.pending[k] = dist.gather(self.bufs[k], gather_list=self.out[k] if self.rank == 0 else None, dst=0,
+        src = self.bufs[k].cpu() if self.host else self.bufs[k]
+        self.pending[k] = dist.gather(src, gather_list=self.out[k] if self.rank == 0 else None, dst=0,
                                       group=self.group, async_op=True)
 
     def reuse(self, k: int) -> None:
