@@ -315,10 +315,14 @@ def main():
     stats = plan.stats()
     if all_dst:
         # V x 20 B per solve (the 4 B per-cell word read, the 16 B record written),
-        # over the dominant kernel: the fill launch (hub plans) or the whole SSSP pass
+        # over the dominant kernel: the fill launch (hub plans) or the whole SSSP pass.  The
+        # fill kernel reads no per-cell word (the specials come from the source's table), so
+        # its own bytes are the 16 B record per cell plus the table: per entry the 44 B label,
+        # its 4 B rank and the special's 32 B static record
         alg_bytes = survey_bytes = float(n_src) * V * BYTES_PER_VERTEX_SOLVE
         fms = plan.fill_ms()
         if stats["solver"] == "hub" and fms > 0:
+            alg_bytes = float(n_src) * (V * 16 + (stats["num_specials"] + 1) * 80)
             kernel_name, pass_ms, kms = "fill_kernel", kms, fms
         else:
             kernel_name, pass_ms = "sssp_kernel", kms
@@ -369,8 +373,9 @@ def main():
                      "pass_ms": pass_ms if all_dst else kms,
                      "alg_bytes_per_launch": alg_bytes,
                      "survey_8d_bytes_per_launch": survey_bytes,
-                     "note": ("all destinations: fill kernel, SURVEY 8d V x 20 B per source (16 B record written, "
-                              "4 B cell word read); pass_ms adds the specials' solve" if all_dst else
+                     "note": ("all destinations: fill kernel, V x 16 B per source (the record written; no per-cell "
+                              "read) + 80 B per table entry; survey_8d_bytes_per_launch is SURVEY 8d's V x 20 B; "
+                              "pass_ms adds the specials' solve" if all_dst else
                               "hub solver: latency-bound per-source wave Dijkstra over the specials; bytes = "
                               "queries in, results and command slots out, per-source region rows, plus V*20 B "
                               "per SSSP fallback source (DESIGN.md section 4)")

@@ -1,4 +1,5 @@
-// mr_kernel.hip — gfx950 single-source solves for the pathfinder hot path.
+// mr_device.hpp — gfx950 device code of the pathfinder hot path (included by the
+// mr_k_*.hip translation units, one per kernel family, so they compile in parallel).
 //
 // Replaces the body of FindPath::eval (src/pathfinder.rs:199-248): the binary
 // heap frontier (src/binary_heap.rs) becomes bucketed parallel settling, the
@@ -29,6 +30,7 @@
 //
 // Grid state lives in LDS when it fits (G=false) and in a per-workgroup HBM
 // slot otherwise (G=true; cross-thread words then go through sc1 loads/stores).
+#pragma once
 #include <hip/hip_runtime.h>
 
 #include "mr_engine.hpp"
@@ -1332,6 +1334,7 @@ __device__ __forceinline__ void finish_launch(const KArgs *__restrict__ a, uint3
         c[kCtrLastWritten] = wr;
         c[kCtrLastOvf] = ov;
         c[kCtrOvf] = 0;
+        c[kCtrFillWide] = 0;
         c[kCtrDequeue] = 0;
         c[kCtrFbCount] = 0;
         c[kCtrFbDequeue] = 0;
@@ -2419,116 +2422,284 @@ __global__ __launch_bounds__(kBS) void hub_wide_kernel(const KArgs *__restrict__
 // ===================================================================================
 // All-destinations fill: the record of every cell of every
 // hub-solved source is the best walk from its boundaries — metrics in comparator
-// order, then the boundary's rank (precomputed by the hub kernel).  One grid row
-// of workgroups per source, a strided sweep over the cells, one 16-byte store each.
+// order, then the boundary's rank (precomputed by the hub kernel).
+//
+// Work is (source, 64x16 tile) items, one per wave, no workgroup barriers.  The
+// waves form groups; a group takes a run of sources one after another, and its
+// waves interleave each source's tiles (wave j of the group takes tiles j, j + G,
+// ...).  Waves running side by side then write neighbouring tiles, whose 1 KB rows
+// join into long runs: on gfx950 that shape stores at ~4.1 TB/s against ~2.6-3.0
+// for 32x32 tiles taken in order (tools/probes/store_probe.hip).  A wave's LDS
+// tables (the boundaries by rank, the specials' own labels by table index) are
+// reloaded only when its source changes; the item loop makes no global load (on
+// gfx950 vmcnt also counts stores, so a load there would wait for earlier stores).
+//
+// Per tile the wave prunes the boundaries whose leading metric is beaten everywhere
+// in it (wave min + ballot).  Lane l owns column l and rows i < 16.  When the three
+// metrics fit one 63-bit key (fields sized per source from the table's maxima) and
+// the tile does not touch the axes through the Center (no detours), a walk's key is
+// K_b + d * slope, so down a column it moves by +-slope per row: the sweep over a
+// boundary's 16 cells is a 64-bit add, a compare and three selects per cell.
+// Otherwise the cell's walk distance and the three-metric compare are evaluated in
+// full.  The specials of the tile and the source then overwrite their cells.
 // =====================================================================================
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t bit_width64(unsigned long long x) { return x ? 64u - uint32_t(__clzll(x)) : 0u; }
+
+// the fill kernel's rare path: a tile whose source's metrics do not fit one key.  Row
+// by row, each cell's walk distance in full and the three-metric compare.  It runs in
+// a launch of its own (fill_kernel<PERM, true>), so its registers do not weigh on the
+// fast path's occupancy.
 template <uint32_t PERM>
-__global__ __launch_bounds__(kBS) void fill_kernel(const KArgs *__restrict__ a) {
+__device__ __forceinline__ void fill_tile_rows(const uint32_t (*B)[64], unsigned long long live, int wx,
+                                                      int y0, int ty0, int cx, bool col_ok, uint32_t S, VRecord *outs) {
     constexpr uint32_t q0 = PERM / 9, q1 = (PERM / 3) % 3, q2 = PERM % 3;
-    // the leading metric of a walk is base + slope * distance (legs 1, money 0, time 180 s)
-    constexpr uint64_t slope1 = q0 == 0 ? 1u : (q0 == 1 ? 0u : 180u);
-    constexpr int kTile = 32;  // 32 x 32 cells per workgroup pass, 4 per thread
-    __shared__ int bx[64], by[64];
-    __shared__ uint32_t bm0[64], bm1[64], bm2[64], bt[64];
-    __shared__ uint32_t nbs;
-    __shared__ unsigned long long minhi, live;
-    const uint32_t NS = a->p.NS, T = NS + 1, V = a->p.V, S = a->p.S;
-    const int H = int(a->p.H);
-    const uint32_t *sinfo = a->sinfo;
-    const uint32_t tps = (S + kTile - 1) / kTile, ntile = tps * tps;
-    const uint32_t tid = threadIdx.x;
-    // each workgroup takes a contiguous run of (source, tile) items, so the boundary
-    // table is reloaded only when its source changes (and the grid stays small: every
-    // workgroup ends with one atomic on the pass's done counter)
-    const unsigned long long total = (unsigned long long)a->nsrc * ntile;
-    const unsigned long long chunk = (total + gridDim.x - 1) / gridDim.x;
-    const unsigned long long w0 = (unsigned long long)blockIdx.x * chunk;
-    const unsigned long long w1 = w0 + chunk < total ? w0 + chunk : total;
-    for (unsigned long long w = w0; w < w1;) {
-        const uint32_t s = uint32_t(w / ntile);
-        const unsigned long long wend = (unsigned long long)(s + 1) * ntile < w1 ? (unsigned long long)(s + 1) * ntile : w1;
-        __syncthreads();
-        if (a->src_state[s] != 1) {  // uniform: solved by the SSSP kernel
-            w = wend;
-            continue;
+#pragma unroll 1
+    for (int i = 0; i < int(kFillTH); ++i) {
+        uint32_t r0 = 0xFFFFFFFFu, r1 = 0xFFFFFFFFu, r2 = 0xFFFFFFFFu, rv = 0xFFFFFFFFu;
+        for (unsigned long long m = live; m; m &= m - 1) {  // rank order: the first of equal metrics wins
+            const uint32_t rr = uint32_t(__ffsll((long long)m) - 1);
+            const uint32_t d = walk_dist(int(B[0][rr]), int(B[1][rr]), wx, y0 + i);
+            const uint32_t b0 = B[2][rr], b1 = B[3][rr], b2 = B[4][rr];
+            const uint32_t mm0 = b0 + d, mm2 = b2 + 180u * d;
+            const uint32_t c1 = q0 == 0 ? mm0 : (q0 == 1 ? b1 : mm2);
+            const uint32_t c2 = q1 == 0 ? mm0 : (q1 == 1 ? b1 : mm2);
+            const uint32_t c3 = q2 == 0 ? mm0 : (q2 == 1 ? b1 : mm2);
+            const uint32_t k1 = q0 == 0 ? r0 : (q0 == 1 ? r1 : r2);
+            const uint32_t k2 = q1 == 0 ? r0 : (q1 == 1 ? r1 : r2);
+            const uint32_t k3 = q2 == 0 ? r0 : (q2 == 1 ? r1 : r2);
+            const bool better = c1 < k1 || (c1 == k1 && (c2 < k2 || (c2 == k2 && c3 < k3)));
+            r0 = better ? mm0 : r0;
+            r1 = better ? b1 : r1;
+            r2 = better ? mm2 : r2;
+            rv = better ? B[5][rr] : rv;
         }
+        const int cy = ty0 + i;
+        if (col_ok && cy < int(S)) outs[uint32_t(cy) * S + uint32_t(cx)] = VRecord{r0, r1, r2, rv};
+    }
+}
+
+#ifndef MR_FILL_WAVES
+#define MR_FILL_WAVES 6  // waves per SIMD the fill kernel is register-bounded to
+#endif
+template <uint32_t PERM, bool WIDE>
+__global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *__restrict__ a) {
+    constexpr uint32_t q0 = PERM / 9, q1 = (PERM / 3) % 3, q2 = PERM % 3;
+    // per unit of walk distance: legs 1, money 0, time 180 s
+    constexpr uint32_t sl[3] = {1u, 0u, 180u};
+    constexpr uint64_t slope1 = sl[q0];
+    constexpr int kTW = int(kFillTW), kTH = int(kFillTH);
+    // per wave: boundaries by rank (x, y, m0, m1, m2, table index, key lo, key hi),
+    // specials by table index (x, y, m0, m1, m2 of their own labels; entry 0 = source)
+    __shared__ uint32_t btab[kBS / 64][13][64];
+    // the wave index through readfirstlane: everything derived from it (tile origins,
+    // key fields, slopes) then lives in SGPRs
+    const uint32_t lane = threadIdx.x & 63u, wv = uint32_t(__builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)));
+    uint32_t(*B)[64] = btab[wv];
+    uint32_t(*P)[64] = btab[wv] + 8;
+    const uint32_t NS = a->p.NS, T = NS + 1, V = a->p.V, S = a->p.S, nsrc = a->nsrc;
+    const int H = int(a->p.H);
+    const uint32_t tpx = (S + kTW - 1) / kTW, tpy = (S + kTH - 1) / kTH, ntile = tpx * tpy;
+    const bool no_prune = (a->dbg_flags & 1u) != 0, no_pack = (a->dbg_flags & 2u) != 0;
+    const uint32_t nwaves = gridDim.x * (kBS / 64), gw = blockIdx.x * (kBS / 64) + wv;
+    const uint32_t ngroups = nsrc < nwaves ? nsrc : nwaves, G = nwaves / ngroups, g = gw / G, j = gw % G;
+    uint32_t s_begin = g < ngroups ? uint32_t(uint64_t(g) * nsrc / ngroups) : 0u;
+    const uint32_t s_end = g < ngroups ? uint32_t(uint64_t(g + 1) * nsrc / ngroups) : 0u;
+    if (WIDE && __hip_atomic_load(a->counter + kCtrFillWide, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+        s_begin = s_end;  // the first launch found none
+    for (uint32_t s = s_begin; s < s_end; ++s) {
+        if (a->src_state[s] != 1) continue;  // solved by the SSSP kernel, which wrote its records
+        // ---- this source's tables -------------------------------------------------
         const unsigned long long tb = (unsigned long long)s * T;
         const uint32_t src = a->src_v[s];
-        if (tid == 0) nbs = 0;
-        __syncthreads();
-        for (uint32_t t = tid; t < T; t += kBS) {
-            const uint32_t r = a->out_lex[tb + t];
-            if (r == kNone32) continue;
-            const Rec &e = a->out_tab[tb + t];
-            bx[r] = t == 0 ? int(src % S) - H : a->sp[t].x;
-            by[r] = t == 0 ? int(src / S) - H : a->sp[t].y;
-            bm0[r] = e.m[0];
-            bm1[r] = e.m[1];
-            bm2[r] = e.m[2];
-            bt[r] = t;
-            atomicAdd(&nbs, 1u);
-        }
-        __syncthreads();
-        const uint32_t nb = nbs;
-        VRecord *out = a->out_rec + (unsigned long long)s * V;
-        for (; w < wend; ++w) {
-            const uint32_t tile = uint32_t(w % ntile);
-            const int tx0 = int(tile % tps) * kTile, ty0 = int(tile / tps) * kTile;
-            const int x0 = tx0 - H, y0 = ty0 - H;
-            const int x1 = min(tx0 + kTile - 1, int(S) - 1) - H, y1 = min(ty0 + kTile - 1, int(S) - 1) - H;
-            if (tid == 0) {
-                minhi = ~0ull;
-                live = 0;
+        wave_sync();  // the previous source's tables have been read
+        uint32_t r = kNone32, e0 = 0, e1 = 0, e2 = 0;
+        if (lane < T) {
+            r = a->out_lex[tb + lane];
+            const Rec &e = a->out_tab[tb + lane];
+            e0 = e.m[0];
+            e1 = e.m[1];
+            e2 = e.m[2];
+            const uint32_t x = lane == 0 ? uint32_t(int(src % S) - H) : uint32_t(a->sp[lane].x);
+            const uint32_t y = lane == 0 ? uint32_t(int(src / S) - H) : uint32_t(a->sp[lane].y);
+            P[0][lane] = x;
+            P[1][lane] = y;
+            P[2][lane] = lane == 0 ? 0u : e0;
+            P[3][lane] = lane == 0 ? 0u : e1;
+            P[4][lane] = lane == 0 ? 0u : e2;
+            if (r != kNone32) {
+                B[0][r] = x;
+                B[1][r] = y;
+                B[2][r] = e0;
+                B[3][r] = e1;
+                B[4][r] = e2;
+                B[5][r] = lane;
             }
-            __syncthreads();
+        }
+        const bool isb = lane < T && r != kNone32;
+        const uint32_t nb = uint32_t(__popcll(__ballot(isb)));
+        // key fields: each metric's maximum over every walk (distance <= 2S + 2)
+        const uint64_t dmax = 2ull * S + 2;
+        const uint64_t em[3] = {e0, e1, e2};
+        uint64_t mx1 = isb ? em[q0] + sl[q0] * dmax : 0, mx2 = isb ? em[q1] + sl[q1] * dmax : 0,
+                 mx3 = isb ? em[q2] + sl[q2] * dmax : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            mx1 = max(mx1, (uint64_t)__shfl_xor((unsigned long long)mx1, o));
+            mx2 = max(mx2, (uint64_t)__shfl_xor((unsigned long long)mx2, o));
+            mx3 = max(mx3, (uint64_t)__shfl_xor((unsigned long long)mx3, o));
+        }
+        const uint32_t w1 = uint32_t(__builtin_amdgcn_readfirstlane(int(max(1u, bit_width64(mx1)))));
+        const uint32_t w2 = uint32_t(__builtin_amdgcn_readfirstlane(int(max(1u, bit_width64(mx2)))));
+        const uint32_t w3 = uint32_t(__builtin_amdgcn_readfirstlane(int(max(1u, bit_width64(mx3)))));
+        const bool packable = !no_pack && w1 + w2 + w3 <= 63u;
+        // the first launch (WIDE = false) fills the sources whose metrics fit one key and
+        // counts the others, which the second launch fills
+        if (packable == WIDE) {
+            if (!WIDE && j == 0 && lane == 0) atomicAdd(a->counter + kCtrFillWide, 1u);
+            continue;
+        }
+        const uint32_t sh2 = w3, sh1 = w2 + w3;
+        const unsigned long long slope = packable ? ((unsigned long long)sl[q0] << sh1) +
+                                                        ((unsigned long long)sl[q1] << sh2) + sl[q2]
+                                                  : 0ull;
+        if (isb && packable) {
+            const unsigned long long K = ((unsigned long long)em[q0] << sh1) | ((unsigned long long)em[q1] << sh2) | em[q2];
+            B[6][r] = uint32_t(K);
+            B[7][r] = uint32_t(K >> 32);
+        }
+        wave_sync();
+        // ---- this wave's tiles of the source ---------------------------------------
+        VRecord *const outs = a->out_rec + (unsigned long long)s * V;
+        for (uint32_t tile = j; tile < ntile; tile += G) {
+            const int tx0 = int(tile % tpx) * kTW, ty0 = int(tile / tpx) * kTH;
+            const int x0 = tx0 - H, y0 = ty0 - H;
+            const int x1 = min(tx0 + kTW - 1, int(S) - 1) - H, y1 = min(ty0 + kTH - 1, int(S) - 1) - H;
             // Prune the boundaries whose leading metric is beaten everywhere in the tile:
             // lo_b > min over b' of hi_b' (walks are at least the L1 distance to the tile
             // and at most the farthest corner's plus the 2-cell detour round the Center).
-            unsigned long long lo = 0;
-            if (tid < nb) {
-                const int bxx = bx[tid], byy = by[tid];
+            unsigned long long lo = ~0ull, hi = ~0ull;
+            if (lane < nb) {
+                const int bxx = int(B[0][lane]), byy = int(B[1][lane]);
                 const int dx = bxx < x0 ? x0 - bxx : (bxx > x1 ? bxx - x1 : 0);
                 const int dy = byy < y0 ? y0 - byy : (byy > y1 ? byy - y1 : 0);
                 const int fx = max(abs(bxx - x0), abs(bxx - x1)), fy = max(abs(byy - y0), abs(byy - y1));
-                const uint32_t base = q0 == 0 ? bm0[tid] : (q0 == 1 ? bm1[tid] : bm2[tid]);
+                const uint32_t base = B[2 + q0][lane];
                 lo = base + slope1 * uint64_t(dx + dy);
-                atomicMin(&minhi, base + slope1 * uint64_t(fx + fy + 2));
+                hi = base + slope1 * uint64_t(fx + fy + 2);
             }
-            __syncthreads();
-            if (tid < nb && (lo <= minhi || (a->dbg_flags & 1u))) atomicOr(&live, 1ull << tid);
-            __syncthreads();
-            const unsigned long long lv = live;
 #pragma unroll
-            for (int part = 0; part < kTile * kTile / kBS; ++part) {
-            const int cx = tx0 + int(tid % kTile), cy = ty0 + int(tid / kTile) + part * (kBS / kTile);
-            if (cx < int(S) && cy < int(S)) {
-                const uint32_t v = uint32_t(cy) * S + uint32_t(cx);
-                VRecord rec{0, 0, 0, kViaSource};
-                const uint32_t t = sinfo[v] & kNone10;
-                if (v == src) {
-                } else if (t != kNone10) {
-                    const Rec &e = a->out_tab[tb + t];
-                    rec = VRecord{e.m[0], e.m[1], e.m[2], kViaSpecial | t};
-                } else {
-                    const int wx = cx - H, wy = cy - H;
-                    uint32_t k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu, k3 = 0xFFFFFFFFu;
-                    for (unsigned long long m = lv; m; m &= m - 1) {  // rank order: the first of equal metrics wins
-                        const uint32_t r = uint32_t(__ffsll((long long)m) - 1);
-                        const uint32_t d = walk_dist(bx[r], by[r], wx, wy);
-                        const uint32_t mm[3] = {bm0[r] + d, bm1[r], bm2[r] + 180u * d};
-                        const uint32_t c1 = mm[q0], c2 = mm[q1], c3 = mm[q2];
-                        if (c1 < k1 || (c1 == k1 && (c2 < k2 || (c2 == k2 && c3 < k3)))) {
-                            k1 = c1;
-                            k2 = c2;
-                            k3 = c3;
-                            rec = VRecord{mm[0], mm[1], mm[2], bt[r]};
-                        }
+            for (int o = 32; o > 0; o >>= 1) {
+                const unsigned long long h2 = __shfl_xor(hi, o);
+                hi = h2 < hi ? h2 : hi;
+            }
+            const unsigned long long live = __ballot(lane < nb && (lo <= hi || no_prune));
+            // the specials (and the source) inside this tile
+            bool in = false;
+            if (lane < T) {
+                const int px = int(P[0][lane]) - x0, py = int(P[1][lane]) - y0;
+                in = px >= 0 && px < kTW && py >= 0 && py < kTH;
+            }
+            const unsigned long long sp_in = __ballot(in);
+            const int wx = x0 + int(lane), cx = tx0 + int(lane);
+            const bool col_ok = cx < int(S);
+            const bool axis = (x0 <= 0 && x1 >= 0) || (y0 <= 0 && y1 >= 0);
+            const unsigned long long mask2 = (1ull << w2) - 1, mask3 = (1ull << w3) - 1;
+            if (!WIDE) {
+                // the best (key, rank) per cell; a rank is the boundary's position in the
+                // (length, command list) order, so the pair orders walks exactly like the
+                // comparator whatever order the boundaries are visited in
+                unsigned long long kb[kTH];
+                uint32_t rv[kTH];
+#pragma unroll
+                for (int i = 0; i < kTH; ++i) {
+                    kb[i] = ~0ull;
+                    rv[i] = 0xFFFFFFFFu;
+                }
+                // boundaries on an axis through the Center, in a tile on an axis, take
+                // walk_dist's 2-cell detour to cells on the same axis across the Center:
+                // they get a loop of their own after the others
+                unsigned long long axm = 0;
+                if (axis) {
+                    const bool on = lane < nb && (B[0][lane] == 0u || B[1][lane] == 0u);
+                    axm = __ballot(on) & live;
+                }
+                for (unsigned long long m = live & ~axm; m; m &= m - 1) {  // rank order: the first of equal keys wins
+                    const uint32_t rr = uint32_t(__ffsll((long long)m) - 1);
+                    // wave-uniform values in SGPRs, so the per-row step is a scalar select
+                    const int bxx = __builtin_amdgcn_readfirstlane(int(B[0][rr]));
+                    const int istar = __builtin_amdgcn_readfirstlane(int(B[1][rr])) - y0;  // the boundary's row in the tile
+                    const unsigned long long K = (unsigned long long)uint32_t(__builtin_amdgcn_readfirstlane(int(B[6][rr]))) |
+                                                 ((unsigned long long)uint32_t(__builtin_amdgcn_readfirstlane(int(B[7][rr]))) << 32);
+                    // down the lane's column the walk distance moves by +-1 per row, so the
+                    // key by +-slope
+                    unsigned long long key = K + slope * uint64_t(uint32_t(abs(bxx - wx)) + uint32_t(abs(istar)));
+                    const unsigned long long up = slope, down = (unsigned long long)(-(long long)slope);
+#pragma unroll
+                    for (int i = 0; i < kTH; ++i) {
+                        if (i > 0) key += i > istar ? up : down;
+                        const bool better = key < kb[i];
+                        kb[i] = better ? key : kb[i];
+                        rv[i] = better ? rr : rv[i];
                     }
                 }
-                out[v] = rec;
+                for (unsigned long long m = axm; m; m &= m - 1) {
+                    const uint32_t rr = uint32_t(__ffsll((long long)m) - 1);
+                    const int bxx = __builtin_amdgcn_readfirstlane(int(B[0][rr]));
+                    const int byy = __builtin_amdgcn_readfirstlane(int(B[1][rr]));
+                    const int istar = byy - y0, i0 = -y0;  // i0: the tile's row y = 0
+                    const unsigned long long K = (unsigned long long)uint32_t(__builtin_amdgcn_readfirstlane(int(B[6][rr]))) |
+                                                 ((unsigned long long)uint32_t(__builtin_amdgcn_readfirstlane(int(B[7][rr]))) << 32);
+                    unsigned long long key = K + slope * uint64_t(uint32_t(abs(bxx - wx)) + uint32_t(abs(istar)));
+                    const unsigned long long up = slope, down = (unsigned long long)(-(long long)slope), det2 = 2 * slope;
+                    const bool detx = byy == 0 && wx != 0 && bxx != 0 && ((wx < 0) != (bxx < 0));
+                    const bool dety = bxx == 0 && wx == 0 && byy != 0;
+#pragma unroll
+                    for (int i = 0; i < kTH; ++i) {
+                        if (i > 0) key += i > istar ? up : down;
+                        const bool det = (i == i0 && detx) || (dety && i != i0 && ((i < i0) != (byy < 0)));
+                        const unsigned long long kk = key + (det ? det2 : 0ull);
+                        const bool better = kk < kb[i] || (kk == kb[i] && rr < rv[i]);
+                        kb[i] = better ? kk : kb[i];
+                        rv[i] = better ? rr : rv[i];
+                    }
+                }
+                // buffer stores off one per-tile base: the lane's offset in a VGPR, the
+                // row's (i * S * 16 B) in an SGPR, so no per-row 64-bit address
+                const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+                    outs + (size_t(ty0) * S + size_t(tx0)), 0, int(16u * kTH * S), 0x00020000);  // the tile's rows
+#pragma unroll
+                for (int i = 0; i < kTH; ++i) {
+                    const int cy = ty0 + i;
+                    if (col_ok && cy < int(S)) {
+                        // c[k] is metric q_k; the rank's table index from the wave's table
+                        const uint32_t c[3] = {uint32_t(kb[i] >> sh1), uint32_t((kb[i] >> sh2) & mask2),
+                                               uint32_t(kb[i] & mask3)};
+                        const u32x4_t rec = {q0 == 0 ? c[0] : (q1 == 0 ? c[1] : c[2]), q0 == 1 ? c[0] : (q1 == 1 ? c[1] : c[2]),
+                                             q0 == 2 ? c[0] : (q1 == 2 ? c[1] : c[2]), B[5][rv[i]]};
+                        __builtin_amdgcn_raw_buffer_store_b128(rec, rsrc, int(lane * 16u), int(uint32_t(i) * S * 16u), 0);
+                    }
+                }
+            } else {
+                fill_tile_rows<PERM>(B, live, wx, y0, ty0, cx, col_ok, S, outs);  // metrics too wide for one key
             }
+            // specials' cells hold their own labels, the source's cell (last: it may also
+            // be a special) the start label.  These stores follow the lane's own store to
+            // the same cell, so they are the ones that land.
+            for (unsigned long long m = sp_in; m;) {
+                uint32_t t;
+                if (m & ~1ull) {
+                    t = uint32_t(__ffsll((long long)(m & ~1ull)) - 1);
+                    m &= ~(1ull << t);
+                } else {
+                    t = 0;
+                    m = 0;
+                }
+                const int px = int(P[0][t]) - x0, py = int(P[1][t]) - y0;
+                if (lane == uint32_t(px))
+                    outs[uint32_t(ty0 + py) * S + uint32_t(cx)] =
+                        VRecord{P[2][t], P[3][t], P[4][t], t == 0 ? kViaSource : (kViaSpecial | t)};
             }
-            __syncthreads();
         }
     }
     __syncthreads();
@@ -2704,131 +2875,6 @@ __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a)
     }
     __syncthreads();
     if (threadIdx.x == 0) finish_launch(a, written);
-}
-
-// ---- host-side launch helpers (called from mr_host.cpp) ------------------------------
-uint32_t lds_bytes(uint32_t NS, uint32_t V, bool grid_in_lds, uint32_t algo) {
-    return lds_layout(NS, V, grid_in_lds, algo).total;
-}
-
-template <bool G, class IdxT, uint32_t ALGO>
-static const void *kfn() {
-    return reinterpret_cast<const void *>(&solve_kernel<G, IdxT, ALGO>);
-}
-
-static const void *select_kernel(bool grid_in_lds, uint32_t algo) {
-    if (grid_in_lds) return algo == kAlgoLegs ? kfn<false, uint16_t, kAlgoLegs>() : kfn<false, uint16_t, kAlgoGeneric>();
-    return algo == kAlgoLegs ? kfn<true, uint32_t, kAlgoLegs>() : kfn<true, uint32_t, kAlgoGeneric>();
-}
-
-hipError_t launch_solve(const KArgs *d_args, bool grid_in_lds, uint32_t algo, uint32_t NS, uint32_t V,
-                        uint32_t blocks, hipStream_t stream) {
-    const uint32_t bytes = lds_bytes(NS, V, grid_in_lds, algo);
-    const void *fn = select_kernel(grid_in_lds, algo);
-    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
-    void *args[] = {const_cast<KArgs **>(&d_args)};
-    return hipLaunchKernel(fn, dim3(blocks), dim3(kBS), args, bytes, stream);
-}
-
-uint32_t hub_lds_bytes(uint32_t NS, uint32_t nreg, uint32_t spw) { return hub_layout(NS, nreg, spw).total; }
-
-template <uint32_t SPW>
-static const void *hub_fn_spw(uint32_t perm) {
-    switch (perm) {
-        case 5: return reinterpret_cast<const void *>(&hub_kernel<5, SPW>);    // legs money time
-        case 7: return reinterpret_cast<const void *>(&hub_kernel<7, SPW>);    // legs time money
-        case 11: return reinterpret_cast<const void *>(&hub_kernel<11, SPW>);  // money legs time
-        case 15: return reinterpret_cast<const void *>(&hub_kernel<15, SPW>);  // money time legs
-        case 19: return reinterpret_cast<const void *>(&hub_kernel<19, SPW>);  // time legs money
-        case 21: return reinterpret_cast<const void *>(&hub_kernel<21, SPW>);  // time money legs
-        default: return nullptr;
-    }
-}
-static const void *hub_fn(const uint32_t perm[3], uint32_t spw) {
-    const uint32_t k = perm[0] * 9 + perm[1] * 3 + perm[2];
-    return spw == 2 ? hub_fn_spw<2>(k) : hub_fn_spw<1>(k);
-}
-
-hipError_t launch_hub(const KArgs *d_args, const uint32_t perm[3], uint32_t spw, uint32_t NS, uint32_t nreg,
-                      uint32_t blocks, hipStream_t stream) {
-    const uint32_t bytes = hub_lds_bytes(NS, nreg, spw);
-    const void *fn = hub_fn(perm, spw);
-    if (!fn) return hipErrorInvalidValue;
-    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
-    void *args[] = {const_cast<KArgs **>(&d_args)};
-    return hipLaunchKernel(fn, dim3(blocks), dim3(kBS), args, bytes, stream);
-}
-
-uint32_t hub_wide_lds_bytes(uint32_t NS, uint32_t nreg) { return wide_layout(NS, nreg).total; }
-
-template <uint32_t SPL>
-static const void *wide_fn_spl(uint32_t perm) {
-    switch (perm) {
-        case 5: return reinterpret_cast<const void *>(&hub_wide_kernel<5, SPL>);
-        case 7: return reinterpret_cast<const void *>(&hub_wide_kernel<7, SPL>);
-        case 11: return reinterpret_cast<const void *>(&hub_wide_kernel<11, SPL>);
-        case 15: return reinterpret_cast<const void *>(&hub_wide_kernel<15, SPL>);
-        case 19: return reinterpret_cast<const void *>(&hub_wide_kernel<19, SPL>);
-        case 21: return reinterpret_cast<const void *>(&hub_wide_kernel<21, SPL>);
-        default: return nullptr;
-    }
-}
-// specials per lane for a table of NS + 1 entries: 2, 5 or 8 (0 if too many)
-uint32_t hub_wide_spl(uint32_t NS) {
-    const uint32_t T = NS + 1;
-    return T <= 128 ? 2u : (T <= 320 ? 5u : (T <= 512 ? 8u : 0u));
-}
-static const void *wide_fn(const uint32_t perm[3], uint32_t NS) {
-    const uint32_t k = perm[0] * 9 + perm[1] * 3 + perm[2];
-    switch (hub_wide_spl(NS)) {
-        case 2: return wide_fn_spl<2>(k);
-        case 5: return wide_fn_spl<5>(k);
-        case 8: return wide_fn_spl<8>(k);
-        default: return nullptr;
-    }
-}
-hipError_t launch_hub_wide(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t blocks,
-                           hipStream_t stream) {
-    const uint32_t bytes = hub_wide_lds_bytes(NS, nreg);
-    const void *fn = wide_fn(perm, NS);
-    if (!fn) return hipErrorInvalidValue;
-    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
-    void *args[] = {const_cast<KArgs **>(&d_args)};
-    return hipLaunchKernel(fn, dim3(blocks), dim3(kBS), args, bytes, stream);
-}
-int hub_wide_blocks_per_cu(const uint32_t perm[3], uint32_t NS, uint32_t bytes) {
-    int n = 0;
-    const void *fn = wide_fn(perm, NS);
-    if (fn) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kBS, bytes);
-    return n;
-}
-
-hipError_t launch_fill(const KArgs *d_args, const uint32_t perm[3], uint32_t gx, uint32_t gy, hipStream_t stream) {
-    const void *fn = nullptr;
-    switch (perm[0] * 9 + perm[1] * 3 + perm[2]) {
-        case 5: fn = reinterpret_cast<const void *>(&fill_kernel<5>); break;
-        case 7: fn = reinterpret_cast<const void *>(&fill_kernel<7>); break;
-        case 11: fn = reinterpret_cast<const void *>(&fill_kernel<11>); break;
-        case 15: fn = reinterpret_cast<const void *>(&fill_kernel<15>); break;
-        case 19: fn = reinterpret_cast<const void *>(&fill_kernel<19>); break;
-        case 21: fn = reinterpret_cast<const void *>(&fill_kernel<21>); break;
-        default: return hipErrorInvalidValue;
-    }
-    void *args[] = {const_cast<KArgs **>(&d_args)};
-    return hipLaunchKernel(fn, dim3(gx, gy), dim3(kBS), args, 0, stream);
-}
-
-int hub_blocks_per_cu(const uint32_t perm[3], uint32_t spw, uint32_t bytes) {
-    int n = 0;
-    const void *fn = hub_fn(perm, spw);
-    if (fn) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kBS, bytes);
-    return n;
-}
-
-int max_blocks_per_cu(bool grid_in_lds, uint32_t algo, uint32_t bytes) {
-    int n = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, select_kernel(grid_in_lds, algo), kBS, bytes);
-    return n;
 }
 
 }  // namespace mr

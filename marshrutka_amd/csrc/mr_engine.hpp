@@ -101,6 +101,11 @@ struct VRecord {
     uint32_t m0, m1, m2, via;
 };
 constexpr uint32_t kViaSpecial = 0x80000000u, kViaSource = 0xFFFFFFFFu;
+// all-destinations fill tiles: one wave per kFillTW x kFillTH cells (a lane per column)
+#ifndef MR_FILL_TH
+#define MR_FILL_TH 16
+#endif
+constexpr uint32_t kFillTW = 64, kFillTH = MR_FILL_TH;
 
 // kernel arguments (one solve launch)
 struct KArgs {
@@ -163,7 +168,8 @@ enum : uint32_t {
     kCtrLastWritten = 7,  // kCtrWritten of the last completed pass
     kCtrOvf = 8,          // command-overflow pool: commands allocated in this pass
     kCtrLastOvf = 9,      // kCtrOvf of the last completed pass
-    kCtrWords = 10
+    kCtrFillWide = 10,    // all-destinations fill: sources left to the second (wide-metric) launch
+    kCtrWords = 11
 };
 // result status (OutResult high half - 16) of a label whose commands went to the
 // overflow pool: its first command slot holds {kOvfTag, offset, count}

@@ -27,8 +27,10 @@ int max_blocks_per_cu(bool grid_in_lds, uint32_t algo, uint32_t bytes);
 uint32_t hub_lds_bytes(uint32_t NS, uint32_t nreg, uint32_t spw);
 hipError_t launch_hub(const KArgs *d_args, const uint32_t perm[3], uint32_t spw, uint32_t NS, uint32_t nreg,
                       uint32_t blocks, hipStream_t stream);
-hipError_t launch_fill(const KArgs *d_args, const uint32_t perm[3], uint32_t gx, uint32_t gy, hipStream_t stream);
+hipError_t launch_fill(const KArgs *d_args, const uint32_t perm[3], uint32_t gx, uint32_t gy, hipStream_t stream,
+                       bool wide);
 int hub_blocks_per_cu(const uint32_t perm[3], uint32_t spw, uint32_t bytes);
+int fill_blocks_per_cu(const uint32_t perm[3]);
 uint32_t hub_wide_lds_bytes(uint32_t NS, uint32_t nreg);
 uint32_t hub_wide_spl(uint32_t NS);
 hipError_t launch_hub_wide(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t blocks,
@@ -700,7 +702,8 @@ struct mr_plan {
     KArgs *d_args = nullptr;
     KArgs *d_args_fb = nullptr;           // SSSP launch over the hub solver's fallback list
     KArgs *d_args_hub_last = nullptr;     // hub launch that ends the pass (fallback known to be empty)
-    KArgs *d_args_fill = nullptr;         // all-destinations mode: the fill launch (ends the pass)
+    KArgs *d_args_fill = nullptr;         // all-destinations mode: the fill launch
+    KArgs *d_args_fill2 = nullptr;        // ... and its wide-metric second launch (ends the pass)
     bool all_mode = false;
     VRecord *d_rec = nullptr;             // all-destinations outputs (KArgs::out_rec ...)
     Rec *d_tab = nullptr;
@@ -712,7 +715,7 @@ struct mr_plan {
     uint32_t *d_near = nullptr, *d_fb = nullptr;
     uint32_t *d_near_sp = nullptr, *d_rb_off = nullptr, *d_rb_cell = nullptr;  // wide hub tables
     OutCmd *d_ovf = nullptr;              // command-overflow pool (labels longer than max_cmds)
-    uint32_t hub_blocks = 0, fb_blocks = 0, spw = 1, cus = 256;
+    uint32_t hub_blocks = 0, fb_blocks = 0, spw = 1, cus = 256, fill_per_cu = 8;
     unsigned long long *d_dbg = nullptr;  // diagnostic builds: per-workgroup phase cycles
     uint32_t algo = kAlgoGeneric;
     SpecialStatic *d_sp = nullptr;
@@ -729,7 +732,8 @@ struct mr_plan {
         for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_rank_inv, (void *)d_src, (void *)d_qb, (void *)d_qd,
                         (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
                         (void *)d_counter, (void *)d_args, (void *)d_dbg, (void *)d_args_fb, (void *)d_near,
-                        (void *)d_fb, (void *)d_args_hub_last, (void *)d_args_fill, (void *)d_rec, (void *)d_tab,
+                        (void *)d_fb, (void *)d_args_hub_last, (void *)d_args_fill, (void *)d_args_fill2, (void *)d_rec,
+                        (void *)d_tab,
                         (void *)d_lex, (void *)d_sstate, (void *)d_near_sp, (void *)d_rb_off, (void *)d_rb_cell, (void *)d_ovf})
             if (p) (void)hipFree(p);
         for (auto *v : {&timed, &timed_fill})
@@ -759,7 +763,11 @@ static int upload_args(mr_plan *pl) {
         if (!put(pl->d_args_fb, f)) return MR_ERR_DEVICE;
         KArgs l = k;
         l.last_launch = 1;
-        if (!put(pl->all_mode ? pl->d_args_fill : pl->d_args_hub_last, l)) return MR_ERR_DEVICE;
+        if (!put(pl->all_mode ? pl->d_args_fill2 : pl->d_args_hub_last, l)) return MR_ERR_DEVICE;
+        if (pl->all_mode) {
+            l.last_launch = 0;
+            if (!put(pl->d_args_fill, l)) return MR_ERR_DEVICE;
+        }
     }
     return MR_OK;
 }
@@ -909,9 +917,11 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
                                                      uint64_t(hper) * prop.multiProcessorCount));
         if (const char *e = std::getenv("MR_HUB_BLOCKS")) pl->hub_blocks = uint32_t(std::max(1, std::atoi(e)));
         pl->fb_blocks = pl->blocks;
+        pl->fill_per_cu = uint32_t(std::max(1, fill_blocks_per_cu(hp.p.perm)));
         if (hipMalloc(reinterpret_cast<void **>(&pl->d_args_fb), sizeof(KArgs)) != hipSuccess ||
             hipMalloc(reinterpret_cast<void **>(&pl->d_args_hub_last), sizeof(KArgs)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&pl->d_args_fill), sizeof(KArgs)) != hipSuccess)
+            hipMalloc(reinterpret_cast<void **>(&pl->d_args_fill), sizeof(KArgs)) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&pl->d_args_fill2), sizeof(KArgs)) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "kernel args"));
     }
 #ifdef MR_HUBDUMP
@@ -962,10 +972,11 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     hipError_t e;
     ++pl->runs;
     if (pl->hp.hub && pl->all_mode) {
-        // hub solve + table export, the SSSP kernel for flagged sources, then the fill
-        // (source, 32x32 tile) items over a resident-sized grid
-        const uint64_t items = uint64_t(pl->ka.nsrc) * ((pl->ka.p.S + 31) / 32) * ((pl->ka.p.S + 31) / 32);
-        uint32_t gx = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(items, 8ull * pl->cus)));
+        // hub solve + table export, the SSSP kernel for flagged sources, then the fill:
+        // (source, tile) items, one per wave, over a resident-sized grid
+        const uint64_t items = uint64_t(pl->ka.nsrc) * ((pl->ka.p.S + kFillTW - 1) / kFillTW) *
+                               ((pl->ka.p.S + kFillTH - 1) / kFillTH);
+        uint32_t gx = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((items + 3) / 4, uint64_t(pl->fill_per_cu) * pl->cus)));
         if (const char *e = std::getenv("MR_FILL_GX")) gx = uint32_t(std::max(1, std::atoi(e)));
         const uint32_t gy = 1;
         e = launch_hub_plan(pl, pl->d_args, s);
@@ -973,7 +984,8 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
             e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, s);
         hipEvent_t f0 = nullptr;
         if (e == hipSuccess && hipEventCreate(&f0) == hipSuccess) (void)hipEventRecord(f0, s);
-        if (e == hipSuccess) e = launch_fill(pl->d_args_fill, pl->ka.p.perm, gx, gy, s);
+        if (e == hipSuccess) e = launch_fill(pl->d_args_fill, pl->ka.p.perm, gx, gy, s, false);
+        if (e == hipSuccess) e = launch_fill(pl->d_args_fill2, pl->ka.p.perm, gx, gy, s, true);
         if (f0) pl->timed_fill.push_back({f0, nullptr});
     } else if (pl->hp.hub && pl->fb_none) {
         // a pass of this plan (same inputs, deterministic result) had no fallback

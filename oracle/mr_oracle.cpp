@@ -804,6 +804,66 @@ extern "C" int mro_find_path_batch(const mro_grid *g, const mr_params *p, const 
     return ret;
 }
 
+// Every destination of one source (test infrastructure for the all-destinations
+// plans): FindPath::eval's Dijkstra (src/pathfinder.rs:199-248) run without the early
+// exit.  By SURVEY 8a's uniqueness lemma the final dist[] label of each cell is the
+// label eval(from, cell) returns (eval pops `to` with that label and stops).  One
+// result per cell in the grid's input (row-major) order; the commands go to pool
+// (results[i].command_offset), MR_ERR_CAPACITY if pool_cap is too small.
+extern "C" int mro_sssp_all(const mro_grid *g, const mr_params *p, mr_cell_index from, mr_result *results,
+                            mr_command *pool, uint64_t pool_cap) {
+    if (!g || !results) return MR_ERR_INVALID_ARG;
+    Query q;
+    int st = make_query(g, p, q);
+    if (st != MR_OK) return st;
+    if (!valid_input(from)) return MR_ERR_INVALID_INDEX;
+    CellIndex f = build_any(from);
+    if (!g->at(f)) return MR_ERR_INVALID_INDEX;
+    std::unordered_map<CellIndex, TotalCost, CellIndexHash> dist;
+    auto heap_less = [&](const TotalCost &a, const TotalCost &b) { return q.cmp(a, b) > 0; };
+    std::priority_queue<TotalCost, std::vector<TotalCost>, decltype(heap_less)> heap(heap_less);
+    dist[f] = total_new(f);
+    heap.push(dist[f]);
+    std::vector<std::pair<CellIndex, EdgeCost>> es;
+    while (!heap.empty()) {
+        TotalCost cost = heap.top();
+        heap.pop();
+        CellIndex lowest = cost.commands.back().to;
+        if (q.cmp(cost, dist[lowest]) > 0) continue;
+        if (!edges(q, lowest, es)) return MR_ERR_INVALID_INDEX;
+        for (auto &[w, e] : es) {
+            TotalCost next = cost;
+            total_add_assign(next, e, q.soe, q.shq, q.sfm, q.fleetfoot, lowest, w);
+            auto it = dist.find(w);
+            if (it == dist.end() || q.cmp(next, it->second) < 0) {
+                dist[w] = next;
+                heap.push(std::move(next));
+            }
+        }
+    }
+    const size_t n = g->grid.size();
+    for (size_t i = 0; i < n; ++i) {
+        std::memset(&results[i], 0, sizeof(mr_result));
+        results[i].status = MR_NOT_FOUND;
+    }
+    int ret = MR_OK;
+    uint64_t off = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const CellIndex &c = g->grid[i].index;
+        auto it = dist.find(c);
+        if (it == dist.end()) continue;
+        // from == to: eval returns the start label
+        const TotalCost &t = c == f ? dist[f] : it->second;
+        uint32_t nc = uint32_t(t.commands.size());
+        bool fits = pool && off + nc <= pool_cap;
+        write_result(t, &results[i], fits ? pool + off : nullptr, nc, MR_OK);
+        results[i].command_offset = uint32_t(off);
+        if (!fits) ret = MR_ERR_CAPACITY;
+        off += nc;
+    }
+    return ret;
+}
+
 // time 0.3 Duration Display (verbose form): d, h, m, s (whole seconds only)
 extern "C" int mro_duration_display(int64_t seconds, char *buf, uint32_t cap) {
     std::string s;

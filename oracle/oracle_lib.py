@@ -14,7 +14,7 @@ from typing import List, Optional, Sequence, Tuple
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
-from marshrutka_amd.abi import (MR_NOT_FOUND, MR_OK, CellIndex, Params, TotalCost,  # noqa: E402
+from marshrutka_amd.abi import (MR_ERR_CAPACITY, MR_NOT_FOUND, MR_OK, CellIndex, Params, TotalCost,  # noqa: E402
                                 cells_to_c, mr_cell, mr_cell_index, mr_command, mr_params,
                                 mr_query, mr_result, queries_to_c, result_from_c)
 
@@ -48,6 +48,9 @@ def lib():
         L.mro_find_path_batch.argtypes = [C.c_void_p, C.POINTER(mr_params), C.POINTER(mr_query), C.c_uint32,
                                           C.POINTER(mr_result), C.POINTER(mr_command), C.c_uint64, C.c_uint32]
         L.mro_find_path_batch.restype = C.c_int
+        L.mro_sssp_all.argtypes = [C.c_void_p, C.POINTER(mr_params), mr_cell_index, C.POINTER(mr_result),
+                                   C.POINTER(mr_command), C.c_uint64]
+        L.mro_sssp_all.restype = C.c_int
         L.mro_duration_display.argtypes = [C.c_int64, C.c_char_p, C.c_uint32]
         L.mro_duration_display.restype = C.c_int
         _lib = L
@@ -113,6 +116,23 @@ class OracleGrid:
     def find_path_batch(self, params: Params, queries, threads: int = 0) -> List[Optional[TotalCost]]:
         res, pool = self.find_path_batch_raw(params, queries, threads)
         return [result_from_c(res[i], pool) for i in range(len(queries))]
+
+
+    def sssp_all(self, params: Params, src: CellIndex) -> List[Optional[TotalCost]]:
+        """Every cell's label from src (the reference's Dijkstra without its early
+        exit), in the grid's input order."""
+        p = params.to_c()
+        res = (mr_result * self.n)()
+        cap = self.n * 24
+        while True:
+            pool = (mr_command * cap)()
+            st = lib().mro_sssp_all(self.h, C.byref(p), src.to_c(), res, pool, cap)
+            if st != -8 or cap > self.n * 4096:  # MR_ERR_CAPACITY: grow the pool
+                break
+            cap *= 4
+        if st != MR_OK:
+            raise ValueError(f"oracle sssp_all failed: {st}")
+        return [result_from_c(res[i], pool) for i in range(self.n)]
 
 
 def duration_display(seconds: int) -> str:

@@ -93,3 +93,48 @@ def test_c3_sample_1025(eng, oracle_lib):
         exp = og.find_path_batch(Params(), [(s, d) for d in dsts], threads=0)
         for d, e in zip(dsts, exp):
             assert as_expected(plan.label(i, d)) == as_expected(e), (s, d)
+
+
+# Maps wide enough for 64x16 fill tiles away from the axes through the Center (the
+# packed-key fast path), with the tile pruning and the key packing each switched off
+# in turn (MR_DBG_FLAGS bit 0 / bit 1), and a small fill grid (MR_FILL_GX) so each
+# wave walks many tiles and several sources.  Every cell's full label (commands
+# included) against the oracle's Dijkstra run to completion.
+FILL_PARAMS = [Params(), Params(sort_by=(SORT_TIME, SORT_MONEY)),
+               Params(sort_by=(SORT_MONEY, SORT_LEGS), use_sfm=True, route_guru=2),
+               Params(sort_by=(SORT_LEGS, SORT_TIME), use_soe=False),
+               Params(sort_by=(SORT_TIME, SORT_LEGS), hq_position=CellIndex.homeland(2, 3, 5), fleetfoot=7),
+               Params(sort_by=(SORT_MONEY, SORT_TIME), scroll_of_escape_cost=0, homeland=3)]
+
+
+@pytest.mark.parametrize("flags,gx", [("", None), ("1", None), ("2", None), ("", "3")])
+@pytest.mark.parametrize("size,k,clustered,pi", [(129, 4, False, 0), (129, 9, True, 1), (161, 6, False, 2),
+                                                  (129, 5, True, 3), (193, 4, False, 4), (161, 7, True, 5)])
+def test_fill_tiles_every_cell(eng, oracle_lib, monkeypatch, flags, gx, size, k, clustered, pi):
+    monkeypatch.delenv("MR_ALGO", raising=False)
+    monkeypatch.delenv("MR_HUB_FALLBACK_ALL", raising=False)
+    monkeypatch.setenv("MR_DBG_FLAGS", flags or "0")
+    if gx:
+        monkeypatch.setenv("MR_FILL_GX", gx)
+    else:
+        monkeypatch.delenv("MR_FILL_GX", raising=False)
+    params = FILL_PARAMS[pi]
+    m = SyntheticMap(size, campfires_per_homeland=k, seed=size * 7 + pi, clustered=clustered)
+    rng = random.Random(size + pi)
+    cells = m.all_indices()
+    sources = [m.campfires()[1], CellIndex.center()] + rng.sample(cells, 3)
+    g = eng.MapGrid(m.cells())
+    og = oracle_lib.OracleGrid(m.cells())
+    plan = eng.SSSPPlan(g, params, sources)
+    plan.run()
+    assert plan.stats()["solver"] == "hub"
+    for i, s in enumerate(sources):
+        exp = og.sssp_all(params, s)
+        rec = plan.records(i)
+        bad = []
+        for j, (d, e) in enumerate(zip(cells, exp)):
+            r = rec[j]
+            if (int(r[0]), int(r[1]), int(r[2])) != (e.legs, e.money, e.time_s) or \
+                    as_expected(plan.label(i, d)) != as_expected(e):
+                bad.append(d)
+        assert not bad, (params, s, len(bad), bad[:4])

@@ -133,3 +133,22 @@ def test_homeland_without_campfire_is_rejected(oracle_lib):
     m = SyntheticMap(7, campfires_per_homeland=0, seed=0, extra_campfires=corner_campfires(7)[:3])
     with pytest.raises(ValueError, match="-2"):
         oracle_lib.OracleGrid(m.cells())
+
+
+@pytest.mark.parametrize("size,k,seed", [(15, 3, 1), (21, 4, 2)])
+def test_sssp_all_equals_per_query_eval(oracle_lib, size, k, seed):
+    """The all-destinations oracle (Dijkstra without the early exit) gives, for every
+    cell, exactly the label a separate eval(src, cell) returns."""
+    import random
+    from marshrutka_amd.abi import SORT_MONEY, SORT_TIME, Params
+    from marshrutka_amd.mapgen import SyntheticMap
+    m = SyntheticMap(size, campfires_per_homeland=k, seed=seed, clustered=seed % 2 == 0)
+    og = oracle_lib.OracleGrid(m.cells())
+    cells = m.all_indices()
+    rng = random.Random(seed)
+    key = lambda t: None if t is None else t.as_tuple()  # noqa: E731
+    for params in (Params(), Params(sort_by=(SORT_TIME, SORT_MONEY), fleetfoot=2, use_sfm=True)):
+        for src in rng.sample(cells, 2):
+            full = og.sssp_all(params, src)
+            each = og.find_path_batch(params, [(src, d) for d in cells])
+            assert [key(a) for a in full] == [key(b) for b in each]
