@@ -2488,7 +2488,7 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
     // per unit of walk distance: legs 1, money 0, time 180 s
     constexpr uint32_t sl[3] = {1u, 0u, 180u};
     constexpr uint64_t slope1 = sl[q0];
-    constexpr int kTW = int(kFillTW), kTH = int(kFillTH);
+    constexpr int kTW = int(kFillTW), kTH = int(kFillTH), kCPL = kTW / 64;  // kCPL columns per lane
     // per wave: boundaries by rank (x, y, m0, m1, m2, table index, key lo, key hi),
     // specials by table index (x, y, m0, m1, m2 of their own labels; entry 0 = source)
     __shared__ uint32_t btab[kBS / 64][13][64];
@@ -2601,18 +2601,17 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
                 in = px >= 0 && px < kTW && py >= 0 && py < kTH;
             }
             const unsigned long long sp_in = __ballot(in);
-            const int wx = x0 + int(lane), cx = tx0 + int(lane);
-            const bool col_ok = cx < int(S);
             const bool axis = (x0 <= 0 && x1 >= 0) || (y0 <= 0 && y1 >= 0);
             const unsigned long long mask2 = (1ull << w2) - 1, mask3 = (1ull << w3) - 1;
             if (!WIDE) {
-                // the best (key, rank) per cell; a rank is the boundary's position in the
-                // (length, command list) order, so the pair orders walks exactly like the
-                // comparator whatever order the boundaries are visited in
-                unsigned long long kb[kTH];
-                uint32_t rv[kTH];
+                // the best (key, rank) per cell (column c = lane + 64k, row i at k * kTH + i);
+                // a rank is the boundary's position in the (length, command list) order, so
+                // the pair orders walks exactly like the comparator whatever order the
+                // boundaries are visited in
+                unsigned long long kb[kCPL * kTH];
+                uint32_t rv[kCPL * kTH];
 #pragma unroll
-                for (int i = 0; i < kTH; ++i) {
+                for (int i = 0; i < kCPL * kTH; ++i) {
                     kb[i] = ~0ull;
                     rv[i] = 0xFFFFFFFFu;
                 }
@@ -2631,16 +2630,19 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
                     const int istar = __builtin_amdgcn_readfirstlane(int(B[1][rr])) - y0;  // the boundary's row in the tile
                     const unsigned long long K = (unsigned long long)uint32_t(__builtin_amdgcn_readfirstlane(int(B[6][rr]))) |
                                                  ((unsigned long long)uint32_t(__builtin_amdgcn_readfirstlane(int(B[7][rr]))) << 32);
-                    // down the lane's column the walk distance moves by +-1 per row, so the
-                    // key by +-slope
-                    unsigned long long key = K + slope * uint64_t(uint32_t(abs(bxx - wx)) + uint32_t(abs(istar)));
                     const unsigned long long up = slope, down = (unsigned long long)(-(long long)slope);
 #pragma unroll
-                    for (int i = 0; i < kTH; ++i) {
-                        if (i > 0) key += i > istar ? up : down;
-                        const bool better = key < kb[i];
-                        kb[i] = better ? key : kb[i];
-                        rv[i] = better ? rr : rv[i];
+                    for (int k = 0; k < kCPL; ++k) {
+                        // down a column the walk distance moves by +-1 per row, so the key by +-slope
+                        const int wx = x0 + 64 * k + int(lane);
+                        unsigned long long key = K + slope * uint64_t(uint32_t(abs(bxx - wx)) + uint32_t(abs(istar)));
+#pragma unroll
+                        for (int i = 0; i < kTH; ++i) {
+                            if (i > 0) key += i > istar ? up : down;
+                            const bool better = key < kb[k * kTH + i];
+                            kb[k * kTH + i] = better ? key : kb[k * kTH + i];
+                            rv[k * kTH + i] = better ? rr : rv[k * kTH + i];
+                        }
                     }
                 }
                 for (unsigned long long m = axm; m; m &= m - 1) {
@@ -2650,38 +2652,51 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
                     const int istar = byy - y0, i0 = -y0;  // i0: the tile's row y = 0
                     const unsigned long long K = (unsigned long long)uint32_t(__builtin_amdgcn_readfirstlane(int(B[6][rr]))) |
                                                  ((unsigned long long)uint32_t(__builtin_amdgcn_readfirstlane(int(B[7][rr]))) << 32);
-                    unsigned long long key = K + slope * uint64_t(uint32_t(abs(bxx - wx)) + uint32_t(abs(istar)));
                     const unsigned long long up = slope, down = (unsigned long long)(-(long long)slope), det2 = 2 * slope;
-                    const bool detx = byy == 0 && wx != 0 && bxx != 0 && ((wx < 0) != (bxx < 0));
-                    const bool dety = bxx == 0 && wx == 0 && byy != 0;
 #pragma unroll
-                    for (int i = 0; i < kTH; ++i) {
-                        if (i > 0) key += i > istar ? up : down;
-                        const bool det = (i == i0 && detx) || (dety && i != i0 && ((i < i0) != (byy < 0)));
-                        const unsigned long long kk = key + (det ? det2 : 0ull);
-                        const bool better = kk < kb[i] || (kk == kb[i] && rr < rv[i]);
-                        kb[i] = better ? kk : kb[i];
-                        rv[i] = better ? rr : rv[i];
+                    for (int k = 0; k < kCPL; ++k) {
+                        const int wx = x0 + 64 * k + int(lane);
+                        unsigned long long key = K + slope * uint64_t(uint32_t(abs(bxx - wx)) + uint32_t(abs(istar)));
+                        const bool detx = byy == 0 && wx != 0 && bxx != 0 && ((wx < 0) != (bxx < 0));
+                        const bool dety = bxx == 0 && wx == 0 && byy != 0;
+#pragma unroll
+                        for (int i = 0; i < kTH; ++i) {
+                            if (i > 0) key += i > istar ? up : down;
+                            const bool det = (i == i0 && detx) || (dety && i != i0 && ((i < i0) != (byy < 0)));
+                            const unsigned long long kk = key + (det ? det2 : 0ull);
+                            const bool better = kk < kb[k * kTH + i] || (kk == kb[k * kTH + i] && rr < rv[k * kTH + i]);
+                            kb[k * kTH + i] = better ? kk : kb[k * kTH + i];
+                            rv[k * kTH + i] = better ? rr : rv[k * kTH + i];
+                        }
                     }
                 }
                 // buffer stores off one per-tile base: the lane's offset in a VGPR, the
-                // row's (i * S * 16 B) in an SGPR, so no per-row 64-bit address
+                // row's (i * S * 16 B) in an SGPR, so no per-row 64-bit address; a row's
+                // kCPL stores are one contiguous run of kTW records
                 const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
                     outs + (size_t(ty0) * S + size_t(tx0)), 0, int(16u * kTH * S), 0x00020000);  // the tile's rows
 #pragma unroll
                 for (int i = 0; i < kTH; ++i) {
-                    const int cy = ty0 + i;
-                    if (col_ok && cy < int(S)) {
-                        // c[k] is metric q_k; the rank's table index from the wave's table
-                        const uint32_t c[3] = {uint32_t(kb[i] >> sh1), uint32_t((kb[i] >> sh2) & mask2),
-                                               uint32_t(kb[i] & mask3)};
-                        const u32x4_t rec = {q0 == 0 ? c[0] : (q1 == 0 ? c[1] : c[2]), q0 == 1 ? c[0] : (q1 == 1 ? c[1] : c[2]),
-                                             q0 == 2 ? c[0] : (q1 == 2 ? c[1] : c[2]), B[5][rv[i]]};
-                        __builtin_amdgcn_raw_buffer_store_b128(rec, rsrc, int(lane * 16u), int(uint32_t(i) * S * 16u), 0);
+#pragma unroll
+                    for (int k = 0; k < kCPL; ++k) {
+                        const int cx = tx0 + 64 * k + int(lane), cy = ty0 + i;
+                        if (cx < int(S) && cy < int(S)) {
+                            // c[.] is metric q_.; the rank's table index from the wave's table
+                            const unsigned long long kv = kb[k * kTH + i];
+                            const uint32_t c[3] = {uint32_t(kv >> sh1), uint32_t((kv >> sh2) & mask2), uint32_t(kv & mask3)};
+                            const u32x4_t rec = {q0 == 0 ? c[0] : (q1 == 0 ? c[1] : c[2]),
+                                                 q0 == 1 ? c[0] : (q1 == 1 ? c[1] : c[2]),
+                                                 q0 == 2 ? c[0] : (q1 == 2 ? c[1] : c[2]), B[5][rv[k * kTH + i]]};
+                            __builtin_amdgcn_raw_buffer_store_b128(rec, rsrc, int((64u * k + lane) * 16u),
+                                                                   int(uint32_t(i) * S * 16u), 0);
+                        }
                     }
                 }
             } else {
-                fill_tile_rows<PERM>(B, live, wx, y0, ty0, cx, col_ok, S, outs);  // metrics too wide for one key
+                for (int k = 0; k < kCPL; ++k) {  // metrics too wide for one key
+                    const int cx = tx0 + 64 * k + int(lane);
+                    fill_tile_rows<PERM>(B, live, x0 + 64 * k + int(lane), y0, ty0, cx, cx < int(S), S, outs);
+                }
             }
             // specials' cells hold their own labels, the source's cell (last: it may also
             // be a special) the start label.  These stores follow the lane's own store to
@@ -2696,8 +2711,8 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
                     m = 0;
                 }
                 const int px = int(P[0][t]) - x0, py = int(P[1][t]) - y0;
-                if (lane == uint32_t(px))
-                    outs[uint32_t(ty0 + py) * S + uint32_t(cx)] =
+                if (lane == uint32_t(px) % 64u)
+                    outs[uint32_t(ty0 + py) * S + uint32_t(tx0 + px)] =
                         VRecord{P[2][t], P[3][t], P[4][t], t == 0 ? kViaSource : (kViaSpecial | t)};
             }
         }

@@ -101,11 +101,15 @@ struct VRecord {
     uint32_t m0, m1, m2, via;
 };
 constexpr uint32_t kViaSpecial = 0x80000000u, kViaSource = 0xFFFFFFFFu;
-// all-destinations fill tiles: one wave per kFillTW x kFillTH cells (a lane per column)
-#ifndef MR_FILL_TH
-#define MR_FILL_TH 16
+// all-destinations fill tiles: one wave per kFillTW x kFillTH cells, MR_FILL_CPL
+// columns per lane (64 apart), MR_FILL_CELLS cells per lane
+#ifndef MR_FILL_CPL
+#define MR_FILL_CPL 4
 #endif
-constexpr uint32_t kFillTW = 64, kFillTH = MR_FILL_TH;
+#ifndef MR_FILL_CELLS
+#define MR_FILL_CELLS 16
+#endif
+constexpr uint32_t kFillTW = 64u * MR_FILL_CPL, kFillTH = MR_FILL_CELLS / MR_FILL_CPL;
 
 // kernel arguments (one solve launch)
 struct KArgs {
