@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py — queries/sec of the gfx950 pathfinder hot path.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5]
 
 One "step" = one pass of the hot path over one batch: every query of the
 rank's shard is answered (one single-source solve per unique source, all
@@ -10,12 +10,13 @@ result records are gathered to rank 0 over RCCL.  Inputs are resident in HBM
 before the timed region starts.
 
 Workloads (BASELINE.json configs; odd sides per SURVEY.md §8a A14):
-  c2 (default) 10k uniform (src,dst) queries per GPU on a 65x65 synthetic map
+  c4 (default) the 1025x1025 map with 1M/8 = 125k uniform queries per GPU
+               (configs[3] shard; weak scaling up to the 1M batch at N=8: the
+               north-star target, >= 1e6 q/s on a 1024x1024 grid at 8 GPUs)
+  c2           10k uniform (src,dst) queries per GPU on a 65x65 synthetic map
                (configs[1]: "10k random (src,dst) batch on 64x64")
   c3           64 sources per GPU, every destination of each on 1025x1025
                (configs[2]: single-source -> all-destinations; V queries per source)
-  c4           the 1025x1025 map with 1M/8 = 125k queries per GPU
-               (configs[3] shard; weak scaling up to the 1M batch at N=8)
   c5           10k uniform queries per GPU on a 4097x4097 map with 64 clustered
                campfires per homeland (261 specials), Time first (configs[4],
                SURVEY 8d c5 option a)
@@ -61,7 +62,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     ap.add_argument("--queries", type=int, default=0, help="override queries per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline budget (CPU-seconds)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

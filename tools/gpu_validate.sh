@@ -1,5 +1,11 @@
+# Full GPU validation: every gpu test, then each workload's bench line (wall time logged)
 set -o pipefail
-mkdir -p gpurun_out/v1
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/v1/pytest.log 2>&1 && echo tests-ok &&
-timeout -k 10 300 python bench.py > gpurun_out/v1/bench_c2.json 2> gpurun_out/v1/bench_c2.err && echo c2-ok &&
-timeout -k 10 400 python bench.py --workload c5 --steps 3 --warmup 1 > gpurun_out/v1/bench_c5.json 2> gpurun_out/v1/bench_c5.err && echo c5-ok
+O=gpurun_out/v2
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 && echo tests-ok || exit 1
+for W in c2 c4 c3 c5; do
+  S=$(date +%s.%N)
+  ST=20; [ $W = c5 ] && ST=3; [ $W = c4 ] && ST=10
+  timeout -k 10 400 python bench.py --workload $W --steps $ST --warmup 2 > $O/bench_$W.json 2> $O/bench_$W.err || exit 1
+  echo "$W wall $(python3 -c "import time;print(round(time.time()-$S,1))") s"
+done
