@@ -12,7 +12,8 @@ LIB_DIR = os.path.join(HERE, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libmarshrutka_pf.so")
 # one translation unit per kernel family (device code shared through mr_device.hpp),
 # compiled in parallel and linked into one shared library
-SOURCES = ["mr_k_wide2.hip", "mr_k_wide5.hip", "mr_k_wide8.hip", "mr_k_hub.hip", "mr_k_wide.hip",
+SOURCES = ["mr_k_wide2.hip", "mr_k_wide5.hip", "mr_k_wide8.hip", "mr_k_hub_lin.hip", "mr_k_hub_nl.hip",
+           "mr_k_hub.hip", "mr_k_wide.hip",
            "mr_k_solve.hip", "mr_k_fill.hip",
            "mr_host.cpp", "mr_html.cpp", "mr_render.cpp"]
 HEADERS = ["mr_engine.hpp", "mr_device.hpp", os.path.join("..", "..", "include", "marshrutka_pf.h")]

@@ -1586,6 +1586,144 @@ struct HubSolver : Core<false> {
         return avail(nbk, x.parent, bx, by, int(u % P.S) - int(P.H), int(u / P.S) - int(P.H));
     }
 
+    // ---- non-linear run times (Fleetfoot 1..3; DESIGN.md section 3a'') ------------
+    // With f(k) = ceil(180 k num / den) a StandardMove extension shifts the time gap of
+    // two walks (k' = k + m legs) by delta = f(k'+1) - f(k') - (f(k+1) - f(k)) in
+    // {-1, 0, 1}, 0 whenever m = 0; the other metrics, lengths and command lists keep
+    // their order.  So a walk q that beats walk(b, .) at a cell u can lose to it one
+    // step further only when every metric before Time in the comparator ties at u, the
+    // time gap there is -1 or 0 and delta = +1.  If no boundary can do that on a
+    // shortest b-path to v, walk(b, .) wins along the whole path, and the closed-form
+    // label of v is the reference's (the last cell where b lost would need such a q).
+    __device__ __forceinline__ bool ff_linear() const { return P.ff_num == P.ff_den; }
+    // the gap f(k + m) - f(k) takes one of {lo, hi} for every k (cm = 180 m num / den)
+    __device__ __forceinline__ bool gap_hits(long long d0, long long m) const {
+        const long long a = 180ll * (long long)P.ff_num * (m < 0 ? -m : m), den = (long long)P.ff_den;
+        long long lo = a / den, hi = (a + den - 1) / den;
+        if (m < 0) {
+            const long long t = lo;
+            lo = -hi;
+            hi = -t;
+        }
+        return d0 + lo == -1 || d0 + lo == 0 || d0 + hi == -1 || d0 + hi == 0;
+    }
+    // Can boundary q (at qx, qy) beat walk(b, .) non-isotonically somewhere on a shortest
+    // b-path to (vx, vy)?  Every cell of those paths lies in the b-v rectangle, where
+    // m = d_q(u) - d_b(u) runs within [L1(q, v) - L1(b, v), L1(q, b) + 2].
+    __device__ __forceinline__ bool near_tie(uint32_t q, int qx, int qy, uint32_t b, int bx, int by, int vx,
+                                             int vy) const {
+        const DevParams &p = P;
+        const int mlo = abs(qx - vx) + abs(qy - vy) - abs(bx - vx) - abs(by - vy);
+        const int mhi = abs(qx - bx) + abs(qy - by) + 2;
+        const long long d0 = (long long)R[q].m[2] - (long long)R[b].m[2];
+        const bool legs_before = p.perm[0] == 0 || (p.perm[1] == 0 && p.perm[0] != 2);
+        const bool money_before = p.perm[0] == 1 || (p.perm[1] == 1 && p.perm[0] != 2);
+        if (money_before && R[q].m[1] != R[b].m[1]) return false;
+        if (legs_before) {  // the legs tie where m = L_b - L_q
+            const long long m = (long long)R[b].m[0] - (long long)R[q].m[0];
+            return m != 0 && m >= mlo && m <= mhi && gap_hits(d0, m);
+        }
+        // d0 + 180 m num / den within (-2, 1): m next to -d0 den / (180 num)
+        const long long c = 180ll * (long long)p.ff_num, num = (-2 - d0) * (long long)p.ff_den;
+        const long long m0 = num >= 0 ? num / c : -((-num + c - 1) / c);
+        for (long long m = m0 - 1; m <= m0 + 2; ++m)
+            if (m != 0 && m >= mlo && m <= mhi && gap_hits(d0, m)) return true;
+        return false;
+    }
+    // Along one L-shaped shortest path from b to v (x first, or y first), is there a
+    // cell u (v excluded) where walk(q, .) beats walk(b, .) and the next leg of the path
+    // flips their order?  That needs the metrics before Time to tie at u, q's distance
+    // to grow on that leg with its run time widening by one second more than b's
+    // (delta = +1), and either a time gap of -1 with the tail (the metric after Time,
+    // then the length; the command lists unknown here) not favouring q, or a time gap
+    // of 0 with the tail not favouring b.  A path through the Center is not a walk: true.
+    __device__ __forceinline__ bool path_tie(uint32_t q, int qx, int qy, uint32_t b, int bx, int by, int vx, int vy,
+                                             bool x_first) const {
+        const DevParams &p = P;
+        const bool legs_before = p.perm[0] == 0 || (p.perm[1] == 0 && p.perm[0] != 2);
+        const bool money_before = p.perm[0] == 1 || (p.perm[1] == 1 && p.perm[0] != 2);
+        // the metric after Time, if any (legs 0, money 1; 3 = none)
+        const uint32_t after = p.perm[0] == 2 ? p.perm[1] : (p.perm[1] == 2 ? p.perm[2] : 3u);
+        if (money_before && R[q].m[1] != R[b].m[1]) return false;
+        const int sx = vx > bx ? 1 : -1, sy = vy > by ? 1 : -1;
+        const int K = abs(vx - bx) + abs(vy - by), kx = abs(vx - bx), ky = K - kx;
+        const long long tb = R[b].m[2], tq = R[q].m[2], lb = R[b].m[0], lq = R[q].m[0];
+        const long long mb = R[b].m[1], mq = R[q].m[1];
+        // the walks' lengths (the source's walk replaces its NoMove: length 1)
+        const long long nq0 = q == 0 ? 1 : R[q].len, nq1 = q == 0 ? 1 : R[q].len + 1;
+        const long long nb0 = b == 0 ? 1 : R[b].len, nb1 = b == 0 ? 1 : R[b].len + 1;
+        auto cell = [&](int k, int &ux, int &uy) {
+            if (x_first) {
+                ux = k < kx ? bx + sx * k : vx;
+                uy = k < kx ? by : by + sy * (k - kx);
+            } else {
+                uy = k < ky ? by + sy * k : vy;
+                ux = k < ky ? bx : bx + sx * (k - ky);
+            }
+        };
+        int ux, uy;
+        cell(0, ux, uy);
+        uint32_t dq = walk_dist(qx, qy, ux, uy);
+        for (int k = 0; k < K; ++k) {
+            if (ux == 0 && uy == 0) return true;
+            int wx, wy;
+            cell(k + 1, wx, wy);
+            const uint32_t dqn = walk_dist(qx, qy, wx, wy);
+            const bool tie_before = !legs_before || lq + dq == lb + k;
+            if (tie_before && dqn > dq) {
+                const long long fq = run_time(dq), fb = run_time(uint32_t(k));
+                const long long delta = ((long long)run_time(dq + 1) - fq) - ((long long)run_time(uint32_t(k) + 1) - fb);
+                const long long gap = tq + fq - tb - fb;
+                if (delta == 1 && (gap == -1 || gap == 0)) {
+                    int tail = 0;  // -1: q ahead, +1: b ahead, 0: undecided
+                    if (after == 0) tail = lq + dq < lb + k ? -1 : (lq + dq > lb + k ? 1 : 0);
+                    else if (after == 1) tail = mq < mb ? -1 : (mq > mb ? 1 : 0);
+                    if (tail == 0) {
+                        const long long nq = dq > 0 ? nq1 : nq0, nbb = k > 0 ? nb1 : nb0;
+                        tail = nq < nbb ? -1 : (nq > nbb ? 1 : 0);
+                    }
+                    if (gap == -1 ? tail != -1 : tail != 1) return true;
+                }
+            }
+            ux = wx;
+            uy = wy;
+            dq = dqn;
+        }
+        return false;
+    }
+    // Does boundary q leave the closed-form walk(b, d_b(v)) certain?  (q = b, the Center
+    // and kNone32 trivially do.)  It must fail near_tie, or leave one of the two L-paths
+    // clean; and the b-v walks must not detour round the Center.
+    __device__ __forceinline__ bool walk_clear(uint32_t q, uint32_t b, int vx, int vy, int sx, int sy) const {
+        int bx, by;
+        bpos(b, sx, sy, bx, by);
+        if ((by == 0 && vy == 0 && bx != 0 && vx != 0 && (bx < 0) != (vx < 0)) ||
+            (bx == 0 && vx == 0 && by != 0 && vy != 0 && (by < 0) != (vy < 0)))
+            return false;  // shortest walks detour round the Center
+        if (q == kNone32 || q == b || vert_of(q) == P.vc) return true;
+        int qx, qy;
+        bpos(q, sx, sy, qx, qy);
+        if (!near_tie(q, qx, qy, b, bx, by, vx, vy)) return true;
+        return !path_tie(q, qx, qy, b, bx, by, vx, vy, true) || !path_tie(q, qx, qy, b, bx, by, vx, vy, false);
+    }
+    // Is the closed-form walk(b, d_b(v)) certain to be the reference's label of v?
+    // Linear run times: always (the blocker check, avail, covers ties).  Otherwise
+    // every boundary must leave it clear.
+    __device__ __forceinline__ bool walk_certain(uint32_t b, int vx, int vy, uint32_t nb, int sx, int sy) const {
+        if (ff_linear()) return true;
+        for (uint32_t j = 0; j < nb; ++j)
+            if (!walk_clear(bnd[j], b, vx, vy, sx, sy)) return false;
+        return true;
+    }
+    // the same for a settled special's label x at (tx, ty): its walk, or the walk to the
+    // cell its Scroll of Escape is read from
+    __device__ __forceinline__ bool label_certain(const View &x, uint32_t nb, int tx, int ty, int sx, int sy) const {
+        if (ff_linear() || (x.t0.kp >> 29) != kStandard) return true;
+        if (x.ntail == 1) return walk_certain(x.parent, tx, ty, nb, sx, sy);
+        const uint32_t u = a->rank_inv[x.t0.to];
+        return walk_certain(x.parent, int(u % P.S) - int(P.H), int(u / P.S) - int(P.H), nb, sx, sy);
+    }
+
     __device__ __forceinline__ void bpos(uint32_t b, int sx, int sy, int &bx, int &by) const {
         bx = b == 0 ? sx : sp[b].x;
         by = b == 0 ? sy : sp[b].y;
@@ -1683,6 +1821,10 @@ struct HubSolver : Core<false> {
                 emit(x, a->q_id[qi]);
                 if (plain && !dest_avail(nbk, bnd[win], w, sx, sy)) unc = true;
             }
+            // non-linear run times: lane j clears boundary j
+            if (!ff_linear() && !(a->dbg_flags & 8u) && qon && plain &&
+                !walk_clear(t < nb ? bnd[t] : kNone32, bnd[win], wx, wy, sx, sy))
+                unc = true;
         }
         for (uint32_t i = qa + t; !few && i < qb; i += LPS) {
             const uint32_t w = a->q_dst[i];
@@ -1695,6 +1837,8 @@ struct HubSolver : Core<false> {
             } else {
                 const uint32_t b = plain_label_serial(w, nb, sx, sy, x);
                 if (!dest_avail(nbk, b, w, sx, sy)) unc = true;
+                if (!(a->dbg_flags & 8u) && !walk_certain(b, int(w % p.S) - int(p.H), int(w / p.S) - int(p.H), nb, sx, sy))
+                    unc = true;
             }
             emit(x, a->q_id[i]);
         }
@@ -1868,6 +2012,8 @@ struct HubSolver : Core<false> {
         // wave must stay converged.
         wave_sync();
         if (__any(nbk != 0) && mine && st == 2 && !label_avail(my, nbk, ss.x, ss.y, sx, sy)) unc = 1;
+        if (!ff_linear() && !(a->dbg_flags & 4u) && mine && st == 2 && !label_certain(my, nb, ss.x, ss.y, sx, sy))
+            unc = 1;
         const bool unc_sp = seg_bits<LPS>(__ballot(unc != 0)) != 0;
         const uint32_t qa = a->q_begin[si];
         bool fallback = have && (unc_sp || a->fb_all || (a->all_mode && nbk != 0));
@@ -1923,7 +2069,7 @@ __host__ __device__ inline HubLayout hub_layout(uint32_t NS, uint32_t nreg, uint
 #ifndef MR_HUB_WAVES
 #define MR_HUB_WAVES 5  // waves per SIMD the register budget is cut for (measured best)
 #endif
-template <uint32_t PERM, uint32_t SPW>
+template <uint32_t PERM, uint32_t SPW, bool NONLIN>
 __global__ __launch_bounds__(kBS, MR_HUB_WAVES) void hub_kernel(const KArgs *__restrict__ a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint32_t NS = a->p.NS, nreg = a->nreg;
@@ -1945,7 +2091,8 @@ __global__ __launch_bounds__(kBS, MR_HUB_WAVES) void hub_kernel(const KArgs *__r
     H.P.perm[0] = PERM / 9;
     H.P.perm[1] = (PERM / 3) % 3;
     H.P.perm[2] = PERM % 3;
-    H.P.ff_num = H.P.ff_den = 1;  // the hub solver runs only with a linear run time
+    // linear run times need no near-tie certification (the compiler folds it away)
+    if (!NONLIN) H.P.ff_num = H.P.ff_den = 1;
     H.rank = a->rank;
     H.sinfo = a->sinfo;
     H.counter = a->counter;

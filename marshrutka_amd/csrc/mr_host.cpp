@@ -25,11 +25,11 @@ hipError_t launch_solve(const KArgs *d_args, bool grid_in_lds, uint32_t algo, ui
                         uint32_t blocks, hipStream_t stream);
 int max_blocks_per_cu(bool grid_in_lds, uint32_t algo, uint32_t bytes);
 uint32_t hub_lds_bytes(uint32_t NS, uint32_t nreg, uint32_t spw);
-hipError_t launch_hub(const KArgs *d_args, const uint32_t perm[3], uint32_t spw, uint32_t NS, uint32_t nreg,
+hipError_t launch_hub(const KArgs *d_args, const uint32_t perm[3], uint32_t spw, bool nonlin, uint32_t NS, uint32_t nreg,
                       uint32_t blocks, hipStream_t stream);
 hipError_t launch_fill(const KArgs *d_args, const uint32_t perm[3], uint32_t gx, uint32_t gy, hipStream_t stream,
                        bool wide);
-int hub_blocks_per_cu(const uint32_t perm[3], uint32_t spw, uint32_t bytes);
+int hub_blocks_per_cu(const uint32_t perm[3], uint32_t spw, bool nonlin, uint32_t bytes);
 int fill_blocks_per_cu(const uint32_t perm[3]);
 uint32_t hub_wide_lds_bytes(uint32_t NS, uint32_t nreg);
 uint32_t hub_wide_spl(uint32_t NS);
@@ -460,7 +460,8 @@ struct HostPlan {
     std::vector<int32_t> q_status;  // per query: MR_OK or a host-side error
     uint32_t nq = 0;
     uint32_t fleetfoot_raw = 0;
-    bool hub = false;                       // hub solver applicable (linear run time, small tables)
+    bool hub = false;                       // hub solver applicable (small tables)
+    bool nonlin = false;                    // hub with a non-linear run time (near-tie certification)
     const std::vector<uint32_t> *near = nullptr;
     uint32_t nreg = 0;
     bool wide = false;                      // hub_wide_kernel (NS > 63 or no V x regions table)
@@ -561,18 +562,19 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     }
     p.n_hubs = uint32_t(hp.hubs.size());
     for (uint32_t t = 1; t <= NS; ++t) hp.sp[t].rid = kNone10;
-    // hub solver: exact when the StandardMove run time is linear (Fleetfoot level 0 or out
-    // of range) — see DESIGN.md §3b; the one non-isotone case is detected per source
-    // and re-solved by the SSSP kernel.  MR_ALGO=sssp|generic disables it.
-    // hub solver: exact when the StandardMove run time is linear (Fleetfoot level 0 or out
-    // of range) — see DESIGN.md §3b; the one non-isotone case is detected per source
-    // and re-solved by the SSSP kernel.  MR_ALGO=sssp|generic disables it.  Up to 63
-    // specials and a V x regions table of <= 2 GB: one special per lane (hub_kernel);
-    // otherwise up to 511 specials with boundary-scanned region rows (hub_wide_kernel,
+    // hub solver: the closed form is exact when the StandardMove run time is linear
+    // (Fleetfoot level 0 or out of range) — DESIGN.md §3a; the one non-isotone case is
+    // detected per source and re-solved by the SSSP kernel.  With Fleetfoot 1..3 every
+    // closed-form label is also certified against near-ties of the time gap (§3a''), the
+    // narrow kernel only.  MR_ALGO=sssp|generic disables the hub, MR_HUB_NONLIN=0 its
+    // non-linear use.  Up to 63 specials and a V x regions table of <= 16 GB: one
+    // special per lane (hub_kernel); otherwise up to 511 specials (hub_wide_kernel,
     // forced by MR_HUB_WIDE=1 for the tests).
-    bool linear = p.ff_num == p.ff_den;
+    bool linear = p.ff_num == p.ff_den, nonlin_ok = !linear;
+    if (const char *e = std::getenv("MR_HUB_NONLIN"))
+        if (!std::strcmp(e, "0")) nonlin_ok = false;
     if (const char *e = std::getenv("MR_ALGO"))
-        if (!std::strcmp(e, "sssp") || !std::strcmp(e, "generic")) linear = false;
+        if (!std::strcmp(e, "sssp") || !std::strcmp(e, "generic")) linear = nonlin_ok = false;
     size_t nregs = 0;
     for (uint32_t v : g->campfires)
         if (g->idx[v].kind == MR_CELL_HOMELAND && g->idx[v].sub == prm->homeland) ++nregs;
@@ -583,8 +585,9 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     const bool table_ok = nregs <= 256 && size_t(V) * nregs * 8 <= (size_t(16) << 30) &&
                           !(fw && !std::strcmp(fw, "scan"));
     const bool narrow_ok = NS <= 63 && nregs <= 63 && table_ok;
-    hp.hub = hp.wide = false;
-    if (linear && narrow_ok && !force_wide) {
+    hp.hub = hp.wide = hp.nonlin = false;
+    if ((linear || nonlin_ok) && narrow_ok && !force_wide) {
+        hp.nonlin = !linear;
         const std::vector<uint32_t> *regs = nullptr;
         const std::vector<uint32_t> &tab = region_table(g, prm->homeland, regs);
         hp.hub = true;
@@ -785,7 +788,8 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         return st;
     }
     HostPlan &hp = pl->hp;
-    if (all_mode && hp.wide) hp.hub = hp.wide = false;  // all destinations: hub_kernel + fill only
+    // all destinations: hub_kernel + fill only, linear run times (the fill's keys)
+    if (all_mode && (hp.wide || hp.nonlin)) hp.hub = hp.wide = hp.nonlin = false;
     auto bail = [&](int code) {
         delete pl;
         return code;
@@ -911,7 +915,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         const uint32_t hb = hp.wide ? hub_wide_lds_bytes(NS, hp.nreg) : hub_lds_bytes(NS, hp.nreg, pl->spw);
         if (hb > 160 * 1024) return bail(fail(MR_ERR_LIMIT, "hub tables exceed LDS"));
         const int hper = std::max(1, hp.wide ? hub_wide_blocks_per_cu(hp.p.perm, NS, hb)
-                                             : hub_blocks_per_cu(hp.p.perm, pl->spw, hb));
+                                             : hub_blocks_per_cu(hp.p.perm, pl->spw, hp.nonlin, hb));
         const uint64_t per_block = 4ull * pl->spw;
         pl->hub_blocks = uint32_t(std::min<uint64_t>((nsrc + per_block - 1) / per_block,
                                                      uint64_t(hper) * prop.multiProcessorCount));
@@ -959,7 +963,7 @@ extern "C" int mr_plan_create_ex(const mr_grid *g, const mr_params *prm, const m
 
 static hipError_t launch_hub_plan(const mr_plan *pl, const KArgs *d_args, hipStream_t s) {
     if (pl->hp.wide) return launch_hub_wide(d_args, pl->ka.p.perm, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
-    return launch_hub(d_args, pl->ka.p.perm, pl->spw, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
+    return launch_hub(d_args, pl->ka.p.perm, pl->spw, pl->hp.nonlin, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
 }
 
 extern "C" int mr_plan_run(mr_plan *pl, void *stream) {

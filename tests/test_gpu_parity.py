@@ -289,3 +289,34 @@ def test_overflow_pool(eng, oracle_lib, grid_state, max_cmds):
             plan.run()
             assert [as_expected(r) for r in plan.fetch()] == exp
         assert any(len(e[3]) > max_cmds for e in exp)
+
+
+@pytest.mark.parametrize("ff", [1, 2, 3])
+@pytest.mark.parametrize("sort_by", [(SORT_LEGS, SORT_MONEY), (SORT_LEGS, SORT_TIME), (SORT_MONEY, SORT_LEGS),
+                                     (SORT_MONEY, SORT_TIME), (SORT_TIME, SORT_LEGS), (SORT_TIME, SORT_MONEY)])
+def test_fleetfoot_hub(eng, oracle_lib, monkeypatch, ff, sort_by):
+    """Non-linear run times (Fleetfoot 1..3) through the hub solver: every closed-form
+    label certified against near-ties of the time gap, uncertain sources re-solved by
+    the SSSP kernel.  Bit-exact against the oracle, with both one and many
+    destinations per source, and most sources answered by the hub itself."""
+    for v in ("MR_ALGO", "MR_HUB_FALLBACK_ALL", "MR_HUB_SPW", "MR_HUB_WIDE", "MR_HUB_NONLIN", "MR_GRID_STATE"):
+        monkeypatch.delenv(v, raising=False)
+    for size, k, clustered, seed in ((33, 4, False, 31), (65, 6, True, 32), (129, 4, False, 33)):
+        m = SyntheticMap(size, campfires_per_homeland=k, seed=seed + ff, clustered=clustered)
+        params = Params(fleetfoot=ff, sort_by=sort_by, route_guru=ff, hq_position=m.campfires()[2])
+        rng = random.Random(seed * 7 + ff)
+        cells = m.all_indices()
+        qs = random_queries(m, 400, seed + ff)
+        src = rng.choice(cells)
+        qs += [(src, d) for d in rng.sample(cells, 120)]  # many destinations for one source
+        g = eng.MapGrid(m.cells())
+        og = oracle_lib.OracleGrid(m.cells())
+        plan = eng.Plan(g, params, qs)
+        plan.run()
+        got = plan.fetch()
+        exp = og.find_path_batch(params, qs, threads=0)
+        bad = [(q, e, r) for q, e, r in zip(qs, exp, got) if as_expected(e) != as_expected(r)]
+        assert not bad, f"S={size} {params}: {len(bad)}/{len(qs)} mismatches; first: {bad[0]}"
+        st = plan.stats()
+        assert st["solver"] == "hub"
+        assert st["fallback_sources"] <= st["num_sources"] // 4, st
