@@ -1631,12 +1631,13 @@ struct HubSolver : Core<false> {
         return false;
     }
     // Along one L-shaped shortest path from b to v (x first, or y first), is there a
-    // cell u (v excluded) where walk(q, .) beats walk(b, .) and the next leg of the path
-    // flips their order?  That needs the metrics before Time to tie at u, q's distance
-    // to grow on that leg with its run time widening by one second more than b's
-    // (delta = +1), and either a time gap of -1 with the tail (the metric after Time,
-    // then the length; the command lists unknown here) not favouring q, or a time gap
-    // of 0 with the tail not favouring b.  A path through the Center is not a walk: true.
+    // cell u (v excluded) where walk(q, .) beats walk(b, .) and the next leg w of the
+    // path flips their order?  That needs the metrics before Time to tie at u, q's
+    // distance to grow on that leg, a time gap of -1 or 0 at u that does not shrink
+    // (delta >= 0), q ahead at u and b ahead at w on (gap, tail) — the tail being the
+    // metric after Time, then the length (a walk from q's own cell appends a command:
+    // the flip of a blocker), the command lists undecided here.  A path through the
+    // Center is not a walk: true.
     __device__ __forceinline__ bool path_tie(uint32_t q, int qx, int qy, uint32_t b, int bx, int by, int vx, int vy,
                                              bool x_first) const {
         const DevParams &p = P;
@@ -1670,19 +1671,26 @@ struct HubSolver : Core<false> {
             cell(k + 1, wx, wy);
             const uint32_t dqn = walk_dist(qx, qy, wx, wy);
             const bool tie_before = !legs_before || lq + dq == lb + k;
-            if (tie_before && dqn > dq) {
+            if (tie_before && dqn > dq) {  // (q getting nearer stays ahead)
                 const long long fq = run_time(dq), fb = run_time(uint32_t(k));
-                const long long delta = ((long long)run_time(dq + 1) - fq) - ((long long)run_time(uint32_t(k) + 1) - fb);
+                const long long delta = ((long long)run_time(dqn) - fq) - ((long long)run_time(uint32_t(k) + 1) - fb);
                 const long long gap = tq + fq - tb - fb;
-                if (delta == 1 && (gap == -1 || gap == 0)) {
-                    int tail = 0;  // -1: q ahead, +1: b ahead, 0: undecided
-                    if (after == 0) tail = lq + dq < lb + k ? -1 : (lq + dq > lb + k ? 1 : 0);
-                    else if (after == 1) tail = mq < mb ? -1 : (mq > mb ? 1 : 0);
-                    if (tail == 0) {
-                        const long long nq = dq > 0 ? nq1 : nq0, nbb = k > 0 ? nb1 : nb0;
-                        tail = nq < nbb ? -1 : (nq > nbb ? 1 : 0);
-                    }
-                    if (gap == -1 ? tail != -1 : tail != 1) return true;
+                if ((gap == -1 || gap == 0) && delta >= 0) {
+                    // the order after Time at u (dq, k) and at the next cell (dqn, k + 1):
+                    // -1 q ahead, +1 b ahead, 0 undecided (the command lists)
+                    auto tail = [&](long long dd, long long kk) -> int {
+                        if (after == 0) {
+                            if (lq + dd != lb + kk) return lq + dd < lb + kk ? -1 : 1;
+                        } else if (after == 1) {
+                            if (mq != mb) return mq < mb ? -1 : 1;
+                        }
+                        const long long nq = dd > 0 ? nq1 : nq0, nbb = kk > 0 ? nb1 : nb0;
+                        return nq < nbb ? -1 : (nq > nbb ? 1 : 0);
+                    };
+                    const bool q_beats_u = gap == -1 || tail(dq, k) != 1;
+                    const long long gw = gap + delta;
+                    const bool b_beats_w = gw > 0 || (gw == 0 && tail(dqn, k + 1) != -1);
+                    if (q_beats_u && b_beats_w) return true;
                 }
             }
             ux = wx;

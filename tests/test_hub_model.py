@@ -41,3 +41,46 @@ def test_hub_closed_form_matches_golden(name):
                 assert _label(out[d]) == e, (pj, s, d)
                 checked += 1
     assert checked > 0
+
+
+@pytest.mark.parametrize("ff", [1, 2, 3])
+@pytest.mark.parametrize("sort_by", [(0, 2), (0, 1), (2, 0), (2, 1), (1, 0), (1, 2)])
+def test_nonlinear_certified_labels_are_exact(oracle_lib, ff, sort_by):
+    """The non-linear hub's certification (tests/nonlin_model.py, a restatement of
+    near_tie / path_tie): whenever it certifies the closed-form walk of a plain cell,
+    that walk is the oracle's label there — and it certifies nearly every cell."""
+    import random
+    from marshrutka_amd.abi import CMD_STANDARD, Params
+    from marshrutka_amd.mapgen import SyntheticMap, index_to_geo
+    from hub_model import walk_dist
+    from nonlin_model import metrics, perm_of, run_time, walk_certified
+    m = SyntheticMap(33, campfires_per_homeland=5, seed=ff * 10 + sort_by[0], clustered=ff == 2)
+    og = oracle_lib.OracleGrid(m.cells())
+    cells = m.all_indices()
+    geo = [index_to_geo(c) for c in cells]
+    pos = {c: i for i, c in enumerate(cells)}
+    perm = perm_of(sort_by)
+    params = Params(fleetfoot=ff, sort_by=sort_by)
+    rng = random.Random(ff)
+    checked = certified = 0
+    for src in rng.sample(cells, 4):
+        lab = og.sssp_all(params, src)
+        si = pos[src]
+        bnd = [i for i, t in enumerate(lab) if t.commands[-1].kind != CMD_STANDARD and geo[i] != (0, 0)]
+        for v, t in enumerate(lab):
+            if t.commands[-1].kind != CMD_STANDARD:
+                continue
+            # the closed form's winner by (metrics in comparator order, length)
+            best = None
+            for b in bnd:
+                d = walk_dist(geo[b], geo[v])
+                mb = metrics(lab[b])
+                mm = (mb[0] + d, mb[1], mb[2] + run_time(d, ff))
+                key = tuple(mm[c] for c in perm) + (1 if b == si else len(lab[b].commands) + 1,)
+                if best is None or key < best[0]:
+                    best = (key, b, mm)
+            checked += 1
+            if walk_certified(best[1], v, bnd, lab, geo, si, perm, ff):
+                certified += 1
+                assert metrics(t) == best[2], (src, cells[v])
+    assert certified >= 0.95 * checked, (certified, checked)
