@@ -199,6 +199,8 @@ int mr_plan_run(mr_plan *plan, void *stream);
 int mr_plan_fetch(mr_plan *plan, mr_result *results, mr_command *pool, uint64_t pool_cap);
 /* Device pointers of the compact per-query output records (for an RCCL
  * gather): n * 16 B result records and n * max_cmds * 16 B command slots.
+ * Records are in grouped order (queries grouped by source, so each source's
+ * records are contiguous); mr_plan_record_queries maps record k to its query.
  * A label longer than max_cmds keeps {0xFFFFFFFF, offset, count} in its first
  * slot and its commands in the plan's own overflow pool. */
 int mr_plan_device_outputs(mr_plan *plan, void **d_results, uint64_t *results_bytes,
@@ -208,6 +210,9 @@ int mr_plan_device_outputs(mr_plan *plan, void **d_results, uint64_t *results_by
  * instead of the plan's own.  Sizes as reported by mr_plan_device_outputs;
  * the caller keeps the buffers alive while the plan uses them. */
 int mr_plan_bind_outputs(mr_plan *plan, void *d_results, void *d_commands);
+/* query_of_record[k] = the input query whose output is record k of
+ * mr_plan_device_outputs (0xFFFFFFFF past the valid queries), k < n. */
+int mr_plan_record_queries(const mr_plan *plan, uint32_t *query_of_record, uint32_t n);
 /* Number of unique sources (= single-source solves per pass). */
 uint32_t mr_plan_num_sources(const mr_plan *plan);
 

@@ -735,11 +735,14 @@ struct Core {
             try_improve(1, c);
         }
     }
-    // materialise label x as query qid's result record and command slots
-    __device__ __forceinline__ void emit(const View &x, uint32_t qid) const {
+    // materialise label x as a result record and command slots
+    // the output record of the query at grouped position qi (queries grouped by source,
+    // so a source's records are contiguous: whole lines, not scattered 16 B stores; the
+    // host maps positions back to query ids)
+    __device__ __forceinline__ void emit(const View &x, uint32_t qi) const {
         const DevParams &p = P;
-        OutResult &o = a->out_res[qid];
-        OutCmd *oc = a->out_cmd + (unsigned long long)qid * p.max_cmds;
+        OutResult &o = a->out_res[qi];
+        OutCmd *oc = a->out_cmd + (unsigned long long)qi * p.max_cmds;
         uint32_t status = 16;
         if (x.len > p.max_cmds) {  // the overflow pool, else MR_ERR_CAPACITY (the host re-runs with more slots)
             const uint32_t off = atomicAdd(a->counter + kCtrOvf, x.len);
@@ -770,17 +773,17 @@ struct Core {
         if (pos != -1 || pp != 0) flag(kErrChain);
         o = OutResult{x.m0, x.m1, x.m2, (status << 16) | (x.len & 0xFFFFu)};
     }
-    __device__ __forceinline__ void write_output(uint32_t w, uint32_t qid) const {
+    __device__ __forceinline__ void write_output(uint32_t w, uint32_t qi) const {
         const uint32_t sw = ld_state(w);
         if (!(sw & kStSettled)) {
-            a->out_res[qid] = OutResult{0, 0, 0, uint32_t(16 + 1) << 16};  // MR_NOT_FOUND
+            a->out_res[qi] = OutResult{0, 0, 0, uint32_t(16 + 1) << 16};  // MR_NOT_FOUND
             return;
         }
         View x;
         const uint32_t t = special_of(w);
         if (t != kNone10) view_rec(t, x);
         else view_walk((sw >> kStBShift) & kNone10, sw & kStKMask, rank[w], x);
-        emit(x, qid);
+        emit(x, qi);
     }
     __device__ __forceinline__ void write_outputs(uint32_t s_idx) const {
         if (a->all_mode) {
@@ -788,7 +791,7 @@ struct Core {
             return;
         }
         const uint32_t q0 = a->q_begin[s_idx], q1 = a->q_begin[s_idx + 1];
-        for (uint32_t i = q0 + threadIdx.x; i < q1; i += kBS) write_output(a->q_dst[i], a->q_id[i]);
+        for (uint32_t i = q0 + threadIdx.x; i < q1; i += kBS) write_output(a->q_dst[i], i);
     }
     // all-destinations mode: the label table and a record for every cell (VRecord)
     __device__ __forceinline__ void write_all(uint32_t s_idx) const {
@@ -1826,7 +1829,7 @@ struct HubSolver : Core<false> {
             else if (w == src) x = st0;
             else view_rec(tw, x);
             if (qon && t == 0) {
-                emit(x, a->q_id[qi]);
+                emit(x, qi);
                 if (plain && !dest_avail(nbk, bnd[win], w, sx, sy)) unc = true;
             }
             // non-linear run times: lane j clears boundary j
@@ -1848,7 +1851,7 @@ struct HubSolver : Core<false> {
                 if (!(a->dbg_flags & 8u) && !walk_certain(b, int(w % p.S) - int(p.H), int(w / p.S) - int(p.H), nb, sx, sy))
                     unc = true;
             }
-            emit(x, a->q_id[i]);
+            emit(x, i);
         }
         wave_sync();
         return unc;
@@ -2331,7 +2334,7 @@ struct HubWide : HubSolver<1> {
                 } else {
                     view_rec(tw, x);
                 }
-                if (j == 0) emit(x, a->q_id[qi]);
+                if (j == 0) emit(x, qi);
             }
         } else {
             for (uint32_t i = qa + j; i < qb; i += 64) {
@@ -2346,7 +2349,7 @@ struct HubWide : HubSolver<1> {
                     const uint32_t b = B::plain_label_serial(w, nb, sx, sy, x);
                     if (!B::dest_avail(nbk, b, w, sx, sy)) unc = true;
                 }
-                emit(x, a->q_id[i]);
+                emit(x, i);
             }
         }
         wave_sync();

@@ -457,6 +457,7 @@ struct HostPlan {
     std::vector<SpecialStatic> sp;
     std::vector<uint16_t> hubs;
     std::vector<uint32_t> src_v, q_begin, q_dst, q_id;
+    std::vector<uint32_t> q_pos;    // per input query: its grouped position (output record), kNone32 if invalid
     std::vector<int32_t> q_status;  // per query: MR_OK or a host-side error
     uint32_t nq = 0;
     uint32_t fleetfoot_raw = 0;
@@ -668,11 +669,13 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     hp.q_begin.push_back(off);
     hp.q_dst.resize(off);
     hp.q_id.resize(off);
+    hp.q_pos.assign(n, kNone32);
     for (uint32_t i = 0; i < n; ++i) {
         if (qs_src[i] == kNone32) continue;
         uint32_t k = start[qs_src[i]]++;
         hp.q_dst[k] = qs_dst[i];
         hp.q_id[k] = i;
+        hp.q_pos[i] = k;  // the device writes query i's record at grouped position k
     }
     return MR_OK;
 }
@@ -1065,6 +1068,13 @@ extern "C" int mr_plan_bind_outputs(mr_plan *pl, void *d_results, void *d_comman
 
 extern "C" uint32_t mr_plan_num_sources(const mr_plan *pl) { return pl ? pl->ka.nsrc : 0; }
 
+extern "C" int mr_plan_record_queries(const mr_plan *pl, uint32_t *query_of_record, uint32_t n) {
+    if (!pl || (n && !query_of_record)) return fail(MR_ERR_INVALID_ARG, "null argument");
+    const std::vector<uint32_t> &ids = pl->hp.q_id;
+    for (uint32_t k = 0; k < n; ++k) query_of_record[k] = k < ids.size() ? ids[k] : kNone32;
+    return MR_OK;
+}
+
 extern "C" double mr_plan_fill_ms(const mr_plan *pl) { return pl ? pl->fill_ms : 0.0; }
 
 extern "C" int mr_plan_get_stats(mr_plan *pl, mr_plan_stats *out) {
@@ -1213,7 +1223,8 @@ extern "C" int mr_plan_fetch(mr_plan *pl, mr_result *results, mr_command *pool, 
             if (ret == MR_OK) ret = hp.q_status[i];
             continue;
         }
-        const OutResult &o = res[i];
+        const uint32_t k = hp.q_pos[i];  // records are in grouped (by source) order
+        const OutResult &o = res[k];
         int status = int(o.ncmd_status >> 16) - 16;
         r.legs = o.legs;
         r.money = o.money;
@@ -1226,9 +1237,9 @@ extern "C" int mr_plan_fetch(mr_plan *pl, mr_result *results, mr_command *pool, 
             continue;
         }
         // a long label: its commands are in the overflow pool at {offset, count}
-        const OutCmd *src = mc ? &cmd[size_t(i) * mc] : nullptr;
+        const OutCmd *src = mc ? &cmd[size_t(k) * mc] : nullptr;
         if (status == int(kStatusOverflow)) {
-            const OutCmd &tag = cmd[size_t(i) * mc];
+            const OutCmd &tag = cmd[size_t(k) * mc];
             if (tag.kp != kOvfTag || tag.to != r.n_commands || uint64_t(tag.from) + tag.to > ovf.size())
                 return fail(MR_ERR_DEVICE, "overflow pool record");
             src = &ovf[tag.from];

@@ -26,7 +26,7 @@ LIB_PATH = os.environ.get("MR_LIB_PATH") or os.path.join(os.path.dirname(os.path
 EXPORTED_SYMBOLS = [
     "mr_grid_create", "mr_grid_destroy", "mr_grid_square_size", "mr_params_default", "mr_find_path",
     "mr_find_path_batch", "mr_plan_create", "mr_plan_create_ex", "mr_plan_run", "mr_plan_fetch", "mr_plan_device_outputs",
-    "mr_plan_num_sources", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_plan_bind_outputs", "mr_abi_version", "mr_last_error",
+    "mr_plan_num_sources", "mr_plan_record_queries", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_plan_bind_outputs", "mr_abi_version", "mr_last_error",
     "mr_device_available", "mr_parse_map_html", "mr_parse_error", "mr_grid_from_html",
     "mr_command_time", "mr_duration_display", "mr_render_schedule",
     "mr_sssp_plan_create", "mr_sssp_records", "mr_sssp_device_records", "mr_sssp_label", "mr_plan_fill_ms",
@@ -78,6 +78,8 @@ def lib():
         L.mr_plan_bind_outputs.restype = C.c_int
         L.mr_plan_num_sources.argtypes = [vp]
         L.mr_plan_num_sources.restype = C.c_uint32
+        L.mr_plan_record_queries.argtypes = [vp, C.POINTER(C.c_uint32), C.c_uint32]
+        L.mr_plan_record_queries.restype = C.c_int
         L.mr_plan_get_stats.argtypes = [vp, C.POINTER(mr_plan_stats)]
         L.mr_plan_get_stats.restype = C.c_int
         L.mr_plan_kernel_ms.argtypes = [vp, C.POINTER(C.c_uint32)]
@@ -302,6 +304,15 @@ class Plan:
     @property
     def num_sources(self) -> int:
         return lib().mr_plan_num_sources(self.handle)
+
+    def record_queries(self) -> List[int]:
+        """query_of_record[k]: the input query whose compact output is device record k
+        (records are grouped by source; 0xFFFFFFFF past the valid queries)."""
+        out = (C.c_uint32 * max(1, self.n))()
+        st = lib().mr_plan_record_queries(self.handle, out, self.n)
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+        return list(out)[:self.n]
 
     def run(self, stream: int = 0) -> None:
         st = lib().mr_plan_run(self.handle, C.c_void_p(stream) if stream else None)

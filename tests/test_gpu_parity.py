@@ -320,3 +320,36 @@ def test_fleetfoot_hub(eng, oracle_lib, monkeypatch, ff, sort_by):
         st = plan.stats()
         assert st["solver"] == "hub"
         assert st["fallback_sources"] <= st["num_sources"] // 4, st
+
+
+def test_device_records_grouped_by_source(eng):
+    """The compact device records (what the multi-GPU gather moves) are grouped by
+    source; mr_plan_record_queries maps record k back to its query, and each record's
+    metrics equal the fetched result of that query."""
+    m = SyntheticMap(33, campfires_per_homeland=3, seed=8)
+    g = eng.MapGrid(m.cells())
+    qs = random_queries(m, 500, 4) + [(CellIndex.homeland(BLUE, 200, 1), m.campfires()[0])]  # one invalid
+    plan = eng.Plan(g, Params(), qs)
+    plan.run()
+    got = plan.fetch()
+    d_res, rb, _, _ = plan.device_outputs()
+    words = _device_words(d_res, rb)
+    qmap = plan.record_queries()
+    valid = [k for k in range(len(qs)) if qmap[k] != 0xFFFFFFFF]
+    assert len(valid) == len(qs) - 1 and sorted(qmap[k] for k in valid) == list(range(len(qs) - 1))
+    srcs = [qs[qmap[k]][0] for k in valid]  # each source's records contiguous
+    assert all(srcs[i] == srcs[i - 1] or srcs[i] not in srcs[:i] for i in range(1, len(srcs)))
+    for k in valid:
+        r = got[qmap[k]]
+        assert (int(words[4 * k]), int(words[4 * k + 1]), int(words[4 * k + 2])) == (r.legs, r.money, r.time_s)
+
+
+def _device_words(ptr: int, nbytes: int):
+    """Copies nbytes of device memory at ptr into a host numpy uint32 array (hipMemcpy)."""
+    import ctypes as C
+    import numpy as np
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    out = np.empty(nbytes // 4, dtype=np.uint32)
+    assert hip.hipMemcpy(out.ctypes.data, C.c_void_p(ptr), nbytes, 2) == 0  # hipMemcpyDeviceToHost
+    return out
