@@ -1,4 +1,4 @@
-"""Pure-Python model of the engine's hub solver (csrc/mr_kernel.hip, HubSolver)
+"""Pure-Python model of the engine's hub solver (csrc/mr_device.hpp, HubSolver)
 — TEST INFRASTRUCTURE.  It restates the closed-form algorithm with full
 reference labels (oracle/py_ref.py) so its exactness claim can be
 checked against the oracle on CPU, independently of the GPU:
