@@ -191,6 +191,12 @@ struct Core {
         else l[i] = IdxT(v);
     }
     __device__ __forceinline__ void flag(uint32_t e) const { atomicOr(counter + kCtrFlags, e); }
+    // metric overflow is sticky per lane and reported once, at the end of the launch
+    // (flush_err): a branch and an atomic per addition would cost issue slots
+    mutable uint32_t err = 0;
+    __device__ __forceinline__ void flush_err() const {
+        if (err) flag(err);
+    }
     __device__ __forceinline__ uint32_t special_of(uint32_t v) const { return sinfo[v] & kNone10; }
     __device__ __forceinline__ uint32_t region_of(uint32_t v) const { return (sinfo[v] >> 10) & kNone10; }
     __device__ __forceinline__ uint32_t vert_of(uint32_t t) const { return t == 0 ? src : sp[t].v; }
@@ -200,7 +206,7 @@ struct Core {
     // ---- arithmetic (u32 like the reference; overflow is reported, not wrapped)
     __device__ __forceinline__ uint32_t add32(uint32_t x, uint32_t y) const {
         uint32_t r = x + y;
-        if (r < x) flag(kErrMetricOverflow);
+        err |= r < x ? kErrMetricOverflow : 0u;
         return r;
     }
     // AggregatedCost::time of a StandardMove run of k legs: Fleetfoot ceil of
@@ -209,7 +215,7 @@ struct Core {
         const DevParams &p = P;
         unsigned long long t = 180ull * k;
         if (p.ff_num != p.ff_den) t = (t * p.ff_num + p.ff_den - 1) / p.ff_den;
-        if (t > 0xFFFFFFFFull) flag(kErrMetricOverflow);
+        err |= t > 0xFFFFFFFFull ? kErrMetricOverflow : 0u;
         return uint32_t(t);
     }
     __device__ __forceinline__ unsigned long long key_of(uint32_t m0, uint32_t m1, uint32_t m2) const {
@@ -2078,7 +2084,7 @@ __host__ __device__ inline HubLayout hub_layout(uint32_t NS, uint32_t nreg, uint
 // PERM = comparator order c1 c2 c3 as metric indices (9*c1 + 3*c2 + c3): a compile-time
 // constant here, so every metric selection and comparison folds.  SPW = sources per wave.
 #ifndef MR_HUB_WAVES
-#define MR_HUB_WAVES 5  // waves per SIMD the register budget is cut for (measured best)
+#define MR_HUB_WAVES 6  // waves per SIMD the register budget is cut for (measured best on c4: 5 -> 6 = -4.5 %)
 #endif
 template <uint32_t PERM, uint32_t SPW, bool NONLIN>
 __global__ __launch_bounds__(kBS, MR_HUB_WAVES) void hub_kernel(const KArgs *__restrict__ a) {
@@ -2135,6 +2141,7 @@ __global__ __launch_bounds__(kBS, MR_HUB_WAVES) void hub_kernel(const KArgs *__r
         if (base >= a->nsrc) break;
         H.solve(uint32_t(base));
     }
+    H.flush_err();
     __shared__ uint32_t wsum;
     if (threadIdx.x == 0) wsum = 0;
     __syncthreads();
@@ -2569,6 +2576,7 @@ __global__ __launch_bounds__(kBS) void hub_wide_kernel(const KArgs *__restrict__
     H.nreg = nreg;
     const uint32_t waves = gridDim.x * (kBS / 64), wid = blockIdx.x * (kBS / 64) + slot;
     for (uint32_t s = wid; s < a->nsrc; s += waves) H.solve(s);
+    H.flush_err();
     __shared__ uint32_t wsum;
     if (threadIdx.x == 0) wsum = 0;
     __syncthreads();
@@ -3008,6 +3016,7 @@ __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a)
             written += a->q_begin[s + 1] - a->q_begin[s];
             ++nsolved;
         }
+        S.flush_err();
 #ifdef MR_STAMPS
         if (threadIdx.x == 0 && a->dbg) {
             for (int i = 0; i < 8; ++i) a->dbg[blockIdx.x * 10 + i] = stamps.acc[i];
@@ -3045,6 +3054,7 @@ __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a)
             S.solve(s);
             written += a->q_begin[s + 1] - a->q_begin[s];
         }
+        S.flush_err();
     }
     __syncthreads();
     if (threadIdx.x == 0) finish_launch(a, written);
