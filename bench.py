@@ -41,16 +41,19 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: Chip-level
 BYTES_PER_VERTEX_SOLVE = 20  # per full single-source solve, V x 20 B
 
 WORKLOADS = {
-    "c2": dict(size=65, queries_per_gpu=10_000, campfires=4, seed=2024,
+    # max_cmds: command slots per query record (what the N > 1 gather moves); the app's
+    # default orders give labels of at most 4 commands on these maps, the Time-first c5
+    # up to 14+; a longer label goes to the rank's overflow pool (its slot is tagged)
+    "c2": dict(size=65, queries_per_gpu=10_000, campfires=4, seed=2024, max_cmds=6,
                desc="configs[1]: 10k uniform (src,dst) per GPU on a 65x65 synthetic map (64x64 -> odd 65), "
                     "default FindPath params"),
     "c3": dict(size=1025, queries_per_gpu=64, campfires=4, seed=4096, all_destinations=True,
                desc="configs[2]: single source -> all 1 050 625 cells of the 1025x1025 synthetic map, 64 sources "
                     "per GPU; a step answers V queries per source (SURVEY 8d c3)"),
-    "c4": dict(size=1025, queries_per_gpu=125_000, campfires=4, seed=4096,
+    "c4": dict(size=1025, queries_per_gpu=125_000, campfires=4, seed=4096, max_cmds=6,
                desc="configs[3] shard: 125k uniform (src,dst) per GPU on a 1025x1025 synthetic map "
                     "(1024 -> odd 1025), default FindPath params; N=8 is the 1M batch"),
-    "c5": dict(size=4097, queries_per_gpu=10_000, campfires=64, clustered=True, seed=4097, sort=(1, 2),
+    "c5": dict(size=4097, queries_per_gpu=10_000, campfires=64, clustered=True, seed=4097, sort=(1, 2), max_cmds=16,
                desc="configs[4]: 10k uniform (src,dst) per GPU on a 4097x4097 synthetic map (4096 -> odd 4097) "
                     "with 64 clustered campfires per homeland (261 specials); sort_by (Time, Money), so caravan "
                     "edges span 102 s .. 240 s x 2S (SURVEY 8d c5 option a)"),
@@ -142,9 +145,9 @@ def algorithmic_bytes(plan, stats, V):
 
     SSSP kernel: V x 20 B per unique source (4 B per-cell record
     read + 16 B final label write).  Hub solver: it never touches the grid, so
-    its bytes are what it reads and writes per query (destination + query id
-    8 B, destination static word 4 B, result record 16 B, 16 B per command
-    slot written), per source (source vertex + range 8 B, its region row
+    its bytes are what it reads and writes per query (destination 4 B,
+    destination static word 4 B, result record 16 B, 16 B per command slot
+    written; records go out in grouped order, so no query id is read), per source (source vertex + range 8 B, its region row
     8 B x regions), plus the SSSP figure for every source it hands to the
     fallback.  Returns (bytes, kernel name, SURVEY-8d-equivalent bytes)."""
     n_src = stats["num_sources"]
@@ -157,7 +160,7 @@ def algorithmic_bytes(plan, stats, V):
     ok = words[:, 6].view(np.int32) == 0
     n_cmds = int(words[ok, 4].astype(np.int64).sum())
     nq = plan.n
-    b = nq * (8 + 4 + 16) + 16 * n_cmds + n_src * (8 + 8 * stats["num_regions"])
+    b = nq * (4 + 4 + 16) + 16 * n_cmds + n_src * (8 + 8 * stats["num_regions"])
     b += 8 * stats["region_boundary_cells"]  # wide solver: the regions' boundary cells, read once (L2-resident)
     b += stats["fallback_sources"] * V * BYTES_PER_VERTEX_SOLVE
     kern = "hub_wide_kernel" if stats["solver"] == "hub_wide" else "hub_kernel"
@@ -241,7 +244,7 @@ def main():
         # N > 1: two plans over the same shard, so the result gather of one batch
         # overlaps the solve of the next (double buffering, shard.PipelinedGather)
         depth = 2 if world > 1 else 1
-        plans = [pathfinder.Plan(grid, params, mine) for _ in range(depth)]
+        plans = [pathfinder.Plan(grid, params, mine, max_cmds=wl.get("max_cmds", 16)) for _ in range(depth)]
         plan = plans[0]
         n_src = plan.num_sources
         _, rbytes, _, cbytes = plan.device_outputs()
