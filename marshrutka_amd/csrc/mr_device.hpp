@@ -1708,29 +1708,32 @@ struct HubSolver : Core<false> {
         }
         return false;
     }
-    // Does boundary q leave the closed-form walk(b, d_b(v)) certain?  (q = b, the Center
-    // and kNone32 trivially do.)  It must fail near_tie, or leave one of the two L-paths
-    // clean; and the b-v walks must not detour round the Center.
-    __device__ __forceinline__ bool walk_clear(uint32_t q, uint32_t b, int vx, int vy, int sx, int sy) const {
+    // Which of the two L-paths from b to v does boundary q leave clean?  Bit 0: the
+    // x-first path, bit 1: the y-first one (3 for q = b, the Center, kNone32 or a q
+    // that fails near_tie; 0 when the b-v walks detour round the Center).  The label
+    // is certain when one path is clean for every boundary: the argument above needs
+    // ONE path on which no boundary flips.
+    __device__ __forceinline__ uint32_t walk_clear(uint32_t q, uint32_t b, int vx, int vy, int sx, int sy) const {
         int bx, by;
         bpos(b, sx, sy, bx, by);
         if ((by == 0 && vy == 0 && bx != 0 && vx != 0 && (bx < 0) != (vx < 0)) ||
             (bx == 0 && vx == 0 && by != 0 && vy != 0 && (by < 0) != (vy < 0)))
-            return false;  // shortest walks detour round the Center
-        if (q == kNone32 || q == b || vert_of(q) == P.vc) return true;
+            return 0u;  // shortest walks detour round the Center
+        if (q == kNone32 || q == b || vert_of(q) == P.vc) return 3u;
         int qx, qy;
         bpos(q, sx, sy, qx, qy);
-        if (!near_tie(q, qx, qy, b, bx, by, vx, vy)) return true;
-        return !path_tie(q, qx, qy, b, bx, by, vx, vy, true) || !path_tie(q, qx, qy, b, bx, by, vx, vy, false);
+        if (!near_tie(q, qx, qy, b, bx, by, vx, vy)) return 3u;
+        return (path_tie(q, qx, qy, b, bx, by, vx, vy, true) ? 0u : 1u) |
+               (path_tie(q, qx, qy, b, bx, by, vx, vy, false) ? 0u : 2u);
     }
     // Is the closed-form walk(b, d_b(v)) certain to be the reference's label of v?
     // Linear run times: always (the blocker check, avail, covers ties).  Otherwise
-    // every boundary must leave it clear.
+    // one L-path must be clean for every boundary.
     __device__ __forceinline__ bool walk_certain(uint32_t b, int vx, int vy, uint32_t nb, int sx, int sy) const {
         if (ff_linear()) return true;
-        for (uint32_t j = 0; j < nb; ++j)
-            if (!walk_clear(bnd[j], b, vx, vy, sx, sy)) return false;
-        return true;
+        uint32_t paths = 3u;
+        for (uint32_t j = 0; j < nb && paths; ++j) paths &= walk_clear(bnd[j], b, vx, vy, sx, sy);
+        return paths != 0;
     }
     // the same for a settled special's label x at (tx, ty): its walk, or the walk to the
     // cell its Scroll of Escape is read from
@@ -1838,10 +1841,13 @@ struct HubSolver : Core<false> {
                 emit(x, qi);
                 if (plain && !dest_avail(nbk, bnd[win], w, sx, sy)) unc = true;
             }
-            // non-linear run times: lane j clears boundary j
-            if (!ff_linear() && !(a->dbg_flags & 8u) && qon && plain &&
-                !walk_clear(t < nb ? bnd[t] : kNone32, bnd[win], wx, wy, sx, sy))
-                unc = true;
+            // non-linear run times: lane j clears boundary j; one path clean for all
+            if (!ff_linear() && !(a->dbg_flags & 8u)) {
+                const uint32_t pc = (qon && plain) ? walk_clear(t < nb ? bnd[t] : kNone32, bnd[win], wx, wy, sx, sy) : 3u;
+                const bool x_bad = seg_bits<LPS>(__ballot(!(pc & 1u))) != 0;
+                const bool y_bad = seg_bits<LPS>(__ballot(!(pc & 2u))) != 0;
+                if (x_bad && y_bad && t == 0) unc = true;
+            }
         }
         for (uint32_t i = qa + t; !few && i < qb; i += LPS) {
             const uint32_t w = a->q_dst[i];

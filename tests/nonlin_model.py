@@ -101,12 +101,13 @@ def path_tie(mq, nq, gq, q_src, mb, nb, gb, b_src, gv, perm, ff, x_first) -> boo
 
 
 def walk_certified(b, v, bnd, lab, geo, src_i, perm, ff) -> bool:
-    """walk_certain: every boundary q leaves walk(b, d_b(v)) clear."""
+    """walk_certain: one L-path (x first or y first) clean for every boundary q."""
     (bx, by), (vx, vy) = geo[b], geo[v]
     if (by == 0 and vy == 0 and bx != 0 and vx != 0 and (bx < 0) != (vx < 0)) or \
        (bx == 0 and vx == 0 and by != 0 and vy != 0 and (by < 0) != (vy < 0)):
         return False
     mb, nb = metrics(lab[b]), len(lab[b].commands)
+    clean = {True, False}  # the paths still clean for every q so far (x_first flags)
     for q in bnd:
         if q == b or geo[q] == (0, 0):
             continue
@@ -114,6 +115,7 @@ def walk_certified(b, v, bnd, lab, geo, src_i, perm, ff) -> bool:
         if not near_tie(mq, geo[q], mb, geo[b], geo[v], perm, ff):
             continue
         args = (mq, nq, geo[q], q == src_i, mb, nb, geo[b], b == src_i, geo[v], perm, ff)
-        if path_tie(*args, True) and path_tie(*args, False):
+        clean = {x for x in clean if not path_tie(*args, x)}
+        if not clean:
             return False
     return True
