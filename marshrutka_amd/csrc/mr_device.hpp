@@ -2090,7 +2090,8 @@ __host__ __device__ inline HubLayout hub_layout(uint32_t NS, uint32_t nreg, uint
 // PERM = comparator order c1 c2 c3 as metric indices (9*c1 + 3*c2 + c3): a compile-time
 // constant here, so every metric selection and comparison folds.  SPW = sources per wave.
 #ifndef MR_HUB_WAVES
-#define MR_HUB_WAVES 6  // waves per SIMD the register budget is cut for (measured best on c4: 5 -> 6 = -4.5 %)
+#define MR_HUB_WAVES 5  // waves per SIMD the register budget is cut for: 6 ran c4 3 % faster but its
+                        // larger scratch spill (64 B/lane) overflowed L2: 0.6 GB of HBM traffic per launch
 #endif
 template <uint32_t PERM, uint32_t SPW, bool NONLIN>
 __global__ __launch_bounds__(kBS, MR_HUB_WAVES) void hub_kernel(const KArgs *__restrict__ a) {
