@@ -138,3 +138,33 @@ def test_fill_tiles_every_cell(eng, oracle_lib, monkeypatch, flags, gx, size, k,
                     as_expected(plan.label(i, d)) != as_expected(e):
                 bad.append(d)
         assert not bad, (params, s, len(bad), bad[:4])
+
+
+@pytest.mark.parametrize("flags,pi", [("", 0), ("2", 1), ("", 2)])
+def test_fill_ragged_last_tile_column(eng, oracle_lib, monkeypatch, flags, pi):
+    """S = 2^k + 1 (every BASELINE side): the last tile column of the fill is one cell
+    wide, on the packed-key path and (MR_DBG_FLAGS=2) the wide-metric launch.  Every
+    cell of 257^2 against the oracle, full labels on the last column."""
+    monkeypatch.delenv("MR_ALGO", raising=False)
+    monkeypatch.delenv("MR_HUB_FALLBACK_ALL", raising=False)
+    monkeypatch.delenv("MR_FILL_GX", raising=False)
+    monkeypatch.setenv("MR_DBG_FLAGS", flags or "0")
+    params = FILL_PARAMS[pi]
+    m = SyntheticMap(257, campfires_per_homeland=4, seed=257 + pi)
+    rng = random.Random(pi)
+    cells = m.all_indices()
+    # a source on the last column, and one anywhere
+    from marshrutka_amd.mapgen import index_to_geo
+    sources = [rng.choice([c for c in cells if index_to_geo(c)[0] == 128]), rng.choice(cells)]
+    g = eng.MapGrid(m.cells())
+    og = oracle_lib.OracleGrid(m.cells())
+    plan = eng.SSSPPlan(g, params, sources)
+    plan.run()
+    assert plan.stats()["solver"] == "hub"
+    for i, s in enumerate(sources):
+        exp = og.sssp_all(params, s)
+        rec = plan.records(i)
+        bad = [j for j, e in enumerate(exp) if (int(rec[j][0]), int(rec[j][1]), int(rec[j][2])) != (e.legs, e.money, e.time_s)]
+        assert not bad, (params, s, len(bad), [cells[j] for j in bad[:4]])
+        for j in range(256, len(cells), 257):  # the last column's full labels
+            assert as_expected(plan.label(i, cells[j])) == as_expected(exp[j]), (s, cells[j])
