@@ -734,6 +734,19 @@ struct mr_plan {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;  // pending event pairs
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timed_fill;  // all-destinations: fill launches
     int device = 0;
+    // All-destinations plans run the specials' solve of pass k + 1 (hub and fallback
+    // kernels, on hub_stream) beside the fill of pass k (on the caller's stream).  The
+    // per-pass buffers and kernel arguments come in two slots; the d_* fields above
+    // always name the slot of the latest pass, `alt` the other one (swap_slot).
+    struct Slot {
+        Rec *tab = nullptr;
+        uint32_t *lex = nullptr, *sstate = nullptr, *fb = nullptr, *counter = nullptr;
+        KArgs *args = nullptr, *args_fb = nullptr, *args_fill = nullptr, *args_fill2 = nullptr;
+    } alt;
+    bool overlap = false;
+    uint32_t slot = 0;  // slot index of the d_* fields
+    hipStream_t hub_stream = nullptr;
+    hipEvent_t ev_hub[2] = {nullptr, nullptr}, ev_fill[2] = {nullptr, nullptr};
     ~mr_plan() {
         for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_rank_inv, (void *)d_src, (void *)d_qb, (void *)d_qd,
                         (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
@@ -742,6 +755,12 @@ struct mr_plan {
                         (void *)d_tab,
                         (void *)d_lex, (void *)d_sstate, (void *)d_near_sp, (void *)d_rb_off, (void *)d_rb_cell, (void *)d_ovf})
             if (p) (void)hipFree(p);
+        for (void *p : {(void *)alt.tab, (void *)alt.lex, (void *)alt.sstate, (void *)alt.fb, (void *)alt.counter,
+                        (void *)alt.args, (void *)alt.args_fb, (void *)alt.args_fill, (void *)alt.args_fill2})
+            if (p) (void)hipFree(p);
+        for (hipEvent_t e : {ev_hub[0], ev_hub[1], ev_fill[0], ev_fill[1]})
+            if (e) (void)hipEventDestroy(e);
+        if (hub_stream) (void)hipStreamDestroy(hub_stream);
         for (auto *v : {&timed, &timed_fill})
             for (auto &e : *v) {
                 (void)hipEventDestroy(e.first);
@@ -750,6 +769,26 @@ struct mr_plan {
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
+
+// all-destinations overlap: make the other slot's buffers and argument blocks current
+static void swap_slot(mr_plan *pl) {
+    mr_plan::Slot &a = pl->alt;
+    std::swap(pl->d_tab, a.tab);
+    std::swap(pl->d_lex, a.lex);
+    std::swap(pl->d_sstate, a.sstate);
+    std::swap(pl->d_fb, a.fb);
+    std::swap(pl->d_counter, a.counter);
+    std::swap(pl->d_args, a.args);
+    std::swap(pl->d_args_fb, a.args_fb);
+    std::swap(pl->d_args_fill, a.args_fill);
+    std::swap(pl->d_args_fill2, a.args_fill2);
+    pl->ka.out_tab = pl->d_tab;
+    pl->ka.out_lex = pl->d_lex;
+    pl->ka.src_state = pl->d_sstate;
+    pl->ka.fb_list = pl->d_fb;
+    pl->ka.counter = pl->d_counter;
+    pl->slot ^= 1u;
+}
 
 // Kernel-argument blocks of a plan: the main launch, and for hub plans the fallback
 // launch and the hub launch that ends a pass on its own (last_launch marks the
@@ -948,6 +987,34 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
 #endif
     if (hipMalloc(reinterpret_cast<void **>(&pl->d_args), sizeof(KArgs)) != hipSuccess || upload_args(pl) != MR_OK)
         return bail(fail(MR_ERR_DEVICE, "kernel args"));
+    // all destinations with the hub: a second slot of per-pass buffers, so that the
+    // specials' solve of the next pass overlaps this pass's fill (MR_FILL_OVERLAP=0: off)
+    const char *ov = std::getenv("MR_FILL_OVERLAP");
+    if (all_mode && hp.hub && !(ov && !std::strcmp(ov, "0"))) {
+        const size_t T = size_t(NS) + 1, ns = std::max<size_t>(nsrc, 1);
+        mr_plan::Slot &a = pl->alt;
+        if (hipMalloc(reinterpret_cast<void **>(&a.tab), ns * T * sizeof(Rec)) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&a.lex), ns * T * 4) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&a.sstate), ns * 4) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&a.fb), ns * 4) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&a.counter), kCtrWords * 4) != hipSuccess ||
+            hipMemset(a.counter, 0, kCtrWords * 4) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&a.args), sizeof(KArgs)) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&a.args_fb), sizeof(KArgs)) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&a.args_fill), sizeof(KArgs)) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&a.args_fill2), sizeof(KArgs)) != hipSuccess ||
+            hipStreamCreateWithFlags(&pl->hub_stream, hipStreamNonBlocking) != hipSuccess)
+            return bail(fail(MR_ERR_DEVICE, "second all-destinations slot"));
+        for (int i = 0; i < 2; ++i)
+            if (hipEventCreateWithFlags(&pl->ev_hub[i], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&pl->ev_fill[i], hipEventDisableTiming) != hipSuccess)
+                return bail(fail(MR_ERR_DEVICE, "overlap events"));
+        swap_slot(pl);
+        const int ua = upload_args(pl);
+        swap_slot(pl);
+        if (ua != MR_OK) return bail(fail(MR_ERR_DEVICE, "kernel args"));
+        pl->overlap = true;
+    }
     *out = pl;
     return MR_OK;
 }
@@ -986,13 +1053,30 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         uint32_t gx = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((items + 3) / 4, uint64_t(pl->fill_per_cu) * pl->cus)));
         if (const char *e = std::getenv("MR_FILL_GX")) gx = uint32_t(std::max(1, std::atoi(e)));
         const uint32_t gy = 1;
-        e = launch_hub_plan(pl, pl->d_args, s);
+        // overlap: this pass takes the other slot, and its specials' solve runs on
+        // hub_stream once the fill two passes back has released that slot
+        hipStream_t hs = s;
+        if (pl->overlap) {
+            if (pl->runs > 1) swap_slot(pl);
+            hs = pl->hub_stream;
+            if (hipStreamWaitEvent(hs, pl->ev_fill[pl->slot], 0) != hipSuccess) return fail(MR_ERR_DEVICE, "wait");
+        }
+        e = launch_hub_plan(pl, pl->d_args, hs);
         if (e == hipSuccess && !pl->fb_none)
-            e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, s);
+            e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, hs);
         hipEvent_t f0 = nullptr;
+        if (e == hipSuccess && pl->overlap) {
+            // the fill waits for this pass's specials (which ran on hub_stream)
+            if (hipEventRecord(pl->ev_hub[pl->slot], pl->hub_stream) != hipSuccess ||
+                hipStreamWaitEvent(s, pl->ev_hub[pl->slot], 0) != hipSuccess)
+                e = hipErrorUnknown;
+        }
         if (e == hipSuccess && hipEventCreate(&f0) == hipSuccess) (void)hipEventRecord(f0, s);
         if (e == hipSuccess) e = launch_fill(pl->d_args_fill, pl->ka.p.perm, gx, gy, s, false);
         if (e == hipSuccess) e = launch_fill(pl->d_args_fill2, pl->ka.p.perm, gx, gy, s, true);
+        // the slot's tables are free again once this fill has read them
+        if (e == hipSuccess && pl->overlap && hipEventRecord(pl->ev_fill[pl->slot], s) != hipSuccess)
+            e = hipErrorUnknown;
         if (f0) pl->timed_fill.push_back({f0, nullptr});
     } else if (pl->hp.hub && pl->fb_none) {
         // a pass of this plan (same inputs, deterministic result) had no fallback

@@ -168,3 +168,39 @@ def test_fill_ragged_last_tile_column(eng, oracle_lib, monkeypatch, flags, pi):
         assert not bad, (params, s, len(bad), [cells[j] for j in bad[:4]])
         for j in range(256, len(cells), 257):  # the last column's full labels
             assert as_expected(plan.label(i, cells[j])) == as_expected(exp[j]), (s, cells[j])
+
+
+@pytest.mark.parametrize("fb", [False, True])
+def test_overlapped_passes_match_serial(eng, oracle_lib, monkeypatch, fb):
+    """All-destinations passes alternate between two slots of label tables, the
+    specials' solve of pass k + 1 running beside the fill of pass k (mr_plan_run).
+    Back-to-back passes (no host sync between them) must leave the records and
+    labels of one serial pass (MR_FILL_OVERLAP=0), after an odd and an even number
+    of passes, with and without sources handed to the SSSP kernel."""
+    monkeypatch.delenv("MR_ALGO", raising=False)
+    monkeypatch.delenv("MR_FILL_GX", raising=False)
+    monkeypatch.delenv("MR_DBG_FLAGS", raising=False)
+    if fb:
+        monkeypatch.setenv("MR_HUB_FALLBACK_ALL", "1")
+    else:
+        monkeypatch.delenv("MR_HUB_FALLBACK_ALL", raising=False)
+    m = SyntheticMap(129, campfires_per_homeland=5, seed=77)
+    rng = random.Random(8)
+    cells = m.all_indices()
+    sources = [CellIndex.center(), m.campfires()[2]] + rng.sample(cells, 6)
+    g = eng.MapGrid(m.cells())
+    monkeypatch.setenv("MR_FILL_OVERLAP", "0")
+    ref = eng.SSSPPlan(g, Params(), sources)
+    ref.run()
+    want = [ref.records(i) for i in range(len(sources))]
+    monkeypatch.delenv("MR_FILL_OVERLAP")
+    plan = eng.SSSPPlan(g, Params(), sources)
+    assert plan.stats()["solver"] == "hub"
+    dsts = rng.sample(cells, 12)
+    for passes in (1, 2, 3):
+        for _ in range(passes):
+            plan.run()
+        for i in range(len(sources)):
+            assert (plan.records(i) == want[i]).all(), (passes, i)
+            for d in dsts[:4]:
+                assert as_expected(plan.label(i, d)) == as_expected(ref.label(i, d)), (passes, i, d)
