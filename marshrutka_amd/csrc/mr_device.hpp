@@ -2725,19 +2725,23 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
         const uint32_t w1 = uint32_t(__builtin_amdgcn_readfirstlane(int(max(1u, bit_width64(mx1)))));
         const uint32_t w2 = uint32_t(__builtin_amdgcn_readfirstlane(int(max(1u, bit_width64(mx2)))));
         const uint32_t w3 = uint32_t(__builtin_amdgcn_readfirstlane(int(max(1u, bit_width64(mx3)))));
-        const bool packable = !no_pack && w1 + w2 + w3 <= 63u;
+        // the boundary's rank rides in the key's low rb bits: (key, rank) pairs order
+        // walks exactly like the comparator, and one 64-bit compare picks the pair
+        const uint32_t rb = max(1u, bit_width64(nb - 1));
+        const bool packable = !no_pack && w1 + w2 + w3 + rb <= 63u;
         // the first launch (WIDE = false) fills the sources whose metrics fit one key and
         // counts the others, which the second launch fills
         if (packable == WIDE) {
             if (!WIDE && j == 0 && lane == 0) atomicAdd(a->counter + kCtrFillWide, 1u);
             continue;
         }
-        const uint32_t sh2 = w3, sh1 = w2 + w3;
+        const uint32_t sh3 = rb, sh2 = w3 + rb, sh1 = w2 + w3 + rb;
         const unsigned long long slope = packable ? ((unsigned long long)sl[q0] << sh1) +
-                                                        ((unsigned long long)sl[q1] << sh2) + sl[q2]
+                                                        ((unsigned long long)sl[q1] << sh2) + ((unsigned long long)sl[q2] << sh3)
                                                   : 0ull;
         if (isb && packable) {
-            const unsigned long long K = ((unsigned long long)em[q0] << sh1) | ((unsigned long long)em[q1] << sh2) | em[q2];
+            const unsigned long long K = ((unsigned long long)em[q0] << sh1) | ((unsigned long long)em[q1] << sh2) |
+                                         ((unsigned long long)em[q2] << sh3) | r;
             B[6][r] = uint32_t(K);
             B[7][r] = uint32_t(K >> 32);
         }
@@ -2775,19 +2779,15 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
             }
             const unsigned long long sp_in = __ballot(in);
             const bool axis = (x0 <= 0 && x1 >= 0) || (y0 <= 0 && y1 >= 0);
-            const unsigned long long mask2 = (1ull << w2) - 1, mask3 = (1ull << w3) - 1;
+            const unsigned long long mask2 = (1ull << w2) - 1, mask3 = (1ull << w3) - 1, maskr = (1ull << rb) - 1;
             if (!WIDE) {
                 // the best (key, rank) per cell (column c = lane + 64k, row i at k * kTH + i);
                 // a rank is the boundary's position in the (length, command list) order, so
                 // the pair orders walks exactly like the comparator whatever order the
                 // boundaries are visited in
                 unsigned long long kb[kCPL * kTH];
-                uint32_t rv[kCPL * kTH];
 #pragma unroll
-                for (int i = 0; i < kCPL * kTH; ++i) {
-                    kb[i] = ~0ull;
-                    rv[i] = 0xFFFFFFFFu;
-                }
+                for (int i = 0; i < kCPL * kTH; ++i) kb[i] = ~0ull;
                 // boundaries on an axis through the Center, in a tile on an axis, take
                 // walk_dist's 2-cell detour to cells on the same axis across the Center:
                 // they get a loop of their own after the others
@@ -2796,7 +2796,7 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
                     const bool on = lane < nb && (B[0][lane] == 0u || B[1][lane] == 0u);
                     axm = __ballot(on) & live;
                 }
-                for (unsigned long long m = live & ~axm; m; m &= m - 1) {  // rank order: the first of equal keys wins
+                for (unsigned long long m = live & ~axm; m; m &= m - 1) {
                     const uint32_t rr = uint32_t(__ffsll((long long)m) - 1);
                     // wave-uniform values in SGPRs, so the per-row step is a scalar select
                     const int bxx = __builtin_amdgcn_readfirstlane(int(B[0][rr]));
@@ -2812,9 +2812,7 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
 #pragma unroll
                         for (int i = 0; i < kTH; ++i) {
                             if (i > 0) key += i > istar ? up : down;
-                            const bool better = key < kb[k * kTH + i];
-                            kb[k * kTH + i] = better ? key : kb[k * kTH + i];
-                            rv[k * kTH + i] = better ? rr : rv[k * kTH + i];
+                            kb[k * kTH + i] = key < kb[k * kTH + i] ? key : kb[k * kTH + i];
                         }
                     }
                 }
@@ -2837,9 +2835,7 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
                             if (i > 0) key += i > istar ? up : down;
                             const bool det = (i == i0 && detx) || (dety && i != i0 && ((i < i0) != (byy < 0)));
                             const unsigned long long kk = key + (det ? det2 : 0ull);
-                            const bool better = kk < kb[k * kTH + i] || (kk == kb[k * kTH + i] && rr < rv[k * kTH + i]);
-                            kb[k * kTH + i] = better ? kk : kb[k * kTH + i];
-                            rv[k * kTH + i] = better ? rr : rv[k * kTH + i];
+                            kb[k * kTH + i] = kk < kb[k * kTH + i] ? kk : kb[k * kTH + i];
                         }
                     }
                 }
@@ -2856,10 +2852,11 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
                         if (cx < int(S) && cy < int(S)) {
                             // c[.] is metric q_.; the rank's table index from the wave's table
                             const unsigned long long kv = kb[k * kTH + i];
-                            const uint32_t c[3] = {uint32_t(kv >> sh1), uint32_t((kv >> sh2) & mask2), uint32_t(kv & mask3)};
+                            const uint32_t c[3] = {uint32_t(kv >> sh1), uint32_t((kv >> sh2) & mask2),
+                                                   uint32_t((kv >> sh3) & mask3)};
                             const u32x4_t rec = {q0 == 0 ? c[0] : (q1 == 0 ? c[1] : c[2]),
                                                  q0 == 1 ? c[0] : (q1 == 1 ? c[1] : c[2]),
-                                                 q0 == 2 ? c[0] : (q1 == 2 ? c[1] : c[2]), B[5][rv[k * kTH + i]]};
+                                                 q0 == 2 ? c[0] : (q1 == 2 ? c[1] : c[2]), B[5][uint32_t(kv & maskr)]};
                             __builtin_amdgcn_raw_buffer_store_b128(rec, rsrc, int((64u * k + lane) * 16u),
                                                                    int(uint32_t(i) * S * 16u), 0);
                         }
