@@ -1073,7 +1073,11 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         }
         if (e == hipSuccess && hipEventCreate(&f0) == hipSuccess) (void)hipEventRecord(f0, s);
         if (e == hipSuccess) e = launch_fill(pl->d_args_fill, pl->ka.p.perm, gx, gy, s, false);
-        if (e == hipSuccess) e = launch_fill(pl->d_args_fill2, pl->ka.p.perm, gx, gy, s, true);
+        // the wide-metric launch mostly finds no source and exits; its grid is one
+        // workgroup per CU, since each workgroup ends with an atomic on one counter
+        // (the last resets the pass's counters) and 1.5k of them cost ~30 us
+        const uint32_t gxw = std::min<uint32_t>(gx, std::max<uint32_t>(1, pl->cus));
+        if (e == hipSuccess) e = launch_fill(pl->d_args_fill2, pl->ka.p.perm, gxw, gy, s, true);
         // the slot's tables are free again once this fill has read them
         if (e == hipSuccess && pl->overlap && hipEventRecord(pl->ev_fill[pl->slot], s) != hipSuccess)
             e = hipErrorUnknown;
