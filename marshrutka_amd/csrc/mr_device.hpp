@@ -1332,12 +1332,19 @@ struct GenericSolver : Core<G> {
 // zeroes the per-pass counters for the next pass.
 __device__ __forceinline__ void finish_launch(const KArgs *__restrict__ a, uint32_t written) {
     uint32_t *c = a->counter;
-    if (written) atomicAdd(c + kCtrWritten, written);
-    if (!a->last_launch) return;
+    if (!a->last_launch) {
+        if (written) atomicAdd(c + kCtrWritten, written);
+        return;
+    }
     __threadfence();
-    if (atomicAdd(c + kCtrDone, 1u) == gridDim.x * gridDim.y * gridDim.z - 1) {  // the grid's last workgroup
+    // one atomic per workgroup: {done, written} share a 64-bit word (a grid's workgroups
+    // end together, and same-address atomics serialise at ~11 ns each)
+    static_assert(kCtrDone % 2 == 0 && kCtrWritten == kCtrDone + 1, "counter pair");
+    const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long *>(c + kCtrDone),
+                                             ((unsigned long long)written << 32) | 1ull);
+    if (uint32_t(old) == gridDim.x * gridDim.y * gridDim.z - 1) {  // the grid's last workgroup
         __threadfence();
-        const uint32_t fb = atomicAdd(c + kCtrFbCount, 0u), wr = atomicAdd(c + kCtrWritten, 0u),
+        const uint32_t fb = atomicAdd(c + kCtrFbCount, 0u), wr = uint32_t(old >> 32) + written,
                        ov = atomicAdd(c + kCtrOvf, 0u);
         c[kCtrLastFb] = fb;
         c[kCtrLastWritten] = wr;

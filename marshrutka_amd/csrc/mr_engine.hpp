@@ -167,9 +167,9 @@ enum : uint32_t {
     kCtrFbCount = 2,      // sources the hub solver handed to the SSSP kernel
     kCtrFbDequeue = 3,    // fallback dequeue
     kCtrLastFb = 4,       // kCtrFbCount of the last completed pass
-    kCtrDone = 5,         // workgroups of the last kernel that finished
-    kCtrWritten = 6,      // result records written
-    kCtrLastWritten = 7,  // kCtrWritten of the last completed pass
+    kCtrLastWritten = 5,  // kCtrWritten of the last completed pass
+    kCtrDone = 6,         // workgroups of the last kernel that finished (low word of one
+    kCtrWritten = 7,      // result records written               64-bit counter with this)
     kCtrOvf = 8,          // command-overflow pool: commands allocated in this pass
     kCtrLastOvf = 9,      // kCtrOvf of the last completed pass
     kCtrFillWide = 10,    // all-destinations fill: sources left to the second (wide-metric) launch
