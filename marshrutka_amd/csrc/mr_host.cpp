@@ -1053,8 +1053,10 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         uint32_t gx = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((items + 3) / 4, uint64_t(pl->fill_per_cu) * pl->cus)));
         if (const char *e = std::getenv("MR_FILL_GX")) gx = uint32_t(std::max(1, std::atoi(e)));
         const uint32_t gy = 1;
-        // overlap: this pass takes the other slot, and its specials' solve runs on
-        // hub_stream once the fill two passes back has released that slot
+        // overlap: this pass takes the other slot, and its hub kernel runs on hub_stream
+        // once the fill two passes back has released that slot.  The hub writes only
+        // the slot's tables; everything that writes the records (the SSSP kernel for
+        // flagged sources, the fill) stays on the caller's stream, in stream order.
         hipStream_t hs = s;
         if (pl->overlap) {
             if (pl->runs > 1) swap_slot(pl);
@@ -1062,15 +1064,13 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
             if (hipStreamWaitEvent(hs, pl->ev_fill[pl->slot], 0) != hipSuccess) return fail(MR_ERR_DEVICE, "wait");
         }
         e = launch_hub_plan(pl, pl->d_args, hs);
-        if (e == hipSuccess && !pl->fb_none)
-            e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, hs);
-        hipEvent_t f0 = nullptr;
         if (e == hipSuccess && pl->overlap) {
-            // the fill waits for this pass's specials (which ran on hub_stream)
-            if (hipEventRecord(pl->ev_hub[pl->slot], pl->hub_stream) != hipSuccess ||
-                hipStreamWaitEvent(s, pl->ev_hub[pl->slot], 0) != hipSuccess)
+            if (hipEventRecord(pl->ev_hub[pl->slot], hs) != hipSuccess || hipStreamWaitEvent(s, pl->ev_hub[pl->slot], 0) != hipSuccess)
                 e = hipErrorUnknown;
         }
+        if (e == hipSuccess && !pl->fb_none)
+            e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, s);
+        hipEvent_t f0 = nullptr;
         if (e == hipSuccess && hipEventCreate(&f0) == hipSuccess) (void)hipEventRecord(f0, s);
         if (e == hipSuccess) e = launch_fill(pl->d_args_fill, pl->ka.p.perm, gx, gy, s, false);
         // the wide-metric launch mostly finds no source and exits; its grid is one
