@@ -251,7 +251,11 @@ typedef struct mr_label_record {
 } mr_label_record;
 /* A plan answering every destination of each source: mr_plan_run computes
  * n_sources x V records on the device; mr_plan_kernel_ms / mr_plan_get_stats /
- * mr_plan_destroy apply.  Sources may repeat (they share a solve). */
+ * mr_plan_destroy apply.  Sources may repeat (they share a solve).  Each pass's
+ * specials' solve runs on a stream of the plan's own, beside the previous pass's
+ * fill, into one of two internal table slots (MR_FILL_OVERLAP=0: one slot, all on
+ * `stream`); the records themselves are only written by work on `stream`, so a
+ * pass's records are complete once `stream` has reached the end of its run. */
 int mr_sssp_plan_create(const mr_grid *grid, const mr_params *params, const mr_cell_index *sources,
                         uint32_t n_sources, mr_plan **out);
 /* All-destinations plans: the fill launch's average time (ms) over the window the
