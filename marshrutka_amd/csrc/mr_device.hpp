@@ -1816,11 +1816,15 @@ struct HubSolver : Core<false> {
             View c;
             view_walk(bj, walk_dist(bx, by, wx, wy), wr, c);
             bool cand = usable && plain;
-            narrow_seg<LPS>(cand, metric(c, p.perm[0]));
-            narrow_seg<LPS>(cand, metric(c, p.perm[1]));
-            narrow_seg<LPS>(cand, metric(c, p.perm[2]));
-            narrow_seg<LPS>(cand, c.len);
-            const unsigned long long m = seg_bits<LPS>(__ballot(cand));
+            // metric by metric, until every segment has at most one candidate left
+            const uint32_t keys[4] = {metric(c, p.perm[0]), metric(c, p.perm[1]), metric(c, p.perm[2]), c.len};
+            unsigned long long m = seg_bits<LPS>(__ballot(cand));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (__all(__popcll(m) <= 1)) break;
+                narrow_seg<LPS>(cand, keys[k]);
+                m = seg_bits<LPS>(__ballot(cand));
+            }
             uint32_t win = __popcll(m) >= 1 ? uint32_t(__ffsll((long long)m) - 1) : 0u;
             if (__any(__popcll(m) > 1)) {  // equal metrics and length: compare the command lists
                 const bool tied = __popcll(m) > 1;
