@@ -379,7 +379,8 @@ def main():
                      "survey_8d_bytes_per_launch": survey_bytes,
                      "note": ("all destinations: fill kernel, V x 16 B per source (the record written; no per-cell "
                               "read) + 80 B per table entry; survey_8d_bytes_per_launch is SURVEY 8d's V x 20 B; "
-                              "pass_ms adds the specials' solve" if all_dst else
+                              "kernel_ms spans the fill's two launches; pass_ms is the caller-stream span of a pass (the specials' "
+                              "solve runs beside the previous pass's fill, DESIGN.md 3b)" if all_dst else
                               "hub solver: latency-bound per-source wave Dijkstra over the specials; bytes = "
                               "queries in, results and command slots out, per-source region rows, plus V*20 B "
                               "per SSSP fallback source (DESIGN.md section 4)")
