@@ -733,6 +733,10 @@ struct mr_plan {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;  // pending event pairs
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timed_fill;  // all-destinations: fill launches
+    // timings of event pairs already folded (a caller that never asks for kernel_ms
+    // must not pile up events: mr_plan_run folds the oldest beyond kMaxTimed)
+    double acc_ms = 0.0, acc_fill_ms = 0.0;
+    uint32_t acc_n = 0, acc_fill_n = 0;
     int device = 0;
     // All-destinations plans run the specials' solve of pass k + 1 (hub and fallback
     // kernels, on hub_stream) beside the fill of pass k (on the caller's stream).  The
@@ -761,11 +765,12 @@ struct mr_plan {
         for (hipEvent_t e : {ev_hub[0], ev_hub[1], ev_fill[0], ev_fill[1]})
             if (e) (void)hipEventDestroy(e);
         if (hub_stream) (void)hipStreamDestroy(hub_stream);
-        for (auto *v : {&timed, &timed_fill})
-            for (auto &e : *v) {
-                (void)hipEventDestroy(e.first);
-                (void)hipEventDestroy(e.second);
-            }
+        for (auto &e : timed) {
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
+        for (auto &f : timed_fill)  // its end event is the pass's, destroyed above
+            if (f.first) (void)hipEventDestroy(f.first);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -1036,10 +1041,14 @@ static hipError_t launch_hub_plan(const mr_plan *pl, const KArgs *d_args, hipStr
     return launch_hub(d_args, pl->ka.p.perm, pl->spw, pl->hp.nonlin, pl->ka.p.NS, pl->ka.nreg, pl->hub_blocks, s);
 }
 
+static void fold_timed(mr_plan *pl, size_t keep);
+static constexpr size_t kMaxTimed = 1024;  // pending timing event pairs per plan
+
 extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     if (!pl) return fail(MR_ERR_INVALID_ARG, "null plan");
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : pl->stream;
     if (pl->ka.nsrc == 0) return MR_OK;
+    if (pl->timed.size() >= kMaxTimed) fold_timed(pl, kMaxTimed / 4);
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return fail(MR_ERR_DEVICE, "event");
     (void)hipEventRecord(e0, s);
@@ -1081,7 +1090,7 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         // the slot's tables are free again once this fill has read them
         if (e == hipSuccess && pl->overlap && hipEventRecord(pl->ev_fill[pl->slot], s) != hipSuccess)
             e = hipErrorUnknown;
-        if (f0) pl->timed_fill.push_back({f0, nullptr});
+        pl->timed_fill.push_back({f0, nullptr});  // one per pass (f0 may be null), as in `timed`
     } else if (pl->hp.hub && pl->fb_none) {
         // a pass of this plan (same inputs, deterministic result) had no fallback
         // sources: the hub launch ends the pass on its own
@@ -1111,35 +1120,45 @@ static int read_counters(mr_plan *pl, uint32_t ctr[kCtrWords]) {
     return MR_OK;
 }
 
-extern "C" double mr_plan_kernel_ms(mr_plan *pl, uint32_t *n_launches) {
-    if (!pl) return 0.0;
-    // all-destinations passes: the fill launch's own time (its end event is the pass's)
-    double ftot = 0.0;
-    uint32_t kf = 0;
-    for (auto &f : pl->timed_fill) {
-        (void)hipEventSynchronize(f.second);
+// Folds the pending event pairs into the plan's running totals, all but the newest
+// `keep` of them (waits for those passes; the fill pairs share their end event
+// with the pass pairs, which destroy it).
+static void fold_timed(mr_plan *pl, size_t keep) {
+    const size_t nf = pl->timed_fill.size() > keep ? pl->timed_fill.size() - keep : 0;
+    for (size_t i = 0; i < nf; ++i) {
+        auto &f = pl->timed_fill[i];
         float ms = 0.f;
-        if (f.second && hipEventElapsedTime(&ms, f.first, f.second) == hipSuccess) {
-            ftot += ms;
-            ++kf;
+        if (f.first && f.second && hipEventSynchronize(f.second) == hipSuccess &&
+            hipEventElapsedTime(&ms, f.first, f.second) == hipSuccess) {
+            pl->acc_fill_ms += ms;
+            ++pl->acc_fill_n;
         }
-        (void)hipEventDestroy(f.first);
+        if (f.first) (void)hipEventDestroy(f.first);
     }
-    pl->timed_fill.clear();
-    pl->fill_ms = kf ? ftot / kf : 0.0;
-    double tot = 0.0;
-    uint32_t k = 0;
-    for (auto &e : pl->timed) {
-        (void)hipEventSynchronize(e.second);
+    pl->timed_fill.erase(pl->timed_fill.begin(), pl->timed_fill.begin() + ptrdiff_t(nf));
+    const size_t n = pl->timed.size() > keep ? pl->timed.size() - keep : 0;
+    for (size_t i = 0; i < n; ++i) {
+        auto &e = pl->timed[i];
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) {
-            tot += ms;
-            ++k;
+        if (hipEventSynchronize(e.second) == hipSuccess && hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) {
+            pl->acc_ms += ms;
+            ++pl->acc_n;
         }
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
     }
-    pl->timed.clear();
+    pl->timed.erase(pl->timed.begin(), pl->timed.begin() + ptrdiff_t(n));
+}
+
+extern "C" double mr_plan_kernel_ms(mr_plan *pl, uint32_t *n_launches) {
+    if (!pl) return 0.0;
+    // all-destinations passes: the fill launches' own time (their end event is the pass's)
+    fold_timed(pl, 0);
+    pl->fill_ms = pl->acc_fill_n ? pl->acc_fill_ms / pl->acc_fill_n : 0.0;
+    const double tot = pl->acc_ms;
+    const uint32_t k = pl->acc_n;
+    pl->acc_ms = pl->acc_fill_ms = 0.0;
+    pl->acc_n = pl->acc_fill_n = 0;
     uint32_t ctr[kCtrWords];
     (void)read_counters(pl, ctr);
     if (n_launches) *n_launches = k;
@@ -1369,6 +1388,8 @@ extern "C" void mr_plan_destroy(mr_plan *pl) {
         }
     }
 #endif
+    // passes may still be in flight on the caller's stream and the plan's hub stream
+    if (pl && pl->runs) (void)hipDeviceSynchronize();
     delete pl;
 }
 

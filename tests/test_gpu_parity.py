@@ -184,6 +184,33 @@ def test_plan_rerun_is_identical(eng):
     assert n == 3 and ms > 0
 
 
+def test_many_passes_without_timing_reads(eng):
+    """A plan run far past the pending-event window (mr_plan_run folds the oldest
+    timing events itself) still reports every pass in kernel_ms and keeps its
+    results; the same for an all-destinations plan (its fill timing too)."""
+    m = SyntheticMap(33, campfires_per_homeland=3, seed=6)
+    g = eng.MapGrid(m.cells())
+    plan = eng.Plan(g, Params(), random_queries(m, 200, 4))
+    plan.run()
+    a = [as_expected(r) for r in plan.fetch()]
+    plan.kernel_ms()
+    for _ in range(1300):
+        plan.run()
+    ms, n = plan.kernel_ms()
+    assert n == 1300 and ms > 0
+    assert [as_expected(r) for r in plan.fetch()] == a
+    sp = eng.SSSPPlan(g, Params(), [CellIndex.center(), m.campfires()[0]])
+    sp.run()
+    rec = sp.records(1).copy()
+    sp.kernel_ms()
+    for _ in range(1100):
+        sp.run()
+    ms, n = sp.kernel_ms()
+    assert n == 1100 and ms > 0 and sp.fill_ms() > 0
+    assert (sp.records(1) == rec).all()
+    del sp, plan  # destroys plans right after their last pass
+
+
 def test_plan_rerun_with_fallback_sources(eng, oracle_lib):
     """A hub plan whose sources partly fall back (clustered map, Time first) keeps
     both launches on every pass; a plan without any skips the empty fallback launch
