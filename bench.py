@@ -168,6 +168,46 @@ def algorithmic_bytes(plan, stats, V):
     return float(b), name, survey
 
 
+def label_digest(pairs):
+    """sha256 over (global query id, label) pairs in id order."""
+    import hashlib
+    h = hashlib.sha256()
+    for qid, lab in sorted(pairs, key=lambda t: t[0]):
+        h.update(repr((qid, as_expected(lab))).encode())
+    return h.hexdigest()
+
+
+def check_gather(pipe, plan, k, grid, params, shards, orders, counts, rows, rw, cw, ovf_cap, rank, world):
+    """After the timed region (N > 1): rank 0 decodes every record of the last batch
+    as gathered (result records, command slots, overflow pool of each rank) on the
+    host, maps record k of rank r to its query shards[r][orders[r][k]], and compares
+    the labels with each rank's own fetch of that batch (a digest per rank).  Returns
+    the check's summary on rank 0."""
+    import torch.distributed as dist
+    from marshrutka_amd import pathfinder
+    own = plan.fetch()  # this rank's labels, in its local query order
+    digests = [None] * world
+    dist.all_gather_object(digests, label_digest([(shards[rank][i], lab) for i, lab in enumerate(own)]))
+    if rank != 0:
+        return None
+    bad_status, mismatched, seen = 0, 0, set()
+    for r, buf in enumerate(pipe.out[k]):
+        words = buf.to("cpu").numpy().view("uint32")
+        n = counts[r]
+        res = words[: n * rw]
+        slots = words[rows * rw: rows * rw + n * cw]
+        ovf = words[rows * (rw + cw): rows * (rw + cw) + ovf_cap * 4]
+        st = res.reshape(-1, rw)[:, 3] >> 16
+        bad_status += int(((st != 16) & (st != 17) & (st != 80)).sum())
+        labels = pathfinder.decode_records(grid, params, res, slots, n, cw // 4, ovf)
+        pairs = [(shards[r][orders[r][j]], lab) for j, lab in enumerate(labels)]
+        seen.update(q for q, _ in pairs)
+        if label_digest(pairs) != digests[r]:
+            mismatched += 1
+    return {"rows": sum(counts), "bad_status": bad_status, "queries_covered": len(seen),
+            "ranks_matching_own_fetch": world - mismatched, "ranks": world}
+
+
 def as_expected(label):
     if label is None:
         return None
@@ -250,14 +290,20 @@ def main():
         _, rbytes, _, cbytes = plan.device_outputs()
     pipe = None
     if world > 1 and not all_dst:
-        # result records then command slots in one flat torch-owned device buffer
-        # per plan, padded to the largest shard: one RCCL gather per batch
+        # result records, command slots and the overflow pool in one flat torch-owned
+        # device buffer per plan, padded to the largest shard: one RCCL gather per batch
+        # moves every record of the batch with all its commands
         rows, nq = max(counts), max(1, len(mine))
         rw, cw = rbytes // nq // 4, cbytes // nq // 4
-        bufs = [torch.zeros(rows * (rw + cw), dtype=torch.int32, device="cuda") for _ in plans]
+        ovf_cap = max(1024, rows // 8)  # commands (16 B) for labels longer than the slots
+        bufs = [torch.zeros(rows * (rw + cw) + ovf_cap * 4, dtype=torch.int32, device="cuda") for _ in plans]
         for p_, b in zip(plans, bufs):
-            p_.bind_outputs(b.data_ptr(), b.data_ptr() + rows * rw * 4)
+            p_.bind_outputs(b.data_ptr(), b.data_ptr() + rows * rw * 4, b.data_ptr() + rows * (rw + cw) * 4, ovf_cap)
         pipe = PipelinedGather(bufs, rank, world, host_staging=backend == "gloo")
+        # record k of rank r's buffer answers query shards[r][order_r[k]]: the grouping
+        # order is fixed per plan, so it crosses once, outside the timed region
+        orders = [None] * world
+        dist.all_gather_object(orders, plan.record_queries())
     elif all_dst:
         plans = [plan]
     it = [0]
@@ -291,14 +337,9 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     gather_check = None
-    if pipe is not None and rank == 0:
-        # every gathered result record of the last batch: status OK (16), not found (17)
-        # or in the rank's overflow pool (16 + 64), per mr_engine.hpp OutResult
-        k_last = (it[0] - 1) % len(plans)
-        rows_all = pipe.rows(k_last, counts, rw)
-        st = torch.cat([r[:, 3] for r in rows_all]).to("cpu").numpy().astype("uint32") >> 16
-        bad = int(((st != 16) & (st != 17) & (st != 80)).sum())
-        gather_check = {"rows": int(st.size), "bad_status": bad}
+    if pipe is not None:
+        gather_check = check_gather(pipe, plans[(it[0] - 1) % len(plans)], (it[0] - 1) % len(plans), grid, params,
+                                    shards, orders, counts, rows, rw, cw, ovf_cap, rank, world)
     kn = [p_.kernel_ms() for p_ in plans]
     nl = sum(n for _, n in kn)
     kms = sum(ms * n for ms, n in kn) / nl if nl else 0.0

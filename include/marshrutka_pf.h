@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MR_ABI_VERSION 2u
+#define MR_ABI_VERSION 3u
 
 /* ---- status codes ------------------------------------------------------ */
 typedef enum mr_status {
@@ -210,6 +210,21 @@ int mr_plan_device_outputs(mr_plan *plan, void **d_results, uint64_t *results_by
  * instead of the plan's own.  Sizes as reported by mr_plan_device_outputs;
  * the caller keeps the buffers alive while the plan uses them. */
 int mr_plan_bind_outputs(mr_plan *plan, void *d_results, void *d_commands);
+/* The same, and the overflow pool too: a label longer than max_cmds then keeps
+ * its commands at d_overflow (overflow_cap commands of 16 B), so that one
+ * collective over one caller buffer moves every record of a pass with all its
+ * commands.  overflow_cap 0 keeps the plan's own pool. */
+int mr_plan_bind_outputs_ex(mr_plan *plan, void *d_results, void *d_commands, void *d_overflow,
+                            uint32_t overflow_cap);
+/* Host-side decoding of compact records as mr_plan_device_outputs lays them out
+ * (e.g. gathered from another rank's plan over the same grid and params): record
+ * k -> out[k] and its commands at pool[out[k].command_offset ..].  `overflow`
+ * holds the overflow pool the records' tags point into (overflow_n commands).
+ * MR_OK; a per-record status in out[k].status; MR_ERR_CAPACITY if pool_cap is too
+ * small; MR_ERR_DEVICE for a record that is not well formed.  Needs no device. */
+int mr_decode_records(const mr_grid *grid, const mr_params *params, const void *results, const void *commands,
+                      uint32_t n, uint32_t max_cmds, const void *overflow, uint64_t overflow_n,
+                      mr_result *out, mr_command *pool, uint64_t pool_cap);
 /* query_of_record[k] = the input query whose output is record k of
  * mr_plan_device_outputs (0xFFFFFFFF past the valid queries), k < n. */
 int mr_plan_record_queries(const mr_plan *plan, uint32_t *query_of_record, uint32_t n);

@@ -2685,6 +2685,7 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
     const int H = int(a->p.H);
     const uint32_t tpx = (S + kTW - 1) / kTW, tpy = (S + kTH - 1) / kTH, ntile = tpx * tpy;
     const bool no_prune = (a->dbg_flags & 1u) != 0, no_pack = (a->dbg_flags & 2u) != 0;
+    if (!WIDE && (a->dbg_flags & kDbgInjectFlag) && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a->counter + kCtrFlags, kErrChain);
     const uint32_t nwaves = gridDim.x * (kBS / 64), gw = blockIdx.x * (kBS / 64) + wv;
     const uint32_t ngroups = nsrc < nwaves ? nsrc : nwaves, G = nwaves / ngroups, g = gw / G, j = gw % G;
     uint32_t s_begin = g < ngroups ? uint32_t(uint64_t(g) * nsrc / ngroups) : 0u;

@@ -181,5 +181,7 @@ constexpr uint32_t kStatusOverflow = 64u, kOvfTag = 0xFFFFFFFFu;
 enum : uint32_t { kAlgoGeneric = 0, kAlgoLegs = 1 };
 
 constexpr uint32_t kErrKOverflow = 1u, kErrMetricOverflow = 2u, kErrBucket = 4u, kErrChain = 8u;
+// KArgs::dbg_flags bit (tests only): the fill launch raises kErrChain
+constexpr uint32_t kDbgInjectFlag = 16u;
 
 }  // namespace mr

@@ -481,6 +481,13 @@ static void comparator_order(uint8_t s1, uint8_t s2, uint8_t out[3]) {
 }
 static uint32_t metric_index(uint8_t c) { return c == MR_SORT_LEGS ? 0u : (c == MR_SORT_MONEY ? 1u : 2u); }
 
+// RouteGuru (src/skill.rs:43-52) on CARAVAN_TIME = 240 s: ceil(240 * r), raw out of range
+static uint32_t caravan_unit_time(uint32_t route_guru) {
+    static const uint32_t rgn[6] = {1, 19, 7, 73, 31, 51}, rgd[6] = {1, 24, 10, 120, 60, 120};
+    const uint32_t rg = route_guru <= 5 ? route_guru : 0;
+    return uint32_t((240ull * rgn[rg] + rgd[rg] - 1) / rgd[rg]);
+}
+
 static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs, uint32_t n, uint32_t max_cmds,
                       HostPlan &hp) {
     if (!g || !prm) return fail(MR_ERR_INVALID_ARG, "null grid or params");
@@ -505,10 +512,7 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     p.ff_num = ffn[ff];
     p.ff_den = ffd[ff];
     p.W = uint32_t((180ull * p.ff_num) / p.ff_den);  // floor(r*180): min StandardMove increment
-    // RouteGuru (src/skill.rs:43-52) on CARAVAN_TIME = 240 s
-    static const uint32_t rgn[6] = {1, 19, 7, 73, 31, 51}, rgd[6] = {1, 24, 10, 120, 60, 120};
-    uint32_t rg = prm->route_guru <= 5 ? prm->route_guru : 0;
-    p.rgt = uint32_t((240ull * rgn[rg] + rgd[rg] - 1) / rgd[rg]);
+    p.rgt = caravan_unit_time(prm->route_guru);
     p.soe_cost = prm->scroll_of_escape_cost;
     p.shq_cost = prm->scroll_of_escape_hq_cost;
     p.sfm_cost = prm->scroll_of_escape_forum_cost;
@@ -730,7 +734,7 @@ struct mr_plan {
     OutCmd *d_cmd = nullptr;
     uint32_t *d_ws = nullptr, *d_counter = nullptr;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev_last = nullptr;         // recorded on the caller's stream at the end of every pass
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;  // pending event pairs
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timed_fill;  // all-destinations: fill launches
     // timings of event pairs already folded (a caller that never asks for kernel_ms
@@ -762,7 +766,7 @@ struct mr_plan {
         for (void *p : {(void *)alt.tab, (void *)alt.lex, (void *)alt.sstate, (void *)alt.fb, (void *)alt.counter,
                         (void *)alt.args, (void *)alt.args_fb, (void *)alt.args_fill, (void *)alt.args_fill2})
             if (p) (void)hipFree(p);
-        for (hipEvent_t e : {ev_hub[0], ev_hub[1], ev_fill[0], ev_fill[1]})
+        for (hipEvent_t e : {ev_hub[0], ev_hub[1], ev_fill[0], ev_fill[1], ev_last})
             if (e) (void)hipEventDestroy(e);
         if (hub_stream) (void)hipStreamDestroy(hub_stream);
         for (auto &e : timed) {
@@ -802,6 +806,10 @@ static int upload_args(mr_plan *pl) {
     auto put = [](KArgs *d, const KArgs &k) { return hipMemcpy(d, &k, sizeof(KArgs), hipMemcpyHostToDevice) == hipSuccess; };
     KArgs k = pl->ka;
     const bool hub = pl->hp.hub;
+    // tests: MR_DBG_INJECT_SLOT=<slot> makes the fill of that slot's passes raise a
+    // device error flag (checks that errors of either overlap slot are reported)
+    if (const char *e = std::getenv("MR_DBG_INJECT_SLOT"))
+        if (pl->all_mode && uint32_t(std::atoi(e)) == pl->slot) k.dbg_flags |= kDbgInjectFlag;
     // the pass ends with: the SSSP kernel (no hub), the fill kernel (all-destinations
     // hub plans), else the fallback launch or a lone hub launch
     k.last_launch = hub ? 0u : 1u;
@@ -1049,8 +1057,25 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : pl->stream;
     if (pl->ka.nsrc == 0) return MR_OK;
     if (pl->timed.size() >= kMaxTimed) fold_timed(pl, kMaxTimed / 4);
-    hipEvent_t e0, e1;
-    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return fail(MR_ERR_DEVICE, "event");
+    if (!pl->ev_last && hipEventCreateWithFlags(&pl->ev_last, hipEventDisableTiming) != hipSuccess)
+        return fail(MR_ERR_DEVICE, "event");
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (hipEventCreate(&e0) != hipSuccess) return fail(MR_ERR_DEVICE, "event");
+    if (hipEventCreate(&e1) != hipSuccess) {
+        (void)hipEventDestroy(e0);
+        return fail(MR_ERR_DEVICE, "event");
+    }
+    // overlap plans: this pass takes the other slot once its last fill has released
+    // it; nothing is launched or recorded before that wait is in place
+    if (pl->hp.hub && pl->all_mode && pl->overlap && pl->runs >= 1) {
+        swap_slot(pl);
+        if (hipStreamWaitEvent(pl->hub_stream, pl->ev_fill[pl->slot], 0) != hipSuccess) {
+            swap_slot(pl);
+            (void)hipEventDestroy(e0);
+            (void)hipEventDestroy(e1);
+            return fail(MR_ERR_DEVICE, "wait");
+        }
+    }
     (void)hipEventRecord(e0, s);
     hipError_t e;
     ++pl->runs;
@@ -1062,16 +1087,11 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         uint32_t gx = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((items + 3) / 4, uint64_t(pl->fill_per_cu) * pl->cus)));
         if (const char *e = std::getenv("MR_FILL_GX")) gx = uint32_t(std::max(1, std::atoi(e)));
         const uint32_t gy = 1;
-        // overlap: this pass takes the other slot, and its hub kernel runs on hub_stream
-        // once the fill two passes back has released that slot.  The hub writes only
+        // overlap: this pass took the other slot above, and its hub kernel runs on
+        // hub_stream behind the wait for the fill two passes back.  The hub writes only
         // the slot's tables; everything that writes the records (the SSSP kernel for
         // flagged sources, the fill) stays on the caller's stream, in stream order.
-        hipStream_t hs = s;
-        if (pl->overlap) {
-            if (pl->runs > 1) swap_slot(pl);
-            hs = pl->hub_stream;
-            if (hipStreamWaitEvent(hs, pl->ev_fill[pl->slot], 0) != hipSuccess) return fail(MR_ERR_DEVICE, "wait");
-        }
+        hipStream_t hs = pl->overlap ? pl->hub_stream : s;
         e = launch_hub_plan(pl, pl->d_args, hs);
         if (e == hipSuccess && pl->overlap) {
             if (hipEventRecord(pl->ev_hub[pl->slot], hs) != hipSuccess || hipStreamWaitEvent(s, pl->ev_hub[pl->slot], 0) != hipSuccess)
@@ -1105,16 +1125,26 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         e = launch_solve(pl->d_args, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->blocks, s);
     }
     (void)hipEventRecord(e1, s);
+    (void)hipEventRecord(pl->ev_last, s);
     pl->timed.push_back({e0, e1});
     if (!pl->timed_fill.empty() && !pl->timed_fill.back().second) pl->timed_fill.back().second = e1;
     if (e != hipSuccess) return fail(MR_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(e));
     return MR_OK;
 }
 
-// counters after the plan's stream has drained; notes a pass without fallback sources
+// Waits for this plan's passes only (the caller's stream up to the last pass, the
+// plan's own and hub streams), never for the whole device.
+static bool plan_sync(mr_plan *pl) {
+    bool ok = true;
+    if (pl->runs && pl->ev_last) ok = hipEventSynchronize(pl->ev_last) == hipSuccess;
+    if (pl->stream) ok = hipStreamSynchronize(pl->stream) == hipSuccess && ok;
+    if (pl->hub_stream) ok = hipStreamSynchronize(pl->hub_stream) == hipSuccess && ok;
+    return ok;
+}
+
+// counters after the plan's passes have drained; notes a pass without fallback sources
 static int read_counters(mr_plan *pl, uint32_t ctr[kCtrWords]) {
-    if (hipStreamSynchronize(pl->stream) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpy(ctr, pl->d_counter, kCtrWords * 4, hipMemcpyDeviceToHost) != hipSuccess)
+    if (!plan_sync(pl) || hipMemcpy(ctr, pl->d_counter, kCtrWords * 4, hipMemcpyDeviceToHost) != hipSuccess)
         return fail(MR_ERR_DEVICE, "copy counter");
     if (pl->hp.hub && pl->runs && !pl->ka.fb_all && ctr[kCtrLastFb] == 0) pl->fb_none = true;
     return MR_OK;
@@ -1165,12 +1195,26 @@ extern "C" double mr_plan_kernel_ms(mr_plan *pl, uint32_t *n_launches) {
     return k ? tot / k : 0.0;
 }
 
-extern "C" int mr_plan_bind_outputs(mr_plan *pl, void *d_results, void *d_commands) {
-    if (!pl || !d_results || !d_commands) return fail(MR_ERR_INVALID_ARG, "null argument");
+extern "C" int mr_plan_bind_outputs_ex(mr_plan *pl, void *d_results, void *d_commands, void *d_overflow,
+                                       uint32_t overflow_cap) {
+    if (!pl || !d_results || !d_commands || (overflow_cap && !d_overflow))
+        return fail(MR_ERR_INVALID_ARG, "null argument");
+    // all-destinations plans write per-cell records, not query records (and keep two
+    // slots of argument blocks)
+    if (pl->all_mode) return fail(MR_ERR_INVALID_ARG, "bind_outputs: not a query plan");
+    if (!plan_sync(pl)) return fail(MR_ERR_DEVICE, "sync");
     pl->ka.out_res = reinterpret_cast<OutResult *>(d_results);
     pl->ka.out_cmd = reinterpret_cast<OutCmd *>(d_commands);
-    if (hipDeviceSynchronize() != hipSuccess || upload_args(pl) != MR_OK) return fail(MR_ERR_DEVICE, "kernel args");
+    if (d_overflow) {
+        pl->ka.ovf = reinterpret_cast<OutCmd *>(d_overflow);
+        pl->ka.ovf_cap = overflow_cap;
+    }
+    if (upload_args(pl) != MR_OK) return fail(MR_ERR_DEVICE, "kernel args");
     return MR_OK;
+}
+
+extern "C" int mr_plan_bind_outputs(mr_plan *pl, void *d_results, void *d_commands) {
+    return mr_plan_bind_outputs_ex(pl, d_results, d_commands, nullptr, 0);
 }
 
 extern "C" uint32_t mr_plan_num_sources(const mr_plan *pl) { return pl ? pl->ka.nsrc : 0; }
@@ -1212,32 +1256,92 @@ extern "C" int mr_plan_device_outputs(mr_plan *pl, void **d_results, uint64_t *r
     return MR_OK;
 }
 
-// expand one compact command (mr_engine.hpp) into the ABI's mr_command
-static void expand_cmd(const mr_grid *g, const HostPlan &hp, const OutCmd &c, mr_command &o) {
+// What a compact command's payload scales by (mr_engine.hpp Cmd): the caravan
+// seconds per distance unit, the scroll prices and the raw Fleetfoot level.
+struct CmdScale {
+    uint32_t rgt, soe, shq, sfm, ff;
+};
+static CmdScale cmd_scale(const HostPlan &hp) {
+    return CmdScale{hp.p.rgt, hp.p.soe_cost, hp.p.shq_cost, hp.p.sfm_cost, hp.fleetfoot_raw};
+}
+static CmdScale cmd_scale(const mr_params &prm) {
+    return CmdScale{caravan_unit_time(prm.route_guru), prm.scroll_of_escape_cost, prm.scroll_of_escape_hq_cost,
+                    prm.scroll_of_escape_forum_cost, prm.fleetfoot};
+}
+
+// expand one compact command (mr_engine.hpp) into the ABI's mr_command; false if it
+// names no cell of the grid
+static bool expand_cmd(const mr_grid *g, const CmdScale &cs, const OutCmd &c, mr_command &o) {
     std::memset(&o, 0, sizeof(o));
     uint32_t kind = c.kp >> 29, pay = c.kp & 0x1FFFFFFFu;
     o.kind = uint8_t(kind);
-    const DevParams &p = hp.p;
     switch (kind) {
         case kCentral: o.time_s = int64_t(10) * pay; break;
         case kStandard:
             o.legs = pay;
             o.time_s = int64_t(180) * pay;
-            o.fleetfoot = hp.fleetfoot_raw;
+            o.fleetfoot = cs.ff;
             break;
         case kCaravan: {
             uint32_t d = pay >> 1;
-            o.time_s = int64_t(p.rgt) * d;
+            o.time_s = int64_t(cs.rgt) * d;
             o.money = d * ((pay & 1u) ? 5u : 2u);
             break;
         }
-        case kSoE: o.money = p.soe_cost; break;
-        case kSHQ: o.money = p.shq_cost; break;
-        case kSFm: o.money = p.sfm_cost; break;
+        case kSoE: o.money = cs.soe; break;
+        case kSHQ: o.money = cs.shq; break;
+        case kSFm: o.money = cs.sfm; break;
         default: break;
     }
+    if (kind > kSFm || c.from >= g->V || c.to >= g->V) return false;
     o.from = g->idx[g->rank_inv[c.from]];  // device commands name cells by rank
     o.to = g->idx[g->rank_inv[c.to]];
+    return true;
+}
+
+// Decodes compact record `o` (its max_cmds slots at `slots`, the overflow pool
+// `ovf` of novf commands) into r, its commands into pool[off..] when they fit
+// (else *ret = MR_ERR_CAPACITY).  Returns MR_OK, or MR_ERR_DEVICE for a record
+// that is not well formed (an overflow tag outside the pool, a bad cell rank).
+static int decode_record(const mr_grid *g, const CmdScale &cs, const OutResult &o, const OutCmd *slots, uint32_t mc,
+                         const OutCmd *ovf, uint64_t novf, mr_result &r, mr_command *pool, uint64_t pool_cap,
+                         uint64_t &off, int &ret) {
+    std::memset(&r, 0, sizeof(r));
+    int status = int(o.ncmd_status >> 16) - 16;
+    r.legs = o.legs;
+    r.money = o.money;
+    r.time_s = int64_t(o.time);
+    r.n_commands = o.ncmd_status & 0xFFFFu;
+    r.status = status;
+    r.command_offset = uint32_t(off);
+    if (status == MR_NOT_FOUND) {
+        r.n_commands = 0;
+        return MR_OK;
+    }
+    // a long label: its commands are in the overflow pool at {offset, count}
+    const OutCmd *src = slots;
+    if (status == int(kStatusOverflow)) {
+        const OutCmd &tag = slots[0];
+        if (!mc || tag.kp != kOvfTag || tag.to != r.n_commands || uint64_t(tag.from) + tag.to > novf)
+            return fail(MR_ERR_DEVICE, "overflow pool record");
+        src = &ovf[tag.from];
+        status = MR_OK;
+        r.status = MR_OK;
+    } else if (status == MR_OK && r.n_commands > mc) {
+        return fail(MR_ERR_DEVICE, "record longer than its command slots");
+    }
+    if (status != MR_OK) {
+        if (ret == MR_OK) ret = status;
+        return MR_OK;
+    }
+    if (off + r.n_commands <= pool_cap && pool) {
+        for (uint32_t j = 0; j < r.n_commands; ++j)
+            if (!expand_cmd(g, cs, src[j], pool[off + j])) return fail(MR_ERR_DEVICE, "command names no cell");
+    } else {
+        ret = MR_ERR_CAPACITY;
+    }
+    off += r.n_commands;
+    return MR_OK;
 }
 
 static int check_device_errors(mr_plan *pl, uint32_t &flags) {
@@ -1245,6 +1349,18 @@ static int check_device_errors(mr_plan *pl, uint32_t &flags) {
     if (int st = read_counters(pl, ctr)) return st;
     flags = ctr[kCtrFlags];
     if (flags) (void)hipMemset(pl->d_counter + kCtrFlags, 0, 4);  // collected
+    // overlap plans: the other slot's counter block belongs to the pass before the
+    // latest one; its flags and written count are checked (and collected) as well
+    if (pl->overlap && pl->runs >= 2) {
+        uint32_t alt[kCtrWords];
+        if (hipMemcpy(alt, pl->alt.counter, kCtrWords * 4, hipMemcpyDeviceToHost) != hipSuccess)
+            return fail(MR_ERR_DEVICE, "copy counter");
+        if (alt[kCtrFlags]) (void)hipMemset(pl->alt.counter + kCtrFlags, 0, 4);
+        flags |= alt[kCtrFlags];
+        if (flags == 0 && alt[kCtrLastWritten] != pl->hp.q_id.size())
+            return fail(MR_ERR_DEVICE, "internal: " + std::to_string(alt[kCtrLastWritten]) + " of " +
+                                           std::to_string(pl->hp.q_id.size()) + " records written (previous pass)");
+    }
 #ifdef MR_HUBDUMP
     if (pl->d_dbg) {
         std::vector<uint32_t> d(64 * 16);
@@ -1290,8 +1406,7 @@ static int check_device_errors(mr_plan *pl, uint32_t &flags) {
 // than max_cmds commands come back with status MR_ERR_CAPACITY in *over.
 static int plan_collect(mr_plan *pl, std::vector<OutResult> &res, std::vector<OutCmd> &cmd,
                         std::vector<OutCmd> &ovf) {
-    if (hipStreamSynchronize(pl->stream) != hipSuccess) return fail(MR_ERR_DEVICE, "sync");
-    if (hipDeviceSynchronize() != hipSuccess) return fail(MR_ERR_DEVICE, "device sync");
+    if (!plan_sync(pl)) return fail(MR_ERR_DEVICE, "sync");
     uint32_t flags = 0;
     int st = check_device_errors(pl, flags);
     if (st != MR_OK) return st;
@@ -1299,7 +1414,7 @@ static int plan_collect(mr_plan *pl, std::vector<OutResult> &res, std::vector<Ou
     if ((st = read_counters(pl, ctr))) return st;
     const uint32_t nov = std::min(ctr[kCtrLastOvf], pl->ka.ovf_cap);
     ovf.resize(nov);
-    if (nov && hipMemcpy(ovf.data(), pl->d_ovf, size_t(nov) * sizeof(OutCmd), hipMemcpyDeviceToHost) != hipSuccess)
+    if (nov && hipMemcpy(ovf.data(), pl->ka.ovf, size_t(nov) * sizeof(OutCmd), hipMemcpyDeviceToHost) != hipSuccess)
         return fail(MR_ERR_DEVICE, "copy overflow pool");
     const uint32_t n = pl->hp.nq, mc = pl->hp.p.max_cmds;
     res.resize(n);
@@ -1319,51 +1434,40 @@ extern "C" int mr_plan_fetch(mr_plan *pl, mr_result *results, mr_command *pool, 
     int st = plan_collect(pl, res, cmd, ovf);
     if (st != MR_OK) return st;
     const HostPlan &hp = pl->hp;
+    const CmdScale cs = cmd_scale(hp);
     const uint32_t mc = hp.p.max_cmds;
     uint64_t off = 0;
     int ret = MR_OK;
     for (uint32_t i = 0; i < hp.nq; ++i) {
         mr_result &r = results[i];
-        std::memset(&r, 0, sizeof(r));
         if (hp.q_status[i] != MR_OK) {
+            std::memset(&r, 0, sizeof(r));
             r.status = hp.q_status[i];
             if (ret == MR_OK) ret = hp.q_status[i];
             continue;
         }
         const uint32_t k = hp.q_pos[i];  // records are in grouped (by source) order
-        const OutResult &o = res[k];
-        int status = int(o.ncmd_status >> 16) - 16;
-        r.legs = o.legs;
-        r.money = o.money;
-        r.time_s = int64_t(o.time);
-        r.n_commands = o.ncmd_status & 0xFFFFu;
-        r.status = status;
-        r.command_offset = uint32_t(off);
-        if (status == MR_NOT_FOUND) {
-            r.n_commands = 0;
-            continue;
-        }
-        // a long label: its commands are in the overflow pool at {offset, count}
-        const OutCmd *src = mc ? &cmd[size_t(k) * mc] : nullptr;
-        if (status == int(kStatusOverflow)) {
-            const OutCmd &tag = cmd[size_t(k) * mc];
-            if (tag.kp != kOvfTag || tag.to != r.n_commands || uint64_t(tag.from) + tag.to > ovf.size())
-                return fail(MR_ERR_DEVICE, "overflow pool record");
-            src = &ovf[tag.from];
-            status = MR_OK;
-            r.status = MR_OK;
-        }
-        if (status != MR_OK) {
-            if (ret == MR_OK) ret = status;
-            continue;
-        }
-        if (off + r.n_commands <= pool_cap && pool) {
-            for (uint32_t j = 0; j < r.n_commands; ++j) expand_cmd(pl->grid, hp, src[j], pool[off + j]);
-        } else {
-            ret = MR_ERR_CAPACITY;
-        }
-        off += r.n_commands;
+        if ((st = decode_record(pl->grid, cs, res[k], mc ? &cmd[size_t(k) * mc] : nullptr, mc, ovf.data(), ovf.size(), r,
+                                pool, pool_cap, off, ret)))
+            return st;
     }
+    return ret;
+}
+
+extern "C" int mr_decode_records(const mr_grid *g, const mr_params *prm, const void *results, const void *commands,
+                                 uint32_t n, uint32_t max_cmds, const void *overflow, uint64_t overflow_n,
+                                 mr_result *out, mr_command *pool, uint64_t pool_cap) {
+    if (!g || !prm || (n && (!results || !out || (max_cmds && !commands))) || (overflow_n && !overflow))
+        return fail(MR_ERR_INVALID_ARG, "null argument");
+    const CmdScale cs = cmd_scale(*prm);
+    const OutResult *res = static_cast<const OutResult *>(results);
+    const OutCmd *cmd = static_cast<const OutCmd *>(commands), *ovf = static_cast<const OutCmd *>(overflow);
+    uint64_t off = 0;
+    int ret = MR_OK;
+    for (uint32_t k = 0; k < n; ++k)
+        if (int st = decode_record(g, cs, res[k], cmd ? cmd + size_t(k) * max_cmds : nullptr, max_cmds, ovf, overflow_n,
+                                   out[k], pool, pool_cap, off, ret))
+            return st;
     return ret;
 }
 
@@ -1389,7 +1493,7 @@ extern "C" void mr_plan_destroy(mr_plan *pl) {
     }
 #endif
     // passes may still be in flight on the caller's stream and the plan's hub stream
-    if (pl && pl->runs) (void)hipDeviceSynchronize();
+    if (pl) (void)plan_sync(pl);
     delete pl;
 }
 
@@ -1533,6 +1637,8 @@ extern "C" int mr_sssp_label(mr_plan *pl, uint32_t i, mr_cell_index dst, mr_resu
         res->status = MR_ERR_CAPACITY;
         return MR_ERR_CAPACITY;
     }
-    for (size_t j = 0; j < seq.size(); ++j) expand_cmd(g, pl->hp, seq[j], cmds[j]);
+    const CmdScale cs = cmd_scale(pl->hp);
+    for (size_t j = 0; j < seq.size(); ++j)
+        if (!expand_cmd(g, cs, seq[j], cmds[j])) return fail(MR_ERR_DEVICE, "command names no cell");
     return MR_OK;
 }

@@ -26,7 +26,7 @@ LIB_PATH = os.environ.get("MR_LIB_PATH") or os.path.join(os.path.dirname(os.path
 EXPORTED_SYMBOLS = [
     "mr_grid_create", "mr_grid_destroy", "mr_grid_square_size", "mr_params_default", "mr_find_path",
     "mr_find_path_batch", "mr_plan_create", "mr_plan_create_ex", "mr_plan_run", "mr_plan_fetch", "mr_plan_device_outputs",
-    "mr_plan_num_sources", "mr_plan_record_queries", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_plan_bind_outputs", "mr_abi_version", "mr_last_error",
+    "mr_plan_num_sources", "mr_plan_record_queries", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_plan_bind_outputs", "mr_plan_bind_outputs_ex", "mr_decode_records", "mr_abi_version", "mr_last_error",
     "mr_device_available", "mr_parse_map_html", "mr_parse_error", "mr_grid_from_html",
     "mr_command_time", "mr_duration_display", "mr_render_schedule",
     "mr_sssp_plan_create", "mr_sssp_records", "mr_sssp_device_records", "mr_sssp_label", "mr_plan_fill_ms",
@@ -76,6 +76,11 @@ def lib():
         L.mr_plan_create_ex.restype = C.c_int
         L.mr_plan_bind_outputs.argtypes = [vp, vp, vp]
         L.mr_plan_bind_outputs.restype = C.c_int
+        L.mr_plan_bind_outputs_ex.argtypes = [vp, vp, vp, vp, C.c_uint32]
+        L.mr_plan_bind_outputs_ex.restype = C.c_int
+        L.mr_decode_records.argtypes = [vp, C.POINTER(mr_params), vp, vp, C.c_uint32, C.c_uint32, vp, C.c_uint64,
+                                        C.POINTER(mr_result), C.POINTER(mr_command), C.c_uint64]
+        L.mr_decode_records.restype = C.c_int
         L.mr_plan_num_sources.argtypes = [vp]
         L.mr_plan_num_sources.restype = C.c_uint32
         L.mr_plan_record_queries.argtypes = [vp, C.POINTER(C.c_uint32), C.c_uint32]
@@ -280,6 +285,32 @@ class FindPath:
         return out
 
 
+def decode_records(grid: MapGrid, params: Params, results, commands, n: int, max_cmds: int,
+                   overflow=None) -> List[Optional[TotalCost]]:
+    """Compact device records (mr_plan_device_outputs layout: 16 B result records,
+    max_cmds 16 B command slots each, an overflow pool) as host buffers — e.g. the
+    rows another rank gathered — decoded into labels, record k -> entry k.  Host
+    only (mr_decode_records).  A record whose status is not OK / NOT_FOUND raises."""
+    import numpy as np
+    res = np.ascontiguousarray(results, dtype=np.uint32)
+    cmd = np.ascontiguousarray(commands, dtype=np.uint32)
+    ovf = np.ascontiguousarray(overflow if overflow is not None else np.zeros(0), dtype=np.uint32)
+    if res.size < 4 * n or cmd.size < 4 * n * max_cmds:
+        raise EngineError(abi.MR_ERR_INVALID_ARG, "decode_records: buffers shorter than n records")
+    out = (mr_result * max(n, 1))()
+    cap = int(n * max_cmds + ovf.size // 4 + 1)
+    pool = (mr_command * cap)()
+    p = params.to_c()
+    st = lib().mr_decode_records(grid.handle, C.byref(p), res.ctypes.data, cmd.ctypes.data, n, max_cmds,
+                                 ovf.ctypes.data if ovf.size else None, ovf.size // 4, out, pool, cap)
+    if st != MR_OK:
+        raise EngineError(st, last_error())
+    for k in range(n):
+        if out[k].status not in (MR_OK, MR_NOT_FOUND):
+            raise EngineError(out[k].status, f"record {k}")
+    return [result_from_c(out[k], pool) for k in range(n)]
+
+
 class Plan:
     """Device-resident batch: inputs uploaded once, `run()` enqueues one pass."""
 
@@ -340,8 +371,11 @@ class Plan:
             raise EngineError(st, last_error())
         return r.value, rb.value, c.value, cb.value
 
-    def bind_outputs(self, d_results: int, d_commands: int) -> None:
-        st = lib().mr_plan_bind_outputs(self.handle, C.c_void_p(d_results), C.c_void_p(d_commands))
+    def bind_outputs(self, d_results: int, d_commands: int, d_overflow: int = 0, overflow_cap: int = 0) -> None:
+        """Caller device buffers for the compact outputs (and, with d_overflow, the
+        overflow pool of overflow_cap commands): one collective then moves them all."""
+        st = lib().mr_plan_bind_outputs_ex(self.handle, C.c_void_p(d_results), C.c_void_p(d_commands),
+                                           C.c_void_p(d_overflow) if d_overflow else None, overflow_cap)
         if st != MR_OK:
             raise EngineError(st, last_error())
 

@@ -46,7 +46,7 @@ def test_library_exports_every_declared_symbol(eng):
 
 def test_abi_version_and_defaults(eng):
     L = eng.lib()
-    assert L.mr_abi_version() == 2
+    assert L.mr_abi_version() == 3
     p = abi.mr_params()
     L.mr_params_default(C.byref(p))
     d = Params().to_c()
@@ -106,3 +106,45 @@ def test_html_writer_schema():
     html = to_html(m)
     assert html.count('class="map-cell"') == 25
     assert '<div class="top-right-text">0#0</div>' in html
+
+
+def _ranks(m):
+    """CellIndex -> rank (position in the derived Ord, src/index.rs:41-46)."""
+    cells = sorted(m.all_indices(), key=lambda c: (c.kind, c.sub, c.x, c.y))
+    return {c: i for i, c in enumerate(cells)}
+
+
+def test_decode_records_on_host(eng):
+    """mr_decode_records: compact records as another rank gathers them (result
+    record, command slots, overflow pool) decode to full labels without a device."""
+    import numpy as np
+    from marshrutka_amd.abi import GREEN, Command, TotalCost
+    m = SyntheticMap(7, campfires_per_homeland=1, seed=4)
+    g = eng.MapGrid(m.cells())
+    rk = _ranks(m)
+    b33, c, g33 = CellIndex.homeland(BLUE, 3, 3), CellIndex.center(), CellIndex.homeland(GREEN, 3, 3)
+    car = lambda d, five: (3 << 29) | (d << 1) | five  # noqa: E731  Caravan payload: d << 1 | coef==5
+    # SURVEY 8c KAT7: (0, 42, 2880, [Caravan{1440,12} B3#3->0#0, Caravan{1440,30} 0#0->G3#3])
+    want = TotalCost(0, 42, 2880, [Command(3, 1440, 0, 12, 0, b33, c), Command(3, 1440, 0, 30, 0, c, g33)])
+    cmds = [[car(6, 0), rk[b33], rk[c], 0], [car(6, 1), rk[c], rk[g33], 0]]
+    p = Params(route_guru=0)
+    # three records, max_cmds 2: the label in its slots, a NOT_FOUND record, the label
+    # again but tagged into the overflow pool at offset 3
+    res = np.array([[0, 42, 2880, (16 << 16) | 2], [0, 0, 0, 17 << 16], [0, 42, 2880, ((16 + 64) << 16) | 2]],
+                   dtype=np.uint32)
+    slots = np.zeros((3, 2, 4), dtype=np.uint32)
+    slots[0] = cmds
+    slots[2, 0] = [0xFFFFFFFF, 3, 2, 0]
+    pool = np.zeros((5, 4), dtype=np.uint32)
+    pool[3:5] = cmds
+    out = eng.decode_records(g, p, res, slots, 3, 2, pool)
+    assert out[0].as_tuple() == want.as_tuple()
+    assert out[1] is None
+    assert out[2].as_tuple() == want.as_tuple()
+    # a tag that points past the pool, and a command naming no cell, are errors
+    with pytest.raises(eng.EngineError, match="DEVICE"):
+        eng.decode_records(g, p, res, slots, 3, 2, pool[:4])
+    bad = slots.copy()
+    bad[0, 1, 2] = 49
+    with pytest.raises(eng.EngineError, match="DEVICE"):
+        eng.decode_records(g, p, res, bad, 3, 2, pool)

@@ -204,3 +204,26 @@ def test_overlapped_passes_match_serial(eng, oracle_lib, monkeypatch, fb):
             assert (plan.records(i) == want[i]).all(), (passes, i)
             for d in dsts[:4]:
                 assert as_expected(plan.label(i, d)) == as_expected(ref.label(i, d)), (passes, i, d)
+
+
+@pytest.mark.parametrize("inject_slot,passes", [(0, 2), (1, 3), (0, 4)])
+def test_overlap_error_of_either_slot_is_reported(eng, monkeypatch, inject_slot, passes):
+    """A device error flag raised by a pass whose slot is not the current one (the
+    other overlap slot) must still be reported, then collected."""
+    for k in ("MR_ALGO", "MR_FILL_GX", "MR_DBG_FLAGS", "MR_HUB_FALLBACK_ALL", "MR_FILL_OVERLAP"):
+        monkeypatch.delenv(k, raising=False)
+    m = SyntheticMap(33, campfires_per_homeland=3, seed=5)
+    sources = m.all_indices()[:4]
+    g = eng.MapGrid(m.cells())
+    monkeypatch.setenv("MR_DBG_INJECT_SLOT", str(inject_slot))
+    plan = eng.SSSPPlan(g, Params(), sources)
+    monkeypatch.delenv("MR_DBG_INJECT_SLOT")
+    # pass p (1-based) runs in slot (p - 1) % 2; after `passes` passes the current slot
+    # is (passes - 1) % 2, and the injected slot's last pass is the other one
+    assert (passes - 1) % 2 != inject_slot
+    for _ in range(passes):
+        plan.run()
+    with pytest.raises(eng.EngineError):
+        plan.records(0)
+    # collected: both slots' flags were cleared by the report
+    plan.records(0)
