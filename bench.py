@@ -361,13 +361,14 @@ def main():
     if all_dst:
         # V x 20 B per solve (the 4 B per-cell word read, the 16 B record written),
         # over the dominant kernel: the fill launch (hub plans) or the whole SSSP pass.  The
-        # fill kernel reads no per-cell word (the specials come from the source's table), so
-        # its own bytes are the 16 B record per cell plus the table: per entry the 44 B label,
-        # its 4 B rank and the special's 32 B static record
+        # fill kernel reads no per-cell word (the specials come from the source's table) and
+        # writes one 4 B cell word per cell (the label's walk over the source's table), so
+        # its own bytes are V x 4 B plus the table: per entry the 44 B label, its 4 B rank
+        # and the special's 32 B static record
         alg_bytes = survey_bytes = float(n_src) * V * BYTES_PER_VERTEX_SOLVE
         fms = plan.fill_ms()
         if stats["solver"] == "hub" and fms > 0:
-            alg_bytes = float(n_src) * (V * 16 + (stats["num_specials"] + 1) * 80)
+            alg_bytes = float(n_src) * (V * 4 + (stats["num_specials"] + 1) * 80)
             kernel_name, pass_ms, kms = "fill_kernel", kms, fms
         else:
             kernel_name, pass_ms = "sssp_kernel", kms
@@ -418,7 +419,7 @@ def main():
                      "pass_ms": pass_ms if all_dst else kms,
                      "alg_bytes_per_launch": alg_bytes,
                      "survey_8d_bytes_per_launch": survey_bytes,
-                     "note": ("all destinations: fill kernel, V x 16 B per source (the record written; no per-cell "
+                     "note": ("all destinations: fill kernel, V x 4 B per source (the cell word written; no per-cell "
                               "read) + 80 B per table entry; survey_8d_bytes_per_launch is SURVEY 8d's V x 20 B; "
                               "kernel_ms spans the fill's two launches; pass_ms is the caller-stream span of a pass (the specials' "
                               "solve runs beside the previous pass's fill, DESIGN.md 3b)" if all_dst else

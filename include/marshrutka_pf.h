@@ -259,13 +259,15 @@ double mr_plan_kernel_ms(mr_plan *plan, uint32_t *n_launches);
 void mr_plan_destroy(mr_plan *plan);
 
 /* ---- all destinations (single source -> every cell) ------- */
-/* One record per (source, cell): the label's metrics and how to rebuild it. */
+/* One record per (source, cell): the label's metrics and how to rebuild it
+ * (mr_sssp_records expands them on the host from the device's cell words). */
 typedef struct mr_label_record {
     uint32_t legs, money, time_s;
-    uint32_t via; /* internal: boundary / special table entry; 0xFFFFFFFF = the source */
+    uint32_t via; /* boundary table entry of the final walk; 0x80000000 | t = special t's own
+                     label; 0xFFFFFFFF = the source */
 } mr_label_record;
 /* A plan answering every destination of each source: mr_plan_run computes
- * n_sources x V records on the device; mr_plan_kernel_ms / mr_plan_get_stats /
+ * n_sources x V cell words on the device; mr_plan_kernel_ms / mr_plan_get_stats /
  * mr_plan_destroy apply.  Sources may repeat (they share a solve).  Each pass's
  * specials' solve runs on a stream of the plan's own, beside the previous pass's
  * fill, into one of two internal table slots (MR_FILL_OVERLAP=0: one slot, all on
@@ -278,8 +280,18 @@ int mr_sssp_plan_create(const mr_grid *grid, const mr_params *params, const mr_c
 double mr_plan_fill_ms(const mr_plan *plan);
 /* The V records of the caller's source i, in row-major cell order (waits for the plan). */
 int mr_sssp_records(mr_plan *plan, uint32_t i, mr_label_record *out);
-/* Device pointer to all records ([plan source][cell], 16 B each) and their size. */
+/* Device pointer to all cell words ([plan source][cell], 4 B each, row-major cells)
+ * and their size.  A cell word carries the whole label over its source's table:
+ *   b << 20 | k     the walk of k legs from boundary table entry b (0 = the source):
+ *                   metrics = entry b's + (k, 0, Fleetfoot-ceil(180 k)), commands =
+ *                   entry b's chain ++ [StandardMove{k} b -> cell]
+ *   0x80000000 | t  special t's own table label;  0xFFFFFFFF  the source
+ * Plan sources are the caller's distinct sources in row-major cell order. */
 int mr_sssp_device_records(mr_plan *plan, void **d_records, uint64_t *bytes);
+/* Device pointer to the label tables ([plan source][NS + 1 entries], 44 B each:
+ * u32 legs, money, time; u16 length; u8 tail count; u8 state; u16 parent entry;
+ * u16 pad; 2 x {u32 kind << 29 | payload, from rank, to rank}) and their size. */
+int mr_sssp_device_tables(mr_plan *plan, void **d_tables, uint64_t *bytes);
 /* The full label (FindPath::eval(sources[i], dst)) rebuilt from its record:
  * MR_OK, MR_ERR_CAPACITY (out->n_commands > cap) or an error. */
 int mr_sssp_label(mr_plan *plan, uint32_t i, mr_cell_index dst, mr_result *out, mr_command *cmds, uint32_t cap);

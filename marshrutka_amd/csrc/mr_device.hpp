@@ -799,7 +799,8 @@ struct Core {
         const uint32_t q0 = a->q_begin[s_idx], q1 = a->q_begin[s_idx + 1];
         for (uint32_t i = q0 + threadIdx.x; i < q1; i += kBS) write_output(a->q_dst[i], i);
     }
-    // all-destinations mode: the label table and a record for every cell (VRecord)
+    // all-destinations mode: the label table and a cell word for every cell (CellWord:
+    // the settled state word's walk (b, k) as it stands)
     __device__ __forceinline__ void write_all(uint32_t s_idx) const {
         const DevParams &p = P;
         const unsigned long long tb = (unsigned long long)s_idx * (p.NS + 1);
@@ -807,19 +808,16 @@ struct Core {
             a->out_tab[tb + t] = R[t];
             a->out_lex[tb + t] = kNone32;
         }
-        VRecord *out = a->out_rec + (unsigned long long)s_idx * p.V;
+        CellWord *out = a->out_rec + (unsigned long long)s_idx * p.V;
         for (uint32_t v = threadIdx.x; v < p.V; v += kBS) {
-            VRecord r{0, 0, 0, kViaSource};
+            CellWord r = kViaSource;
             const uint32_t sw = ld_state(v);
             const uint32_t t = special_of(v);
             if (v == src) {
             } else if (t != kNone10) {
-                r = VRecord{R[t].m[0], R[t].m[1], R[t].m[2], kViaSpecial | t};
+                r = kViaSpecial | t;
             } else if (sw & kStSettled) {
-                View x;
-                const uint32_t b = (sw >> kStBShift) & kNone10;
-                view_walk(b, sw & kStKMask, 0, x);
-                r = VRecord{x.m0, x.m1, x.m2, b};
+                r = sw & ((kNone10 << kStBShift) | kStKMask);
             } else {
                 flag(kErrBucket);  // every cell of the connected grid settles
             }
@@ -2627,7 +2625,6 @@ __global__ __launch_bounds__(kBS) void hub_wide_kernel(const KArgs *__restrict__
 // Otherwise the cell's walk distance and the three-metric compare are evaluated in
 // full.  The specials of the tile and the source then overwrite their cells.
 // =====================================================================================
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t bit_width64(unsigned long long x) { return x ? 64u - uint32_t(__clzll(x)) : 0u; }
 
 // the fill kernel's rare path: a tile whose source's metrics do not fit one key.  Row
@@ -2636,7 +2633,7 @@ __device__ __forceinline__ uint32_t bit_width64(unsigned long long x) { return x
 // fast path's occupancy.
 template <uint32_t PERM>
 __device__ __forceinline__ void fill_tile_rows(const uint32_t (*B)[64], unsigned long long live, int wx,
-                                                      int y0, int ty0, int cx, bool col_ok, uint32_t S, VRecord *outs) {
+                                                      int y0, int ty0, int cx, bool col_ok, uint32_t S, CellWord *outs) {
     constexpr uint32_t q0 = PERM / 9, q1 = (PERM / 3) % 3, q2 = PERM % 3;
 #pragma unroll 1
     for (int i = 0; i < int(kFillTH); ++i) {
@@ -2658,8 +2655,9 @@ __device__ __forceinline__ void fill_tile_rows(const uint32_t (*B)[64], unsigned
             r2 = better ? mm2 : r2;
             rv = better ? B[5][rr] : rv;
         }
+        // the cell word b << 20 | k: B[5] holds (b << 20) - legs(b), r0 = legs(b) + k
         const int cy = ty0 + i;
-        if (col_ok && cy < int(S)) outs[uint32_t(cy) * S + uint32_t(cx)] = VRecord{r0, r1, r2, rv};
+        if (col_ok && cy < int(S)) outs[uint32_t(cy) * S + uint32_t(cx)] = rv + r0;
     }
 }
 
@@ -2673,9 +2671,9 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
     constexpr uint32_t sl[3] = {1u, 0u, 180u};
     constexpr uint64_t slope1 = sl[q0];
     constexpr int kTW = int(kFillTW), kTH = int(kFillTH), kCPL = kTW / 64;  // kCPL columns per lane
-    // per wave: boundaries by rank (x, y, m0, m1, m2, table index, key lo, key hi),
-    // specials by table index (x, y, m0, m1, m2 of their own labels; entry 0 = source)
-    __shared__ uint32_t btab[kBS / 64][13][64];
+    // per wave: boundaries by rank (x, y, m0, m1, m2, cell-word base (b << 20) - legs(b),
+    // key lo, key hi), specials by table index (x, y; entry 0 = source)
+    __shared__ uint32_t btab[kBS / 64][10][64];
     // the wave index through readfirstlane: everything derived from it (tile origins,
     // key fields, slopes) then lives in SGPRs
     const uint32_t lane = threadIdx.x & 63u, wv = uint32_t(__builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)));
@@ -2709,16 +2707,13 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
             const uint32_t y = lane == 0 ? uint32_t(int(src / S) - H) : uint32_t(a->sp[lane].y);
             P[0][lane] = x;
             P[1][lane] = y;
-            P[2][lane] = lane == 0 ? 0u : e0;
-            P[3][lane] = lane == 0 ? 0u : e1;
-            P[4][lane] = lane == 0 ? 0u : e2;
             if (r != kNone32) {
                 B[0][r] = x;
                 B[1][r] = y;
                 B[2][r] = e0;
                 B[3][r] = e1;
                 B[4][r] = e2;
-                B[5][r] = lane;
+                B[5][r] = (lane << kStBShift) - e0;  // + the cell's legs = b << 20 | k
             }
         }
         const bool isb = lane < T && r != kNone32;
@@ -2759,7 +2754,7 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
         }
         wave_sync();
         // ---- this wave's tiles of the source ---------------------------------------
-        VRecord *const outs = a->out_rec + (unsigned long long)s * V;
+        CellWord *const outs = a->out_rec + (unsigned long long)s * V;
         for (uint32_t tile = j; tile < ntile; tile += G) {
             const int tx0 = int(tile % tpx) * kTW, ty0 = int(tile / tpx) * kTH;
             const int x0 = tx0 - H, y0 = ty0 - H;
@@ -2852,25 +2847,23 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
                     }
                 }
                 // buffer stores off one per-tile base: the lane's offset in a VGPR, the
-                // row's (i * S * 16 B) in an SGPR, so no per-row 64-bit address; a row's
-                // kCPL stores are one contiguous run of kTW records
+                // row's (i * S * 4 B) in an SGPR, so no per-row 64-bit address; a row's
+                // kCPL stores are one contiguous run of kTW cell words
                 const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-                    outs + (size_t(ty0) * S + size_t(tx0)), 0, int(16u * kTH * S), 0x00020000);  // the tile's rows
+                    outs + (size_t(ty0) * S + size_t(tx0)), 0, int(4u * kTH * S), 0x00020000);  // the tile's rows
 #pragma unroll
                 for (int i = 0; i < kTH; ++i) {
 #pragma unroll
                     for (int k = 0; k < kCPL; ++k) {
                         const int cx = tx0 + 64 * k + int(lane), cy = ty0 + i;
                         if (cx < int(S) && cy < int(S)) {
-                            // c[.] is metric q_.; the rank's table index from the wave's table
+                            // the cell word: the rank's base (b << 20) - legs(b) plus the
+                            // key's legs field, legs(b) + k
                             const unsigned long long kv = kb[k * kTH + i];
-                            const uint32_t c[3] = {uint32_t(kv >> sh1), uint32_t((kv >> sh2) & mask2),
-                                                   uint32_t((kv >> sh3) & mask3)};
-                            const u32x4_t rec = {q0 == 0 ? c[0] : (q1 == 0 ? c[1] : c[2]),
-                                                 q0 == 1 ? c[0] : (q1 == 1 ? c[1] : c[2]),
-                                                 q0 == 2 ? c[0] : (q1 == 2 ? c[1] : c[2]), B[5][uint32_t(kv & maskr)]};
-                            __builtin_amdgcn_raw_buffer_store_b128(rec, rsrc, int((64u * k + lane) * 16u),
-                                                                   int(uint32_t(i) * S * 16u), 0);
+                            const uint32_t legs = q0 == 0 ? uint32_t(kv >> sh1)
+                                                          : (q1 == 0 ? uint32_t((kv >> sh2) & mask2) : uint32_t((kv >> sh3) & mask3));
+                            __builtin_amdgcn_raw_buffer_store_b32(B[5][uint32_t(kv & maskr)] + legs, rsrc,
+                                                                  int((64u * k + lane) * 4u), int(uint32_t(i) * S * 4u), 0);
                         }
                     }
                 }
@@ -2894,8 +2887,7 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
                 }
                 const int px = int(P[0][t]) - x0, py = int(P[1][t]) - y0;
                 if (lane == uint32_t(px) % 64u)
-                    outs[uint32_t(ty0 + py) * S + uint32_t(tx0 + px)] =
-                        VRecord{P[2][t], P[3][t], P[4][t], t == 0 ? kViaSource : (kViaSpecial | t)};
+                    outs[uint32_t(ty0 + py) * S + uint32_t(tx0 + px)] = t == 0 ? kViaSource : (kViaSpecial | t);
             }
         }
     }

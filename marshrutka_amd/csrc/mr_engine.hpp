@@ -93,13 +93,16 @@ struct OutResult {
 struct OutCmd {
     uint32_t kp, from, to, pad;
 };
-// all-destinations output: one record per source and cell.  via =
-// the table index b of the boundary whose walk ends here (the label is the table
-// chain of b ++ [StandardMove{d_b(v)} b -> v]), kViaSpecial | t for special t (its
-// own table label), kViaSource for the source (the start label).
-struct VRecord {
-    uint32_t m0, m1, m2, via;
-};
+// all-destinations output: one 32-bit cell word per source and cell,
+// the label's walk in the grid-state layout above:
+//   b << kStBShift | k   the walk of k legs from boundary b (table index; 0 = the
+//                        source): commands = table chain of b ++ [StandardMove{k}
+//                        b -> v], metrics = the table label's + (k, 0, run_time(k))
+//   kViaSpecial | t      special t: its own table label
+//   kViaSource           the source: the start label
+// The metrics are the table's plus the walk's, so 4 B per cell carry the whole label
+// (mr_sssp_records expands them on the host).
+typedef uint32_t CellWord;
 constexpr uint32_t kViaSpecial = 0x80000000u, kViaSource = 0xFFFFFFFFu;
 // all-destinations fill tiles: one wave per kFillTW x kFillTH cells, MR_FILL_CPL
 // columns per lane (64 apart), MR_FILL_CELLS cells per lane
@@ -144,7 +147,7 @@ struct KArgs {
     // all-destinations mode: no per-query outputs; per source, a record per cell, the
     // label table (NS+1 entries), the boundaries' lexicographic ranks and how it was solved
     uint32_t all_mode;
-    VRecord *out_rec;            // nsrc * V
+    CellWord *out_rec;           // nsrc * V cell words
     Rec *out_tab;                // nsrc * (NS+1)
     uint32_t *out_lex;           // nsrc * (NS+1): rank of boundary t by (length, command list), else kNone32
     uint32_t *src_state;         // nsrc: 1 hub solved (records by the fill kernel), 2 SSSP kernel

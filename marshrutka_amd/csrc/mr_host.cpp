@@ -715,7 +715,7 @@ struct mr_plan {
     KArgs *d_args_fill = nullptr;         // all-destinations mode: the fill launch
     KArgs *d_args_fill2 = nullptr;        // ... and its wide-metric second launch (ends the pass)
     bool all_mode = false;
-    VRecord *d_rec = nullptr;             // all-destinations outputs (KArgs::out_rec ...)
+    CellWord *d_rec = nullptr;            // all-destinations outputs (KArgs::out_rec ...)
     Rec *d_tab = nullptr;
     uint32_t *d_lex = nullptr, *d_sstate = nullptr;
     std::vector<uint32_t> src_of_input;   // caller's source i -> plan source index
@@ -928,7 +928,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     pl->all_mode = all_mode;
     if (all_mode) {  // per source: a record per cell, the label table, the boundary ranks
         const size_t T = size_t(NS) + 1;
-        if (hipMalloc(reinterpret_cast<void **>(&pl->d_rec), std::max<size_t>(nsrc, 1) * V * sizeof(VRecord)) != hipSuccess ||
+        if (hipMalloc(reinterpret_cast<void **>(&pl->d_rec), std::max<size_t>(nsrc, 1) * V * sizeof(CellWord)) != hipSuccess ||
             hipMalloc(reinterpret_cast<void **>(&pl->d_tab), std::max<size_t>(nsrc, 1) * T * sizeof(Rec)) != hipSuccess ||
             hipMalloc(reinterpret_cast<void **>(&pl->d_lex), std::max<size_t>(nsrc, 1) * T * 4) != hipSuccess ||
             hipMalloc(reinterpret_cast<void **>(&pl->d_sstate), std::max<size_t>(nsrc, 1) * 4) != hipSuccess)
@@ -1567,21 +1567,64 @@ static int sssp_source(mr_plan *pl, uint32_t i, uint32_t &si) {
     return check_device_errors(pl, flags);
 }
 
+// The source's label table (NS + 1 entries) as the last pass exported it.
+static int sssp_table(mr_plan *pl, uint32_t si, std::vector<Rec> &tab) {
+    const uint32_t T = pl->ka.p.NS + 1;
+    tab.resize(T);
+    if (hipMemcpy(tab.data(), pl->d_tab + size_t(si) * T, T * sizeof(Rec), hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(MR_ERR_DEVICE, "copy label table");
+    return MR_OK;
+}
+
+// A cell word (CellWord, mr_engine.hpp) over its source's table: the label's metrics
+// (the table label's plus the final walk's) and `via`.  False if it names no entry.
+static bool expand_word(const HostPlan &hp, const std::vector<Rec> &tab, CellWord w, mr_label_record &o) {
+    const uint32_t T = uint32_t(tab.size());
+    if (w == kViaSource) {
+        o = mr_label_record{0, 0, 0, kViaSource};
+        return true;
+    }
+    if (w & kViaSpecial) {
+        const uint32_t t = w & kNone10;
+        if (t >= T || (w & ~(kViaSpecial | kNone10))) return false;
+        o = mr_label_record{tab[t].m[0], tab[t].m[1], tab[t].m[2], w};
+        return true;
+    }
+    const uint32_t b = w >> kStBShift, k = w & kStKMask;
+    if (b >= T) return false;
+    // AggregatedCost::time of the walk's run (src/cost.rs:122-124): Fleetfoot's ceil
+    const uint64_t t = (uint64_t(180) * k * hp.p.ff_num + hp.p.ff_den - 1) / hp.p.ff_den;
+    o = mr_label_record{tab[b].m[0] + k, tab[b].m[1], uint32_t(tab[b].m[2] + t), b};
+    return true;
+}
+
 extern "C" int mr_sssp_records(mr_plan *pl, uint32_t i, mr_label_record *out) {
     uint32_t si = 0;
     if (int st = sssp_source(pl, i, si)) return st;
     if (!out) return fail(MR_ERR_INVALID_ARG, "null output");
-    static_assert(sizeof(mr_label_record) == sizeof(VRecord), "record layout");
-    if (hipMemcpy(out, pl->d_rec + size_t(si) * pl->ka.p.V, size_t(pl->ka.p.V) * sizeof(VRecord),
-                  hipMemcpyDeviceToHost) != hipSuccess)
+    const uint32_t V = pl->ka.p.V;
+    std::vector<CellWord> words(V);
+    std::vector<Rec> tab;
+    if (hipMemcpy(words.data(), pl->d_rec + size_t(si) * V, size_t(V) * sizeof(CellWord), hipMemcpyDeviceToHost) !=
+        hipSuccess)
         return fail(MR_ERR_DEVICE, "copy records");
+    if (int st = sssp_table(pl, si, tab)) return st;
+    for (uint32_t v = 0; v < V; ++v)
+        if (!expand_word(pl->hp, tab, words[v], out[v])) return fail(MR_ERR_DEVICE, "cell word names no table entry");
     return MR_OK;
 }
 
 extern "C" int mr_sssp_device_records(mr_plan *pl, void **d_records, uint64_t *bytes) {
     if (!pl || !pl->all_mode) return fail(MR_ERR_INVALID_ARG, "not an all-destinations plan");
     if (d_records) *d_records = pl->d_rec;
-    if (bytes) *bytes = uint64_t(pl->ka.nsrc) * pl->ka.p.V * sizeof(VRecord);
+    if (bytes) *bytes = uint64_t(pl->ka.nsrc) * pl->ka.p.V * sizeof(CellWord);
+    return MR_OK;
+}
+
+extern "C" int mr_sssp_device_tables(mr_plan *pl, void **d_tables, uint64_t *bytes) {
+    if (!pl || !pl->all_mode) return fail(MR_ERR_INVALID_ARG, "not an all-destinations plan");
+    if (d_tables) *d_tables = pl->d_tab;
+    if (bytes) *bytes = uint64_t(pl->ka.nsrc) * (pl->ka.p.NS + 1) * sizeof(Rec);
     return MR_OK;
 }
 
@@ -1596,11 +1639,13 @@ extern "C" int mr_sssp_label(mr_plan *pl, uint32_t i, mr_cell_index dst, mr_resu
     uint32_t w;
     if (!g->find(dst, w)) return fail(MR_ERR_INVALID_INDEX, "destination is not a grid cell");
     const uint32_t T = pl->ka.p.NS + 1;
-    VRecord rec;
-    std::vector<Rec> tab(T);
-    if (hipMemcpy(&rec, pl->d_rec + size_t(si) * pl->ka.p.V + w, sizeof(rec), hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(tab.data(), pl->d_tab + size_t(si) * T, T * sizeof(Rec), hipMemcpyDeviceToHost) != hipSuccess)
+    CellWord word;
+    std::vector<Rec> tab;
+    if (hipMemcpy(&word, pl->d_rec + size_t(si) * pl->ka.p.V + w, sizeof(word), hipMemcpyDeviceToHost) != hipSuccess)
         return fail(MR_ERR_DEVICE, "copy label");
+    if (int st = sssp_table(pl, si, tab)) return st;
+    mr_label_record rec;
+    if (!expand_word(pl->hp, tab, word, rec)) return fail(MR_ERR_DEVICE, "cell word names no table entry");
     const uint32_t src = pl->hp.src_v[si];
     std::vector<OutCmd> seq;
     auto chain = [&](uint32_t t) {  // commands of table label t (parent 0 ends the chain)
@@ -1626,12 +1671,13 @@ extern "C" int mr_sssp_label(mr_plan *pl, uint32_t i, mr_cell_index dst, mr_resu
         if ((ay == 0 && by == 0 && ax != 0 && bx != 0 && ((ax < 0) != (bx < 0))) ||
             (ax == 0 && bx == 0 && ay != 0 && by != 0 && ((ay < 0) != (by < 0))))
             k += 2;  // the walk goes round the Center
+        if (k != (word & kStKMask)) return fail(MR_ERR_DEVICE, "cell word's walk is not the boundary's distance");
         seq.push_back(OutCmd{(kStandard << 29) | k, g->rank[vb], g->rank[w], 0});
     }
     std::memset(res, 0, sizeof(*res));
-    res->legs = rec.m0;
-    res->money = rec.m1;
-    res->time_s = int64_t(rec.m2);
+    res->legs = rec.legs;
+    res->money = rec.money;
+    res->time_s = int64_t(rec.time_s);
     res->n_commands = uint32_t(seq.size());
     if (seq.size() > cap || (!cmds && !seq.empty())) {
         res->status = MR_ERR_CAPACITY;
