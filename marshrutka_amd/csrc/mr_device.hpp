@@ -2718,39 +2718,60 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
         }
         const bool isb = lane < T && r != kNone32;
         const uint32_t nb = uint32_t(__popcll(__ballot(isb)));
-        // key fields: each metric's maximum over every walk (distance <= 2S + 2)
-        const uint64_t dmax = 2ull * S + 2;
+        const uint64_t dmax = 2ull * S + 2;  // the longest walk (round the Center)
         const uint64_t em[3] = {e0, e1, e2};
-        uint64_t mx1 = isb ? em[q0] + sl[q0] * dmax : 0, mx2 = isb ? em[q1] + sl[q1] * dmax : 0,
-                 mx3 = isb ? em[q2] + sl[q2] * dmax : 0;
+        // The lead metric: the first in comparator order that grows along a walk.  With
+        // Money first every walk keeps its boundary's money, so only the boundaries of
+        // the least money can win anywhere ("kept"); the lead is then the second metric.
+        // Where two walks tie on the lead, their distances differ by a fixed amount, so
+        // every metric after it compares as a per-boundary constant c_q = sL * base_q -
+        // s_q * base_L, then the boundary's rank: (c, rank) order the tied walks exactly
+        // like the comparator.  A walk's key is therefore lead << rbs | srank, srank the
+        // boundary's position in that constant order: 32 bits, one add and one min per
+        // cell and boundary.
+        constexpr uint32_t L = q0 == 1 ? q1 : q0, T1 = q0 == 1 ? q2 : q1, T2 = q0 == 1 ? 3u : q2;
+        constexpr uint32_t sL = sl[L];
+        bool kept = isb;
+        if (q0 == 1) {
+            uint32_t mmin = isb ? e1 : 0xFFFFFFFFu;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            mx1 = max(mx1, (uint64_t)__shfl_xor((unsigned long long)mx1, o));
-            mx2 = max(mx2, (uint64_t)__shfl_xor((unsigned long long)mx2, o));
-            mx3 = max(mx3, (uint64_t)__shfl_xor((unsigned long long)mx3, o));
+            for (int o = 32; o > 0; o >>= 1) mmin = min(mmin, uint32_t(__shfl_xor(int(mmin), o)));
+            kept = isb && e1 == mmin;
         }
-        const uint32_t w1 = uint32_t(__builtin_amdgcn_readfirstlane(int(max(1u, bit_width64(mx1)))));
-        const uint32_t w2 = uint32_t(__builtin_amdgcn_readfirstlane(int(max(1u, bit_width64(mx2)))));
-        const uint32_t w3 = uint32_t(__builtin_amdgcn_readfirstlane(int(max(1u, bit_width64(mx3)))));
-        // the boundary's rank rides in the key's low rb bits: (key, rank) pairs order
-        // walks exactly like the comparator, and one 64-bit compare picks the pair
-        const uint32_t rb = max(1u, bit_width64(nb - 1));
-        const bool packable = !no_pack && w1 + w2 + w3 + rb <= 63u;
-        // the first launch (WIDE = false) fills the sources whose metrics fit one key and
+        const unsigned long long keptm = __ballot(kept);
+        const uint32_t nk = uint32_t(__popcll(keptm));
+        // the kept boundaries below this one in (c_T1, c_T2, rank) order (every lane takes
+        // part in the shuffles)
+        uint32_t srank = 0;
+        const long long c1 = (long long)sL * (long long)em[T1] - (long long)sl[T1] * (long long)em[L];
+        const long long c2 = T2 < 3u ? (long long)sL * (long long)em[T2 % 3u] - (long long)sl[T2 % 3u] * (long long)em[L] : 0;
+        for (unsigned long long m = keptm; m; m &= m - 1) {
+            const int o = __ffsll((long long)m) - 1;  // table index of a kept boundary
+            const uint32_t ro = uint32_t(__shfl(int(r), o));
+            const long long o1 = __shfl(c1, o), o2 = __shfl(c2, o);
+            srank += (o1 < c1 || (o1 == c1 && (o2 < c2 || (o2 == c2 && ro < r)))) ? 1u : 0u;
+        }
+        uint64_t mxL = kept ? em[L] + sL * dmax : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mxL = max(mxL, (uint64_t)__shfl_xor((unsigned long long)mxL, o));
+        const uint32_t rbs = max(1u, bit_width64(nk - 1));
+        const uint32_t wL = uint32_t(__builtin_amdgcn_readfirstlane(int(max(1u, bit_width64(mxL)))));
+        const bool packable = !no_pack && wL + rbs <= 32u;
+        // the first launch (WIDE = false) fills the sources whose keys fit 32 bits and
         // counts the others, which the second launch fills
         if (packable == WIDE) {
             if (!WIDE && j == 0 && lane == 0) atomicAdd(a->counter + kCtrFillWide, 1u);
             continue;
         }
-        const uint32_t sh3 = rb, sh2 = w3 + rb, sh1 = w2 + w3 + rb;
-        const unsigned long long slope = packable ? ((unsigned long long)sl[q0] << sh1) +
-                                                        ((unsigned long long)sl[q1] << sh2) + ((unsigned long long)sl[q2] << sh3)
-                                                  : 0ull;
-        if (isb && packable) {
-            const unsigned long long K = ((unsigned long long)em[q0] << sh1) | ((unsigned long long)em[q1] << sh2) |
-                                         ((unsigned long long)em[q2] << sh3) | r;
-            B[6][r] = uint32_t(K);
-            B[7][r] = uint32_t(K >> 32);
+        const uint32_t stepL = packable ? sL << rbs : 0u, maskr = (1u << rbs) - 1u;
+        if (packable) {
+            if (isb) B[6][r] = kept ? uint32_t(em[L] << rbs) | srank : 0xFFFFFFFFu;  // by rank
+            if (kept) {  // by srank: the cell word's table index and the lead's base
+                B[5][srank] = lane << kStBShift;
+                B[7][srank] = uint32_t(em[L]);
+            }
+        } else if (isb) {
+            B[5][r] = (lane << kStBShift) - e0;  // full compare (fill_tile_rows): + the cell's legs
         }
         wave_sync();
         // ---- this wave's tiles of the source ---------------------------------------
@@ -2759,25 +2780,30 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
             const int tx0 = int(tile % tpx) * kTW, ty0 = int(tile / tpx) * kTH;
             const int x0 = tx0 - H, y0 = ty0 - H;
             const int x1 = min(tx0 + kTW - 1, int(S) - 1) - H, y1 = min(ty0 + kTH - 1, int(S) - 1) - H;
-            // Prune the boundaries whose leading metric is beaten everywhere in the tile:
+            // Prune the boundaries whose lead metric is beaten everywhere in the tile:
             // lo_b > min over b' of hi_b' (walks are at least the L1 distance to the tile
             // and at most the farthest corner's plus the 2-cell detour round the Center).
+            // The full-compare launch prunes on the first metric over every boundary.
+            constexpr uint32_t PL = WIDE ? q0 : L;
+            constexpr uint64_t sP = sl[PL];
             unsigned long long lo = ~0ull, hi = ~0ull;
-            if (lane < nb) {
+            // rank `lane`'s boundary; whether it is kept (Money first) is read off its key
+            const bool cnd = lane < nb && (WIDE || B[6][lane] != 0xFFFFFFFFu);
+            if (cnd) {
                 const int bxx = int(B[0][lane]), byy = int(B[1][lane]);
                 const int dx = bxx < x0 ? x0 - bxx : (bxx > x1 ? bxx - x1 : 0);
                 const int dy = byy < y0 ? y0 - byy : (byy > y1 ? byy - y1 : 0);
                 const int fx = max(abs(bxx - x0), abs(bxx - x1)), fy = max(abs(byy - y0), abs(byy - y1));
-                const uint32_t base = B[2 + q0][lane];
-                lo = base + slope1 * uint64_t(dx + dy);
-                hi = base + slope1 * uint64_t(fx + fy + 2);
+                const uint32_t base = B[2 + PL][lane];
+                lo = base + sP * uint64_t(dx + dy);
+                hi = base + sP * uint64_t(fx + fy + 2);
             }
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) {
                 const unsigned long long h2 = __shfl_xor(hi, o);
                 hi = h2 < hi ? h2 : hi;
             }
-            const unsigned long long live = __ballot(lane < nb && (lo <= hi || no_prune));
+            const unsigned long long live = __ballot(cnd && (lo <= hi || no_prune));
             // the specials (and the source) inside this tile
             bool in = false;
             if (lane < T) {
@@ -2786,15 +2812,11 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
             }
             const unsigned long long sp_in = __ballot(in);
             const bool axis = (x0 <= 0 && x1 >= 0) || (y0 <= 0 && y1 >= 0);
-            const unsigned long long mask2 = (1ull << w2) - 1, mask3 = (1ull << w3) - 1, maskr = (1ull << rb) - 1;
             if (!WIDE) {
-                // the best (key, rank) per cell (column c = lane + 64k, row i at k * kTH + i);
-                // a rank is the boundary's position in the (length, command list) order, so
-                // the pair orders walks exactly like the comparator whatever order the
-                // boundaries are visited in
-                unsigned long long kb[kCPL * kTH];
+                // the least key per cell (column c = lane + 64k, row i at k * kTH + i)
+                uint32_t kb[kCPL * kTH];
 #pragma unroll
-                for (int i = 0; i < kCPL * kTH; ++i) kb[i] = ~0ull;
+                for (int i = 0; i < kCPL * kTH; ++i) kb[i] = 0xFFFFFFFFu;
                 // boundaries on an axis through the Center, in a tile on an axis, take
                 // walk_dist's 2-cell detour to cells on the same axis across the Center:
                 // they get a loop of their own after the others
@@ -2808,18 +2830,17 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
                     // wave-uniform values in SGPRs, so the per-row step is a scalar select
                     const int bxx = __builtin_amdgcn_readfirstlane(int(B[0][rr]));
                     const int istar = __builtin_amdgcn_readfirstlane(int(B[1][rr])) - y0;  // the boundary's row in the tile
-                    const unsigned long long K = (unsigned long long)uint32_t(__builtin_amdgcn_readfirstlane(int(B[6][rr]))) |
-                                                 ((unsigned long long)uint32_t(__builtin_amdgcn_readfirstlane(int(B[7][rr]))) << 32);
-                    const unsigned long long up = slope, down = (unsigned long long)(-(long long)slope);
+                    const uint32_t K = uint32_t(__builtin_amdgcn_readfirstlane(int(B[6][rr])));
+                    const uint32_t up = stepL, down = 0u - stepL;
 #pragma unroll
                     for (int k = 0; k < kCPL; ++k) {
-                        // down a column the walk distance moves by +-1 per row, so the key by +-slope
+                        // down a column the walk distance moves by +-1 per row, so the key by +-stepL
                         const int wx = x0 + 64 * k + int(lane);
-                        unsigned long long key = K + slope * uint64_t(uint32_t(abs(bxx - wx)) + uint32_t(abs(istar)));
+                        uint32_t key = K + stepL * (uint32_t(abs(bxx - wx)) + uint32_t(abs(istar)));
 #pragma unroll
                         for (int i = 0; i < kTH; ++i) {
                             if (i > 0) key += i > istar ? up : down;
-                            kb[k * kTH + i] = key < kb[k * kTH + i] ? key : kb[k * kTH + i];
+                            kb[k * kTH + i] = min(kb[k * kTH + i], key);
                         }
                     }
                 }
@@ -2828,21 +2849,19 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
                     const int bxx = __builtin_amdgcn_readfirstlane(int(B[0][rr]));
                     const int byy = __builtin_amdgcn_readfirstlane(int(B[1][rr]));
                     const int istar = byy - y0, i0 = -y0;  // i0: the tile's row y = 0
-                    const unsigned long long K = (unsigned long long)uint32_t(__builtin_amdgcn_readfirstlane(int(B[6][rr]))) |
-                                                 ((unsigned long long)uint32_t(__builtin_amdgcn_readfirstlane(int(B[7][rr]))) << 32);
-                    const unsigned long long up = slope, down = (unsigned long long)(-(long long)slope), det2 = 2 * slope;
+                    const uint32_t K = uint32_t(__builtin_amdgcn_readfirstlane(int(B[6][rr])));
+                    const uint32_t up = stepL, down = 0u - stepL, det2 = 2u * stepL;
 #pragma unroll
                     for (int k = 0; k < kCPL; ++k) {
                         const int wx = x0 + 64 * k + int(lane);
-                        unsigned long long key = K + slope * uint64_t(uint32_t(abs(bxx - wx)) + uint32_t(abs(istar)));
+                        uint32_t key = K + stepL * (uint32_t(abs(bxx - wx)) + uint32_t(abs(istar)));
                         const bool detx = byy == 0 && wx != 0 && bxx != 0 && ((wx < 0) != (bxx < 0));
                         const bool dety = bxx == 0 && wx == 0 && byy != 0;
 #pragma unroll
                         for (int i = 0; i < kTH; ++i) {
                             if (i > 0) key += i > istar ? up : down;
                             const bool det = (i == i0 && detx) || (dety && i != i0 && ((i < i0) != (byy < 0)));
-                            const unsigned long long kk = key + (det ? det2 : 0ull);
-                            kb[k * kTH + i] = kk < kb[k * kTH + i] ? kk : kb[k * kTH + i];
+                            kb[k * kTH + i] = min(kb[k * kTH + i], key + (det ? det2 : 0u));
                         }
                     }
                 }
@@ -2857,18 +2876,16 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
                     for (int k = 0; k < kCPL; ++k) {
                         const int cx = tx0 + 64 * k + int(lane), cy = ty0 + i;
                         if (cx < int(S) && cy < int(S)) {
-                            // the cell word: the rank's base (b << 20) - legs(b) plus the
-                            // key's legs field, legs(b) + k
-                            const unsigned long long kv = kb[k * kTH + i];
-                            const uint32_t legs = q0 == 0 ? uint32_t(kv >> sh1)
-                                                          : (q1 == 0 ? uint32_t((kv >> sh2) & mask2) : uint32_t((kv >> sh3) & mask3));
-                            __builtin_amdgcn_raw_buffer_store_b32(B[5][uint32_t(kv & maskr)] + legs, rsrc,
-                                                                  int((64u * k + lane) * 4u), int(uint32_t(i) * S * 4u), 0);
+                            // the cell word b << 20 | k: k = (lead - the boundary's lead) / sL
+                            const uint32_t kv = kb[k * kTH + i], sr = kv & maskr;
+                            const uint32_t d = ((kv >> rbs) - B[7][sr]) / sL;
+                            __builtin_amdgcn_raw_buffer_store_b32(B[5][sr] + d, rsrc, int((64u * k + lane) * 4u),
+                                                                  int(uint32_t(i) * S * 4u), 0);
                         }
                     }
                 }
             } else {
-                for (int k = 0; k < kCPL; ++k) {  // metrics too wide for one key
+                for (int k = 0; k < kCPL; ++k) {  // keys too wide for 32 bits
                     const int cx = tx0 + 64 * k + int(lane);
                     fill_tile_rows<PERM>(B, live, x0 + 64 * k + int(lane), y0, ty0, cx, cx < int(S), S, outs);
                 }
