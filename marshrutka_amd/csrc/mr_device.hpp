@@ -1348,7 +1348,6 @@ __device__ __forceinline__ void finish_launch(const KArgs *__restrict__ a, uint3
         c[kCtrLastWritten] = wr;
         c[kCtrLastOvf] = ov;
         c[kCtrOvf] = 0;
-        c[kCtrFillWide] = 0;
         c[kCtrDequeue] = 0;
         c[kCtrFbCount] = 0;
         c[kCtrFbDequeue] = 0;
@@ -2627,10 +2626,8 @@ __global__ __launch_bounds__(kBS) void hub_wide_kernel(const KArgs *__restrict__
 // =====================================================================================
 __device__ __forceinline__ uint32_t bit_width64(unsigned long long x) { return x ? 64u - uint32_t(__clzll(x)) : 0u; }
 
-// the fill kernel's rare path: a tile whose source's metrics do not fit one key.  Row
-// by row, each cell's walk distance in full and the three-metric compare.  It runs in
-// a launch of its own (fill_kernel<PERM, true>), so its registers do not weigh on the
-// fast path's occupancy.
+// the fill kernel's rare path: a tile whose source's keys do not fit 32 bits.  Row
+// by row, each cell's walk distance in full and the three-metric compare.
 template <uint32_t PERM>
 __device__ __forceinline__ void fill_tile_rows(const uint32_t (*B)[64], unsigned long long live, int wx,
                                                       int y0, int ty0, int cx, bool col_ok, uint32_t S, CellWord *outs) {
@@ -2664,15 +2661,15 @@ __device__ __forceinline__ void fill_tile_rows(const uint32_t (*B)[64], unsigned
 #ifndef MR_FILL_WAVES
 #define MR_FILL_WAVES 6  // waves per SIMD the fill kernel is register-bounded to
 #endif
-template <uint32_t PERM, bool WIDE>
+template <uint32_t PERM>
 __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *__restrict__ a) {
     constexpr uint32_t q0 = PERM / 9, q1 = (PERM / 3) % 3, q2 = PERM % 3;
     // per unit of walk distance: legs 1, money 0, time 180 s
     constexpr uint32_t sl[3] = {1u, 0u, 180u};
-    constexpr uint64_t slope1 = sl[q0];
     constexpr int kTW = int(kFillTW), kTH = int(kFillTH), kCPL = kTW / 64;  // kCPL columns per lane
-    // per wave: boundaries by rank (x, y, m0, m1, m2, cell-word base (b << 20) - legs(b),
-    // key lo, key hi), specials by table index (x, y; entry 0 = source)
+    // per wave: boundaries by rank (x, y, m0, m1, m2, key), the cell word's parts by
+    // srank (or by rank for the full compare), specials by table index (x, y; entry 0 =
+    // the source)
     __shared__ uint32_t btab[kBS / 64][10][64];
     // the wave index through readfirstlane: everything derived from it (tile origins,
     // key fields, slopes) then lives in SGPRs
@@ -2683,13 +2680,11 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
     const int H = int(a->p.H);
     const uint32_t tpx = (S + kTW - 1) / kTW, tpy = (S + kTH - 1) / kTH, ntile = tpx * tpy;
     const bool no_prune = (a->dbg_flags & 1u) != 0, no_pack = (a->dbg_flags & 2u) != 0;
-    if (!WIDE && (a->dbg_flags & kDbgInjectFlag) && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a->counter + kCtrFlags, kErrChain);
+    if ((a->dbg_flags & kDbgInjectFlag) && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a->counter + kCtrFlags, kErrChain);
     const uint32_t nwaves = gridDim.x * (kBS / 64), gw = blockIdx.x * (kBS / 64) + wv;
     const uint32_t ngroups = nsrc < nwaves ? nsrc : nwaves, G = nwaves / ngroups, g = gw / G, j = gw % G;
-    uint32_t s_begin = g < ngroups ? uint32_t(uint64_t(g) * nsrc / ngroups) : 0u;
+    const uint32_t s_begin = g < ngroups ? uint32_t(uint64_t(g) * nsrc / ngroups) : 0u;
     const uint32_t s_end = g < ngroups ? uint32_t(uint64_t(g + 1) * nsrc / ngroups) : 0u;
-    if (WIDE && __hip_atomic_load(a->counter + kCtrFillWide, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-        s_begin = s_end;  // the first launch found none
     for (uint32_t s = s_begin; s < s_end; ++s) {
         if (a->src_state[s] != 1) continue;  // solved by the SSSP kernel, which wrote its records
         // ---- this source's tables -------------------------------------------------
@@ -2713,7 +2708,6 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
                 B[2][r] = e0;
                 B[3][r] = e1;
                 B[4][r] = e2;
-                B[5][r] = (lane << kStBShift) - e0;  // + the cell's legs = b << 20 | k
             }
         }
         const bool isb = lane < T && r != kNone32;
@@ -2756,24 +2750,23 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
         for (int o = 32; o > 0; o >>= 1) mxL = max(mxL, (uint64_t)__shfl_xor((unsigned long long)mxL, o));
         const uint32_t rbs = max(1u, bit_width64(nk - 1));
         const uint32_t wL = uint32_t(__builtin_amdgcn_readfirstlane(int(max(1u, bit_width64(mxL)))));
+        // keys wider than 32 bits (or MR_DBG_FLAGS bit 1): the rare full-compare path
         const bool packable = !no_pack && wL + rbs <= 32u;
-        // the first launch (WIDE = false) fills the sources whose keys fit 32 bits and
-        // counts the others, which the second launch fills
-        if (packable == WIDE) {
-            if (!WIDE && j == 0 && lane == 0) atomicAdd(a->counter + kCtrFillWide, 1u);
-            continue;
-        }
         const uint32_t stepL = packable ? sL << rbs : 0u, maskr = (1u << rbs) - 1u;
         if (packable) {
             if (isb) B[6][r] = kept ? uint32_t(em[L] << rbs) | srank : 0xFFFFFFFFu;  // by rank
             if (kept) {  // by srank: the cell word's table index and the lead's base
-                B[5][srank] = lane << kStBShift;
+                // (sL = 1: one word, (b << 20) - base, + the lead = b << 20 | k)
+                B[5][srank] = sL == 1u ? (lane << kStBShift) - uint32_t(em[L]) : lane << kStBShift;
                 B[7][srank] = uint32_t(em[L]);
             }
         } else if (isb) {
             B[5][r] = (lane << kStBShift) - e0;  // full compare (fill_tile_rows): + the cell's legs
         }
         wave_sync();
+        // prune on the lead metric (the full compare: on the first one, every boundary)
+        const uint32_t PL = packable ? L : q0;
+        const uint64_t sP = packable ? sL : sl[q0];
         // ---- this wave's tiles of the source ---------------------------------------
         CellWord *const outs = a->out_rec + (unsigned long long)s * V;
         for (uint32_t tile = j; tile < ntile; tile += G) {
@@ -2783,12 +2776,9 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
             // Prune the boundaries whose lead metric is beaten everywhere in the tile:
             // lo_b > min over b' of hi_b' (walks are at least the L1 distance to the tile
             // and at most the farthest corner's plus the 2-cell detour round the Center).
-            // The full-compare launch prunes on the first metric over every boundary.
-            constexpr uint32_t PL = WIDE ? q0 : L;
-            constexpr uint64_t sP = sl[PL];
             unsigned long long lo = ~0ull, hi = ~0ull;
             // rank `lane`'s boundary; whether it is kept (Money first) is read off its key
-            const bool cnd = lane < nb && (WIDE || B[6][lane] != 0xFFFFFFFFu);
+            const bool cnd = lane < nb && (!packable || B[6][lane] != 0xFFFFFFFFu);
             if (cnd) {
                 const int bxx = int(B[0][lane]), byy = int(B[1][lane]);
                 const int dx = bxx < x0 ? x0 - bxx : (bxx > x1 ? bxx - x1 : 0);
@@ -2812,7 +2802,7 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
             }
             const unsigned long long sp_in = __ballot(in);
             const bool axis = (x0 <= 0 && x1 >= 0) || (y0 <= 0 && y1 >= 0);
-            if (!WIDE) {
+            if (packable) {
                 // the least key per cell (column c = lane + 64k, row i at k * kTH + i)
                 uint32_t kb[kCPL * kTH];
 #pragma unroll
@@ -2878,8 +2868,8 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
                         if (cx < int(S) && cy < int(S)) {
                             // the cell word b << 20 | k: k = (lead - the boundary's lead) / sL
                             const uint32_t kv = kb[k * kTH + i], sr = kv & maskr;
-                            const uint32_t d = ((kv >> rbs) - B[7][sr]) / sL;
-                            __builtin_amdgcn_raw_buffer_store_b32(B[5][sr] + d, rsrc, int((64u * k + lane) * 4u),
+                            const uint32_t w = sL == 1u ? B[5][sr] + (kv >> rbs) : B[5][sr] + ((kv >> rbs) - B[7][sr]) / sL;
+                            __builtin_amdgcn_raw_buffer_store_b32(w, rsrc, int((64u * k + lane) * 4u),
                                                                   int(uint32_t(i) * S * 4u), 0);
                         }
                     }

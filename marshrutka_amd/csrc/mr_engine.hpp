@@ -107,7 +107,7 @@ constexpr uint32_t kViaSpecial = 0x80000000u, kViaSource = 0xFFFFFFFFu;
 // all-destinations fill tiles: one wave per kFillTW x kFillTH cells, MR_FILL_CPL
 // columns per lane (64 apart), MR_FILL_CELLS cells per lane
 #ifndef MR_FILL_CPL
-#define MR_FILL_CPL 4
+#define MR_FILL_CPL 1
 #endif
 #ifndef MR_FILL_CELLS
 #define MR_FILL_CELLS 16
@@ -175,8 +175,7 @@ enum : uint32_t {
     kCtrWritten = 7,      // result records written               64-bit counter with this)
     kCtrOvf = 8,          // command-overflow pool: commands allocated in this pass
     kCtrLastOvf = 9,      // kCtrOvf of the last completed pass
-    kCtrFillWide = 10,    // all-destinations fill: sources left to the second (wide-metric) launch
-    kCtrWords = 11
+    kCtrWords = 10
 };
 // result status (OutResult high half - 16) of a label whose commands went to the
 // overflow pool: its first command slot holds {kOvfTag, offset, count}

@@ -27,8 +27,7 @@ int max_blocks_per_cu(bool grid_in_lds, uint32_t algo, uint32_t bytes);
 uint32_t hub_lds_bytes(uint32_t NS, uint32_t nreg, uint32_t spw);
 hipError_t launch_hub(const KArgs *d_args, const uint32_t perm[3], uint32_t spw, bool nonlin, uint32_t NS, uint32_t nreg,
                       uint32_t blocks, hipStream_t stream);
-hipError_t launch_fill(const KArgs *d_args, const uint32_t perm[3], uint32_t gx, uint32_t gy, hipStream_t stream,
-                       bool wide);
+hipError_t launch_fill(const KArgs *d_args, const uint32_t perm[3], uint32_t gx, uint32_t gy, hipStream_t stream);
 int hub_blocks_per_cu(const uint32_t perm[3], uint32_t spw, bool nonlin, uint32_t bytes);
 int fill_blocks_per_cu(const uint32_t perm[3]);
 uint32_t hub_wide_lds_bytes(uint32_t NS, uint32_t nreg);
@@ -712,8 +711,7 @@ struct mr_plan {
     KArgs *d_args = nullptr;
     KArgs *d_args_fb = nullptr;           // SSSP launch over the hub solver's fallback list
     KArgs *d_args_hub_last = nullptr;     // hub launch that ends the pass (fallback known to be empty)
-    KArgs *d_args_fill = nullptr;         // all-destinations mode: the fill launch
-    KArgs *d_args_fill2 = nullptr;        // ... and its wide-metric second launch (ends the pass)
+    KArgs *d_args_fill = nullptr;         // all-destinations mode: the fill launch (ends the pass)
     bool all_mode = false;
     CellWord *d_rec = nullptr;            // all-destinations outputs (KArgs::out_rec ...)
     Rec *d_tab = nullptr;
@@ -749,7 +747,7 @@ struct mr_plan {
     struct Slot {
         Rec *tab = nullptr;
         uint32_t *lex = nullptr, *sstate = nullptr, *fb = nullptr, *counter = nullptr;
-        KArgs *args = nullptr, *args_fb = nullptr, *args_fill = nullptr, *args_fill2 = nullptr;
+        KArgs *args = nullptr, *args_fb = nullptr, *args_fill = nullptr;
     } alt;
     bool overlap = false;
     uint32_t slot = 0;  // slot index of the d_* fields
@@ -759,12 +757,12 @@ struct mr_plan {
         for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_rank_inv, (void *)d_src, (void *)d_qb, (void *)d_qd,
                         (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
                         (void *)d_counter, (void *)d_args, (void *)d_dbg, (void *)d_args_fb, (void *)d_near,
-                        (void *)d_fb, (void *)d_args_hub_last, (void *)d_args_fill, (void *)d_args_fill2, (void *)d_rec,
+                        (void *)d_fb, (void *)d_args_hub_last, (void *)d_args_fill, (void *)d_rec,
                         (void *)d_tab,
                         (void *)d_lex, (void *)d_sstate, (void *)d_near_sp, (void *)d_rb_off, (void *)d_rb_cell, (void *)d_ovf})
             if (p) (void)hipFree(p);
         for (void *p : {(void *)alt.tab, (void *)alt.lex, (void *)alt.sstate, (void *)alt.fb, (void *)alt.counter,
-                        (void *)alt.args, (void *)alt.args_fb, (void *)alt.args_fill, (void *)alt.args_fill2})
+                        (void *)alt.args, (void *)alt.args_fb, (void *)alt.args_fill})
             if (p) (void)hipFree(p);
         for (hipEvent_t e : {ev_hub[0], ev_hub[1], ev_fill[0], ev_fill[1], ev_last})
             if (e) (void)hipEventDestroy(e);
@@ -790,7 +788,6 @@ static void swap_slot(mr_plan *pl) {
     std::swap(pl->d_args, a.args);
     std::swap(pl->d_args_fb, a.args_fb);
     std::swap(pl->d_args_fill, a.args_fill);
-    std::swap(pl->d_args_fill2, a.args_fill2);
     pl->ka.out_tab = pl->d_tab;
     pl->ka.out_lex = pl->d_lex;
     pl->ka.src_state = pl->d_sstate;
@@ -821,11 +818,7 @@ static int upload_args(mr_plan *pl) {
         if (!put(pl->d_args_fb, f)) return MR_ERR_DEVICE;
         KArgs l = k;
         l.last_launch = 1;
-        if (!put(pl->all_mode ? pl->d_args_fill2 : pl->d_args_hub_last, l)) return MR_ERR_DEVICE;
-        if (pl->all_mode) {
-            l.last_launch = 0;
-            if (!put(pl->d_args_fill, l)) return MR_ERR_DEVICE;
-        }
+        if (!put(pl->all_mode ? pl->d_args_fill : pl->d_args_hub_last, l)) return MR_ERR_DEVICE;
     }
     return MR_OK;
 }
@@ -979,8 +972,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         pl->fill_per_cu = uint32_t(std::max(1, fill_blocks_per_cu(hp.p.perm)));
         if (hipMalloc(reinterpret_cast<void **>(&pl->d_args_fb), sizeof(KArgs)) != hipSuccess ||
             hipMalloc(reinterpret_cast<void **>(&pl->d_args_hub_last), sizeof(KArgs)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&pl->d_args_fill), sizeof(KArgs)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&pl->d_args_fill2), sizeof(KArgs)) != hipSuccess)
+            hipMalloc(reinterpret_cast<void **>(&pl->d_args_fill), sizeof(KArgs)) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "kernel args"));
     }
 #ifdef MR_HUBDUMP
@@ -1015,7 +1007,6 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
             hipMalloc(reinterpret_cast<void **>(&a.args), sizeof(KArgs)) != hipSuccess ||
             hipMalloc(reinterpret_cast<void **>(&a.args_fb), sizeof(KArgs)) != hipSuccess ||
             hipMalloc(reinterpret_cast<void **>(&a.args_fill), sizeof(KArgs)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&a.args_fill2), sizeof(KArgs)) != hipSuccess ||
             hipStreamCreateWithFlags(&pl->hub_stream, hipStreamNonBlocking) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "second all-destinations slot"));
         for (int i = 0; i < 2; ++i)
@@ -1101,12 +1092,7 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
             e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, s);
         hipEvent_t f0 = nullptr;
         if (e == hipSuccess && hipEventCreate(&f0) == hipSuccess) (void)hipEventRecord(f0, s);
-        if (e == hipSuccess) e = launch_fill(pl->d_args_fill, pl->ka.p.perm, gx, gy, s, false);
-        // the wide-metric launch mostly finds no source and exits; its grid is one
-        // workgroup per CU, since each workgroup ends with an atomic on one counter
-        // (the last resets the pass's counters) and 1.5k of them cost ~30 us
-        const uint32_t gxw = std::min<uint32_t>(gx, std::max<uint32_t>(1, pl->cus));
-        if (e == hipSuccess) e = launch_fill(pl->d_args_fill2, pl->ka.p.perm, gxw, gy, s, true);
+        if (e == hipSuccess) e = launch_fill(pl->d_args_fill, pl->ka.p.perm, gx, gy, s);
         // the slot's tables are free again once this fill has read them
         if (e == hipSuccess && pl->overlap && hipEventRecord(pl->ev_fill[pl->slot], s) != hipSuccess)
             e = hipErrorUnknown;
