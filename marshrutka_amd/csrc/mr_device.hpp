@@ -149,6 +149,29 @@ __device__ __forceinline__ Cmd tail_at(const View &x, int i) {
     const uint32_t m = 0u - uint32_t(i == 0);
     return Cmd{(x.t0.kp & m) | (x.t1.kp & ~m), (x.t0.from & m) | (x.t1.from & ~m), (x.t0.to & m) | (x.t1.to & ~m)};
 }
+// A tentative label held in registers by the hub solvers: a View without the fields
+// every such label derives.  The label builders (start, walk, SoE from a region,
+// ext_view, SHQ/SFm) all give t0.from = the rank of the parent entry's cell (the
+// source's for parent 0), t0.to = u (the special's own rank unless ntail = 2), and
+// t1 = {SoE, u, own rank} when ntail = 2; so 6 words hold it where a View takes 12,
+// and an improvement selects 6 fields.
+struct RLab {
+    uint32_t m0, m1, m2;
+    uint32_t lpn;  // len | parent << 16 | (ntail - 1) << 31
+    uint32_t kp0, u;
+};
+__device__ __forceinline__ RLab compact(const View &c) {
+    return RLab{c.m0, c.m1, c.m2, c.len | (c.parent << 16) | ((c.ntail - 1u) << 31), c.t0.kp, c.t0.to};
+}
+__device__ __forceinline__ uint32_t rl_len(const RLab &x) { return x.lpn & 0xFFFFu; }
+__device__ __forceinline__ void sel_rlab(bool take, RLab &d, const RLab &c) {
+    d.m0 = take ? c.m0 : d.m0;
+    d.m1 = take ? c.m1 : d.m1;
+    d.m2 = take ? c.m2 : d.m2;
+    d.lpn = take ? c.lpn : d.lpn;
+    d.kp0 = take ? c.kp0 : d.kp0;
+    d.u = take ? c.u : d.u;
+}
 
 template <bool G>
 struct Core {
@@ -202,6 +225,19 @@ struct Core {
     __device__ __forceinline__ uint32_t vert_of(uint32_t t) const { return t == 0 ? src : sp[t].v; }
     // commands name cells by CellIndex rank, so comparing them needs no memory access
     __device__ __forceinline__ uint32_t rk_of(uint32_t t) const { return t == 0 ? src_rk : sp[t].rk; }
+    // the View of register label x of the special whose cell has rank `own` (RLab)
+    __device__ __forceinline__ View expand(const RLab &x, uint32_t own) const {
+        View v;
+        v.m0 = x.m0;
+        v.m1 = x.m1;
+        v.m2 = x.m2;
+        v.len = x.lpn & 0xFFFFu;
+        v.parent = (x.lpn >> 16) & kNone10;
+        v.ntail = (x.lpn >> 31) + 1u;
+        v.t0 = Cmd{x.kp0, rk_of(v.parent), x.u};
+        v.t1 = v.ntail == 2 ? Cmd{kSoE << 29, x.u, own} : Cmd{0, 0, 0};
+        return v;
+    }
 
     // ---- arithmetic (u32 like the reference; overflow is reported, not wrapped)
     __device__ __forceinline__ uint32_t add32(uint32_t x, uint32_t y) const {
@@ -563,6 +599,9 @@ struct Core {
     // the settle candidate, then every lane relaxes the edges from the settled
     // special into itself — no shared-write races.
     __device__ __forceinline__ static uint32_t metric(const View &x, uint32_t i) {
+        return i == 0 ? x.m0 : (i == 1 ? x.m1 : x.m2);
+    }
+    __device__ __forceinline__ static uint32_t metric(const RLab &x, uint32_t i) {
         return i == 0 ? x.m0 : (i == 1 ? x.m1 : x.m2);
     }
     // among the lanes with c set, the one holding the smallest table label (lane t holds
@@ -1334,8 +1373,11 @@ __device__ __forceinline__ void finish_launch(const KArgs *__restrict__ a, uint3
         if (written) atomicAdd(c + kCtrWritten, written);
         return;
     }
-    __threadfence();
-    // one atomic per workgroup: {done, written} share a 64-bit word (a grid's workgroups
+    // No fence before the count: the counters this workgroup added to were updated by
+    // atomics whose returned values it waited for, and the records need no ordering
+    // (the host reads them after the kernel).  An agent-scope release here writes the
+    // XCD's L2 back: one per workgroup made the fill 1.7x slower.
+    // One atomic per workgroup: {done, written} share a 64-bit word (a grid's workgroups
     // end together, and same-address atomics serialise at ~11 ns each)
     static_assert(kCtrDone % 2 == 0 && kCtrWritten == kCtrDone + 1, "counter pair");
     const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long *>(c + kCtrDone),
@@ -1446,36 +1488,27 @@ struct HubSolver : Core<false> {
     // receives a label when it settles (command chains and list compares read it).
     // The update is a per-field select under an explicit mask, never a divergent
     // block assignment.
-    __device__ __forceinline__ void improve_reg(bool active, uint32_t &st, View &my, const View &c) const {
+    // (own: the rank of the lane's special, for the rare command-list compare)
+    __device__ __forceinline__ void improve_reg(bool active, uint32_t &st, RLab &my, const View &c, uint32_t own) const {
         bool take = active && st != 2;
         if (take && st == 1) {
             const int cm = cmp_metrics(c.m0, c.m1, c.m2, my.m0, my.m1, my.m2);
             if (cm != 0) take = cm < 0;
-            else if (c.len != my.len) take = c.len < my.len;
-            else take = cmp_list(c, kOwn, my, kOwn) < 0;
+            else if (c.len != rl_len(my)) take = c.len < rl_len(my);
+            else take = cmp_list(c, kOwn, expand(my, own), kOwn) < 0;
         }
-        my.m0 = take ? c.m0 : my.m0;
-        my.m1 = take ? c.m1 : my.m1;
-        my.m2 = take ? c.m2 : my.m2;
-        my.len = take ? c.len : my.len;
-        my.parent = take ? c.parent : my.parent;
-        my.ntail = take ? c.ntail : my.ntail;
-        my.t0.kp = take ? c.t0.kp : my.t0.kp;
-        my.t0.from = take ? c.t0.from : my.t0.from;
-        my.t0.to = take ? c.t0.to : my.t0.to;
-        my.t1.kp = take ? c.t1.kp : my.t1.kp;
-        my.t1.from = take ? c.t1.from : my.t1.from;
-        my.t1.to = take ? c.t1.to : my.t1.to;
+        sel_rlab(take, my, compact(c));
         st = take ? 1u : st;
     }
     // Per segment, the settle candidate: the smallest tentative label, resolved
     // metric by metric on the DPP network (exit once every segment has at most one
     // lane left).  Exact ties of metrics and length publish the tied labels to the
     // table and compare command lists.  Returns the segment lane, or kNone32.
-    __device__ __forceinline__ uint32_t select_reg(bool c, const View &my) const {
+    __device__ __forceinline__ uint32_t select_reg(bool c, const RLab &my, uint32_t own) const {
         const DevParams &p = P;
         unsigned long long m = seg_bits<LPS>(__ballot(c));
-        const uint32_t keys[4] = {metric(my, p.perm[0]), metric(my, p.perm[1]), metric(my, p.perm[2]), my.len};
+        const uint32_t mm3[3] = {my.m0, my.m1, my.m2};
+        const uint32_t keys[4] = {mm3[p.perm[0]], mm3[p.perm[1]], mm3[p.perm[2]], rl_len(my)};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             if (__all(__popcll(m) <= 1)) break;
@@ -1486,7 +1519,7 @@ struct HubSolver : Core<false> {
         if (__any(__popcll(m) > 1)) {
             const bool tied = __popcll(m) > 1;
             const uint32_t t = seg_lane();
-            if (tied && c) write_rec(t, my, 1);
+            if (tied && c) write_rec(t, expand(my, own), 1);
             wave_sync();
             uint32_t mm = (tied && c) ? t : kNone32;
 #pragma unroll
@@ -1508,7 +1541,7 @@ struct HubSolver : Core<false> {
     }
     // walks and SoE-region edges from boundary b (label lb, at bx, by) into lane t's special
     __device__ __forceinline__ void relax_boundary(bool live, const View &lb, uint32_t b, int bx, int by, uint32_t t,
-                                                   uint32_t &st, View &my, const SpecialStatic &ss, uint32_t &bwh,
+                                                   uint32_t &st, RLab &my, const SpecialStatic &ss, uint32_t &bwh,
                                                    uint32_t &b0, uint32_t &b1, uint32_t &b2) const {
         const DevParams &p = P;
         live = live && st != 2;
@@ -1526,17 +1559,17 @@ struct HubSolver : Core<false> {
     // the walk from boundary b into lane t's special: not into the Center (entry 1)
     // nor b's own cell
     __device__ __forceinline__ void relax_walk(bool live, const View &lb, uint32_t b, int bx, int by, uint32_t t,
-                                               uint32_t &st, View &my, const SpecialStatic &ss, uint32_t &bwh,
+                                               uint32_t &st, RLab &my, const SpecialStatic &ss, uint32_t &bwh,
                                                uint32_t &b0, uint32_t &b1, uint32_t &b2) const {
         const bool on = live && st != 2 && t != 1 && t != b && !(b == 0 && ss.v == src);
         View c;
         view_walk_lab(lb, b, walk_dist(bx, by, ss.x, ss.y), ss.rk, c);
         note_walk(on, c, bwh, b0, b1, b2);
-        improve_reg(on, st, my, c);
+        improve_reg(on, st, my, c, ss.rk);
     }
     // the SoE-region edge from boundary b into lane t's special, with b's region row
     // entry {d, u} for t's region already read
-    __device__ __forceinline__ void relax_soe(bool live, const View &lb, uint32_t b, uint32_t t, uint32_t &st, View &my,
+    __device__ __forceinline__ void relax_soe(bool live, const View &lb, uint32_t b, uint32_t t, uint32_t &st, RLab &my,
                                               const SpecialStatic &ss, uint32_t d, uint32_t u) const {
         const DevParams &p = P;
         (void)t;
@@ -1554,7 +1587,7 @@ struct HubSolver : Core<false> {
                 c.ntail = 2;
                 c.t1 = Cmd{kSoE << 29, u, ss.rk};
             }
-            improve_reg(on, st, my, c);
+            improve_reg(on, st, my, c, ss.rk);
         }
     }
 
@@ -1930,9 +1963,9 @@ struct HubSolver : Core<false> {
         const int sx = int(src % p.S) - int(p.H), sy = int(src / p.S) - int(p.H);
         const uint32_t ts = sinfo[src] & kNone10;
         const SpecialStatic ss = sp[t <= p.NS ? t : 0u];
-        View my, st0;
+        View st0;
         view_start(st0);
-        my = st0;
+        RLab my = compact(st0);
         uint32_t st = 0, bwh = 0, b0 = 0, b1 = 0, b2 = 0, unc = 0, nbk = 0;
         if (t == 0) {
             write_rec(0, st0, 2);
@@ -1944,15 +1977,15 @@ struct HubSolver : Core<false> {
             srow[2 * t + 1] = e.y;
         }
         wave_sync();
-        improve_reg(mine && t == ts, st, my, st0);
+        improve_reg(mine && t == ts, st, my, st0, ss.rk);
         {  // SHQ / SFm: only the source's own edges can be minimal
             View c = st0;
             c.m1 = p.shq_cost;
             c.t0 = Cmd{kSHQ << 29, src_rk, ss.rk};
-            improve_reg(mine && t == p.hq_t, st, my, c);
+            improve_reg(mine && t == p.hq_t, st, my, c, ss.rk);
             c.m1 = p.sfm_cost;
             c.t0 = Cmd{kSFm << 29, src_rk, sp[1].rk};
-            improve_reg(mine && p.use_sfm && t == 1, st, my, c);
+            improve_reg(mine && p.use_sfm && t == 1, st, my, c, ss.rk);
         }
         uint32_t nb = 1;
         MR_HSTAMP(3);
@@ -1966,14 +1999,14 @@ struct HubSolver : Core<false> {
         MR_HSTAMP(6);
         MR_HCOUNT(0, 1);
         for (uint32_t it = 0; it <= p.NS; ++it) {
-            const uint32_t s = select_reg(mine && st == 1, my);
+            const uint32_t s = select_reg(mine && st == 1, my, ss.rk);
             if (__all(s == kNone32)) break;
             MR_HCOUNT(1, 1);
             const bool act = s != kNone32;  // this segment settles a special
             const uint32_t sc = act ? s : 0u;
             if (act && t == s) {
                 st = 2;
-                write_rec(s, my, 2);
+                write_rec(s, expand(my, ss.rk), 2);
             }
             wave_sync();
             View ls;  // the settled label, from the table
@@ -1994,7 +2027,7 @@ struct HubSolver : Core<false> {
                     View c;
                     ext_view(ls, sc, sS.rk, kCentral, 1, 0, 10, ss.rk, c);
                     const uint32_t want = (sS.flags & kSpCenter) ? kSpBorder1 : kSpCenter;
-                    improve_reg(live && central_s && (ss.flags & want), st, my, c);
+                    improve_reg(live && central_s && (ss.flags & want), st, my, c, ss.rk);
                 }
                 const bool hub_s = act && p.use_caravans && (sS.flags & kSpHub);
                 if (__any(hub_s)) {
@@ -2002,13 +2035,13 @@ struct HubSolver : Core<false> {
                     const uint32_t d = uint32_t(abs(sS.x - ss.x) + abs(sS.y - ss.y));
                     const uint32_t coef = ss.coef5 ? 5u : 2u;
                     ext_view(ls, sc, sS.rk, kCaravan, (d << 1) | ss.coef5, coef * d, p.rgt * d, ss.rk, c);
-                    improve_reg(live && hub_s && (ss.flags & kSpHub), st, my, c);
+                    improve_reg(live && hub_s && (ss.flags & kSpHub), st, my, c, ss.rk);
                 }
                 const bool soe_s = act && p.use_soe && sS.region != kNone10 && sS.region != sc;
                 if (__any(soe_s)) {
                     View c;
                     ext_view(ls, sc, sS.rk, kSoE, 0, p.soe_cost, 0, ss.rk, c);
-                    improve_reg(live && soe_s && sS.region == t, st, my, c);
+                    improve_reg(live && soe_s && sS.region == t, st, my, c, ss.rk);
                 }
             }
             MR_HSTAMP(5);
@@ -2042,8 +2075,9 @@ struct HubSolver : Core<false> {
         // any blocker does: the fill kernel cannot check cells).  No early return: the
         // wave must stay converged.
         wave_sync();
-        if (__any(nbk != 0) && mine && st == 2 && !label_avail(my, nbk, ss.x, ss.y, sx, sy)) unc = 1;
-        if (!ff_linear() && !(a->dbg_flags & 4u) && mine && st == 2 && !label_certain(my, nb, ss.x, ss.y, sx, sy))
+        if (__any(nbk != 0) && mine && st == 2 && !label_avail(expand(my, ss.rk), nbk, ss.x, ss.y, sx, sy)) unc = 1;
+        if (!ff_linear() && !(a->dbg_flags & 4u) && mine && st == 2 &&
+            !label_certain(expand(my, ss.rk), nb, ss.x, ss.y, sx, sy))
             unc = 1;
         const bool unc_sp = seg_bits<LPS>(__ballot(unc != 0)) != 0;
         const uint32_t qa = a->q_begin[si];
@@ -2253,25 +2287,35 @@ struct HubWide : HubSolver<1> {
         }
     }
 
+    // full comparator of two register labels (own: their specials' ranks)
+    __device__ __forceinline__ int cmp_rlab(const RLab &x, uint32_t ox, const RLab &y, uint32_t oy) const {
+        const int r = cmp_metrics(x.m0, x.m1, x.m2, y.m0, y.m1, y.m2);
+        if (r) return r;
+        if (rl_len(x) != rl_len(y)) return rl_len(x) < rl_len(y) ? -1 : 1;
+        return cmp_list(expand(x, ox), kOwn, expand(y, oy), kOwn);
+    }
     // the wave's best tentative label over every lane's owned specials; returns its
     // table index (wave-uniform) or kNone32
-    __device__ __forceinline__ uint32_t select_wide(const bool (&c)[SPL], const View (&my)[SPL]) const {
+    template <class SSF>
+    __device__ __forceinline__ uint32_t select_wide(const bool (&c)[SPL], const RLab (&my)[SPL], SSF SS) const {
         const DevParams &p = P;
         const uint32_t j = lane_id();
         bool any = false;
-        View bv = my[0];
-        uint32_t bt = kNone32;
+        RLab bv = my[0];
+        uint32_t bt = kNone32, bown = 0;
 #pragma unroll
         for (uint32_t i = 0; i < SPL; ++i) {
-            const bool take = c[i] && (!any || cmp_view(my[i], kOwn, bv, kOwn) < 0);
-            sel_view(take, bv, my[i]);
+            const uint32_t own = SS(i).rk;
+            const bool take = c[i] && (!any || cmp_rlab(my[i], own, bv, bown) < 0);
+            sel_rlab(take, bv, my[i]);
             bt = take ? j + 64u * i : bt;
+            bown = take ? own : bown;
             any = any || c[i];
         }
         bool cand = any;
         unsigned long long m = __ballot(cand);
         if (m == 0) return kNone32;
-        const uint32_t keys[4] = {metric(bv, p.perm[0]), metric(bv, p.perm[1]), metric(bv, p.perm[2]), bv.len};
+        const uint32_t keys[4] = {metric(bv, p.perm[0]), metric(bv, p.perm[1]), metric(bv, p.perm[2]), rl_len(bv)};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             if (__popcll(m) <= 1) break;
@@ -2280,7 +2324,7 @@ struct HubWide : HubSolver<1> {
         }
         if (__popcll(m) == 1) return bcast(bt, uint32_t(__ffsll((long long)m) - 1));
         // equal metrics and length in several lanes: compare the command lists
-        if (cand) write_rec(bt, bv, 1);
+        if (cand) write_rec(bt, expand(bv, bown), 1);
         wave_sync();
         uint32_t mm = cand ? bt : kNone32;
 #pragma unroll
@@ -2387,7 +2431,7 @@ struct HubWide : HubSolver<1> {
         const uint32_t ts = sinfo[src] & kNone10;
         View st0;
         view_start(st0);
-        View my[SPL];
+        RLab my[SPL];
         uint32_t st[SPL], bwh[SPL], b0[SPL], b1[SPL], b2[SPL];
         bool mine[SPL];
         uint32_t unc = 0, nbk = 0;
@@ -2416,16 +2460,16 @@ struct HubWide : HubSolver<1> {
             const uint32_t t = j + 64u * i;
             mine[i] = t >= 1 && t <= p.NS;
             const SpecialStatic ss = SS(i);
-            my[i] = st0;
+            my[i] = compact(st0);
             st[i] = bwh[i] = b0[i] = b1[i] = b2[i] = 0;
-            improve_reg(mine[i] && t == ts, st[i], my[i], st0);
+            improve_reg(mine[i] && t == ts, st[i], my[i], st0, ss.rk);
             View c = st0;
             c.m1 = p.shq_cost;
             c.t0 = Cmd{kSHQ << 29, src_rk, ss.rk};
-            improve_reg(mine[i] && t == p.hq_t, st[i], my[i], c);
+            improve_reg(mine[i] && t == p.hq_t, st[i], my[i], c, ss.rk);
             c.m1 = p.sfm_cost;
             c.t0 = Cmd{kSFm << 29, src_rk, sp[1].rk};
-            improve_reg(mine[i] && p.use_sfm && t == 1, st[i], my[i], c);
+            improve_reg(mine[i] && p.use_sfm && t == 1, st[i], my[i], c, ss.rk);
             relax_boundary(mine[i] && src != p.vc, l0, 0, sx, sy, t, st[i], my[i], ss, bwh[i], b0[i], b1[i], b2[i]);
         }
         wave_sync();
@@ -2434,7 +2478,7 @@ struct HubWide : HubSolver<1> {
             bool c[SPL];
 #pragma unroll
             for (uint32_t i = 0; i < SPL; ++i) c[i] = mine[i] && st[i] == 1;
-            const uint32_t s = select_wide(c, my);
+            const uint32_t s = select_wide(c, my, SS);
             if (s == kNone32) break;
             const uint32_t so = s & 63u, si = s >> 6;
             // s's region-row entries for the owned specials' regions, read before the
@@ -2455,7 +2499,7 @@ struct HubWide : HubSolver<1> {
             for (uint32_t i = 0; i < SPL; ++i)
                 if (j == so && i == si) {
                     st[i] = 2;
-                    write_rec(s, my[i], 2);
+                    write_rec(s, expand(my[i], SS(i).rk), 2);
                 }
             wave_sync();
             View ls;
@@ -2488,19 +2532,19 @@ struct HubWide : HubSolver<1> {
                 if (central_s) {
                     View c = cc;
                     c.t0.to = ss.rk;
-                    improve_reg(live && (ss.flags & want), st[i], my[i], c);
+                    improve_reg(live && (ss.flags & want), st[i], my[i], c, ss.rk);
                 }
                 if (hub_s) {
                     View c;
                     const uint32_t d = uint32_t(abs(sS.x - ss.x) + abs(sS.y - ss.y));
                     const uint32_t coef = ss.coef5 ? 5u : 2u;
                     ext_view(ls, s, sS.rk, kCaravan, (d << 1) | ss.coef5, coef * d, p.rgt * d, ss.rk, c);
-                    improve_reg(live && (ss.flags & kSpHub), st[i], my[i], c);
+                    improve_reg(live && (ss.flags & kSpHub), st[i], my[i], c, ss.rk);
                 }
                 if (soe_s) {
                     View c;
                     ext_view(ls, s, sS.rk, kSoE, 0, p.soe_cost, 0, ss.rk, c);
-                    improve_reg(live && sS.region == t, st[i], my[i], c);
+                    improve_reg(live && sS.region == t, st[i], my[i], c, ss.rk);
                 }
                 if (walks) {
                     B::relax_walk(live, ls, s, sS.x, sS.y, t, st[i], my[i], ss, bwh[i], b0[i], b1[i], b2[i]);
@@ -2516,7 +2560,7 @@ struct HubWide : HubSolver<1> {
 #pragma unroll
             for (uint32_t i = 0; i < SPL; ++i) {
                 const SpecialStatic ss = SS(i);
-                if (mine[i] && st[i] == 2 && !B::label_avail(my[i], nbk, ss.x, ss.y, sx, sy)) unc = 1;
+                if (mine[i] && st[i] == 2 && !B::label_avail(B::expand(my[i], ss.rk), nbk, ss.x, ss.y, sx, sy)) unc = 1;
             }
         }
         bool fallback = __ballot(unc != 0) != 0 || a->fb_all;
