@@ -288,9 +288,14 @@ int mr_sssp_records(mr_plan *plan, uint32_t i, mr_label_record *out);
  *   0x80000000 | t  special t's own table label;  0xFFFFFFFF  the source
  * Plan sources are the caller's distinct sources in row-major cell order. */
 int mr_sssp_device_records(mr_plan *plan, void **d_records, uint64_t *bytes);
-/* Device pointer to the label tables ([plan source][NS + 1 entries], 44 B each:
- * u32 legs, money, time; u16 length; u8 tail count; u8 state; u16 parent entry;
- * u16 pad; 2 x {u32 kind << 29 | payload, from rank, to rank}) and their size. */
+/* Device pointer to the label tables ([plan source][NS + 1 entries], 28 B each:
+ * u32 legs, money, time; u32 meta = length (16 b) | parent entry (10 b) << 16 |
+ * state (2 b) << 26 | (tail count - 1) << 31; u32 kp0; u32 from0; u32 u) and their
+ * size.  An entry's label is its parent's commands, then {kp0, from0, u} and,
+ * with two tail commands, {Scroll of Escape, cell u, the entry's own cell} (from0 =
+ * the parent's cell); kp0 =
+ * kind << 29 | payload (Standard: legs; Central: moves; Caravan: distance << 1 |
+ * coefficient 5), cells by rank in CellIndex order. */
 int mr_sssp_device_tables(mr_plan *plan, void **d_tables, uint64_t *bytes);
 /* The full label (FindPath::eval(sources[i], dst)) rebuilt from its record:
  * MR_OK, MR_ERR_CAPACITY (out->n_commands > cap) or an error. */

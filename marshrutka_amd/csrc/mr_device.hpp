@@ -271,11 +271,11 @@ struct Core {
         x.m0 = r.m[0];
         x.m1 = r.m[1];
         x.m2 = r.m[2];
-        x.len = r.len;
-        x.parent = r.parent;
-        x.ntail = r.ntail;
-        x.t0 = r.tail[0];
-        x.t1 = r.tail[1];
+        x.len = r.len();
+        x.parent = r.parent();
+        x.ntail = r.ntail();
+        x.t0 = Cmd{r.kp0, r.from0, r.u};
+        x.t1 = x.ntail == 2 ? Cmd{kSoE << 29, r.u, rk_of(t)} : Cmd{0, 0, 0};
     }
     // the start label TotalCost::new(src) (src/cost.rs:196-205)
     __device__ __forceinline__ void view_start(View &x) const {
@@ -296,7 +296,7 @@ struct Core {
         x.m0 = add32(rb.m[0], k);
         x.m1 = rb.m[1];
         x.m2 = add32(rb.m[2], run_time(k));
-        x.len = (b == 0 ? 0u : rb.len) + 1u;
+        x.len = (b == 0 ? 0u : rb.len()) + 1u;
         x.parent = b;
         x.ntail = 1;
         x.t0 = Cmd{(kStandard << 29) | k, rk_of(b), vr};
@@ -323,12 +323,10 @@ struct Core {
         r.m[0] = c.m0;
         r.m[1] = c.m1;
         r.m[2] = c.m2;
-        r.len = uint16_t(c.len);
-        r.ntail = uint8_t(c.ntail);
-        r.parent = uint16_t(c.parent);
-        r.tail[0] = c.t0;
-        r.tail[1] = c.t1;
-        r.state = uint8_t(state);
+        r.meta = Rec::pack(c.len, c.parent, c.ntail, state);
+        r.kp0 = c.t0.kp;
+        r.from0 = c.t0.from;
+        r.u = c.t0.to;
     }
 
     // ---- comparator: CostComparator::and_then (src/cost.rs:411-426) ------------
@@ -340,8 +338,8 @@ struct Core {
     }
     // command i of table entry t, by value (no pointer into LDS escapes)
     __device__ __forceinline__ Cmd rec_tail(uint32_t t, int i) const {
-        const uint32_t *w = reinterpret_cast<const uint32_t *>(&R[t].tail[0]) + 3 * i;
-        return Cmd{w[0], w[1], w[2]};
+        const Rec &r = R[t];
+        return i == 0 ? Cmd{r.kp0, r.from0, r.u} : Cmd{kSoE << 29, r.u, rk_of(t)};
     }
     // lexicographic compare of two command lists of equal length, walking from
     // the last command towards the first; xid/yid name the table entries the
@@ -358,17 +356,17 @@ struct Core {
             if (r) res = r;
             if (xt > 0) --xt;
             else {
-                uint32_t pp = (xe == kOwn) ? x.parent : R[xe].parent;
+                uint32_t pp = (xe == kOwn) ? x.parent : R[xe].parent();
                 if (pp == 0) return res;
                 xe = pp;
-                xt = int(R[pp].ntail) - 1;
+                xt = int(R[pp].ntail()) - 1;
             }
             if (yt > 0) --yt;
             else {
-                uint32_t pp = (ye == kOwn) ? y.parent : R[ye].parent;
+                uint32_t pp = (ye == kOwn) ? y.parent : R[ye].parent();
                 if (pp == 0) return res;
                 ye = pp;
-                yt = int(R[pp].ntail) - 1;
+                yt = int(R[pp].ntail()) - 1;
             }
         }
         flag(kErrChain);
@@ -396,7 +394,7 @@ struct Core {
         const Rec &rs = R[s], &rt = R[t];
         int r = cmp_metrics(rs.m[0], rs.m[1], rs.m[2], rt.m[0], rt.m[1], rt.m[2]);
         if (r) return r;
-        if (rs.len != rt.len) return rs.len < rt.len ? -1 : 1;
+        if (rs.len() != rt.len()) return rs.len() < rt.len() ? -1 : 1;
         View x, y;
         view_rec(s, x);
         view_rec(t, y);
@@ -405,29 +403,21 @@ struct Core {
 
     // ---- special table updates --------------------------------------------------
     __device__ __forceinline__ void try_improve(uint32_t t, const View &c) const {
-        Rec &r = R[t];
-        if (r.state == 2) return;
-        if (r.state == 1) {
+        const Rec &r = R[t];
+        if (r.state() == 2) return;
+        if (r.state() == 1) {
             int cm = cmp_metrics(c.m0, c.m1, c.m2, r.m[0], r.m[1], r.m[2]);
             if (cm > 0) return;
             if (cm == 0) {
-                if (c.len > r.len) return;
-                if (c.len == r.len) {
+                if (c.len > r.len()) return;
+                if (c.len == r.len()) {
                     View cur;
                     view_rec(t, cur);
                     if (cmp_list(c, kOwn, cur, t) >= 0) return;
                 }
             }
         }
-        r.m[0] = c.m0;
-        r.m[1] = c.m1;
-        r.m[2] = c.m2;
-        r.len = uint16_t(c.len);
-        r.ntail = uint8_t(c.ntail);
-        r.parent = uint16_t(c.parent);
-        r.tail[0] = c.t0;
-        r.tail[1] = c.t1;
-        r.state = 1;
+        write_rec(t, c, 1);
     }
     // extend the settled label r of special s (rank rs) by a non-Standard edge
     // to the cell of rank rt (TotalCost += edge, src/cost.rs:208-315)
@@ -512,15 +502,15 @@ struct Core {
         const uint32_t lane = lane_id();
         const uint32_t vs = sp[s].v;
         Rec &r = R[s];
-        const Cmd last = r.ntail == 2 ? r.tail[1] : r.tail[0];
-        const uint32_t lk = last.kp >> 29;
+        const uint32_t last_kp = r.ntail() == 2 ? (kSoE << 29) : r.kp0;
+        const uint32_t lk = last_kp >> 29;
         uint32_t seed;
         bool boundary;
         if (lk == kNoMove) {  // the source itself
             seed = 0;
             boundary = false;
         } else if (lk == kStandard) {  // continues the walk of its parent boundary
-            seed = (uint32_t(r.parent) << kStBShift) | (last.kp & kStKMask);
+            seed = (r.parent() << kStBShift) | (last_kp & kStKMask);
             boundary = false;
         } else {  // a boundary: walks restart here
             seed = s << kStBShift;
@@ -528,7 +518,7 @@ struct Core {
         }
         wave_sync();
         if (lane == 0) {
-            r.state = 2;
+            r.set_state(2);
             st_state(vs, kStSettled | par_bits | seed);
         }
         wave_sync();
@@ -551,7 +541,7 @@ struct Core {
             const SpecialStatic ss = sp[s];
             for (uint32_t h = lane; h < p.n_hubs; h += 64) {
                 const uint32_t t = hubs[h];
-                if (t == s || R[t].state == 2) continue;
+                if (t == s || R[t].state() == 2) continue;
                 const SpecialStatic st = sp[t];
                 const uint32_t d = uint32_t(abs(ss.x - st.x) + abs(ss.y - st.y));
                 const uint32_t coef = st.coef5 ? 5u : 2u;
@@ -579,7 +569,7 @@ struct Core {
         const uint32_t lane = lane_id();
         uint32_t mine = kNone32;
         for (uint32_t t = 1 + lane; t <= p.NS; t += 64) {
-            if (R[t].state != 1) continue;
+            if (R[t].state() != 1) continue;
             const unsigned long long k = key_rec(t);
             if (k < K) flag(kErrBucket);
             if (k > K) continue;
@@ -636,16 +626,7 @@ struct Core {
         }
         my = c;
         st = 1;
-        Rec &r = R[t];
-        r.m[0] = c.m0;
-        r.m[1] = c.m1;
-        r.m[2] = c.m2;
-        r.len = uint16_t(c.len);
-        r.ntail = uint8_t(c.ntail);
-        r.parent = uint16_t(c.parent);
-        r.tail[0] = c.t0;
-        r.tail[1] = c.t1;
-        r.state = 1;
+        write_rec(t, c, 1);
     }
     template <class OnSettle>
     __device__ __forceinline__ void specials_reg(unsigned long long K, uint32_t par_bits, OnSettle on_settle) const {
@@ -656,7 +637,7 @@ struct Core {
         uint32_t st = 0;
         SpecialStatic ss{};
         if (mine) {
-            st = R[t].state;
+            st = R[t].state();
             view_rec(t, my);
             ss = sp[t];
         } else {
@@ -690,7 +671,7 @@ struct Core {
             if (t == s) st = 2;
             wave_sync();
             if (t == 0) {
-                R[s].state = 2;
+                R[s].set_state(2);
                 st_state(sS.v, kStSettled | par_bits | seed);
             }
             on_settle(s, sS.v, boundary);
@@ -720,7 +701,7 @@ struct Core {
         const DevParams &p = P;
         unsigned long long smin = kInf64;
         for (uint32_t t = 1 + lane_id(); t <= p.NS; t += 64)
-            if (R[t].state == 1) {
+            if (R[t].state() == 1) {
                 const unsigned long long k = key_rec(t);
                 if (k < smin) smin = k;
             }
@@ -755,7 +736,7 @@ struct Core {
         } else {
             for (uint32_t v = tid; v < p.V; v += kBS) state[v] = kStUntouched | a->sinfo[v];
         }
-        for (uint32_t t = tid; t <= p.NS; t += kBS) R[t].state = 0;
+        for (uint32_t t = tid; t <= p.NS; t += kBS) R[t].set_state(0);
         const uint32_t q0 = a->q_begin[s_idx], q1 = a->q_begin[s_idx + 1];
         if (tid == 0) sh->ndst = q1 - q0;
         if (q1 - q0 <= a->early_exit_max)
@@ -811,9 +792,11 @@ struct Core {
         uint32_t pp = x.parent;
         while (pp != 0 && pos >= 0) {
             const Rec &r = R[pp];
-            for (int j = int(r.ntail) - 1; j >= 0 && pos >= 0; --j, --pos)
-                oc[pos] = OutCmd{r.tail[j].kp, r.tail[j].from, r.tail[j].to, 0};
-            pp = r.parent;
+            for (int j = int(r.ntail()) - 1; j >= 0 && pos >= 0; --j, --pos) {
+                const Cmd cj = rec_tail(pp, j);
+                oc[pos] = OutCmd{cj.kp, cj.from, cj.to, 0};
+            }
+            pp = r.parent();
         }
         if (pos != -1 || pp != 0) flag(kErrChain);
         o = OutResult{x.m0, x.m1, x.m2, (status << 16) | (x.len & 0xFFFFu)};
@@ -876,13 +859,7 @@ struct Core {
     __device__ __forceinline__ void seed_root() const {
         View st;
         view_start(st);
-        Rec &r0 = R[0];  // entry 0: the source, root of every command chain
-        r0.m[0] = r0.m[1] = r0.m[2] = 0;
-        r0.len = 1;
-        r0.ntail = 1;
-        r0.parent = 0;
-        r0.tail[0] = st.t0;
-        r0.state = 2;
+        write_rec(0, st, 2);  // entry 0: the source, root of every command chain
     }
 };
 
@@ -917,7 +894,7 @@ struct LegsSolver : Core<G> {
         const uint32_t t1 = this->add32(r1.m[2], this->run_time(k1)), t2 = this->add32(r2.m[2], this->run_time(k2));
         int c = this->cmp_metrics(L, r1.m[1], t1, L, r2.m[1], t2);
         if (c) return c;
-        const uint32_t l1 = (b1 == 0 ? 0u : r1.len), l2 = (b2 == 0 ? 0u : r2.len);
+        const uint32_t l1 = (b1 == 0 ? 0u : r1.len()), l2 = (b2 == 0 ? 0u : r2.len());
         if (l1 != l2) return l1 < l2 ? -1 : 1;
         if (b1 == b2) return 0;
         View x, y;  // equal prefix lengths >= 1: both are table entries; compare full(b1), full(b2)
@@ -945,7 +922,7 @@ struct LegsSolver : Core<G> {
             if (key == kInf64) continue;
             best64[t] = kInf64;
             fired[t] = 1;
-            if (R[t].state == 2) continue;
+            if (R[t].state() == 2) continue;
             const uint32_t u = a->rank_inv[uint32_t(key)];
             const uint32_t su = this->ld_state(u);
             View c;
@@ -1198,7 +1175,7 @@ struct GenericSolver : Core<G> {
             if (u == kNone32) continue;
             best[t] = kNone32;
             fired[t] = 1;
-            if (R[t].state == 2) continue;
+            if (R[t].state() == 2) continue;
             const uint32_t su = this->ld_state(u);
             View c;
             this->soe_from_plain((su >> kStBShift) & kNone10, su & kStKMask, rank[u], t, c);
@@ -1697,8 +1674,8 @@ struct HubSolver : Core<false> {
         const long long tb = R[b].m[2], tq = R[q].m[2], lb = R[b].m[0], lq = R[q].m[0];
         const long long mb = R[b].m[1], mq = R[q].m[1];
         // the walks' lengths (the source's walk replaces its NoMove: length 1)
-        const long long nq0 = q == 0 ? 1 : R[q].len, nq1 = q == 0 ? 1 : R[q].len + 1;
-        const long long nb0 = b == 0 ? 1 : R[b].len, nb1 = b == 0 ? 1 : R[b].len + 1;
+        const long long nq0 = q == 0 ? 1 : R[q].len(), nq1 = q == 0 ? 1 : R[q].len() + 1;
+        const long long nb0 = b == 0 ? 1 : R[b].len(), nb1 = b == 0 ? 1 : R[b].len() + 1;
         auto cell = [&](int k, int &ux, int &uy) {
             if (x_first) {
                 ux = k < kx ? bx + sx * k : vx;
@@ -1928,8 +1905,8 @@ struct HubSolver : Core<false> {
                 bool less;
                 if (bi == 0 || bj == 0) {
                     less = bi == 0;
-                } else if (R[bi].len != R[bj].len) {
-                    less = R[bi].len < R[bj].len;
+                } else if (R[bi].len() != R[bj].len()) {
+                    less = R[bi].len() < R[bj].len();
                 } else {
                     View xi, xj;
                     view_rec(bi, xi);
@@ -2060,7 +2037,7 @@ struct HubSolver : Core<false> {
             unsigned int *d = reinterpret_cast<unsigned int *>(a->dbg);
             const uint32_t *rw = reinterpret_cast<const uint32_t *>(&R[t]);
             if (t <= p.NS)
-                for (int i = 0; i < 11; ++i) d[t * 16 + i] = rw[i];
+                for (int i = 0; i < 7; ++i) d[t * 16 + i] = rw[i];
             d[t * 16 + 11] = st;
             d[t * 16 + 12] = my.m0;
             d[t * 16 + 13] = my.m1;
@@ -2598,8 +2575,12 @@ __host__ __device__ inline WideLayout wide_layout(uint32_t NS, uint32_t nreg) {
     return L;
 }
 
+#ifndef MR_WIDE_WAVES
+#define MR_WIDE_WAVES 3  // waves per SIMD the wide kernel's register budget is cut for: 3 ran c5 27 %
+                         // faster than 2 (LDS holds 3 workgroups of 28 B label tables); 4 spilled 480 B
+#endif
 template <uint32_t PERM, uint32_t SPL>
-__global__ __launch_bounds__(kBS) void hub_wide_kernel(const KArgs *__restrict__ a) {
+__global__ __launch_bounds__(kBS, MR_WIDE_WAVES) void hub_wide_kernel(const KArgs *__restrict__ a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint32_t NS = a->p.NS, nreg = a->nreg;
     const WideLayout L = wide_layout(NS, nreg);

@@ -9,8 +9,8 @@
 //    L(b).commands ++ [StandardMove{k} b->v] from a *boundary* b that is the
 //    source or a special (src/cost.rs:246-264 merges the run).  Such a label is
 //    stored in ONE 32-bit word: (b, k).
-//  * specials (<= ~300) keep full labels in an LDS table as a parent pointer
-//    plus <= 2 tail commands; command lists compare by walking parents.
+//  * specials (<= ~1000) keep full labels in an LDS table as a parent pointer
+//    plus <= 2 tail commands (Rec); command lists compare by walking parents.
 // Vertices are settled bucket by bucket on the comparator's leading metric
 // (plain vertices of one bucket are independent), specials inside a bucket by
 // an exact one-wave Dijkstra.
@@ -43,16 +43,27 @@ struct Cmd {
 
 // A full label of a special (or the source), src/cost.rs:187-206:
 //   commands = full(parent) ++ tail[0..ntail)   (parent 0 = empty prefix)
+// Stored in 28 B: every label the engine builds (the start label, walks, SoE from a
+// region cell, TotalCost += edge, SHQ/SFm) has tail[0] = {kp0, from0 = the rank of
+// the parent entry's cell (the source's for parent 0), u} and, when ntail = 2,
+// tail[1] = {SoE, u, rank of the entry's own cell}; u is the own cell's rank when
+// ntail = 1.
 struct Rec {
-    uint32_t m[3];     // legs, money, time  (metric index order)
-    uint16_t len;      // commands.len()
-    uint8_t ntail;     // 1 or 2
-    uint8_t state;     // 0 none, 1 tentative, 2 settled
-    uint16_t parent;   // table index of the prefix label, 0 = root
-    uint16_t pad;
-    Cmd tail[2];
+    uint32_t m[3];  // legs, money, time  (metric index order)
+    uint32_t meta;  // len (16 b) | parent (10 b) << 16 | state (2 b) << 26 | (ntail - 1) << 31
+    uint32_t kp0;   // tail[0].kp
+    uint32_t from0; // tail[0].from
+    uint32_t u;     // tail[0].to (= tail[1].from when ntail = 2)
+    __host__ __device__ uint32_t len() const { return meta & 0xFFFFu; }
+    __host__ __device__ uint32_t parent() const { return (meta >> 16) & 0x3FFu; }
+    __host__ __device__ uint32_t state() const { return (meta >> 26) & 3u; }  // 0 none, 1 tentative, 2 settled
+    __host__ __device__ uint32_t ntail() const { return (meta >> 31) + 1u; }
+    __host__ __device__ void set_state(uint32_t st) { meta = (meta & ~(3u << 26)) | (st << 26); }
+    __host__ __device__ static uint32_t pack(uint32_t len, uint32_t parent, uint32_t ntail, uint32_t state) {
+        return (len & 0xFFFFu) | ((parent & 0x3FFu) << 16) | ((state & 3u) << 26) | ((ntail - 1u) << 31);
+    }
 };
-static_assert(sizeof(Rec) == 44, "Rec layout");
+static_assert(sizeof(Rec) == 28, "Rec layout");
 
 // Static per-special info (one entry per table index 1..NS; entry 0 unused).
 struct SpecialStatic {

@@ -1355,15 +1355,13 @@ static int check_device_errors(mr_plan *pl, uint32_t &flags) {
             const uint32_t *r = &d[t * 16];
             const uint32_t v = t ? pl->hp.sp[t].v : pl->ka.dbg_blocks;
             const mr_cell_index &c = pl->grid->idx[v];
-            std::fprintf(stderr, "T%2u (%u,%u,%u,%u) R.m=(%u,%u,%u) len=%u ntail=%u state=%u par=%u", t, c.kind, c.sub,
-                         c.x, c.y, r[0], r[1], r[2], r[3] & 0xFFFF, (r[3] >> 16) & 0xFF, r[3] >> 24, r[4] & 0xFFFF);
-            for (uint32_t i = 0; i < 2; ++i) {
-                const uint32_t f = r[6 + 3 * i], to = r[7 + 3 * i];
-                const mr_cell_index &cf = pl->grid->idx[pl->grid->rank_inv[f < pl->grid->V ? f : 0]];
-                const mr_cell_index &ct = pl->grid->idx[pl->grid->rank_inv[to < pl->grid->V ? to : 0]];
-                std::fprintf(stderr, " [k%u p%u (%u,%u,%u,%u)->(%u,%u,%u,%u)]", r[5 + 3 * i] >> 29, r[5 + 3 * i] & 0x1FFFFFFF,
-                             cf.kind, cf.sub, cf.x, cf.y, ct.kind, ct.sub, ct.x, ct.y);
-            }
+            Rec rec;
+            std::memcpy(&rec, r, sizeof(Rec));
+            const uint32_t ut = rec.u < pl->grid->V ? rec.u : 0;
+            const mr_cell_index &cu = pl->grid->idx[pl->grid->rank_inv[ut]];
+            std::fprintf(stderr, "T%2u (%u,%u,%u,%u) R.m=(%u,%u,%u) len=%u ntail=%u state=%u par=%u k%u p%u u=(%u,%u,%u,%u)",
+                         t, c.kind, c.sub, c.x, c.y, r[0], r[1], r[2], rec.len(), rec.ntail(), rec.state(), rec.parent(),
+                         rec.kp0 >> 29, rec.kp0 & 0x1FFFFFFF, cu.kind, cu.sub, cu.x, cu.y);
             std::fprintf(stderr, " st=%u my=(%u,%u,%u) %08x\n", r[11], r[12], r[13], r[14], r[15]);
         }
     }
@@ -1634,12 +1632,16 @@ extern "C" int mr_sssp_label(mr_plan *pl, uint32_t i, mr_cell_index dst, mr_resu
     if (!expand_word(pl->hp, tab, word, rec)) return fail(MR_ERR_DEVICE, "cell word names no table entry");
     const uint32_t src = pl->hp.src_v[si];
     std::vector<OutCmd> seq;
+    // rank of table entry e's cell (entry 0: the source)
+    auto rk = [&](uint32_t e) { return g->rank[e == 0 ? src : pl->hp.sp[e].v]; };
     auto chain = [&](uint32_t t) {  // commands of table label t (parent 0 ends the chain)
         std::vector<uint32_t> path;
-        for (uint32_t e = t, guard = 0; e != 0 && guard <= T; e = tab[e].parent, ++guard) path.push_back(e);
-        for (size_t j = path.size(); j-- > 0;)
-            for (uint32_t c = 0; c < tab[path[j]].ntail; ++c)
-                seq.push_back(OutCmd{tab[path[j]].tail[c].kp, tab[path[j]].tail[c].from, tab[path[j]].tail[c].to, 0});
+        for (uint32_t e = t, guard = 0; e != 0 && guard <= T; e = tab[e].parent(), ++guard) path.push_back(e);
+        for (size_t j = path.size(); j-- > 0;) {
+            const Rec &r = tab[path[j]];  // tails as Rec (mr_engine.hpp) derives them
+            seq.push_back(OutCmd{r.kp0, r.from0, r.u, 0});
+            if (r.ntail() == 2) seq.push_back(OutCmd{kSoE << 29, r.u, rk(path[j]), 0});
+        }
     };
     if (rec.via == kViaSource) {
         seq.push_back(OutCmd{kNoMove << 29, g->rank[src], g->rank[src], 0});
