@@ -1431,6 +1431,40 @@ template <uint32_t LPS>
 __device__ __forceinline__ uint32_t seg_max_u32(uint32_t x) {
     return ~seg_min_u32<LPS>(~x);
 }
+// every segment of wave ballot `bal` has at most one lane set (SALU: the ballot is uniform)
+template <uint32_t LPS>
+__device__ __forceinline__ bool seg_single(unsigned long long bal) {
+    if constexpr (LPS == 64) return __popcll(bal) <= 1;
+    else return __popc(uint32_t(bal)) <= 1 && __popc(uint32_t(bal >> 32)) <= 1;
+}
+// Keeps in c, per segment, the lanes holding the smallest (k1, k2, k3, len) and returns
+// the final ballot; stops once every segment has at most one lane left.  The first
+// round narrows on k1 and k2 packed into one word (k1 saturated to W1 bits, k2 to
+// 32 - W1): packing is monotone, so the survivors are exactly the lanes of the least
+// (k1, k2) unless the least packed word holds a saturated field, in which case k1 and
+// k2 get rounds of their own.
+template <uint32_t LPS, uint32_t W1>
+__device__ __forceinline__ unsigned long long seg_narrow(bool &c, uint32_t k1, uint32_t k2, uint32_t k3, uint32_t len) {
+    constexpr uint32_t M1 = (1u << W1) - 1u, M2 = (W1 == 0u) ? 0xFFFFFFFFu : (0xFFFFFFFFu >> W1);
+    unsigned long long bal = __ballot(c);
+    if (seg_single<LPS>(bal)) return bal;
+    const uint32_t pk = (min(k1, M1) << (32u - W1)) | min(k2, M2);
+    const uint32_t m = seg_min_u32<LPS>(c ? pk : 0xFFFFFFFFu);
+    c = c && pk == m;
+    bal = __ballot(c);
+    if (seg_single<LPS>(bal)) return bal;
+    if (__any(c && ((m >> (32u - W1)) == M1 || (m & M2) == M2))) {  // a saturated field: exact rounds
+        narrow_seg<LPS>(c, k1);
+        narrow_seg<LPS>(c, k2);
+        bal = __ballot(c);
+        if (seg_single<LPS>(bal)) return bal;
+    }
+    narrow_seg<LPS>(c, k3);
+    bal = __ballot(c);
+    if (seg_single<LPS>(bal)) return bal;
+    narrow_seg<LPS>(c, len);
+    return __ballot(c);
+}
 
 template <uint32_t SPW>
 struct HubSolver : Core<false> {
@@ -1483,17 +1517,16 @@ struct HubSolver : Core<false> {
     // table and compare command lists.  Returns the segment lane, or kNone32.
     __device__ __forceinline__ uint32_t select_reg(bool c, const RLab &my, uint32_t own) const {
         const DevParams &p = P;
-        unsigned long long m = seg_bits<LPS>(__ballot(c));
         const uint32_t mm3[3] = {my.m0, my.m1, my.m2};
-        const uint32_t keys[4] = {mm3[p.perm[0]], mm3[p.perm[1]], mm3[p.perm[2]], rl_len(my)};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (__all(__popcll(m) <= 1)) break;
-            narrow_seg<LPS>(c, keys[i]);
-            m = seg_bits<LPS>(__ballot(c));
-        }
+        // (the packed first round: a time-first key takes 20 bits, legs or money 16)
+        unsigned long long bal;
+        if (p.perm[0] == 2u)
+            bal = seg_narrow<LPS, 20u>(c, mm3[p.perm[0]], mm3[p.perm[1]], mm3[p.perm[2]], rl_len(my));
+        else
+            bal = seg_narrow<LPS, 16u>(c, mm3[p.perm[0]], mm3[p.perm[1]], mm3[p.perm[2]], rl_len(my));
+        const unsigned long long m = seg_bits<LPS>(bal);
         uint32_t win = __popcll(m) == 1 ? uint32_t(__ffsll((long long)m) - 1) : kNone32;
-        if (__any(__popcll(m) > 1)) {
+        if (!seg_single<LPS>(bal)) {
             const bool tied = __popcll(m) > 1;
             const uint32_t t = seg_lane();
             if (tied && c) write_rec(t, expand(my, own), 1);
@@ -1824,16 +1857,14 @@ struct HubSolver : Core<false> {
             view_walk(bj, walk_dist(bx, by, wx, wy), wr, c);
             bool cand = usable && plain;
             // metric by metric, until every segment has at most one candidate left
-            const uint32_t keys[4] = {metric(c, p.perm[0]), metric(c, p.perm[1]), metric(c, p.perm[2]), c.len};
-            unsigned long long m = seg_bits<LPS>(__ballot(cand));
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (__all(__popcll(m) <= 1)) break;
-                narrow_seg<LPS>(cand, keys[k]);
-                m = seg_bits<LPS>(__ballot(cand));
-            }
+            unsigned long long bal;
+            if (p.perm[0] == 2u)
+                bal = seg_narrow<LPS, 20u>(cand, metric(c, p.perm[0]), metric(c, p.perm[1]), metric(c, p.perm[2]), c.len);
+            else
+                bal = seg_narrow<LPS, 16u>(cand, metric(c, p.perm[0]), metric(c, p.perm[1]), metric(c, p.perm[2]), c.len);
+            const unsigned long long m = seg_bits<LPS>(bal);
             uint32_t win = __popcll(m) >= 1 ? uint32_t(__ffsll((long long)m) - 1) : 0u;
-            if (__any(__popcll(m) > 1)) {  // equal metrics and length: compare the command lists
+            if (!seg_single<LPS>(bal)) {  // equal metrics and length: compare the command lists
                 const bool tied = __popcll(m) > 1;
                 uint32_t mm = (tied && cand) ? t : kNone32;
 #pragma unroll
@@ -2290,15 +2321,10 @@ struct HubWide : HubSolver<1> {
             any = any || c[i];
         }
         bool cand = any;
-        unsigned long long m = __ballot(cand);
-        if (m == 0) return kNone32;
-        const uint32_t keys[4] = {metric(bv, p.perm[0]), metric(bv, p.perm[1]), metric(bv, p.perm[2]), rl_len(bv)};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (__popcll(m) <= 1) break;
-            narrow(cand, keys[i]);
-            m = __ballot(cand);
-        }
+        if (__ballot(cand) == 0) return kNone32;
+        const unsigned long long m =
+            p.perm[0] == 2u ? seg_narrow<64, 20u>(cand, metric(bv, p.perm[0]), metric(bv, p.perm[1]), metric(bv, p.perm[2]), rl_len(bv))
+                            : seg_narrow<64, 16u>(cand, metric(bv, p.perm[0]), metric(bv, p.perm[1]), metric(bv, p.perm[2]), rl_len(bv));
         if (__popcll(m) == 1) return bcast(bt, uint32_t(__ffsll((long long)m) - 1));
         // equal metrics and length in several lanes: compare the command lists
         if (cand) write_rec(bt, expand(bv, bown), 1);
