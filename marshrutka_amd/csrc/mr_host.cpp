@@ -732,7 +732,8 @@ struct mr_plan {
     OutCmd *d_cmd = nullptr;
     uint32_t *d_ws = nullptr, *d_counter = nullptr;
     hipStream_t stream = nullptr;
-    hipEvent_t ev_last = nullptr;         // recorded on the caller's stream at the end of every pass
+    hipEvent_t ev_last = nullptr;         // the end event of the latest pass (on the caller's stream)
+    bool ev_last_orphan = false;          // ev_last was folded out of `timed` and is owned here
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;  // pending event pairs
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timed_fill;  // all-destinations: fill launches
     // timings of event pairs already folded (a caller that never asks for kernel_ms
@@ -740,20 +741,46 @@ struct mr_plan {
     double acc_ms = 0.0, acc_fill_ms = 0.0;
     uint32_t acc_n = 0, acc_fill_n = 0;
     int device = 0;
-    // All-destinations plans run the specials' solve of pass k + 1 (hub and fallback
-    // kernels, on hub_stream) beside the fill of pass k (on the caller's stream).  The
-    // per-pass buffers and kernel arguments come in two slots; the d_* fields above
-    // always name the slot of the latest pass, `alt` the other one (swap_slot).
+    // All-destinations plans run the specials' solves of the next passes (hub kernels,
+    // in order on the plan's hub stream) beside the fill of pass k (on the caller's
+    // stream).  The per-pass buffers and kernel arguments come in slots taken round
+    // robin; the d_* fields above always name the slot of the latest pass (use_slot).
+    // One hub stream for every slot: more streams than the process's hardware queues
+    // (GPU_MAX_HW_QUEUES, 4) alias, and a hub queued behind a fill serialises the two.
     struct Slot {
         Rec *tab = nullptr;
         uint32_t *lex = nullptr, *sstate = nullptr, *fb = nullptr, *counter = nullptr;
         KArgs *args = nullptr, *args_fb = nullptr, *args_fill = nullptr;
-    } alt;
+        hipEvent_t ev_hub = nullptr, ev_fill = nullptr;
+        bool used = false;  // a pass has run in this slot
+    };
+    std::vector<Slot> slots;  // slot 0 holds the plan's first buffers; empty: no overlap
+    hipStream_t hub_stream = nullptr;
     bool overlap = false;
     uint32_t slot = 0;  // slot index of the d_* fields
-    hipStream_t hub_stream = nullptr;
-    hipEvent_t ev_hub[2] = {nullptr, nullptr}, ev_fill[2] = {nullptr, nullptr};
     ~mr_plan() {
+        if (!slots.empty()) {  // the d_* fields may name another slot: free each slot's once
+            Slot &k = slots[0];
+            d_tab = k.tab;
+            d_lex = k.lex;
+            d_sstate = k.sstate;
+            d_fb = k.fb;
+            d_counter = k.counter;
+            d_args = k.args;
+            d_args_fb = k.args_fb;
+            d_args_fill = k.args_fill;
+            k.tab = nullptr;
+            k.lex = k.sstate = k.fb = k.counter = nullptr;
+            k.args = k.args_fb = k.args_fill = nullptr;
+        }
+        for (Slot &k : slots) {
+            for (void *p : {(void *)k.tab, (void *)k.lex, (void *)k.sstate, (void *)k.fb, (void *)k.counter,
+                            (void *)k.args, (void *)k.args_fb, (void *)k.args_fill})
+                if (p) (void)hipFree(p);
+            for (hipEvent_t e : {k.ev_hub, k.ev_fill})
+                if (e) (void)hipEventDestroy(e);
+        }
+        if (hub_stream) (void)hipStreamDestroy(hub_stream);
         for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_rank_inv, (void *)d_src, (void *)d_qb, (void *)d_qd,
                         (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
                         (void *)d_counter, (void *)d_args, (void *)d_dbg, (void *)d_args_fb, (void *)d_near,
@@ -761,12 +788,7 @@ struct mr_plan {
                         (void *)d_tab,
                         (void *)d_lex, (void *)d_sstate, (void *)d_near_sp, (void *)d_rb_off, (void *)d_rb_cell, (void *)d_ovf})
             if (p) (void)hipFree(p);
-        for (void *p : {(void *)alt.tab, (void *)alt.lex, (void *)alt.sstate, (void *)alt.fb, (void *)alt.counter,
-                        (void *)alt.args, (void *)alt.args_fb, (void *)alt.args_fill})
-            if (p) (void)hipFree(p);
-        for (hipEvent_t e : {ev_hub[0], ev_hub[1], ev_fill[0], ev_fill[1], ev_last})
-            if (e) (void)hipEventDestroy(e);
-        if (hub_stream) (void)hipStreamDestroy(hub_stream);
+        if (ev_last && ev_last_orphan) (void)hipEventDestroy(ev_last);
         for (auto &e : timed) {
             (void)hipEventDestroy(e.first);
             (void)hipEventDestroy(e.second);
@@ -777,23 +799,23 @@ struct mr_plan {
     }
 };
 
-// all-destinations overlap: make the other slot's buffers and argument blocks current
-static void swap_slot(mr_plan *pl) {
-    mr_plan::Slot &a = pl->alt;
-    std::swap(pl->d_tab, a.tab);
-    std::swap(pl->d_lex, a.lex);
-    std::swap(pl->d_sstate, a.sstate);
-    std::swap(pl->d_fb, a.fb);
-    std::swap(pl->d_counter, a.counter);
-    std::swap(pl->d_args, a.args);
-    std::swap(pl->d_args_fb, a.args_fb);
-    std::swap(pl->d_args_fill, a.args_fill);
-    pl->ka.out_tab = pl->d_tab;
-    pl->ka.out_lex = pl->d_lex;
-    pl->ka.src_state = pl->d_sstate;
-    pl->ka.fb_list = pl->d_fb;
-    pl->ka.counter = pl->d_counter;
-    pl->slot ^= 1u;
+// all-destinations overlap: make slot i's buffers and argument blocks current
+static void use_slot(mr_plan *pl, uint32_t i) {
+    const mr_plan::Slot &k = pl->slots[i];
+    pl->d_tab = k.tab;
+    pl->d_lex = k.lex;
+    pl->d_sstate = k.sstate;
+    pl->d_fb = k.fb;
+    pl->d_counter = k.counter;
+    pl->d_args = k.args;
+    pl->d_args_fb = k.args_fb;
+    pl->d_args_fill = k.args_fill;
+    pl->ka.out_tab = k.tab;
+    pl->ka.out_lex = k.lex;
+    pl->ka.src_state = k.sstate;
+    pl->ka.fb_list = k.fb;
+    pl->ka.counter = k.counter;
+    pl->slot = i;
 }
 
 // Kernel-argument blocks of a plan: the main launch, and for hub plans the fallback
@@ -992,31 +1014,50 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
 #endif
     if (hipMalloc(reinterpret_cast<void **>(&pl->d_args), sizeof(KArgs)) != hipSuccess || upload_args(pl) != MR_OK)
         return bail(fail(MR_ERR_DEVICE, "kernel args"));
-    // all destinations with the hub: a second slot of per-pass buffers, so that the
-    // specials' solve of the next pass overlaps this pass's fill (MR_FILL_OVERLAP=0: off)
+    // all destinations with the hub: slots of per-pass buffers, so that the specials'
+    // solves of the next passes overlap this pass's fill (MR_FILL_OVERLAP=0: off;
+    // MR_FILL_SLOTS: the slot count, 2..8, default 2 — at c3 the specials' solve of a
+    // pass is shorter than a fill, and 3 or 4 slots measured the same pass time)
     const char *ov = std::getenv("MR_FILL_OVERLAP");
     if (all_mode && hp.hub && !(ov && !std::strcmp(ov, "0"))) {
+        uint32_t nslots = 2;
+        if (const char *e = std::getenv("MR_FILL_SLOTS")) nslots = uint32_t(std::min(8, std::max(2, std::atoi(e))));
         const size_t T = size_t(NS) + 1, ns = std::max<size_t>(nsrc, 1);
-        mr_plan::Slot &a = pl->alt;
-        if (hipMalloc(reinterpret_cast<void **>(&a.tab), ns * T * sizeof(Rec)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&a.lex), ns * T * 4) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&a.sstate), ns * 4) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&a.fb), ns * 4) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&a.counter), kCtrWords * 4) != hipSuccess ||
-            hipMemset(a.counter, 0, kCtrWords * 4) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&a.args), sizeof(KArgs)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&a.args_fb), sizeof(KArgs)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&a.args_fill), sizeof(KArgs)) != hipSuccess ||
-            hipStreamCreateWithFlags(&pl->hub_stream, hipStreamNonBlocking) != hipSuccess)
-            return bail(fail(MR_ERR_DEVICE, "second all-destinations slot"));
-        for (int i = 0; i < 2; ++i)
-            if (hipEventCreateWithFlags(&pl->ev_hub[i], hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&pl->ev_fill[i], hipEventDisableTiming) != hipSuccess)
-                return bail(fail(MR_ERR_DEVICE, "overlap events"));
-        swap_slot(pl);
-        const int ua = upload_args(pl);
-        swap_slot(pl);
-        if (ua != MR_OK) return bail(fail(MR_ERR_DEVICE, "kernel args"));
+        pl->slots.resize(nslots);
+        mr_plan::Slot &k0 = pl->slots[0];
+        k0.tab = pl->d_tab;
+        k0.lex = pl->d_lex;
+        k0.sstate = pl->d_sstate;
+        k0.fb = pl->d_fb;
+        k0.counter = pl->d_counter;
+        k0.args = pl->d_args;
+        k0.args_fb = pl->d_args_fb;
+        k0.args_fill = pl->d_args_fill;
+        for (uint32_t i = 0; i < nslots; ++i) {
+            mr_plan::Slot &k = pl->slots[i];
+            if (i > 0 &&
+                (hipMalloc(reinterpret_cast<void **>(&k.tab), ns * T * sizeof(Rec)) != hipSuccess ||
+                 hipMalloc(reinterpret_cast<void **>(&k.lex), ns * T * 4) != hipSuccess ||
+                 hipMalloc(reinterpret_cast<void **>(&k.sstate), ns * 4) != hipSuccess ||
+                 hipMalloc(reinterpret_cast<void **>(&k.fb), ns * 4) != hipSuccess ||
+                 hipMalloc(reinterpret_cast<void **>(&k.counter), kCtrWords * 4) != hipSuccess ||
+                 hipMemset(k.counter, 0, kCtrWords * 4) != hipSuccess ||
+                 hipMalloc(reinterpret_cast<void **>(&k.args), sizeof(KArgs)) != hipSuccess ||
+                 hipMalloc(reinterpret_cast<void **>(&k.args_fb), sizeof(KArgs)) != hipSuccess ||
+                 hipMalloc(reinterpret_cast<void **>(&k.args_fill), sizeof(KArgs)) != hipSuccess))
+                return bail(fail(MR_ERR_DEVICE, "all-destinations slots"));
+            if (hipEventCreateWithFlags(&k.ev_hub, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&k.ev_fill, hipEventDisableTiming) != hipSuccess)
+                return bail(fail(MR_ERR_DEVICE, "overlap streams"));
+            if (i > 0) {
+                use_slot(pl, i);
+                const int ua = upload_args(pl);
+                use_slot(pl, 0);
+                if (ua != MR_OK) return bail(fail(MR_ERR_DEVICE, "kernel args"));
+            }
+        }
+        if (hipStreamCreateWithFlags(&pl->hub_stream, hipStreamNonBlocking) != hipSuccess)
+            return bail(fail(MR_ERR_DEVICE, "hub stream"));
         pl->overlap = true;
     }
     *out = pl;
@@ -1048,24 +1089,24 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : pl->stream;
     if (pl->ka.nsrc == 0) return MR_OK;
     if (pl->timed.size() >= kMaxTimed) fold_timed(pl, kMaxTimed / 4);
-    if (!pl->ev_last && hipEventCreateWithFlags(&pl->ev_last, hipEventDisableTiming) != hipSuccess)
-        return fail(MR_ERR_DEVICE, "event");
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (hipEventCreate(&e0) != hipSuccess) return fail(MR_ERR_DEVICE, "event");
     if (hipEventCreate(&e1) != hipSuccess) {
         (void)hipEventDestroy(e0);
         return fail(MR_ERR_DEVICE, "event");
     }
-    // overlap plans: this pass takes the other slot once its last fill has released
-    // it; nothing is launched or recorded before that wait is in place
-    if (pl->hp.hub && pl->all_mode && pl->overlap && pl->runs >= 1) {
-        swap_slot(pl);
-        if (hipStreamWaitEvent(pl->hub_stream, pl->ev_fill[pl->slot], 0) != hipSuccess) {
-            swap_slot(pl);
+    // overlap plans: this pass takes the next slot once the fill that last read it has
+    // released it; nothing is launched or recorded before that wait is in place
+    if (pl->hp.hub && pl->all_mode && pl->overlap) {
+        const uint32_t prev = pl->slot, next = pl->runs >= 1 ? (pl->slot + 1) % uint32_t(pl->slots.size()) : 0u;
+        use_slot(pl, next);
+        if (pl->slots[next].used && hipStreamWaitEvent(pl->hub_stream, pl->slots[next].ev_fill, 0) != hipSuccess) {
+            use_slot(pl, prev);
             (void)hipEventDestroy(e0);
             (void)hipEventDestroy(e1);
             return fail(MR_ERR_DEVICE, "wait");
         }
+        pl->slots[next].used = true;
     }
     (void)hipEventRecord(e0, s);
     hipError_t e;
@@ -1078,14 +1119,15 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         uint32_t gx = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((items + 3) / 4, uint64_t(pl->fill_per_cu) * pl->cus)));
         if (const char *e = std::getenv("MR_FILL_GX")) gx = uint32_t(std::max(1, std::atoi(e)));
         const uint32_t gy = 1;
-        // overlap: this pass took the other slot above, and its hub kernel runs on
-        // hub_stream behind the wait for the fill two passes back.  The hub writes only
-        // the slot's tables; everything that writes the records (the SSSP kernel for
+        // overlap: this pass took its slot above, and its hub kernel runs on the slot's
+        // stream behind the wait for the fill that last read the slot.  The hub writes
+        // only the slot's tables; everything that writes the records (the SSSP kernel for
         // flagged sources, the fill) stays on the caller's stream, in stream order.
         hipStream_t hs = pl->overlap ? pl->hub_stream : s;
         e = launch_hub_plan(pl, pl->d_args, hs);
         if (e == hipSuccess && pl->overlap) {
-            if (hipEventRecord(pl->ev_hub[pl->slot], hs) != hipSuccess || hipStreamWaitEvent(s, pl->ev_hub[pl->slot], 0) != hipSuccess)
+            if (hipEventRecord(pl->slots[pl->slot].ev_hub, hs) != hipSuccess ||
+                hipStreamWaitEvent(s, pl->slots[pl->slot].ev_hub, 0) != hipSuccess)
                 e = hipErrorUnknown;
         }
         if (e == hipSuccess && !pl->fb_none)
@@ -1094,7 +1136,7 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         if (e == hipSuccess && hipEventCreate(&f0) == hipSuccess) (void)hipEventRecord(f0, s);
         if (e == hipSuccess) e = launch_fill(pl->d_args_fill, pl->ka.p.perm, gx, gy, s);
         // the slot's tables are free again once this fill has read them
-        if (e == hipSuccess && pl->overlap && hipEventRecord(pl->ev_fill[pl->slot], s) != hipSuccess)
+        if (e == hipSuccess && pl->overlap && hipEventRecord(pl->slots[pl->slot].ev_fill, s) != hipSuccess)
             e = hipErrorUnknown;
         pl->timed_fill.push_back({f0, nullptr});  // one per pass (f0 may be null), as in `timed`
     } else if (pl->hp.hub && pl->fb_none) {
@@ -1111,7 +1153,11 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         e = launch_solve(pl->d_args, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->blocks, s);
     }
     (void)hipEventRecord(e1, s);
-    (void)hipEventRecord(pl->ev_last, s);
+    // the pass's end event doubles as the plan's last event (plan_sync): a record of
+    // its own cost ~6 us of command-processor time per pass
+    if (pl->ev_last_orphan) (void)hipEventDestroy(pl->ev_last);
+    pl->ev_last = e1;
+    pl->ev_last_orphan = false;
     pl->timed.push_back({e0, e1});
     if (!pl->timed_fill.empty() && !pl->timed_fill.back().second) pl->timed_fill.back().second = e1;
     if (e != hipSuccess) return fail(MR_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(e));
@@ -1161,7 +1207,8 @@ static void fold_timed(mr_plan *pl, size_t keep) {
             ++pl->acc_n;
         }
         (void)hipEventDestroy(e.first);
-        (void)hipEventDestroy(e.second);
+        if (e.second == pl->ev_last) pl->ev_last_orphan = true;  // plan_sync still waits on it
+        else (void)hipEventDestroy(e.second);
     }
     pl->timed.erase(pl->timed.begin(), pl->timed.begin() + ptrdiff_t(n));
 }
@@ -1335,17 +1382,19 @@ static int check_device_errors(mr_plan *pl, uint32_t &flags) {
     if (int st = read_counters(pl, ctr)) return st;
     flags = ctr[kCtrFlags];
     if (flags) (void)hipMemset(pl->d_counter + kCtrFlags, 0, 4);  // collected
-    // overlap plans: the other slot's counter block belongs to the pass before the
-    // latest one; its flags and written count are checked (and collected) as well
-    if (pl->overlap && pl->runs >= 2) {
-        uint32_t alt[kCtrWords];
-        if (hipMemcpy(alt, pl->alt.counter, kCtrWords * 4, hipMemcpyDeviceToHost) != hipSuccess)
+    // overlap plans: the other slots' counter blocks belong to earlier passes; their
+    // flags and written counts are checked (and collected) as well
+    for (uint32_t i = 0; i < pl->slots.size(); ++i) {
+        const mr_plan::Slot &k = pl->slots[i];
+        if (i == pl->slot || !k.used) continue;
+        uint32_t oc[kCtrWords];
+        if (hipMemcpy(oc, k.counter, kCtrWords * 4, hipMemcpyDeviceToHost) != hipSuccess)
             return fail(MR_ERR_DEVICE, "copy counter");
-        if (alt[kCtrFlags]) (void)hipMemset(pl->alt.counter + kCtrFlags, 0, 4);
-        flags |= alt[kCtrFlags];
-        if (flags == 0 && alt[kCtrLastWritten] != pl->hp.q_id.size())
-            return fail(MR_ERR_DEVICE, "internal: " + std::to_string(alt[kCtrLastWritten]) + " of " +
-                                           std::to_string(pl->hp.q_id.size()) + " records written (previous pass)");
+        if (oc[kCtrFlags]) (void)hipMemset(k.counter + kCtrFlags, 0, 4);
+        flags |= oc[kCtrFlags];
+        if (flags == 0 && oc[kCtrLastWritten] != pl->hp.q_id.size())
+            return fail(MR_ERR_DEVICE, "internal: " + std::to_string(oc[kCtrLastWritten]) + " of " +
+                                           std::to_string(pl->hp.q_id.size()) + " records written (an earlier pass)");
     }
 #ifdef MR_HUBDUMP
     if (pl->d_dbg) {

@@ -170,13 +170,14 @@ def test_fill_ragged_last_tile_column(eng, oracle_lib, monkeypatch, flags, pi):
             assert as_expected(plan.label(i, cells[j])) == as_expected(exp[j]), (s, cells[j])
 
 
-@pytest.mark.parametrize("fb", [False, True])
-def test_overlapped_passes_match_serial(eng, oracle_lib, monkeypatch, fb):
-    """All-destinations passes alternate between two slots of label tables, the
-    specials' solve of pass k + 1 running beside the fill of pass k (mr_plan_run).
+@pytest.mark.parametrize("fb,slots", [(False, 2), (True, 2), (False, 3), (True, 3)])
+def test_overlapped_passes_match_serial(eng, oracle_lib, monkeypatch, fb, slots):
+    """All-destinations passes take slots of label tables round robin, the specials'
+    solves of the next passes running beside the fill of pass k (mr_plan_run).
     Back-to-back passes (no host sync between them) must leave the records and
-    labels of one serial pass (MR_FILL_OVERLAP=0), after an odd and an even number
-    of passes, with and without sources handed to the SSSP kernel."""
+    labels of one serial pass (MR_FILL_OVERLAP=0), after every count of passes up to
+    a wrap round the slots, with and without sources handed to the SSSP kernel."""
+    monkeypatch.setenv("MR_FILL_SLOTS", str(slots))
     monkeypatch.delenv("MR_ALGO", raising=False)
     monkeypatch.delenv("MR_FILL_GX", raising=False)
     monkeypatch.delenv("MR_DBG_FLAGS", raising=False)
@@ -197,7 +198,7 @@ def test_overlapped_passes_match_serial(eng, oracle_lib, monkeypatch, fb):
     plan = eng.SSSPPlan(g, Params(), sources)
     assert plan.stats()["solver"] == "hub"
     dsts = rng.sample(cells, 12)
-    for passes in (1, 2, 3):
+    for passes in (1, 2, 3, 4):
         for _ in range(passes):
             plan.run()
         for i in range(len(sources)):
@@ -206,21 +207,23 @@ def test_overlapped_passes_match_serial(eng, oracle_lib, monkeypatch, fb):
                 assert as_expected(plan.label(i, d)) == as_expected(ref.label(i, d)), (passes, i, d)
 
 
-@pytest.mark.parametrize("inject_slot,passes", [(0, 2), (1, 3), (0, 4)])
+@pytest.mark.parametrize("inject_slot,passes", [(0, 2), (1, 3), (2, 4), (0, 5)])
 def test_overlap_error_of_either_slot_is_reported(eng, monkeypatch, inject_slot, passes):
-    """A device error flag raised by a pass whose slot is not the current one (the
-    other overlap slot) must still be reported, then collected."""
+    """A device error flag raised by a pass whose slot is not the current one (an
+    earlier overlap slot) must still be reported, then collected."""
     for k in ("MR_ALGO", "MR_FILL_GX", "MR_DBG_FLAGS", "MR_HUB_FALLBACK_ALL", "MR_FILL_OVERLAP"):
         monkeypatch.delenv(k, raising=False)
+    nslots = 3
+    monkeypatch.setenv("MR_FILL_SLOTS", str(nslots))
     m = SyntheticMap(33, campfires_per_homeland=3, seed=5)
     sources = m.all_indices()[:4]
     g = eng.MapGrid(m.cells())
     monkeypatch.setenv("MR_DBG_INJECT_SLOT", str(inject_slot))
     plan = eng.SSSPPlan(g, Params(), sources)
     monkeypatch.delenv("MR_DBG_INJECT_SLOT")
-    # pass p (1-based) runs in slot (p - 1) % 2; after `passes` passes the current slot
-    # is (passes - 1) % 2, and the injected slot's last pass is the other one
-    assert (passes - 1) % 2 != inject_slot
+    # pass p (1-based) runs in slot (p - 1) % nslots; after `passes` passes the current
+    # slot is (passes - 1) % nslots, and the injected slot ran an earlier pass
+    assert (passes - 1) % nslots != inject_slot and passes > inject_slot
     for _ in range(passes):
         plan.run()
     with pytest.raises(eng.EngineError):
