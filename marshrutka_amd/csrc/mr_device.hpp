@@ -2815,9 +2815,17 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
             B[5][r] = (lane << kStBShift) - e0;  // full compare (fill_tile_rows): + the cell's legs
         }
         wave_sync();
-        // prune on the lead metric (the full compare: on the first one, every boundary)
+        // rank `lane`'s boundary position and key in registers: the boundary loop reads
+        // them with v_readlane (no LDS round trip per boundary and tile)
+        const uint32_t bx_l = lane < nb ? B[0][lane] : 0u, by_l = lane < nb ? B[1][lane] : 0u;
+        const uint32_t px_l = lane < T ? P[0][lane] : 0u, py_l = lane < T ? P[1][lane] : 0u;  // specials by table index
+        const uint32_t bk_l = lane < nb && packable ? B[6][lane] : 0u;
+        // prune on the lead metric (the full compare: on the first one, every boundary);
+        // whether rank `lane`'s boundary is kept (Money first) is read off its key
         const uint32_t PL = packable ? L : q0;
         const uint64_t sP = packable ? sL : sl[q0];
+        const uint32_t pb_l = lane < nb ? B[2 + PL][lane] : 0u;
+        const bool cnd = lane < nb && (!packable || bk_l != 0xFFFFFFFFu);
         // ---- this wave's tiles of the source ---------------------------------------
         CellWord *const outs = a->out_rec + (unsigned long long)s * V;
         for (uint32_t tile = j; tile < ntile; tile += G) {
@@ -2827,31 +2835,56 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
             // Prune the boundaries whose lead metric is beaten everywhere in the tile:
             // lo_b > min over b' of hi_b' (walks are at least the L1 distance to the tile
             // and at most the farthest corner's plus the 2-cell detour round the Center).
-            unsigned long long lo = ~0ull, hi = ~0ull;
-            // rank `lane`'s boundary; whether it is kept (Money first) is read off its key
-            const bool cnd = lane < nb && (!packable || B[6][lane] != 0xFFFFFFFFu);
-            if (cnd) {
-                const int bxx = int(B[0][lane]), byy = int(B[1][lane]);
-                const int dx = bxx < x0 ? x0 - bxx : (bxx > x1 ? bxx - x1 : 0);
-                const int dy = byy < y0 ? y0 - byy : (byy > y1 ? byy - y1 : 0);
-                const int fx = max(abs(bxx - x0), abs(bxx - x1)), fy = max(abs(byy - y0), abs(byy - y1));
-                const uint32_t base = B[2 + PL][lane];
-                lo = base + sP * uint64_t(dx + dy);
-                hi = base + sP * uint64_t(fx + fy + 2);
-            }
+            const int bxx_l = int(bx_l), byy_l = int(by_l);
+            const int dx = bxx_l < x0 ? x0 - bxx_l : (bxx_l > x1 ? bxx_l - x1 : 0);
+            const int dy = byy_l < y0 ? y0 - byy_l : (byy_l > y1 ? byy_l - y1 : 0);
+            const int fx = max(abs(bxx_l - x0), abs(bxx_l - x1)), fy = max(abs(byy_l - y0), abs(byy_l - y1));
+            unsigned long long live;
+            if (packable) {  // the lead fits 32 bits (<= mxL): DPP wave mins, no LDS round trips
+                const uint32_t sP32 = uint32_t(sP);
+                const uint32_t lo = pb_l + sP32 * uint32_t(dx + dy);
+                const uint32_t hi = cnd ? pb_l + sP32 * uint32_t(fx + fy + 2) : 0xFFFFFFFFu;
+                const uint32_t hmin = wave_min_u32(hi);
+                // Corner dominance: L1(b*, c) - L1(b, c) splits into an x and a y term, each
+                // monotone in its coordinate, so over the tile its maximum sits at a corner.
+                // A boundary b* whose lead, with the 2-cell Center detour as slack, beats b's
+                // at all four corners beats it at every cell of the tile (strictly, on the
+                // lead), and b is dropped.  b* = the least lead at the tile's centre.
+                const int cxm = (x0 + x1) >> 1, cym = (y0 + y1) >> 1;
+                const uint32_t vc = cnd ? pb_l + sP32 * uint32_t(abs(bxx_l - cxm) + abs(byy_l - cym)) : 0xFFFFFFFFu;
+                const uint32_t vmin = wave_min_u32(vc);
+                const unsigned long long bs = __ballot(cnd && vc == vmin);
+                const int star = bs ? __ffsll((long long)bs) - 1 : 0;
+                const uint32_t c00 = pb_l + sP32 * uint32_t(abs(bxx_l - x0) + abs(byy_l - y0));
+                const uint32_t c10 = pb_l + sP32 * uint32_t(abs(bxx_l - x1) + abs(byy_l - y0));
+                const uint32_t c01 = pb_l + sP32 * uint32_t(abs(bxx_l - x0) + abs(byy_l - y1));
+                const uint32_t c11 = pb_l + sP32 * uint32_t(abs(bxx_l - x1) + abs(byy_l - y1));
+                const uint32_t slack = 2u * sP32;
+                // b*'s corners read with every lane active (a v_readlane of a value computed
+                // under a narrower exec mask reads a stale register), then compared without
+                // short-circuit branches
+                const uint32_t s00 = uint32_t(__builtin_amdgcn_readlane(int(c00), star)) + slack;
+                const uint32_t s10 = uint32_t(__builtin_amdgcn_readlane(int(c10), star)) + slack;
+                const uint32_t s01 = uint32_t(__builtin_amdgcn_readlane(int(c01), star)) + slack;
+                const uint32_t s11 = uint32_t(__builtin_amdgcn_readlane(int(c11), star)) + slack;
+                const bool dom = (bs != 0ull) & (s00 < c00) & (s10 < c10) & (s01 < c01) & (s11 < c11);
+                live = __ballot(cnd && ((lo <= hmin && !dom) || no_prune));
+            } else {
+                unsigned long long lo = ~0ull, hi = ~0ull;
+                if (cnd) {
+                    lo = pb_l + sP * uint64_t(dx + dy);
+                    hi = pb_l + sP * uint64_t(fx + fy + 2);
+                }
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const unsigned long long h2 = __shfl_xor(hi, o);
-                hi = h2 < hi ? h2 : hi;
+                for (int o = 32; o > 0; o >>= 1) {
+                    const unsigned long long h2 = __shfl_xor(hi, o);
+                    hi = h2 < hi ? h2 : hi;
+                }
+                live = __ballot(cnd && (lo <= hi || no_prune));
             }
-            const unsigned long long live = __ballot(cnd && (lo <= hi || no_prune));
             // the specials (and the source) inside this tile
-            bool in = false;
-            if (lane < T) {
-                const int px = int(P[0][lane]) - x0, py = int(P[1][lane]) - y0;
-                in = px >= 0 && px < kTW && py >= 0 && py < kTH;
-            }
-            const unsigned long long sp_in = __ballot(in);
+            const int px = int(px_l) - x0, py = int(py_l) - y0;
+            const unsigned long long sp_in = __ballot(lane < T && px >= 0 && px < kTW && py >= 0 && py < kTH);
             const bool axis = (x0 <= 0 && x1 >= 0) || (y0 <= 0 && y1 >= 0);
             if (packable) {
                 // the least key per cell (column c = lane + 64k, row i at k * kTH + i)
@@ -2863,34 +2896,50 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
                 // they get a loop of their own after the others
                 unsigned long long axm = 0;
                 if (axis) {
-                    const bool on = lane < nb && (B[0][lane] == 0u || B[1][lane] == 0u);
+                    const bool on = lane < nb && (bx_l == 0u || by_l == 0u);
                     axm = __ballot(on) & live;
                 }
                 for (unsigned long long m = live & ~axm; m; m &= m - 1) {
                     const uint32_t rr = uint32_t(__ffsll((long long)m) - 1);
-                    // wave-uniform values in SGPRs, so the per-row step is a scalar select
-                    const int bxx = __builtin_amdgcn_readfirstlane(int(B[0][rr]));
-                    const int istar = __builtin_amdgcn_readfirstlane(int(B[1][rr])) - y0;  // the boundary's row in the tile
-                    const uint32_t K = uint32_t(__builtin_amdgcn_readfirstlane(int(B[6][rr])));
+                    // wave-uniform values in SGPRs
+                    const int bxx = __builtin_amdgcn_readlane(int(bx_l), int(rr));
+                    const int istar = __builtin_amdgcn_readlane(int(by_l), int(rr)) - y0;  // the boundary's row in the tile
+                    const uint32_t K = uint32_t(__builtin_amdgcn_readlane(int(bk_l), int(rr)));
                     const uint32_t up = stepL, down = 0u - stepL;
+                    // down a column the walk distance moves by +-1 per row, so the key by
+                    // +-stepL; a boundary above (below) the tile's rows steps every row the
+                    // same way, which needs no per-row select
+                    if (istar <= 0 || istar >= kTH - 1) {
+                        const uint32_t step = istar <= 0 ? up : down;
 #pragma unroll
-                    for (int k = 0; k < kCPL; ++k) {
-                        // down a column the walk distance moves by +-1 per row, so the key by +-stepL
-                        const int wx = x0 + 64 * k + int(lane);
-                        uint32_t key = K + stepL * (uint32_t(abs(bxx - wx)) + uint32_t(abs(istar)));
+                        for (int k = 0; k < kCPL; ++k) {
+                            const int wx = x0 + 64 * k + int(lane);
+                            uint32_t key = K + stepL * (uint32_t(abs(bxx - wx)) + uint32_t(abs(istar)));
 #pragma unroll
-                        for (int i = 0; i < kTH; ++i) {
-                            if (i > 0) key += i > istar ? up : down;
-                            kb[k * kTH + i] = min(kb[k * kTH + i], key);
+                            for (int i = 0; i < kTH; ++i) {
+                                if (i > 0) key += step;
+                                kb[k * kTH + i] = min(kb[k * kTH + i], key);
+                            }
+                        }
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < kCPL; ++k) {
+                            const int wx = x0 + 64 * k + int(lane);
+                            uint32_t key = K + stepL * (uint32_t(abs(bxx - wx)) + uint32_t(abs(istar)));
+#pragma unroll
+                            for (int i = 0; i < kTH; ++i) {
+                                if (i > 0) key += i > istar ? up : down;
+                                kb[k * kTH + i] = min(kb[k * kTH + i], key);
+                            }
                         }
                     }
                 }
                 for (unsigned long long m = axm; m; m &= m - 1) {
                     const uint32_t rr = uint32_t(__ffsll((long long)m) - 1);
-                    const int bxx = __builtin_amdgcn_readfirstlane(int(B[0][rr]));
-                    const int byy = __builtin_amdgcn_readfirstlane(int(B[1][rr]));
+                    const int bxx = __builtin_amdgcn_readlane(int(bx_l), int(rr));
+                    const int byy = __builtin_amdgcn_readlane(int(by_l), int(rr));
                     const int istar = byy - y0, i0 = -y0;  // i0: the tile's row y = 0
-                    const uint32_t K = uint32_t(__builtin_amdgcn_readfirstlane(int(B[6][rr])));
+                    const uint32_t K = uint32_t(__builtin_amdgcn_readlane(int(bk_l), int(rr)));
                     const uint32_t up = stepL, down = 0u - stepL, det2 = 2u * stepL;
 #pragma unroll
                     for (int k = 0; k < kCPL; ++k) {
