@@ -168,43 +168,37 @@ def algorithmic_bytes(plan, stats, V):
     return float(b), name, survey
 
 
-def label_digest(pairs):
-    """sha256 over (global query id, label) pairs in id order."""
-    import hashlib
-    h = hashlib.sha256()
-    for qid, lab in sorted(pairs, key=lambda t: t[0]):
-        h.update(repr((qid, as_expected(lab))).encode())
-    return h.hexdigest()
-
-
 def check_gather(pipe, plan, k, grid, params, shards, orders, counts, rows, rw, cw, ovf_cap, rank, world):
     """After the timed region (N > 1): rank 0 decodes every record of the last batch
     as gathered (result records, command slots, overflow pool of each rank) on the
-    host, maps record k of rank r to its query shards[r][orders[r][k]], and compares
-    the labels with each rank's own fetch of that batch (a digest per rank).  Returns
-    the check's summary on rank 0."""
+    host, puts record j of rank r at its query shards[r][orders[r][j]], and compares
+    the labels with each rank's own fetch of that batch (mr_plan_fetch, in the rank's
+    query order): one digest per rank.  Returns the check's summary on rank 0."""
+    import numpy as np
     import torch.distributed as dist
     from marshrutka_amd import pathfinder
-    own = plan.fetch()  # this rank's labels, in its local query order
+    res, pool = plan.fetch_raw()  # this rank's labels, in its local query order
     digests = [None] * world
-    dist.all_gather_object(digests, label_digest([(shards[rank][i], lab) for i, lab in enumerate(own)]))
+    dist.all_gather_object(digests, pathfinder.labels_digest(res, pool, counts[rank]))
     if rank != 0:
         return None
-    bad_status, mismatched, seen = 0, 0, set()
+    bad_status, mismatched, seen = 0, 0, np.zeros(sum(counts), dtype=bool)
     for r, buf in enumerate(pipe.out[k]):
         words = buf.to("cpu").numpy().view("uint32")
         n = counts[r]
-        res = words[: n * rw]
+        rres = words[: n * rw]
         slots = words[rows * rw: rows * rw + n * cw]
         ovf = words[rows * (rw + cw): rows * (rw + cw) + ovf_cap * 4]
-        st = res.reshape(-1, rw)[:, 3] >> 16
+        st = rres.reshape(-1, rw)[:, 3] >> 16
         bad_status += int(((st != 16) & (st != 17) & (st != 80)).sum())
-        labels = pathfinder.decode_records(grid, params, res, slots, n, cw // 4, ovf)
-        pairs = [(shards[r][orders[r][j]], lab) for j, lab in enumerate(labels)]
-        seen.update(q for q, _ in pairs)
-        if label_digest(pairs) != digests[r]:
+        out, opool = pathfinder.decode_records_raw(grid, params, rres, slots, n, cw // 4, ovf)
+        order = np.asarray(orders[r][:n], dtype=np.int64)  # record j answers local query order[j]
+        inv = np.empty(n, dtype=np.int64)
+        inv[order] = np.arange(n)  # local query i is record inv[i]
+        seen[np.asarray(shards[r], dtype=np.int64)[order]] = True
+        if pathfinder.labels_digest(out, opool, n, inv) != digests[r]:
             mismatched += 1
-    return {"rows": sum(counts), "bad_status": bad_status, "queries_covered": len(seen),
+    return {"rows": sum(counts), "bad_status": bad_status, "queries_covered": int(seen.sum()),
             "ranks_matching_own_fetch": world - mismatched, "ranks": world}
 
 

@@ -287,12 +287,11 @@ class FindPath:
         return out
 
 
-def decode_records(grid: MapGrid, params: Params, results, commands, n: int, max_cmds: int,
-                   overflow=None) -> List[Optional[TotalCost]]:
+def decode_records_raw(grid: MapGrid, params: Params, results, commands, n: int, max_cmds: int, overflow=None):
     """Compact device records (mr_plan_device_outputs layout: 16 B result records,
     max_cmds 16 B command slots each, an overflow pool) as host buffers — e.g. the
-    rows another rank gathered — decoded into labels, record k -> entry k.  Host
-    only (mr_decode_records).  A record whose status is not OK / NOT_FOUND raises."""
+    rows another rank gathered — decoded on the host (mr_decode_records): returns the
+    (mr_result array, mr_command pool), record k -> entry k."""
     import numpy as np
     res = np.ascontiguousarray(results, dtype=np.uint32)
     cmd = np.ascontiguousarray(commands, dtype=np.uint32)
@@ -307,10 +306,40 @@ def decode_records(grid: MapGrid, params: Params, results, commands, n: int, max
                                  ovf.ctypes.data if ovf.size else None, ovf.size // 4, out, pool, cap)
     if st != MR_OK:
         raise EngineError(st, last_error())
+    return out, pool
+
+
+def decode_records(grid: MapGrid, params: Params, results, commands, n: int, max_cmds: int,
+                   overflow=None) -> List[Optional[TotalCost]]:
+    """decode_records_raw as labels.  A record whose status is not OK / NOT_FOUND raises."""
+    out, pool = decode_records_raw(grid, params, results, commands, n, max_cmds, overflow)
     for k in range(n):
         if out[k].status not in (MR_OK, MR_NOT_FOUND):
             raise EngineError(out[k].status, f"record {k}")
     return [result_from_c(out[k], pool) for k in range(n)]
+
+
+def labels_digest(results, pool, n: int, order=None) -> str:
+    """sha256 over n decoded labels (mr_result array + command pool, as mr_plan_fetch
+    or decode_records_raw return them), taken in `order` (entry order[i] first..., or
+    entry order by default): metrics, command count, status, then the commands.
+    Numpy only, so a rank's million labels hash in well under a second."""
+    import hashlib
+    import numpy as np
+    rdt = np.dtype([("legs", "<u4"), ("money", "<u4"), ("time_s", "<i8"), ("n", "<u4"), ("off", "<u4"),
+                    ("status", "<i4"), ("reserved", "<u4")])
+    r = np.frombuffer(results, dtype=rdt, count=n)
+    if order is not None:
+        r = r[np.asarray(order, dtype=np.int64)]
+    ncmd = r["n"].astype(np.int64)
+    cmds = np.frombuffer(pool, dtype=np.uint8).reshape(-1, C.sizeof(mr_command))
+    starts = np.repeat(r["off"].astype(np.int64), ncmd)
+    within = np.arange(int(ncmd.sum()), dtype=np.int64) - np.repeat(np.cumsum(ncmd) - ncmd, ncmd)
+    h = hashlib.sha256()
+    for f in ("legs", "money", "time_s", "n", "status"):
+        h.update(np.ascontiguousarray(r[f]).tobytes())
+    h.update(cmds[starts + within].tobytes())
+    return h.hexdigest()
 
 
 class Plan:

@@ -148,3 +148,25 @@ def test_decode_records_on_host(eng):
     bad[0, 1, 2] = 49
     with pytest.raises(eng.EngineError, match="DEVICE"):
         eng.decode_records(g, p, res, bad, 3, 2, pool)
+
+
+def test_labels_digest_follows_query_order(eng):
+    """labels_digest (the N > 1 gather check): the same labels stored in another
+    order hash alike once the order is given, and differently without it."""
+    import numpy as np
+    from marshrutka_amd.abi import mr_command, mr_result
+    n, perm = 4, [2, 0, 3, 1]
+    res, pool = (mr_result * n)(), (mr_command * (2 * n))()
+    res2, pool2 = (mr_result * n)(), (mr_command * (2 * n))()
+    for i in range(n):
+        res[i].legs, res[i].n_commands, res[i].command_offset = i, 2, 2 * i
+        for c in range(2):
+            pool[2 * i + c].kind, pool[2 * i + c].money = c, 10 * i + c
+    for k, i in enumerate(perm):  # record k holds query i
+        res2[k].legs, res2[k].n_commands, res2[k].command_offset = i, 2, 2 * k
+        for c in range(2):
+            pool2[2 * k + c].kind, pool2[2 * k + c].money = c, 10 * i + c
+    inv = np.empty(n, dtype=np.int64)
+    inv[np.array(perm)] = np.arange(n)
+    assert eng.labels_digest(res2, pool2, n, inv) == eng.labels_digest(res, pool, n)
+    assert eng.labels_digest(res2, pool2, n) != eng.labels_digest(res, pool, n)
