@@ -394,6 +394,22 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    # the issue side of the roofline (the hub kernels are instruction-bound, DESIGN.md
+    # section 5): SQ instruction counts per launch from a committed SQ pass of the same
+    # workload, VALU busy = VALU wave-instructions x 2 cycles (wave64 on a SIMD-32)
+    # over 1 024 SIMDs x the kernel's time at the 2.4 GHz peak clock
+    issue = None
+    sq_path = os.path.join(ROOT, "profiles", f"sq_{args.workload}.json")
+    if os.path.exists(sq_path) and kms > 0:
+        try:
+            with open(sq_path) as f:
+                sq = json.load(f)["per_launch"]
+            busy = sq["SQ_INSTS_VALU"] * 2.0 / (1024 * kms * 1e-3 * 2.4e9)
+            issue = {"valu_per_launch": sq["SQ_INSTS_VALU"], "salu_per_launch": sq["SQ_INSTS_SALU"],
+                     "lds_per_launch": sq["SQ_INSTS_LDS"], "valu_busy_frac_at_2_4GHz": busy,
+                     "source": os.path.relpath(sq_path, ROOT)}
+        except (OSError, ValueError, KeyError):
+            issue = None
     out = {
         "metric": METRIC, "value": value, "unit": "queries/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -411,7 +427,7 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": kernel_name, "kernel_ms": kms, "launches": nl,
                      "pass_ms": pass_ms if all_dst else kms,
-                     "alg_bytes_per_launch": alg_bytes,
+                     "alg_bytes_per_launch": alg_bytes, "issue": issue,
                      "survey_8d_bytes_per_launch": survey_bytes,
                      "note": ("all destinations: fill kernel, V x 4 B per source (the cell word written; no per-cell "
                               "read) + 80 B per table entry; survey_8d_bytes_per_launch is SURVEY 8d's V x 20 B; "
