@@ -2239,6 +2239,10 @@ __device__ __forceinline__ void sel_view(bool take, View &d, const View &s) {
     d.t1.to = take ? s.t1.to : d.t1.to;
 }
 
+#ifndef MR_WIDE_REG_STATIC
+#define MR_WIDE_REG_STATIC 0  // owned specials' static records in registers up to this SPL: at 3 waves per
+                              // SIMD they spilled 156 B per lane; read from LDS the kernel spills none (c5 -0.5 %)
+#endif
 template <uint32_t SPL>
 struct HubWide : HubSolver<1> {
     using B = HubSolver<1>;
@@ -2438,9 +2442,9 @@ struct HubWide : HubSolver<1> {
         uint32_t st[SPL], bwh[SPL], b0[SPL], b1[SPL], b2[SPL];
         bool mine[SPL];
         uint32_t unc = 0, nbk = 0;
-        // the owned specials' static records: in registers up to 5 per lane (LDS
-        // occupancy, not registers, bounds this kernel), else re-read from LDS
-        constexpr bool kRegStatic = SPL <= 5;
+        // the owned specials' static records: re-read from LDS (MR_WIDE_REG_STATIC: held
+        // in registers up to that many per lane)
+        constexpr bool kRegStatic = SPL <= MR_WIDE_REG_STATIC;
         SpecialStatic ssr[kRegStatic ? SPL : 1];
 #pragma unroll
         for (uint32_t i = 0; i < SPL; ++i)
