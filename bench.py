@@ -10,6 +10,8 @@ result records are gathered to rank 0 over RCCL.  Inputs are resident in HBM
 before the timed region starts.
 
 Workloads (BASELINE.json configs; odd sides per SURVEY.md §8a A14):
+  c1           one query on a 15x15 game-like map (configs[0]: plumbing; latency of
+               one query through the device path)
   c4 (default) the 1025x1025 map with 1M/8 = 125k uniform queries per GPU
                (configs[3] shard; weak scaling up to the 1M batch at N=8: the
                north-star target, >= 1e6 q/s on a 1024x1024 grid at 8 GPUs)
@@ -41,6 +43,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: Chip-level
 BYTES_PER_VERTEX_SOLVE = 20  # per full single-source solve, V x 20 B
 
 WORKLOADS = {
+    "c1": dict(size=15, queries_per_gpu=1, campfires=4, seed=15, max_cmds=16,
+               desc="configs[0]: one (src,dst) query on a 15x15 game-like synthetic map (no game map ships with "
+                    "the reference, SURVEY 8c), default FindPath params; a step is one whole query through the "
+                    "device path (the reference runs it on the CPU)"),
     # max_cmds: command slots per query record (what the N > 1 gather moves); the app's
     # default orders give labels of at most 4 commands on these maps, the Time-first c5
     # up to 14+; a longer label goes to the rank's overflow pool (its slot is tagged)
