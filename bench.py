@@ -369,7 +369,9 @@ def main():
         fms = plan.fill_ms()
         if stats["solver"] == "hub" and fms > 0:
             alg_bytes = float(n_src) * (V * 4 + (stats["num_specials"] + 1) * 80)
-            kernel_name, pass_ms, kms = "fill_kernel", kms, fms
+            # fused: the launch also solves the next pass's specials (priced as the fill's alone)
+            kernel_name = "hub_fill_kernel" if stats["fill_launch"] == "fused" else "fill_kernel"
+            pass_ms, kms = kms, fms
         else:
             kernel_name, pass_ms = "sssp_kernel", kms
     else:

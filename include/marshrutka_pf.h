@@ -249,7 +249,14 @@ typedef struct mr_plan_stats {
     uint32_t sssp_workgroups;   /* SSSP launch size */
     uint32_t specials_per_lane; /* hub solver: table entries each lane owns (1 = one per lane) */
     uint32_t region_boundary_cells; /* MR_SOLVER_HUB_WIDE: cells scanned for each source's region row */
+    uint32_t fill_launch;       /* all-destinations hub plans: MR_FILL_* (how the fill is launched) */
 } mr_plan_stats;
+enum {
+    MR_FILL_NONE = 0,    /* not an all-destinations hub plan */
+    MR_FILL_SERIAL = 1,  /* specials' solve, then the fill, on `stream` */
+    MR_FILL_STREAMS = 2, /* the specials' solve on a stream of the plan's own, beside the previous fill */
+    MR_FILL_FUSED = 3    /* one launch per pass: the fill + the next pass's specials' solve */
+};
 /* Fills *out; waits for the plan's stream.  MR_OK or MR_ERR_INVALID_ARG. */
 int mr_plan_get_stats(mr_plan *plan, mr_plan_stats *out);
 /* Average device time (ms) of the main solve kernel over the last
@@ -269,10 +276,11 @@ typedef struct mr_label_record {
 /* A plan answering every destination of each source: mr_plan_run computes
  * n_sources x V cell words on the device; mr_plan_kernel_ms / mr_plan_get_stats /
  * mr_plan_destroy apply.  Sources may repeat (they share a solve).  Each pass's
- * specials' solve runs on a stream of the plan's own, beside the previous pass's
- * fill, into one of two internal table slots (MR_FILL_OVERLAP=0: one slot, all on
- * `stream`); the records themselves are only written by work on `stream`, so a
- * pass's records are complete once `stream` has reached the end of its run. */
+ * specials' solve runs inside the previous pass's fill launch, into one of two
+ * internal table slots (the first pass solves its own first; MR_FILL_FUSED=0: on a
+ * stream of the plan's own beside the previous fill; MR_FILL_OVERLAP=0: one slot,
+ * all on `stream`); the records themselves are only written by work on `stream`, so
+ * a pass's records are complete once `stream` has reached the end of its run. */
 int mr_sssp_plan_create(const mr_grid *grid, const mr_params *params, const mr_cell_index *sources,
                         uint32_t n_sources, mr_plan **out);
 /* All-destinations plans: the fill launch's average time (ms) over the window the

@@ -1344,7 +1344,8 @@ struct GenericSolver : Core<G> {
 // End of a workgroup (thread 0, after a barrier): add its written records; in the
 // pass's last kernel the last workgroup to finish publishes the pass's counts and
 // zeroes the per-pass counters for the next pass.
-__device__ __forceinline__ void finish_launch(const KArgs *__restrict__ a, uint32_t written) {
+__device__ __forceinline__ void finish_launch(const KArgs *__restrict__ a, uint32_t written,
+                                              uint32_t nblocks = 0xFFFFFFFFu) {
     uint32_t *c = a->counter;
     if (!a->last_launch) {
         if (written) atomicAdd(c + kCtrWritten, written);
@@ -1359,7 +1360,10 @@ __device__ __forceinline__ void finish_launch(const KArgs *__restrict__ a, uint3
     static_assert(kCtrDone % 2 == 0 && kCtrWritten == kCtrDone + 1, "counter pair");
     const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long *>(c + kCtrDone),
                                              ((unsigned long long)written << 32) | 1ull);
-    if (uint32_t(old) == gridDim.x * gridDim.y * gridDim.z - 1) {  // the grid's last workgroup
+    // the grid's last workgroup (nblocks: the workgroups that count, when a launch fuses
+    // two kernels' work)
+    const uint32_t nb = nblocks != 0xFFFFFFFFu ? nblocks : gridDim.x * gridDim.y * gridDim.z;
+    if (uint32_t(old) == nb - 1) {
         __threadfence();
         const uint32_t fb = atomicAdd(c + kCtrFbCount, 0u), wr = uint32_t(old >> 32) + written,
                        ov = atomicAdd(c + kCtrOvf, 0u);
@@ -2143,9 +2147,10 @@ __host__ __device__ inline HubLayout hub_layout(uint32_t NS, uint32_t nreg, uint
 #define MR_HUB_WAVES 5  // waves per SIMD the register budget is cut for: 6 ran c4 3 % faster but its
                         // larger scratch spill (64 B/lane) overflowed L2: 0.6 GB of HBM traffic per launch
 #endif
+// the hub kernel's work as workgroup `block` of `nblocks` (a launch of its own, or the
+// first workgroups of a fused hub + fill launch, hub_fill_kernel)
 template <uint32_t PERM, uint32_t SPW, bool NONLIN>
-__global__ __launch_bounds__(kBS, MR_HUB_WAVES) void hub_kernel(const KArgs *__restrict__ a) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void hub_body(const KArgs *__restrict__ a, char *smem, uint32_t block, uint32_t nblocks) {
     const uint32_t NS = a->p.NS, nreg = a->nreg;
     const HubLayout L = hub_layout(NS, nreg, SPW);
     SpecialStatic *spl = reinterpret_cast<SpecialStatic *>(smem + L.off_sp);
@@ -2189,7 +2194,7 @@ __global__ __launch_bounds__(kBS, MR_HUB_WAVES) void hub_kernel(const KArgs *__r
 #endif
     // sources are strided over the launch's waves (no dequeue atomics: one word
     // would saturate at ~88 dequeues/us, MI355X_MICROARCH.md)
-    const uint32_t waves = gridDim.x * (kBS / 64), wid = blockIdx.x * (kBS / 64) + (threadIdx.x >> 6);
+    const uint32_t waves = nblocks * (kBS / 64), wid = block * (kBS / 64) + (threadIdx.x >> 6);
     for (uint32_t k = 0;; ++k) {
         const unsigned long long base = ((unsigned long long)k * waves + wid) * SPW;
 #ifdef MR_STAMPS
@@ -2204,13 +2209,18 @@ __global__ __launch_bounds__(kBS, MR_HUB_WAVES) void hub_kernel(const KArgs *__r
     __syncthreads();
     if (H.written) atomicAdd(&wsum, H.written);
     __syncthreads();
-    if (threadIdx.x == 0) finish_launch(a, wsum);
+    if (threadIdx.x == 0) finish_launch(a, wsum, nblocks);
 #ifdef MR_STAMPS
     if (lane_id() == 0 && a->dbg) {
         unsigned long long *h = a->dbg + (unsigned long long)a->dbg_blocks * 10;
         for (int i = 0; i < 9; ++i) atomicAdd(h + i, H.hs[i]);
     }
 #endif
+}
+template <uint32_t PERM, uint32_t SPW, bool NONLIN>
+__global__ __launch_bounds__(kBS, MR_HUB_WAVES) void hub_kernel(const KArgs *__restrict__ a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    hub_body<PERM, SPW, NONLIN>(a, smem, blockIdx.x, gridDim.x);
 }
 
 // ===================================================================================
@@ -2716,8 +2726,10 @@ __device__ __forceinline__ void fill_tile_rows(const uint32_t (*B)[64], unsigned
 #ifndef MR_FILL_WAVES
 #define MR_FILL_WAVES 6  // waves per SIMD the fill kernel is register-bounded to
 #endif
+// the fill's work as workgroup `block` of `nblocks` (its own launch, or the workgroups
+// after the hub's in a fused hub + fill launch)
 template <uint32_t PERM>
-__global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *__restrict__ a) {
+__device__ __forceinline__ void fill_body(const KArgs *__restrict__ a, uint32_t block, uint32_t nblocks) {
     constexpr uint32_t q0 = PERM / 9, q1 = (PERM / 3) % 3, q2 = PERM % 3;
     // per unit of walk distance: legs 1, money 0, time 180 s
     constexpr uint32_t sl[3] = {1u, 0u, 180u};
@@ -2735,8 +2747,8 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
     const int H = int(a->p.H);
     const uint32_t tpx = (S + kTW - 1) / kTW, tpy = (S + kTH - 1) / kTH, ntile = tpx * tpy;
     const bool no_prune = (a->dbg_flags & 1u) != 0, no_pack = (a->dbg_flags & 2u) != 0;
-    if ((a->dbg_flags & kDbgInjectFlag) && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a->counter + kCtrFlags, kErrChain);
-    const uint32_t nwaves = gridDim.x * (kBS / 64), gw = blockIdx.x * (kBS / 64) + wv;
+    if ((a->dbg_flags & kDbgInjectFlag) && block == 0 && threadIdx.x == 0) atomicOr(a->counter + kCtrFlags, kErrChain);
+    const uint32_t nwaves = nblocks * (kBS / 64), gw = block * (kBS / 64) + wv;
     const uint32_t ngroups = nsrc < nwaves ? nsrc : nwaves, G = nwaves / ngroups, g = gw / G, j = gw % G;
     const uint32_t s_begin = g < ngroups ? uint32_t(uint64_t(g) * nsrc / ngroups) : 0u;
     const uint32_t s_end = g < ngroups ? uint32_t(uint64_t(g + 1) * nsrc / ngroups) : 0u;
@@ -3003,7 +3015,23 @@ __global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *_
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) finish_launch(a, 0);
+    if (threadIdx.x == 0) finish_launch(a, 0, nblocks);
+}
+template <uint32_t PERM>
+__global__ __launch_bounds__(kBS, MR_FILL_WAVES) void fill_kernel(const KArgs *__restrict__ a) {
+    fill_body<PERM>(a, blockIdx.x, gridDim.x);
+}
+// All destinations, one launch per pass: the first hub_blocks workgroups solve the
+// specials of the NEXT pass into its slot (hub_a), the others fill this pass's cell
+// words from the tables the previous launch left (fill_a).  The specials' solve (~85 us
+// for 64 sources on 32 waves) then runs beside the fill with no cross-stream events.
+template <uint32_t PERM, uint32_t SPW>
+__global__ __launch_bounds__(kBS, MR_HUB_WAVES) void hub_fill_kernel(const KArgs *__restrict__ hub_a,
+                                                                     const KArgs *__restrict__ fill_a,
+                                                                     uint32_t hub_blocks) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if (blockIdx.x < hub_blocks) hub_body<PERM, SPW, false>(hub_a, smem, blockIdx.x, hub_blocks);
+    else fill_body<PERM>(fill_a, blockIdx.x - hub_blocks, gridDim.x - hub_blocks);
 }
 
 // ===================================================================================

@@ -30,6 +30,9 @@ hipError_t launch_hub(const KArgs *d_args, const uint32_t perm[3], uint32_t spw,
 hipError_t launch_fill(const KArgs *d_args, const uint32_t perm[3], uint32_t gx, uint32_t gy, hipStream_t stream);
 int hub_blocks_per_cu(const uint32_t perm[3], uint32_t spw, bool nonlin, uint32_t bytes);
 int fill_blocks_per_cu(const uint32_t perm[3]);
+hipError_t launch_hub_fill(const KArgs *hub_args, const KArgs *fill_args, const uint32_t perm[3], uint32_t spw,
+                           uint32_t hub_blocks, uint32_t fill_blocks, uint32_t lds_bytes, hipStream_t stream);
+int hub_fill_blocks_per_cu(const uint32_t perm[3], uint32_t spw, uint32_t lds_bytes);
 uint32_t hub_wide_lds_bytes(uint32_t NS, uint32_t nreg);
 uint32_t hub_wide_spl(uint32_t NS);
 hipError_t launch_hub_wide(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t blocks,
@@ -735,7 +738,12 @@ struct mr_plan {
     hipEvent_t ev_last = nullptr;         // the end event of the latest pass (on the caller's stream)
     bool ev_last_orphan = false;          // ev_last was folded out of `timed` and is owned here
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;  // pending event pairs
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> timed_fill;  // all-destinations: fill launches
+    // whole: the pass is the fill launch (the pass pair times it)
+    struct FillTimed {
+        hipEvent_t first, second;
+        bool whole;
+    };
+    std::vector<FillTimed> timed_fill;  // all-destinations: fill launches
     // timings of event pairs already folded (a caller that never asks for kernel_ms
     // must not pile up events: mr_plan_run folds the oldest beyond kMaxTimed)
     double acc_ms = 0.0, acc_fill_ms = 0.0;
@@ -757,6 +765,11 @@ struct mr_plan {
     std::vector<Slot> slots;  // slot 0 holds the plan's first buffers; empty: no overlap
     hipStream_t hub_stream = nullptr;
     bool overlap = false;
+    // overlap in one launch per pass (hub_fill_kernel): the specials of pass k + 1 are
+    // solved by the first workgroups of pass k's fill launch (MR_FILL_FUSED=0: the two
+    // streams instead)
+    bool fused = false;
+    uint32_t hub_lds = 0, fused_per_cu = 0;
     uint32_t slot = 0;  // slot index of the d_* fields
     ~mr_plan() {
         if (!slots.empty()) {  // the d_* fields may name another slot: free each slot's once
@@ -1059,6 +1072,12 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         if (hipStreamCreateWithFlags(&pl->hub_stream, hipStreamNonBlocking) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "hub stream"));
         pl->overlap = true;
+        const char *fz = std::getenv("MR_FILL_FUSED");
+        if (!hp.wide && !hp.nonlin && !(fz && !std::strcmp(fz, "0"))) {
+            pl->hub_lds = hub_lds_bytes(NS, hp.nreg, pl->spw);
+            pl->fused_per_cu = uint32_t(std::max(0, hub_fill_blocks_per_cu(hp.p.perm, pl->spw, pl->hub_lds)));
+            pl->fused = pl->fused_per_cu > 0;
+        }
     }
     *out = pl;
     return MR_OK;
@@ -1095,9 +1114,12 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         (void)hipEventDestroy(e0);
         return fail(MR_ERR_DEVICE, "event");
     }
-    // overlap plans: this pass takes the next slot once the fill that last read it has
-    // released it; nothing is launched or recorded before that wait is in place
-    if (pl->hp.hub && pl->all_mode && pl->overlap) {
+    if (pl->hp.hub && pl->all_mode && pl->fused) {  // one launch per pass, see below
+        const uint32_t cur = pl->runs >= 1 ? (pl->slot + 1) % uint32_t(pl->slots.size()) : 0u;
+        use_slot(pl, cur);
+    } else if (pl->hp.hub && pl->all_mode && pl->overlap) {
+        // overlap plans: this pass takes the next slot once the fill that last read it
+        // has released it; nothing is launched or recorded before that wait is in place
         const uint32_t prev = pl->slot, next = pl->runs >= 1 ? (pl->slot + 1) % uint32_t(pl->slots.size()) : 0u;
         use_slot(pl, next);
         if (pl->slots[next].used && hipStreamWaitEvent(pl->hub_stream, pl->slots[next].ev_fill, 0) != hipSuccess) {
@@ -1111,7 +1133,34 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     (void)hipEventRecord(e0, s);
     hipError_t e;
     ++pl->runs;
-    if (pl->hp.hub && pl->all_mode) {
+    if (pl->hp.hub && pl->all_mode && pl->fused) {
+        // Fused: this pass's specials were solved into its slot by the previous pass's
+        // launch (the first pass solves its own first).  The SSSP kernel takes the
+        // sources that solve flagged, then one launch fills this pass's cells while its
+        // first workgroups solve the next pass's specials into the next slot (which the
+        // previous launch's fill has finished reading: stream order).  Each pass thus runs
+        // one specials' solve and one fill; the last pass's look-ahead solve is extra work.
+        const uint32_t nslots = uint32_t(pl->slots.size()), cur = pl->slot, nxt = (cur + 1) % nslots;
+        const uint64_t items = uint64_t(pl->ka.nsrc) * ((pl->ka.p.S + kFillTW - 1) / kFillTW) *
+                               ((pl->ka.p.S + kFillTH - 1) / kFillTH);
+        const uint64_t resident = uint64_t(pl->fused_per_cu) * pl->cus;
+        const uint32_t fb_blocks = uint32_t(std::max<uint64_t>(
+            1, std::min<uint64_t>((items + 3) / 4, resident > pl->hub_blocks ? resident - pl->hub_blocks : 1)));
+        e = hipSuccess;
+        if (pl->runs == 1) e = launch_hub_plan(pl, pl->slots[cur].args, s);  // the first pass's specials
+        if (e == hipSuccess && !pl->fb_none)
+            e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, s);
+        // with no SSSP launch the pass is the fused launch: its time is the pass's (an
+        // event of its own costs command-processor time, see ev_last below)
+        hipEvent_t f0 = nullptr;
+        const bool own = pl->runs == 1 || !pl->fb_none;
+        if (e == hipSuccess && own && hipEventCreate(&f0) == hipSuccess) (void)hipEventRecord(f0, s);
+        if (e == hipSuccess)
+            e = launch_hub_fill(pl->slots[nxt].args, pl->slots[cur].args_fill, pl->ka.p.perm, pl->spw, pl->hub_blocks,
+                                fb_blocks, pl->hub_lds, s);
+        pl->slots[cur].used = true;  // a fill ran in it: its counters hold a finished pass
+        pl->timed_fill.push_back({f0, nullptr, !own});
+    } else if (pl->hp.hub && pl->all_mode) {
         // hub solve + table export, the SSSP kernel for flagged sources, then the fill:
         // (source, tile) items, one per wave, over a resident-sized grid
         const uint64_t items = uint64_t(pl->ka.nsrc) * ((pl->ka.p.S + kFillTW - 1) / kFillTW) *
@@ -1138,7 +1187,7 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         // the slot's tables are free again once this fill has read them
         if (e == hipSuccess && pl->overlap && hipEventRecord(pl->slots[pl->slot].ev_fill, s) != hipSuccess)
             e = hipErrorUnknown;
-        pl->timed_fill.push_back({f0, nullptr});  // one per pass (f0 may be null), as in `timed`
+        pl->timed_fill.push_back({f0, nullptr, false});  // one per pass (f0 may be null), as in `timed`
     } else if (pl->hp.hub && pl->fb_none) {
         // a pass of this plan (same inputs, deterministic result) had no fallback
         // sources: the hub launch ends the pass on its own
@@ -1190,8 +1239,10 @@ static void fold_timed(mr_plan *pl, size_t keep) {
     for (size_t i = 0; i < nf; ++i) {
         auto &f = pl->timed_fill[i];
         float ms = 0.f;
-        if (f.first && f.second && hipEventSynchronize(f.second) == hipSuccess &&
-            hipEventElapsedTime(&ms, f.first, f.second) == hipSuccess) {
+        // all-destinations plans push one pair to each list per pass: the lists align
+        const hipEvent_t f0 = f.whole && pl->timed.size() == pl->timed_fill.size() ? pl->timed[i].first : f.first;
+        if (f0 && f.second && hipEventSynchronize(f.second) == hipSuccess &&
+            hipEventElapsedTime(&ms, f0, f.second) == hipSuccess) {
             pl->acc_fill_ms += ms;
             ++pl->acc_fill_n;
         }
@@ -1277,6 +1328,10 @@ extern "C" int mr_plan_get_stats(mr_plan *pl, mr_plan_stats *out) {
     out->sssp_workgroups = pl->blocks;
     out->specials_per_lane = !pl->hp.hub ? 0u : (pl->hp.wide ? hub_wide_spl(pl->ka.p.NS) : 1u);
     out->region_boundary_cells = pl->hp.wide && pl->hp.rb_off && !pl->hp.rb_off->empty() ? pl->hp.rb_off->back() : 0u;
+    out->fill_launch = !(pl->hp.hub && pl->all_mode) ? MR_FILL_NONE
+                       : pl->fused                   ? MR_FILL_FUSED
+                       : pl->overlap                 ? MR_FILL_STREAMS
+                                                     : MR_FILL_SERIAL;
     return MR_OK;
 }
 
@@ -1386,13 +1441,13 @@ static int check_device_errors(mr_plan *pl, uint32_t &flags) {
     // flags and written counts are checked (and collected) as well
     for (uint32_t i = 0; i < pl->slots.size(); ++i) {
         const mr_plan::Slot &k = pl->slots[i];
-        if (i == pl->slot || !k.used) continue;
+        if (i == pl->slot || !k.counter) continue;
         uint32_t oc[kCtrWords];
         if (hipMemcpy(oc, k.counter, kCtrWords * 4, hipMemcpyDeviceToHost) != hipSuccess)
             return fail(MR_ERR_DEVICE, "copy counter");
         if (oc[kCtrFlags]) (void)hipMemset(k.counter + kCtrFlags, 0, 4);
-        flags |= oc[kCtrFlags];
-        if (flags == 0 && oc[kCtrLastWritten] != pl->hp.q_id.size())
+        flags |= oc[kCtrFlags];  // a fused plan's look-ahead solve may have flagged a slot not yet filled
+        if (flags == 0 && k.used && oc[kCtrLastWritten] != pl->hp.q_id.size())
             return fail(MR_ERR_DEVICE, "internal: " + std::to_string(oc[kCtrLastWritten]) + " of " +
                                            std::to_string(pl->hp.q_id.size()) + " records written (an earlier pass)");
     }

@@ -388,6 +388,7 @@ class Plan:
             raise EngineError(rc, last_error())
         d = {f: getattr(st, f) for f, _ in mr_plan_stats._fields_}
         d["solver"] = {0: "bucketed", 1: "levels", 2: "hub", 3: "hub_wide"}.get(st.solver, str(st.solver))
+        d["fill_launch"] = {0: None, 1: "serial", 2: "streams", 3: "fused"}.get(st.fill_launch, str(st.fill_launch))
         return d
 
     def kernel_ms(self) -> Tuple[float, int]:

@@ -170,14 +170,17 @@ def test_fill_ragged_last_tile_column(eng, oracle_lib, monkeypatch, flags, pi):
             assert as_expected(plan.label(i, cells[j])) == as_expected(exp[j]), (s, cells[j])
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("fb,slots", [(False, 2), (True, 2), (False, 3), (True, 3)])
-def test_overlapped_passes_match_serial(eng, oracle_lib, monkeypatch, fb, slots):
+def test_overlapped_passes_match_serial(eng, oracle_lib, monkeypatch, fb, slots, fused):
     """All-destinations passes take slots of label tables round robin, the specials'
-    solves of the next passes running beside the fill of pass k (mr_plan_run).
+    solve of pass k + 1 running beside the fill of pass k (mr_plan_run): in the same
+    launch (fused, the default) or on a stream of the plan's own (MR_FILL_FUSED=0).
     Back-to-back passes (no host sync between them) must leave the records and
     labels of one serial pass (MR_FILL_OVERLAP=0), after every count of passes up to
     a wrap round the slots, with and without sources handed to the SSSP kernel."""
     monkeypatch.setenv("MR_FILL_SLOTS", str(slots))
+    monkeypatch.setenv("MR_FILL_FUSED", fused)
     monkeypatch.delenv("MR_ALGO", raising=False)
     monkeypatch.delenv("MR_FILL_GX", raising=False)
     monkeypatch.delenv("MR_DBG_FLAGS", raising=False)
@@ -194,9 +197,11 @@ def test_overlapped_passes_match_serial(eng, oracle_lib, monkeypatch, fb, slots)
     ref = eng.SSSPPlan(g, Params(), sources)
     ref.run()
     want = [ref.records(i) for i in range(len(sources))]
+    assert ref.stats()["fill_launch"] == "serial"
     monkeypatch.delenv("MR_FILL_OVERLAP")
     plan = eng.SSSPPlan(g, Params(), sources)
     assert plan.stats()["solver"] == "hub"
+    assert plan.stats()["fill_launch"] == ("fused" if fused == "1" else "streams")
     dsts = rng.sample(cells, 12)
     for passes in (1, 2, 3, 4):
         for _ in range(passes):
@@ -211,7 +216,7 @@ def test_overlapped_passes_match_serial(eng, oracle_lib, monkeypatch, fb, slots)
 def test_overlap_error_of_either_slot_is_reported(eng, monkeypatch, inject_slot, passes):
     """A device error flag raised by a pass whose slot is not the current one (an
     earlier overlap slot) must still be reported, then collected."""
-    for k in ("MR_ALGO", "MR_FILL_GX", "MR_DBG_FLAGS", "MR_HUB_FALLBACK_ALL", "MR_FILL_OVERLAP"):
+    for k in ("MR_ALGO", "MR_FILL_GX", "MR_DBG_FLAGS", "MR_HUB_FALLBACK_ALL", "MR_FILL_OVERLAP", "MR_FILL_FUSED"):
         monkeypatch.delenv(k, raising=False)
     nslots = 3
     monkeypatch.setenv("MR_FILL_SLOTS", str(nslots))

@@ -20,10 +20,10 @@ for W in $WLS; do
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 240 rocprofv3 --pmc $C --kernel-trace --stats -d $O/pmc_${C}_$W -o run --output-format csv -- python3 "$R/bench.py" --workload $W --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_${C}_$W.log 2>&1 || exit 1
   done
-  K=""; [ $W = c3 ] && K="--kernels fill_kernel"  # c3 prices the fill (bench.py roofline.kernel)
+  K=""; [ $W = c3 ] && K="--kernels hub_fill_kernel"  # c3 prices the fill (bench.py roofline.kernel)
   python3 "$R/tools/pmc_summary.py" $K --workload $W --queries $(qpg $W) --fetch $O/pmc_FETCH_SIZE_$W --write $O/pmc_WRITE_SIZE_$W --out $O/pmc_$W.json > /dev/null || exit 1
   echo "$W pmc ok"
-  K2=hub_kernel; [ $W = c3 ] && K2=fill_kernel; [ $W = c5 ] && K2=hub_wide_kernel
+  K2=hub_kernel; [ $W = c3 ] && K2=hub_fill_kernel; [ $W = c5 ] && K2=hub_wide_kernel
   bash "$R/tools/gpu_sq.sh" $W $O/sq_$W && python3 "$R/tools/sq_summary.py" --workload $W --kernel $K2 --sq $O/sq_$W --out $O/sq_$W.json > /dev/null || exit 1
   echo "$W sq ok"
 done
