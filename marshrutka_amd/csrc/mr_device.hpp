@@ -1833,12 +1833,16 @@ struct HubSolver : Core<false> {
         return avail(nbk, b, bx, by, int(w % P.S) - int(P.H), int(w / P.S) - int(P.H));
     }
 
-    // Destinations.  A segment with few (<= kEmitWaveMax) takes them one at a time,
-    // lane j evaluating boundary j's walk and the winner picked on the DPP network
-    // (exact metric + length ties: full compare); one with many gives each lane a query.
+    // Destinations.  A segment with few (<= kEmitWaveMax) picks each one's winning
+    // boundary in turn, lane j evaluating boundary j's walk and the winner found on the
+    // DPP network (exact metric + length ties: full compare); lane i loads destination
+    // i's cell data up front and writes its record at the end, so the queries' loads and
+    // records overlap instead of queueing one query at a time.  A segment with many
+    // gives each lane a query.
     static constexpr uint32_t kEmitWaveMax = 32;
     __device__ __forceinline__ bool emit_all(uint32_t qa, uint32_t qb, uint32_t nb, uint32_t nbk, int sx, int sy,
                                              const View &st0) const {
+        static_assert(kEmitWaveMax <= LPS, "one lane per destination");
         bool unc = false;
         const DevParams &p = P;
         const uint32_t t = seg_lane();
@@ -1849,14 +1853,20 @@ struct HubSolver : Core<false> {
         const bool usable = t < nb && vert_of(bj) != p.vc;
         int bx, by;
         bpos(bj, sx, sy, bx, by);
+        // lane t: destination t's cell, its special entry and rank
+        const bool mine_q = few && t < nq;
+        const uint32_t wq = mine_q ? a->q_dst[qa + t] : src;
+        const uint32_t twq = sinfo[wq] & kNone10, wrq = rank[wq];
+        const uint32_t seg0 = lane_id() - t;
+        uint32_t wbq = 0;  // lane t: destination t's winning boundary (plain destinations)
         for (uint32_t i = 0; i < trip; ++i) {
             const bool qon = few && i < nq;
-            const uint32_t qi = qa + (qon ? i : 0u);
-            const uint32_t w = qon ? a->q_dst[qi] : src;
-            const uint32_t tw = sinfo[w] & kNone10;
+            const uint32_t from = seg0 + (qon ? i : 0u);
+            const uint32_t w = qon ? uint32_t(__shfl(int(wq), int(from), 64)) : src;
+            const uint32_t tw = uint32_t(__shfl(int(twq), int(from), 64));
+            const uint32_t wr = uint32_t(__shfl(int(wrq), int(from), 64));
             const bool plain = qon && w != src && tw == kNone10;
             const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
-            const uint32_t wr = rank[w];
             View c;
             view_walk(bj, walk_dist(bx, by, wx, wy), wr, c);
             bool cand = usable && plain;
@@ -1886,14 +1896,7 @@ struct HubSolver : Core<false> {
                 }
                 if (tied) win = mm;
             }
-            View x;
-            if (plain) walk_to(bnd[win], sx, sy, wx, wy, wr, x);
-            else if (w == src) x = st0;
-            else view_rec(tw, x);
-            if (qon && t == 0) {
-                emit(x, qi);
-                if (plain && !dest_avail(nbk, bnd[win], w, sx, sy)) unc = true;
-            }
+            wbq = (qon && t == i) ? win : wbq;
             // non-linear run times: lane j clears boundary j; one path clean for all
             if (!ff_linear() && !(a->dbg_flags & 8u)) {
                 const uint32_t pc = (qon && plain) ? walk_clear(t < nb ? bnd[t] : kNone32, bnd[win], wx, wy, sx, sy) : 3u;
@@ -1901,6 +1904,16 @@ struct HubSolver : Core<false> {
                 const bool y_bad = seg_bits<LPS>(__ballot(!(pc & 2u))) != 0;
                 if (x_bad && y_bad && t == 0) unc = true;
             }
+        }
+        if (mine_q) {  // lane t writes destination t's record
+            View x;
+            const bool plain = wq != src && twq == kNone10;
+            const int wx = int(wq % p.S) - int(p.H), wy = int(wq / p.S) - int(p.H);
+            if (plain) walk_to(bnd[wbq], sx, sy, wx, wy, wrq, x);
+            else if (wq == src) x = st0;
+            else view_rec(twq, x);
+            emit(x, qa + t);
+            if (plain && !dest_avail(nbk, bnd[wbq], wq, sx, sy)) unc = true;
         }
         for (uint32_t i = qa + t; !few && i < qb; i += LPS) {
             const uint32_t w = a->q_dst[i];
