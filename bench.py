@@ -227,6 +227,11 @@ def cpu_model():
 
 def main():
     args = parse()
+    # stdout carries the one JSON line only: native libraries that print to fd 1 (RCCL's
+    # version banner at communicator creation) go to stderr instead
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -243,12 +248,15 @@ def main():
     # MR_BENCH_BACKEND=gloo: a rehearsal of the N>1 path with every rank on the one
     # visible GPU and the gather staged through host memory (RCCL needs a GPU per rank)
     backend = os.environ.get("MR_BENCH_BACKEND", "nccl")
+    # MR_BENCH_DIST=1: the N > 1 code path (process group, double-buffered RCCL gather,
+    # gather check) at world size 1 too, to exercise it on a one-GPU box
+    dist_on = world > 1 or os.environ.get("MR_BENCH_DIST") == "1"
     device = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
     torch.cuda.set_device(device)
     # a dedicated stream: the solve kernel and the RCCL gather are ordered on it
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
-    if world > 1:
+    if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "gloo":
             dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -283,13 +291,13 @@ def main():
         counts = [len(s) for s in shards]
         # N > 1: two plans over the same shard, so the result gather of one batch
         # overlaps the solve of the next (double buffering, shard.PipelinedGather)
-        depth = 2 if world > 1 else 1
+        depth = 2 if dist_on else 1
         plans = [pathfinder.Plan(grid, params, mine, max_cmds=wl.get("max_cmds", 16)) for _ in range(depth)]
         plan = plans[0]
         n_src = plan.num_sources
         _, rbytes, _, cbytes = plan.device_outputs()
     pipe = None
-    if world > 1 and not all_dst:
+    if dist_on and not all_dst:
         # result records, command slots and the overflow pool in one flat torch-owned
         # device buffer per plan, padded to the largest shard: one RCCL gather per batch
         # moves every record of the batch with all its commands
@@ -324,7 +332,7 @@ def main():
     torch.cuda.synchronize()
     for p_ in plans:
         p_.kernel_ms()  # reset the per-launch event window to the timed region
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -333,7 +341,7 @@ def main():
     if pipe is not None:
         pipe.drain()  # every batch's results are at rank 0 inside the timed region
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     gather_check = None
@@ -343,7 +351,7 @@ def main():
     kn = [p_.kernel_ms() for p_ in plans]
     nl = sum(n for _, n in kn)
     kms = sum(ms * n for ms, n in kn) / nl if nl else 0.0
-    if world > 1:
+    if dist_on:
         rdev = "cpu" if backend == "gloo" else "cuda"
         t = torch.tensor([elapsed, kms], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -376,7 +384,7 @@ def main():
             kernel_name, pass_ms = "sssp_kernel", kms
     else:
         alg_bytes, kernel_name, survey_bytes = algorithmic_bytes(plan, stats, V)
-    if world > 1:
+    if dist_on:
         t = torch.tensor([alg_bytes, survey_bytes, stats["fallback_sources"]], dtype=torch.float64,
                          device="cpu" if backend == "gloo" else "cuda")
         dist.all_reduce(t)
@@ -461,8 +469,8 @@ def main():
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
+        print(json.dumps(out), file=json_out, flush=True)
+    if dist_on:
         dist.destroy_process_group()
 
 
