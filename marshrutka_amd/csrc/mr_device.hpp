@@ -2984,22 +2984,40 @@ __device__ __forceinline__ void fill_body(const KArgs *__restrict__ a, uint32_t 
                         }
                     }
                 }
-                // buffer stores off one per-tile base: the lane's offset in a VGPR, the
-                // row's (i * S * 4 B) in an SGPR, so no per-row 64-bit address; a row's
-                // kCPL stores are one contiguous run of kTW cell words
+                // The cell words first: every row's LDS read issued before one wait (kb's
+                // unused cells hold all ones, a valid srank).  Then buffer stores off one
+                // per-tile base: the lane's offset in a VGPR, the row's (i * S * 4 B) in an
+                // SGPR, so no per-row 64-bit address; a row's kCPL stores are one
+                // contiguous run of kTW cell words.  A tile inside the grid stores with no
+                // per-row mask.
+                uint32_t wd[kCPL * kTH];
+#pragma unroll
+                for (int i = 0; i < kCPL * kTH; ++i) {
+                    // the cell word b << 20 | k: k = (lead - the boundary's lead) / sL
+                    const uint32_t kv = kb[i], sr = kv & maskr;
+                    wd[i] = sL == 1u ? B[5][sr] + (kv >> rbs) : B[5][sr] + ((kv >> rbs) - B[7][sr]) / sL;
+                }
                 const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
                     outs + (size_t(ty0) * S + size_t(tx0)), 0, int(4u * kTH * S), 0x00020000);  // the tile's rows
+                if (tx0 + kTW <= int(S) && ty0 + kTH <= int(S)) {
+                    // (row offsets stepped in a VGPR: per-row SGPR offsets ran out of SGPRs)
+                    uint32_t vo = lane * 4u;
 #pragma unroll
-                for (int i = 0; i < kTH; ++i) {
+                    for (int i = 0; i < kTH; ++i) {
 #pragma unroll
-                    for (int k = 0; k < kCPL; ++k) {
-                        const int cx = tx0 + 64 * k + int(lane), cy = ty0 + i;
-                        if (cx < int(S) && cy < int(S)) {
-                            // the cell word b << 20 | k: k = (lead - the boundary's lead) / sL
-                            const uint32_t kv = kb[k * kTH + i], sr = kv & maskr;
-                            const uint32_t w = sL == 1u ? B[5][sr] + (kv >> rbs) : B[5][sr] + ((kv >> rbs) - B[7][sr]) / sL;
-                            __builtin_amdgcn_raw_buffer_store_b32(w, rsrc, int((64u * k + lane) * 4u),
-                                                                  int(uint32_t(i) * S * 4u), 0);
+                        for (int k = 0; k < kCPL; ++k)
+                            __builtin_amdgcn_raw_buffer_store_b32(wd[k * kTH + i], rsrc, int(vo + 256u * k), 0, 0);
+                        vo += S * 4u;
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < kTH; ++i) {
+#pragma unroll
+                        for (int k = 0; k < kCPL; ++k) {
+                            const int cx = tx0 + 64 * k + int(lane), cy = ty0 + i;
+                            if (cx < int(S) && cy < int(S))
+                                __builtin_amdgcn_raw_buffer_store_b32(wd[k * kTH + i], rsrc, int((64u * k + lane) * 4u),
+                                                                      int(uint32_t(i) * S * 4u), 0);
                         }
                     }
                 }
