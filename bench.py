@@ -17,7 +17,7 @@ Workloads (BASELINE.json configs; odd sides per SURVEY.md §8a A14):
                north-star target, >= 1e6 q/s on a 1024x1024 grid at 8 GPUs)
   c2           10k uniform (src,dst) queries per GPU on a 65x65 synthetic map
                (configs[1]: "10k random (src,dst) batch on 64x64")
-  c3           64 sources per GPU, every destination of each on 1025x1025
+  c3           1024 sources per GPU, every destination of each on 1025x1025
                (configs[2]: single-source -> all-destinations; V queries per source)
   c5           10k uniform queries per GPU on a 4097x4097 map with 64 clustered
                campfires per homeland (261 specials), Time first (configs[4],
@@ -53,9 +53,11 @@ WORKLOADS = {
     "c2": dict(size=65, queries_per_gpu=10_000, campfires=4, seed=2024, max_cmds=6,
                desc="configs[1]: 10k uniform (src,dst) per GPU on a 65x65 synthetic map (64x64 -> odd 65), "
                     "default FindPath params"),
-    "c3": dict(size=1025, queries_per_gpu=64, campfires=4, seed=4096, all_destinations=True,
-               desc="configs[2]: single source -> all 1 050 625 cells of the 1025x1025 synthetic map, 64 sources "
-                    "per GPU; a step answers V queries per source (SURVEY 8d c3)"),
+    # c3: 1024 sources a pass (4.5 GB of cell words), far past the 256 MiB Infinity Cache,
+    # so the stores are priced at HBM (64 sources, 269 MB, were partly absorbed by it)
+    "c3": dict(size=1025, queries_per_gpu=1024, campfires=4, seed=4096, all_destinations=True,
+               desc="configs[2]: single source -> all 1 050 625 cells of the 1025x1025 synthetic map, 1024 "
+                    "sources per GPU per pass; a step answers V queries per source (SURVEY 8d c3)"),
     "c4": dict(size=1025, queries_per_gpu=125_000, campfires=4, seed=4096, max_cmds=6,
                desc="configs[3] shard: 125k uniform (src,dst) per GPU on a 1025x1025 synthetic map "
                     "(1024 -> odd 1025), default FindPath params; N=8 is the 1M batch"),

@@ -830,7 +830,8 @@ struct Core {
             a->out_tab[tb + t] = R[t];
             a->out_lex[tb + t] = kNone32;
         }
-        CellWord *out = a->out_rec + (unsigned long long)s_idx * p.V;
+        const uint32_t pitch = a->rec_pitch;
+        CellWord *out = a->out_rec + (unsigned long long)s_idx * p.S * pitch;
         for (uint32_t v = threadIdx.x; v < p.V; v += kBS) {
             CellWord r = kViaSource;
             const uint32_t sw = ld_state(v);
@@ -843,7 +844,8 @@ struct Core {
             } else {
                 flag(kErrBucket);  // every cell of the connected grid settles
             }
-            out[v] = r;
+            const uint32_t y = v / p.S;
+            out[y * pitch + (v - y * p.S)] = r;
         }
         if (threadIdx.x == 0) a->src_state[s_idx] = 2;
     }
@@ -2708,7 +2710,7 @@ __device__ __forceinline__ uint32_t bit_width64(unsigned long long x) { return x
 // by row, each cell's walk distance in full and the three-metric compare.
 template <uint32_t PERM>
 __device__ __forceinline__ void fill_tile_rows(const uint32_t (*B)[64], unsigned long long live, int wx,
-                                                      int y0, int ty0, int cx, bool col_ok, uint32_t S, CellWord *outs) {
+                                                      int y0, int ty0, int cx, uint32_t S, uint32_t pitch, CellWord *outs) {
     constexpr uint32_t q0 = PERM / 9, q1 = (PERM / 3) % 3, q2 = PERM % 3;
 #pragma unroll 1
     for (int i = 0; i < int(kFillTH); ++i) {
@@ -2732,7 +2734,7 @@ __device__ __forceinline__ void fill_tile_rows(const uint32_t (*B)[64], unsigned
         }
         // the cell word b << 20 | k: B[5] holds (b << 20) - legs(b), r0 = legs(b) + k
         const int cy = ty0 + i;
-        if (col_ok && cy < int(S)) outs[uint32_t(cy) * S + uint32_t(cx)] = rv + r0;
+        if (cy < int(S)) outs[uint32_t(cy) * pitch + uint32_t(cx)] = rv + r0;  // (pad columns too)
     }
 }
 
@@ -2756,7 +2758,7 @@ __device__ __forceinline__ void fill_body(const KArgs *__restrict__ a, uint32_t 
     const uint32_t lane = threadIdx.x & 63u, wv = uint32_t(__builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)));
     uint32_t(*B)[64] = btab[wv];
     uint32_t(*P)[64] = btab[wv] + 8;
-    const uint32_t NS = a->p.NS, T = NS + 1, V = a->p.V, S = a->p.S, nsrc = a->nsrc;
+    const uint32_t NS = a->p.NS, T = NS + 1, S = a->p.S, nsrc = a->nsrc, pitch = a->rec_pitch;
     const int H = int(a->p.H);
     const uint32_t tpx = (S + kTW - 1) / kTW, tpy = (S + kTH - 1) / kTH, ntile = tpx * tpy;
     const bool no_prune = (a->dbg_flags & 1u) != 0, no_pack = (a->dbg_flags & 2u) != 0;
@@ -2856,7 +2858,7 @@ __device__ __forceinline__ void fill_body(const KArgs *__restrict__ a, uint32_t 
         const uint32_t pb_l = lane < nb ? B[2 + PL][lane] : 0u;
         const bool cnd = lane < nb && (!packable || bk_l != 0xFFFFFFFFu);
         // ---- this wave's tiles of the source ---------------------------------------
-        CellWord *const outs = a->out_rec + (unsigned long long)s * V;
+        CellWord *const outs = a->out_rec + (unsigned long long)s * S * pitch;
         for (uint32_t tile = j; tile < ntile; tile += G) {
             const int tx0 = int(tile % tpx) * kTW, ty0 = int(tile / tpx) * kTH;
             const int x0 = tx0 - H, y0 = ty0 - H;
@@ -2997,9 +2999,14 @@ __device__ __forceinline__ void fill_body(const KArgs *__restrict__ a, uint32_t 
                     const uint32_t kv = kb[i], sr = kv & maskr;
                     wd[i] = sL == 1u ? B[5][sr] + (kv >> rbs) : B[5][sr] + ((kv >> rbs) - B[7][sr]) / sL;
                 }
+                // Rows are padded to a multiple of 64 cells (rec_pitch), so every tile row is
+                // whole aligned 256 B runs, pad columns included: no store ever writes part
+                // of a line another wave writes (partial lines from two XCDs' L2s halve the
+                // HBM write rate once the output outgrows the Infinity Cache); only the
+                // last tile row of the grid masks rows.
                 const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-                    outs + (size_t(ty0) * S + size_t(tx0)), 0, int(4u * kTH * S), 0x00020000);  // the tile's rows
-                if (tx0 + kTW <= int(S) && ty0 + kTH <= int(S)) {
+                    outs + (size_t(ty0) * pitch + size_t(tx0)), 0, int(4u * kTH * pitch), 0x00020000);  // the tile's rows
+                if (ty0 + kTH <= int(S)) {
                     // (row offsets stepped in a VGPR: per-row SGPR offsets ran out of SGPRs)
                     uint32_t vo = lane * 4u;
 #pragma unroll
@@ -3007,24 +3014,23 @@ __device__ __forceinline__ void fill_body(const KArgs *__restrict__ a, uint32_t 
 #pragma unroll
                         for (int k = 0; k < kCPL; ++k)
                             __builtin_amdgcn_raw_buffer_store_b32(wd[k * kTH + i], rsrc, int(vo + 256u * k), 0, 0);
-                        vo += S * 4u;
+                        vo += pitch * 4u;
                     }
                 } else {
 #pragma unroll
                     for (int i = 0; i < kTH; ++i) {
 #pragma unroll
                         for (int k = 0; k < kCPL; ++k) {
-                            const int cx = tx0 + 64 * k + int(lane), cy = ty0 + i;
-                            if (cx < int(S) && cy < int(S))
+                            if (ty0 + i < int(S))
                                 __builtin_amdgcn_raw_buffer_store_b32(wd[k * kTH + i], rsrc, int((64u * k + lane) * 4u),
-                                                                      int(uint32_t(i) * S * 4u), 0);
+                                                                      int(uint32_t(i) * pitch * 4u), 0);
                         }
                     }
                 }
             } else {
                 for (int k = 0; k < kCPL; ++k) {  // keys too wide for 32 bits
                     const int cx = tx0 + 64 * k + int(lane);
-                    fill_tile_rows<PERM>(B, live, x0 + 64 * k + int(lane), y0, ty0, cx, cx < int(S), S, outs);
+                    fill_tile_rows<PERM>(B, live, x0 + 64 * k + int(lane), y0, ty0, cx, S, pitch, outs);
                 }
             }
             // specials' cells hold their own labels, the source's cell (last: it may also
@@ -3041,7 +3047,7 @@ __device__ __forceinline__ void fill_body(const KArgs *__restrict__ a, uint32_t 
                 }
                 const int px = int(P[0][t]) - x0, py = int(P[1][t]) - y0;
                 if (lane == uint32_t(px) % 64u)
-                    outs[uint32_t(ty0 + py) * S + uint32_t(tx0 + px)] = t == 0 ? kViaSource : (kViaSpecial | t);
+                    outs[uint32_t(ty0 + py) * pitch + uint32_t(tx0 + px)] = t == 0 ? kViaSource : (kViaSpecial | t);
             }
         }
     }

@@ -158,7 +158,8 @@ struct KArgs {
     // all-destinations mode: no per-query outputs; per source, a record per cell, the
     // label table (NS+1 entries), the boundaries' lexicographic ranks and how it was solved
     uint32_t all_mode;
-    CellWord *out_rec;           // nsrc * V cell words
+    CellWord *out_rec;           // nsrc * S rows of rec_pitch cell words (rows padded to 64 cells)
+    uint32_t rec_pitch;          // cell words per row of out_rec: S rounded up to a multiple of 64
     Rec *out_tab;                // nsrc * (NS+1)
     uint32_t *out_lex;           // nsrc * (NS+1): rank of boundary t by (length, command list), else kNone32
     uint32_t *src_state;         // nsrc: 1 hub solved (records by the fill kernel), 2 SSSP kernel

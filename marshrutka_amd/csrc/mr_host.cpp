@@ -956,7 +956,11 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     pl->all_mode = all_mode;
     if (all_mode) {  // per source: a record per cell, the label table, the boundary ranks
         const size_t T = size_t(NS) + 1;
-        if (hipMalloc(reinterpret_cast<void **>(&pl->d_rec), std::max<size_t>(nsrc, 1) * V * sizeof(CellWord)) != hipSuccess ||
+        // rows padded to whole fill tiles (rec_pitch): aligned 256 B store runs
+        const uint32_t pitch = (hp.p.S + kFillTW - 1) / kFillTW * kFillTW;
+        ka.rec_pitch = pitch;
+        if (hipMalloc(reinterpret_cast<void **>(&pl->d_rec),
+                      std::max<size_t>(nsrc, 1) * hp.p.S * pitch * sizeof(CellWord)) != hipSuccess ||
             hipMalloc(reinterpret_cast<void **>(&pl->d_tab), std::max<size_t>(nsrc, 1) * T * sizeof(Rec)) != hipSuccess ||
             hipMalloc(reinterpret_cast<void **>(&pl->d_lex), std::max<size_t>(nsrc, 1) * T * 4) != hipSuccess ||
             hipMalloc(reinterpret_cast<void **>(&pl->d_sstate), std::max<size_t>(nsrc, 1) * 4) != hipSuccess)
@@ -1693,8 +1697,9 @@ extern "C" int mr_sssp_records(mr_plan *pl, uint32_t i, mr_label_record *out) {
     const uint32_t V = pl->ka.p.V;
     std::vector<CellWord> words(V);
     std::vector<Rec> tab;
-    if (hipMemcpy(words.data(), pl->d_rec + size_t(si) * V, size_t(V) * sizeof(CellWord), hipMemcpyDeviceToHost) !=
-        hipSuccess)
+    const uint32_t S = pl->ka.p.S, pitch = pl->ka.rec_pitch;
+    if (hipMemcpy2D(words.data(), S * sizeof(CellWord), pl->d_rec + size_t(si) * S * pitch, pitch * sizeof(CellWord),
+                    S * sizeof(CellWord), S, hipMemcpyDeviceToHost) != hipSuccess)
         return fail(MR_ERR_DEVICE, "copy records");
     if (int st = sssp_table(pl, si, tab)) return st;
     for (uint32_t v = 0; v < V; ++v)
@@ -1705,7 +1710,14 @@ extern "C" int mr_sssp_records(mr_plan *pl, uint32_t i, mr_label_record *out) {
 extern "C" int mr_sssp_device_records(mr_plan *pl, void **d_records, uint64_t *bytes) {
     if (!pl || !pl->all_mode) return fail(MR_ERR_INVALID_ARG, "not an all-destinations plan");
     if (d_records) *d_records = pl->d_rec;
-    if (bytes) *bytes = uint64_t(pl->ka.nsrc) * pl->ka.p.V * sizeof(CellWord);
+    if (bytes) *bytes = uint64_t(pl->ka.nsrc) * pl->ka.p.S * pl->ka.rec_pitch * sizeof(CellWord);
+    return MR_OK;
+}
+
+extern "C" int mr_sssp_record_pitch(mr_plan *pl, uint32_t *cells_per_row) {
+    if (!pl || !pl->all_mode) return fail(MR_ERR_INVALID_ARG, "not an all-destinations plan");
+    if (!cells_per_row) return fail(MR_ERR_INVALID_ARG, "null output");
+    *cells_per_row = pl->ka.rec_pitch;
     return MR_OK;
 }
 
@@ -1729,7 +1741,8 @@ extern "C" int mr_sssp_label(mr_plan *pl, uint32_t i, mr_cell_index dst, mr_resu
     const uint32_t T = pl->ka.p.NS + 1;
     CellWord word;
     std::vector<Rec> tab;
-    if (hipMemcpy(&word, pl->d_rec + size_t(si) * pl->ka.p.V + w, sizeof(word), hipMemcpyDeviceToHost) != hipSuccess)
+    const size_t at = (size_t(si) * g->S + w / g->S) * pl->ka.rec_pitch + w % g->S;  // padded rows
+    if (hipMemcpy(&word, pl->d_rec + at, sizeof(word), hipMemcpyDeviceToHost) != hipSuccess)
         return fail(MR_ERR_DEVICE, "copy label");
     if (int st = sssp_table(pl, si, tab)) return st;
     mr_label_record rec;

@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = [
     "mr_plan_num_sources", "mr_plan_record_queries", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_plan_bind_outputs", "mr_plan_bind_outputs_ex", "mr_decode_records", "mr_abi_version", "mr_last_error",
     "mr_device_available", "mr_parse_map_html", "mr_parse_error", "mr_grid_from_html",
     "mr_command_time", "mr_duration_display", "mr_render_schedule",
-    "mr_sssp_plan_create", "mr_sssp_records", "mr_sssp_device_records", "mr_sssp_device_tables", "mr_sssp_label", "mr_plan_fill_ms",
+    "mr_sssp_plan_create", "mr_sssp_records", "mr_sssp_device_records", "mr_sssp_record_pitch", "mr_sssp_device_tables", "mr_sssp_label", "mr_plan_fill_ms",
 ]
 
 
@@ -112,6 +112,8 @@ def lib():
         L.mr_sssp_records.restype = C.c_int
         L.mr_sssp_device_records.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_uint64)]
         L.mr_sssp_device_records.restype = C.c_int
+        L.mr_sssp_record_pitch.argtypes = [vp, C.POINTER(C.c_uint32)]
+        L.mr_sssp_record_pitch.restype = C.c_int
         L.mr_sssp_device_tables.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_uint64)]
         L.mr_sssp_device_tables.restype = C.c_int
         L.mr_sssp_label.argtypes = [vp, C.c_uint32, mr_cell_index, C.POINTER(mr_result), C.POINTER(mr_command),
@@ -471,6 +473,14 @@ class SSSPPlan(Plan):
         if st != MR_OK:
             raise EngineError(st, last_error())
         return ptr.value, n.value
+
+    def record_pitch(self) -> int:
+        """Cell words per row of device_records() (rows padded to a multiple of 64)."""
+        p = C.c_uint32()
+        st = lib().mr_sssp_record_pitch(self.handle, C.byref(p))
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+        return p.value
 
     def label(self, i: int, dst: CellIndex) -> TotalCost:
         res = mr_result()

@@ -235,3 +235,38 @@ def test_overlap_error_of_either_slot_is_reported(eng, monkeypatch, inject_slot,
         plan.records(0)
     # collected: both slots' flags were cleared by the report
     plan.records(0)
+
+
+@pytest.mark.parametrize("size,mode_env", [(33, None), (65, None), (33, "fallback")])
+def test_device_records_padded_rows(eng, monkeypatch, size, mode_env):
+    """The device cell words sit in rows padded to mr_sssp_record_pitch cells (a
+    multiple of 64): word y * pitch + x of each source is cell (x, y)'s word, and it
+    names the same boundary / special / source as the expanded record."""
+    import ctypes as C
+
+    import numpy as np
+    if mode_env == "fallback":
+        monkeypatch.setenv("MR_HUB_FALLBACK_ALL", "1")  # the SSSP kernel's writes
+    m = SyntheticMap(size, campfires_per_homeland=3, seed=size)
+    g = eng.MapGrid(m.cells())
+    cells = m.all_indices()
+    sources = [cells[0], cells[len(cells) // 2], cells[-1], cells[size + 3]]
+    plan = eng.SSSPPlan(g, Params(), sources)
+    plan.run()
+    via = [plan.records(i)[:, 3] for i in range(len(sources))]  # (waits for the plan's passes)
+    pitch = plan.record_pitch()
+    assert pitch % 64 == 0 and size <= pitch < size + 64
+    ptr, nbytes = plan.device_records()
+    assert nbytes == plan.num_sources * size * pitch * 4
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    words = np.empty(nbytes // 4, dtype=np.uint32)
+    assert hip.hipMemcpy(words.ctypes.data, C.c_void_p(ptr), nbytes, 2) == 0
+    words = words.reshape(plan.num_sources, size, pitch)[:, :, :size].reshape(plan.num_sources, -1)
+    # plan sources are the distinct sources in row-major cell order
+    order = sorted(set(range(len(sources))), key=lambda i: cells.index(sources[i]))
+    for ps, i in enumerate(order):
+        w = words[ps]
+        plain = (w & 0x80000000) == 0
+        assert np.array_equal(w[plain] >> 20, via[i][plain])
+        assert np.array_equal(w[~plain], via[i][~plain])

@@ -10,7 +10,7 @@ mkdir -p $O
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 steps() { case $1 in c5) echo 3;; c4) echo 10;; *) echo 20;; esac; }
-qpg() { case $1 in c2) echo 10000;; c3) echo 64;; c4) echo 125000;; c5) echo 10000;; esac; }
+qpg() { case $1 in c2) echo 10000;; c3) echo 1024;; c4) echo 125000;; c5) echo 10000;; esac; }
 for W in $WLS; do
   ST=$(steps $W)
   timeout -k 10 300 python3 "$R/bench.py" --workload $W --steps $ST --warmup 2 > $O/bench_$W.json 2> $O/bench_$W.err || exit 1
