@@ -290,8 +290,8 @@ double mr_plan_fill_ms(const mr_plan *plan);
 int mr_sssp_records(mr_plan *plan, uint32_t i, mr_label_record *out);
 /* Device pointer to all cell words and their size: [plan source][row y][pitch], 4 B
  * each, cell (x, y) of a source's grid at word y * pitch + x, rows padded to
- * mr_sssp_record_pitch cells (a multiple of 64: every fill tile row stores whole
- * aligned 256 B runs; pad words are unspecified).  A cell word carries the whole
+ * mr_sssp_record_pitch cells (a multiple of 32: the fill stores whole aligned
+ * 128 B lines; pad words are unspecified).  A cell word carries the whole
  * label over its source's table:
  *   b << 20 | k     the walk of k legs from boundary table entry b (0 = the source):
  *                   metrics = entry b's + (k, 0, Fleetfoot-ceil(180 k)), commands =
@@ -299,7 +299,7 @@ int mr_sssp_records(mr_plan *plan, uint32_t i, mr_label_record *out);
  *   0x80000000 | t  special t's own table label;  0xFFFFFFFF  the source
  * Plan sources are the caller's distinct sources in row-major cell order. */
 int mr_sssp_device_records(mr_plan *plan, void **d_records, uint64_t *bytes);
-/* Cell words per row of the device records (S rounded up to a multiple of 64). */
+/* Cell words per row of the device records (S rounded up to a multiple of 32). */
 int mr_sssp_record_pitch(mr_plan *plan, uint32_t *cells_per_row);
 /* Device pointer to the label tables ([plan source][NS + 1 entries], 28 B each:
  * u32 legs, money, time; u32 meta = length (16 b) | parent entry (10 b) << 16 |

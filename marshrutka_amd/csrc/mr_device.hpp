@@ -2734,7 +2734,7 @@ __device__ __forceinline__ void fill_tile_rows(const uint32_t (*B)[64], unsigned
         }
         // the cell word b << 20 | k: B[5] holds (b << 20) - legs(b), r0 = legs(b) + k
         const int cy = ty0 + i;
-        if (cy < int(S)) outs[uint32_t(cy) * pitch + uint32_t(cx)] = rv + r0;  // (pad columns too)
+        if (cy < int(S) && cx < int(pitch)) outs[uint32_t(cy) * pitch + uint32_t(cx)] = rv + r0;  // (pad columns too)
     }
 }
 
@@ -2999,14 +2999,15 @@ __device__ __forceinline__ void fill_body(const KArgs *__restrict__ a, uint32_t 
                     const uint32_t kv = kb[i], sr = kv & maskr;
                     wd[i] = sL == 1u ? B[5][sr] + (kv >> rbs) : B[5][sr] + ((kv >> rbs) - B[7][sr]) / sL;
                 }
-                // Rows are padded to a multiple of 64 cells (rec_pitch), so every tile row is
-                // whole aligned 256 B runs, pad columns included: no store ever writes part
-                // of a line another wave writes (partial lines from two XCDs' L2s halve the
-                // HBM write rate once the output outgrows the Infinity Cache); only the
-                // last tile row of the grid masks rows.
+                // Rows are padded to a multiple of 32 cells (rec_pitch: 128 B, one line), so
+                // every tile row is whole aligned lines, pad columns included: no store ever
+                // writes part of a line (partial lines, from one wave or from two XCDs' L2s,
+                // halve the HBM write rate once the output outgrows the Infinity Cache).
+                // Only the grid's last tile row masks rows, and its last tile column the
+                // lanes past the pitch (a 32-cell line).
                 const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
                     outs + (size_t(ty0) * pitch + size_t(tx0)), 0, int(4u * kTH * pitch), 0x00020000);  // the tile's rows
-                if (ty0 + kTH <= int(S)) {
+                if (ty0 + kTH <= int(S) && tx0 + kTW <= int(pitch)) {
                     // (row offsets stepped in a VGPR: per-row SGPR offsets ran out of SGPRs)
                     uint32_t vo = lane * 4u;
 #pragma unroll
@@ -3021,7 +3022,7 @@ __device__ __forceinline__ void fill_body(const KArgs *__restrict__ a, uint32_t 
                     for (int i = 0; i < kTH; ++i) {
 #pragma unroll
                         for (int k = 0; k < kCPL; ++k) {
-                            if (ty0 + i < int(S))
+                            if (ty0 + i < int(S) && tx0 + 64 * k + int(lane) < int(pitch))
                                 __builtin_amdgcn_raw_buffer_store_b32(wd[k * kTH + i], rsrc, int((64u * k + lane) * 4u),
                                                                       int(uint32_t(i) * pitch * 4u), 0);
                         }

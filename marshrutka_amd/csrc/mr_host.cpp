@@ -956,8 +956,12 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     pl->all_mode = all_mode;
     if (all_mode) {  // per source: a record per cell, the label table, the boundary ranks
         const size_t T = size_t(NS) + 1;
-        // rows padded to whole fill tiles (rec_pitch): aligned 256 B store runs
-        const uint32_t pitch = (hp.p.S + kFillTW - 1) / kFillTW * kFillTW;
+        // rows padded to whole 128 B lines (rec_pitch; MR_REC_ALIGN=64 pads to whole
+        // 64-cell tile rows): the fill never stores part of a line
+        uint32_t align = 32;
+        if (const char *e = std::getenv("MR_REC_ALIGN"))
+            if (std::atoi(e) == 64) align = 64;
+        const uint32_t pitch = (hp.p.S + align - 1) / align * align;
         ka.rec_pitch = pitch;
         if (hipMalloc(reinterpret_cast<void **>(&pl->d_rec),
                       std::max<size_t>(nsrc, 1) * hp.p.S * pitch * sizeof(CellWord)) != hipSuccess ||

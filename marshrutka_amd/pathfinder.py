@@ -475,7 +475,7 @@ class SSSPPlan(Plan):
         return ptr.value, n.value
 
     def record_pitch(self) -> int:
-        """Cell words per row of device_records() (rows padded to a multiple of 64)."""
+        """Cell words per row of device_records() (rows padded to a multiple of 32)."""
         p = C.c_uint32()
         st = lib().mr_sssp_record_pitch(self.handle, C.byref(p))
         if st != MR_OK:

@@ -240,7 +240,7 @@ def test_overlap_error_of_either_slot_is_reported(eng, monkeypatch, inject_slot,
 @pytest.mark.parametrize("size,mode_env", [(33, None), (65, None), (33, "fallback")])
 def test_device_records_padded_rows(eng, monkeypatch, size, mode_env):
     """The device cell words sit in rows padded to mr_sssp_record_pitch cells (a
-    multiple of 64): word y * pitch + x of each source is cell (x, y)'s word, and it
+    multiple of 32: whole 128 B lines): word y * pitch + x of each source is cell (x, y)'s word, and it
     names the same boundary / special / source as the expanded record."""
     import ctypes as C
 
@@ -255,7 +255,7 @@ def test_device_records_padded_rows(eng, monkeypatch, size, mode_env):
     plan.run()
     via = [plan.records(i)[:, 3] for i in range(len(sources))]  # (waits for the plan's passes)
     pitch = plan.record_pitch()
-    assert pitch % 64 == 0 and size <= pitch < size + 64
+    assert pitch % 32 == 0 and size <= pitch < size + 32
     ptr, nbytes = plan.device_records()
     assert nbytes == plan.num_sources * size * pitch * 4
     hip = C.CDLL("libamdhip64.so")
