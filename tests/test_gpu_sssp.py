@@ -270,3 +270,24 @@ def test_device_records_padded_rows(eng, monkeypatch, size, mode_env):
         plain = (w & 0x80000000) == 0
         assert np.array_equal(w[plain] >> 20, via[i][plain])
         assert np.array_equal(w[~plain], via[i][~plain])
+
+
+def test_many_sources_per_pass_match_single_source_plans(eng):
+    """More sources in one pass than the fill has wave groups (every cell of a 41x41
+    map: 1 681 sources, so groups take several sources one after another): each
+    sampled source's records equal those of a plan holding that source alone, and
+    every source's own cell holds the source word."""
+    import numpy as np
+    m = SyntheticMap(41, campfires_per_homeland=4, seed=41)
+    g = eng.MapGrid(m.cells())
+    cells = m.all_indices()
+    plan = eng.SSSPPlan(g, Params(), cells)
+    plan.run()
+    assert plan.num_sources == len(cells)
+    rng = random.Random(3)
+    for i in sorted(rng.sample(range(len(cells)), 12)) + [0, len(cells) - 1]:
+        one = eng.SSSPPlan(g, Params(), [cells[i]])
+        one.run()
+        got, exp = plan.records(i), one.records(0)
+        assert np.array_equal(got, exp), (i, cells[i])
+        assert got[i, 3] == 0xFFFFFFFF
