@@ -1152,8 +1152,12 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         const uint64_t items = uint64_t(pl->ka.nsrc) * ((pl->ka.p.S + kFillTW - 1) / kFillTW) *
                                ((pl->ka.p.S + kFillTH - 1) / kFillTH);
         const uint64_t resident = uint64_t(pl->fused_per_cu) * pl->cus;
+        // the look-ahead solve takes at most a quarter of the resident workgroups: with
+        // as many hub workgroups as fit (8 k+ sources a pass at 1025^2) the fill was left
+        // with one workgroup (12 288 sources: 4.3 s a pass; 17 ms with 256 fill workgroups)
+        const uint32_t hub_fused = uint32_t(std::min<uint64_t>(pl->hub_blocks, std::max<uint64_t>(1, resident / 4)));
         const uint32_t fb_blocks = uint32_t(std::max<uint64_t>(
-            1, std::min<uint64_t>((items + 3) / 4, resident > pl->hub_blocks ? resident - pl->hub_blocks : 1)));
+            1, std::min<uint64_t>((items + 3) / 4, resident > hub_fused ? resident - hub_fused : 1)));
         e = hipSuccess;
         if (pl->runs == 1) e = launch_hub_plan(pl, pl->slots[cur].args, s);  // the first pass's specials
         if (e == hipSuccess && !pl->fb_none)
@@ -1164,7 +1168,7 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         const bool own = pl->runs == 1 || !pl->fb_none;
         if (e == hipSuccess && own && hipEventCreate(&f0) == hipSuccess) (void)hipEventRecord(f0, s);
         if (e == hipSuccess)
-            e = launch_hub_fill(pl->slots[nxt].args, pl->slots[cur].args_fill, pl->ka.p.perm, pl->spw, pl->hub_blocks,
+            e = launch_hub_fill(pl->slots[nxt].args, pl->slots[cur].args_fill, pl->ka.p.perm, pl->spw, hub_fused,
                                 fb_blocks, pl->hub_lds, s);
         pl->slots[cur].used = true;  // a fill ran in it: its counters hold a finished pass
         pl->timed_fill.push_back({f0, nullptr, !own});
