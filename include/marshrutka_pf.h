@@ -193,8 +193,14 @@ int mr_plan_create(const mr_grid *grid, const mr_params *params, const mr_query 
 int mr_plan_create_ex(const mr_grid *grid, const mr_params *params, const mr_query *queries,
                       uint32_t n, uint32_t max_cmds, mr_plan **out);
 /* Enqueues one full pass of the hot path on `stream` (a hipStream_t, or NULL
- * for the plan's own stream).  Asynchronous. */
+ * for the plan's own stream).  Asynchronous.  The passes of one plan execute in
+ * the order they were enqueued even when they are given different streams (a pass
+ * on a new stream first waits for the previous pass to end). */
 int mr_plan_run(mr_plan *plan, void *stream);
+/* Ordering for consumers of the device outputs: makes `stream` wait (without
+ * blocking the host) until every pass enqueued so far has finished; with stream
+ * NULL the calling thread waits instead. */
+int mr_plan_wait(mr_plan *plan, void *stream);
 /* Waits for the plan's work and copies results/commands to host buffers. */
 int mr_plan_fetch(mr_plan *plan, mr_result *results, mr_command *pool, uint64_t pool_cap);
 /* Device pointers of the compact per-query output records (for an RCCL
@@ -202,7 +208,10 @@ int mr_plan_fetch(mr_plan *plan, mr_result *results, mr_command *pool, uint64_t 
  * Records are in grouped order (queries grouped by source, so each source's
  * records are contiguous); mr_plan_record_queries maps record k to its query.
  * A label longer than max_cmds keeps {0xFFFFFFFF, offset, count} in its first
- * slot and its commands in the plan's own overflow pool. */
+ * slot and its commands in the plan's own overflow pool.  The call waits for the
+ * passes enqueued so far, so the words behind the pointers are whole when it
+ * returns; a later mr_plan_run rewrites them (order a reader on another stream with
+ * mr_plan_wait). */
 int mr_plan_device_outputs(mr_plan *plan, void **d_results, uint64_t *results_bytes,
                            void **d_commands, uint64_t *commands_bytes);
 /* Makes subsequent mr_plan_run calls write their compact outputs into caller
@@ -213,7 +222,8 @@ int mr_plan_bind_outputs(mr_plan *plan, void *d_results, void *d_commands);
 /* The same, and the overflow pool too: a label longer than max_cmds then keeps
  * its commands at d_overflow (overflow_cap commands of 16 B), so that one
  * collective over one caller buffer moves every record of a pass with all its
- * commands.  overflow_cap 0 keeps the plan's own pool. */
+ * commands.  overflow_cap 0 keeps the plan's own pool (d_overflow is then ignored);
+ * a non-zero overflow_cap needs a d_overflow. */
 int mr_plan_bind_outputs_ex(mr_plan *plan, void *d_results, void *d_commands, void *d_overflow,
                             uint32_t overflow_cap);
 /* Host-side decoding of compact records as mr_plan_device_outputs lays them out
@@ -297,7 +307,9 @@ int mr_sssp_records(mr_plan *plan, uint32_t i, mr_label_record *out);
  *                   metrics = entry b's + (k, 0, Fleetfoot-ceil(180 k)), commands =
  *                   entry b's chain ++ [StandardMove{k} b -> cell]
  *   0x80000000 | t  special t's own table label;  0xFFFFFFFF  the source
- * Plan sources are the caller's distinct sources in row-major cell order. */
+ * Plan sources are the caller's distinct sources in row-major cell order.  Waits for
+ * the passes enqueued so far (the words are whole when it returns); the next
+ * mr_plan_run rewrites them (mr_plan_wait orders a reader on another stream). */
 int mr_sssp_device_records(mr_plan *plan, void **d_records, uint64_t *bytes);
 /* Cell words per row of the device records (S rounded up to a multiple of 32). */
 int mr_sssp_record_pitch(mr_plan *plan, uint32_t *cells_per_row);
@@ -308,11 +320,20 @@ int mr_sssp_record_pitch(mr_plan *plan, uint32_t *cells_per_row);
  * with two tail commands, {Scroll of Escape, cell u, the entry's own cell} (from0 =
  * the parent's cell); kp0 =
  * kind << 29 | payload (Standard: legs; Central: moves; Caravan: distance << 1 |
- * coefficient 5), cells by rank in CellIndex order. */
+ * coefficient 5), cells by rank in CellIndex order.  Waits for the passes enqueued so
+ * far.  The pointer names the latest pass's table slot: it is valid until the next
+ * mr_plan_run (passes rotate through slots, and a pass solves the next pass's tables
+ * into another slot), so call this again after every run. */
 int mr_sssp_device_tables(mr_plan *plan, void **d_tables, uint64_t *bytes);
 /* The full label (FindPath::eval(sources[i], dst)) rebuilt from its record:
  * MR_OK, MR_ERR_CAPACITY (out->n_commands > cap) or an error. */
 int mr_sssp_label(mr_plan *plan, uint32_t i, mr_cell_index dst, mr_result *out, mr_command *cmds, uint32_t cap);
+/* Every destination's full label from the caller's source i (mr_sssp_label for all V
+ * cells at once, the all-destinations analogue of mr_plan_fetch): results[v] for
+ * row-major cell v, commands at pool[results[v].command_offset ..].  Waits for the
+ * plan.  MR_OK, MR_ERR_CAPACITY if pool_cap is too small (results[] are still filled,
+ * so the caller can size the pool), or an error. */
+int mr_sssp_labels(mr_plan *plan, uint32_t i, mr_result *results, mr_command *pool, uint64_t pool_cap);
 
 /* ---- misc ---------------------------------------------------------------- */
 uint32_t mr_abi_version(void);

@@ -735,6 +735,7 @@ struct mr_plan {
     OutCmd *d_cmd = nullptr;
     uint32_t *d_ws = nullptr, *d_counter = nullptr;
     hipStream_t stream = nullptr;
+    hipStream_t last_stream = nullptr;    // the stream the latest pass ran on
     hipEvent_t ev_last = nullptr;         // the end event of the latest pass (on the caller's stream)
     bool ev_last_orphan = false;          // ev_last was folded out of `timed` and is owned here
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;  // pending event pairs
@@ -760,7 +761,8 @@ struct mr_plan {
         uint32_t *lex = nullptr, *sstate = nullptr, *fb = nullptr, *counter = nullptr;
         KArgs *args = nullptr, *args_fb = nullptr, *args_fill = nullptr;
         hipEvent_t ev_hub = nullptr, ev_fill = nullptr;
-        bool used = false;  // a pass has run in this slot
+        bool used = false;    // a pass has run in this slot
+        bool solved = false;  // fused: a launch has solved the specials of this slot's next pass
     };
     std::vector<Slot> slots;  // slot 0 holds the plan's first buffers; empty: no overlap
     hipStream_t hub_stream = nullptr;
@@ -1122,6 +1124,16 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         (void)hipEventDestroy(e0);
         return fail(MR_ERR_DEVICE, "event");
     }
+    // Passes of one plan run in submission order whatever streams they are given:
+    // a pass reads what the previous one left (the fused look-ahead tables, the
+    // counters it resets, a slot the previous fill read), so a pass on another stream
+    // first waits for the previous pass's end.  plan_sync then only needs the last.
+    if (pl->ev_last && pl->last_stream != s && hipStreamWaitEvent(s, pl->ev_last, 0) != hipSuccess) {
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        return fail(MR_ERR_DEVICE, "wait for the previous pass");
+    }
+    const uint32_t prev_slot = pl->slot;
     if (pl->hp.hub && pl->all_mode && pl->fused) {  // one launch per pass, see below
         const uint32_t cur = pl->runs >= 1 ? (pl->slot + 1) % uint32_t(pl->slots.size()) : 0u;
         use_slot(pl, cur);
@@ -1159,18 +1171,31 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         const uint32_t fb_blocks = uint32_t(std::max<uint64_t>(
             1, std::min<uint64_t>((items + 3) / 4, resident > hub_fused ? resident - hub_fused : 1)));
         e = hipSuccess;
-        if (pl->runs == 1) e = launch_hub_plan(pl, pl->slots[cur].args, s);  // the first pass's specials
+        // the first pass (or one after a failed launch) solves its own specials first
+        const bool solve_own = !pl->slots[cur].solved;
+        if (solve_own) e = launch_hub_plan(pl, pl->slots[cur].args, s);
+        if (e == hipSuccess) pl->slots[cur].solved = true;
         if (e == hipSuccess && !pl->fb_none)
             e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, s);
         // with no SSSP launch the pass is the fused launch: its time is the pass's (an
         // event of its own costs command-processor time, see ev_last below)
         hipEvent_t f0 = nullptr;
-        const bool own = pl->runs == 1 || !pl->fb_none;
+        const bool own = solve_own || !pl->fb_none;
         if (e == hipSuccess && own && hipEventCreate(&f0) == hipSuccess) (void)hipEventRecord(f0, s);
         if (e == hipSuccess)
             e = launch_hub_fill(pl->slots[nxt].args, pl->slots[cur].args_fill, pl->ka.p.perm, pl->spw, hub_fused,
                                 fb_blocks, pl->hub_lds, s);
-        pl->slots[cur].used = true;  // a fill ran in it: its counters hold a finished pass
+        if (e == hipSuccess) {
+            pl->slots[cur].used = true;  // a fill ran in it: its counters hold a finished pass
+            pl->slots[nxt].solved = true;
+        } else {
+            // nothing of this pass is trusted: the next run re-takes this slot, and the
+            // slot the failed launch may have half-written is solved again
+            pl->slots[nxt].solved = false;
+            --pl->runs;
+            use_slot(pl, prev_slot);
+            if (pl->runs == 0) pl->slots[cur].solved = false;
+        }
         pl->timed_fill.push_back({f0, nullptr, !own});
     } else if (pl->hp.hub && pl->all_mode) {
         // hub solve + table export, the SSSP kernel for flagged sources, then the fill:
@@ -1219,6 +1244,7 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     if (pl->ev_last_orphan) (void)hipEventDestroy(pl->ev_last);
     pl->ev_last = e1;
     pl->ev_last_orphan = false;
+    pl->last_stream = s;
     pl->timed.push_back({e0, e1});
     if (!pl->timed_fill.empty() && !pl->timed_fill.back().second) pl->timed_fill.back().second = e1;
     if (e != hipSuccess) return fail(MR_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(e));
@@ -1301,7 +1327,7 @@ extern "C" int mr_plan_bind_outputs_ex(mr_plan *pl, void *d_results, void *d_com
     if (!plan_sync(pl)) return fail(MR_ERR_DEVICE, "sync");
     pl->ka.out_res = reinterpret_cast<OutResult *>(d_results);
     pl->ka.out_cmd = reinterpret_cast<OutCmd *>(d_commands);
-    if (d_overflow) {
+    if (d_overflow && overflow_cap) {  // overflow_cap 0 keeps the plan's own pool
         pl->ka.ovf = reinterpret_cast<OutCmd *>(d_overflow);
         pl->ka.ovf_cap = overflow_cap;
     }
@@ -1347,8 +1373,25 @@ extern "C" int mr_plan_get_stats(mr_plan *pl, mr_plan_stats *out) {
     return MR_OK;
 }
 
+// Makes `stream` (or, with NULL, the calling thread) wait until every pass enqueued
+// on the plan so far has finished: how a consumer on another stream reads the device
+// outputs without a host sync (passes are chained, so the last pass's end suffices).
+extern "C" int mr_plan_wait(mr_plan *pl, void *stream) {
+    if (!pl) return fail(MR_ERR_INVALID_ARG, "null plan");
+    if (!stream) return plan_sync(pl) ? MR_OK : fail(MR_ERR_DEVICE, "sync");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    // (a pass's hub-stream work is waited for by its own records' stream before the
+    // pass's end event, so that event covers it)
+    if (pl->ev_last && hipStreamWaitEvent(s, pl->ev_last, 0) != hipSuccess) return fail(MR_ERR_DEVICE, "wait");
+    return MR_OK;
+}
+
 extern "C" int mr_plan_device_outputs(mr_plan *pl, void **d_results, uint64_t *rb, void **d_commands, uint64_t *cb) {
     if (!pl) return fail(MR_ERR_INVALID_ARG, "null plan");
+    // the pointers are handed out once the plan's passes so far have finished, so a
+    // raw read right after this call sees whole records (mr_plan_wait orders a stream
+    // instead of the host)
+    if (!plan_sync(pl)) return fail(MR_ERR_DEVICE, "sync");
     if (d_results) *d_results = pl->ka.out_res;
     if (rb) *rb = uint64_t(pl->hp.nq) * sizeof(OutResult);
     if (d_commands) *d_commands = pl->ka.out_cmd;
@@ -1717,6 +1760,7 @@ extern "C" int mr_sssp_records(mr_plan *pl, uint32_t i, mr_label_record *out) {
 
 extern "C" int mr_sssp_device_records(mr_plan *pl, void **d_records, uint64_t *bytes) {
     if (!pl || !pl->all_mode) return fail(MR_ERR_INVALID_ARG, "not an all-destinations plan");
+    if (!plan_sync(pl)) return fail(MR_ERR_DEVICE, "sync");  // whole records behind the pointer
     if (d_records) *d_records = pl->d_rec;
     if (bytes) *bytes = uint64_t(pl->ka.nsrc) * pl->ka.p.S * pl->ka.rec_pitch * sizeof(CellWord);
     return MR_OK;
@@ -1731,6 +1775,7 @@ extern "C" int mr_sssp_record_pitch(mr_plan *pl, uint32_t *cells_per_row) {
 
 extern "C" int mr_sssp_device_tables(mr_plan *pl, void **d_tables, uint64_t *bytes) {
     if (!pl || !pl->all_mode) return fail(MR_ERR_INVALID_ARG, "not an all-destinations plan");
+    if (!plan_sync(pl)) return fail(MR_ERR_DEVICE, "sync");  // the latest pass's slot, finished
     if (d_tables) *d_tables = pl->d_tab;
     if (bytes) *bytes = uint64_t(pl->ka.nsrc) * (pl->ka.p.NS + 1) * sizeof(Rec);
     return MR_OK;
@@ -1739,30 +1784,24 @@ extern "C" int mr_sssp_device_tables(mr_plan *pl, void **d_tables, uint64_t *byt
 // The full label of destination dst from source i: the record's boundary chain in
 // the source's label table, plus the final walk (its length is the boundary's
 // grid distance to dst).
-extern "C" int mr_sssp_label(mr_plan *pl, uint32_t i, mr_cell_index dst, mr_result *res, mr_command *cmds, uint32_t cap) {
-    uint32_t si = 0;
-    if (int st = sssp_source(pl, i, si)) return st;
-    if (!res) return fail(MR_ERR_INVALID_ARG, "null result");
+// The label of cell w from plan source si, given its cell word and the source's
+// table: metrics into rec, compact commands into seq.  MR_OK or MR_ERR_DEVICE for a
+// word that names no entry or whose walk is not the boundary's distance.
+static int sssp_expand(const mr_plan *pl, uint32_t si, const std::vector<Rec> &tab, uint32_t w, CellWord word,
+                       mr_label_record &rec, std::vector<OutCmd> &seq) {
     const mr_grid *g = pl->grid;
-    uint32_t w;
-    if (!g->find(dst, w)) return fail(MR_ERR_INVALID_INDEX, "destination is not a grid cell");
     const uint32_t T = pl->ka.p.NS + 1;
-    CellWord word;
-    std::vector<Rec> tab;
-    const size_t at = (size_t(si) * g->S + w / g->S) * pl->ka.rec_pitch + w % g->S;  // padded rows
-    if (hipMemcpy(&word, pl->d_rec + at, sizeof(word), hipMemcpyDeviceToHost) != hipSuccess)
-        return fail(MR_ERR_DEVICE, "copy label");
-    if (int st = sssp_table(pl, si, tab)) return st;
-    mr_label_record rec;
+    seq.clear();
     if (!expand_word(pl->hp, tab, word, rec)) return fail(MR_ERR_DEVICE, "cell word names no table entry");
     const uint32_t src = pl->hp.src_v[si];
-    std::vector<OutCmd> seq;
     // rank of table entry e's cell (entry 0: the source)
     auto rk = [&](uint32_t e) { return g->rank[e == 0 ? src : pl->hp.sp[e].v]; };
     auto chain = [&](uint32_t t) {  // commands of table label t (parent 0 ends the chain)
-        std::vector<uint32_t> path;
-        for (uint32_t e = t, guard = 0; e != 0 && guard <= T; e = tab[e].parent(), ++guard) path.push_back(e);
-        for (size_t j = path.size(); j-- > 0;) {
+        uint32_t path[kMaxSpecials + 2];
+        uint32_t np = 0;
+        for (uint32_t e = t, guard = 0; e != 0 && guard <= T && np < kMaxSpecials + 2; e = tab[e].parent(), ++guard)
+            path[np++] = e;
+        for (uint32_t j = np; j-- > 0;) {
             const Rec &r = tab[path[j]];  // tails as Rec (mr_engine.hpp) derives them
             seq.push_back(OutCmd{r.kp0, r.from0, r.u, 0});
             if (r.ntail() == 2) seq.push_back(OutCmd{kSoE << 29, r.u, rk(path[j]), 0});
@@ -1787,6 +1826,25 @@ extern "C" int mr_sssp_label(mr_plan *pl, uint32_t i, mr_cell_index dst, mr_resu
         if (k != (word & kStKMask)) return fail(MR_ERR_DEVICE, "cell word's walk is not the boundary's distance");
         seq.push_back(OutCmd{(kStandard << 29) | k, g->rank[vb], g->rank[w], 0});
     }
+    return MR_OK;
+}
+
+extern "C" int mr_sssp_label(mr_plan *pl, uint32_t i, mr_cell_index dst, mr_result *res, mr_command *cmds, uint32_t cap) {
+    uint32_t si = 0;
+    if (int st = sssp_source(pl, i, si)) return st;
+    if (!res) return fail(MR_ERR_INVALID_ARG, "null result");
+    const mr_grid *g = pl->grid;
+    uint32_t w;
+    if (!g->find(dst, w)) return fail(MR_ERR_INVALID_INDEX, "destination is not a grid cell");
+    CellWord word;
+    std::vector<Rec> tab;
+    const size_t at = (size_t(si) * g->S + w / g->S) * pl->ka.rec_pitch + w % g->S;  // padded rows
+    if (hipMemcpy(&word, pl->d_rec + at, sizeof(word), hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(MR_ERR_DEVICE, "copy label");
+    if (int st = sssp_table(pl, si, tab)) return st;
+    mr_label_record rec;
+    std::vector<OutCmd> seq;
+    if (int st = sssp_expand(pl, si, tab, w, word, rec, seq)) return st;
     std::memset(res, 0, sizeof(*res));
     res->legs = rec.legs;
     res->money = rec.money;
@@ -1800,4 +1858,42 @@ extern "C" int mr_sssp_label(mr_plan *pl, uint32_t i, mr_cell_index dst, mr_resu
     for (size_t j = 0; j < seq.size(); ++j)
         if (!expand_cmd(g, cs, seq[j], cmds[j])) return fail(MR_ERR_DEVICE, "command names no cell");
     return MR_OK;
+}
+
+extern "C" int mr_sssp_labels(mr_plan *pl, uint32_t i, mr_result *results, mr_command *pool, uint64_t pool_cap) {
+    uint32_t si = 0;
+    if (int st = sssp_source(pl, i, si)) return st;
+    if (!results) return fail(MR_ERR_INVALID_ARG, "null results");
+    const mr_grid *g = pl->grid;
+    const uint32_t V = pl->ka.p.V, S = pl->ka.p.S, pitch = pl->ka.rec_pitch;
+    std::vector<CellWord> words(V);
+    std::vector<Rec> tab;
+    if (hipMemcpy2D(words.data(), S * sizeof(CellWord), pl->d_rec + size_t(si) * S * pitch, pitch * sizeof(CellWord),
+                    S * sizeof(CellWord), S, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(MR_ERR_DEVICE, "copy records");
+    if (int st = sssp_table(pl, si, tab)) return st;
+    const CmdScale cs = cmd_scale(pl->hp);
+    std::vector<OutCmd> seq;
+    uint64_t off = 0;
+    int ret = MR_OK;
+    for (uint32_t w = 0; w < V; ++w) {
+        mr_label_record rec;
+        if (int st = sssp_expand(pl, si, tab, w, words[w], rec, seq)) return st;
+        mr_result &r = results[w];
+        std::memset(&r, 0, sizeof(r));
+        r.legs = rec.legs;
+        r.money = rec.money;
+        r.time_s = int64_t(rec.time_s);
+        r.n_commands = uint32_t(seq.size());
+        r.command_offset = uint32_t(std::min<uint64_t>(off, 0xFFFFFFFFu));
+        r.status = MR_OK;
+        if (pool && off + seq.size() <= pool_cap && off + seq.size() <= 0xFFFFFFFFull) {
+            for (size_t j = 0; j < seq.size(); ++j)
+                if (!expand_cmd(g, cs, seq[j], pool[off + j])) return fail(MR_ERR_DEVICE, "command names no cell");
+        } else {
+            ret = MR_ERR_CAPACITY;
+        }
+        off += seq.size();
+    }
+    return ret;
 }

@@ -156,6 +156,25 @@ class SyntheticMap:
             out["poi"][(py + H) * S + (px + H)] = p
         return out
 
+    def query_array(self, src: Sequence[int], dst: Sequence[int], cells=None):
+        """Queries (row-major cell src[i] -> cell dst[i]) as a numpy array with
+        mr_query's 16 B layout (pathfinder.Plan(query_array=...)), vectorised;
+        `cells` = this map's cells_array() when the caller already has it."""
+        import numpy as np
+        if cells is None:
+            cells = self.cells_array()
+        ix = np.dtype([("kind", "u1"), ("sub", "u1"), ("x", "<u2"), ("y", "<u2"), ("res", "<u2")])
+        out = np.zeros(len(src), dtype=np.dtype([("from", ix), ("to", ix)]))
+        for side, idx in (("from", np.asarray(src, dtype=np.int64)), ("to", np.asarray(dst, dtype=np.int64))):
+            for f in ("kind", "sub", "x", "y"):
+                out[side][f] = cells[f][idx]
+        return out
+
+    def cell_of(self, ci: CellIndex) -> int:
+        """Row-major position of a cell (inverse of index_at)."""
+        x, y = index_to_geo(ci)
+        return (y + self.h) * self.size + (x + self.h)
+
     def campfires(self) -> List[CellIndex]:
         return sorted(geo_to_index(x, y) for (x, y), p in self.poi.items() if p == POI_CAMPFIRE)
 

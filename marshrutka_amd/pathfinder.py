@@ -26,10 +26,10 @@ LIB_PATH = os.environ.get("MR_LIB_PATH") or os.path.join(os.path.dirname(os.path
 EXPORTED_SYMBOLS = [
     "mr_grid_create", "mr_grid_destroy", "mr_grid_square_size", "mr_params_default", "mr_find_path",
     "mr_find_path_batch", "mr_plan_create", "mr_plan_create_ex", "mr_plan_run", "mr_plan_fetch", "mr_plan_device_outputs",
-    "mr_plan_num_sources", "mr_plan_record_queries", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_plan_bind_outputs", "mr_plan_bind_outputs_ex", "mr_decode_records", "mr_abi_version", "mr_last_error",
+    "mr_plan_num_sources", "mr_plan_record_queries", "mr_plan_wait", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_plan_bind_outputs", "mr_plan_bind_outputs_ex", "mr_decode_records", "mr_abi_version", "mr_last_error",
     "mr_device_available", "mr_parse_map_html", "mr_parse_error", "mr_grid_from_html",
     "mr_command_time", "mr_duration_display", "mr_render_schedule",
-    "mr_sssp_plan_create", "mr_sssp_records", "mr_sssp_device_records", "mr_sssp_record_pitch", "mr_sssp_device_tables", "mr_sssp_label", "mr_plan_fill_ms",
+    "mr_sssp_plan_create", "mr_sssp_records", "mr_sssp_device_records", "mr_sssp_record_pitch", "mr_sssp_device_tables", "mr_sssp_label", "mr_sssp_labels", "mr_plan_fill_ms",
 ]
 
 
@@ -66,6 +66,8 @@ def lib():
         L.mr_plan_create.restype = C.c_int
         L.mr_plan_run.argtypes = [vp, vp]
         L.mr_plan_run.restype = C.c_int
+        L.mr_plan_wait.argtypes = [vp, vp]
+        L.mr_plan_wait.restype = C.c_int
         L.mr_plan_fetch.argtypes = [vp, C.POINTER(mr_result), C.POINTER(mr_command), C.c_uint64]
         L.mr_plan_fetch.restype = C.c_int
         L.mr_plan_device_outputs.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_uint64), C.POINTER(vp),
@@ -119,6 +121,8 @@ def lib():
         L.mr_sssp_label.argtypes = [vp, C.c_uint32, mr_cell_index, C.POINTER(mr_result), C.POINTER(mr_command),
                                     C.c_uint32]
         L.mr_sssp_label.restype = C.c_int
+        L.mr_sssp_labels.argtypes = [vp, C.c_uint32, C.POINTER(mr_result), C.POINTER(mr_command), C.c_uint64]
+        L.mr_sssp_labels.restype = C.c_int
         L.mr_plan_fill_ms.argtypes = [vp]
         L.mr_plan_fill_ms.restype = C.c_double
         _lib = L
@@ -348,13 +352,22 @@ class Plan:
     """Device-resident batch: inputs uploaded once, `run()` enqueues one pass."""
 
     def __init__(self, grid: MapGrid, params: Params, pairs: Sequence[Tuple[CellIndex, CellIndex]],
-                 max_cmds: int = 0):
+                 max_cmds: int = 0, query_array=None):
         """max_cmds: command slots per query in the device output (0 = the C default, 16);
-        longer labels go through the plan's overflow pool."""
+        longer labels go through the plan's overflow pool.  query_array: the queries as
+        a contiguous numpy array of mr_query records (16 B each) instead of `pairs`
+        (millions of queries without one Python object each)."""
         self.grid = grid
-        self.n = len(pairs)
         self.max_cmds = max_cmds or 16
-        self._qs = queries_to_c(pairs)
+        if query_array is not None:
+            if query_array.dtype.itemsize != C.sizeof(mr_query) or not query_array.flags["C_CONTIGUOUS"]:
+                raise EngineError(abi.MR_ERR_INVALID_ARG, "query array must be contiguous mr_query records")
+            self.n = len(query_array)
+            self._qarr = query_array
+            self._qs = C.cast(query_array.ctypes.data, C.POINTER(mr_query))
+        else:
+            self.n = len(pairs)
+            self._qs = queries_to_c(pairs)
         self._p = params.to_c()
         h = C.c_void_p()
         if max_cmds:
@@ -380,6 +393,12 @@ class Plan:
 
     def run(self, stream: int = 0) -> None:
         st = lib().mr_plan_run(self.handle, C.c_void_p(stream) if stream else None)
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+
+    def wait(self, stream: int = 0) -> None:
+        """mr_plan_wait: `stream` (or, with 0, this thread) waits for every pass so far."""
+        st = lib().mr_plan_wait(self.handle, C.c_void_p(stream) if stream else None)
         if st != MR_OK:
             raise EngineError(st, last_error())
 
@@ -496,6 +515,25 @@ class SSSPPlan(Plan):
             raise EngineError(st, last_error())
         res.command_offset = 0
         return result_from_c(res, cmds)
+
+    def labels_raw(self, i: int):
+        """Every cell's full label from source i (mr_sssp_labels): (mr_result array of
+        V entries in row-major cell order, mr_command pool, commands used)."""
+        V = self.grid.square_size ** 2
+        res = (mr_result * V)()
+        cap = V * 6
+        while True:
+            pool = (mr_command * cap)()
+            st = lib().mr_sssp_labels(self.handle, i, res, pool, cap)
+            if st == MR_ERR_CAPACITY:
+                need = max(res[V - 1].command_offset + res[V - 1].n_commands, cap + 1)
+                cap = need
+                continue
+            break
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+        used = res[V - 1].command_offset + res[V - 1].n_commands
+        return res, pool, used
 
     def fill_ms(self) -> float:
         """Average fill-kernel time of the window the last kernel_ms() closed."""

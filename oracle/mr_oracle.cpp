@@ -810,16 +810,11 @@ extern "C" int mro_find_path_batch(const mro_grid *g, const mr_params *p, const 
 // label eval(from, cell) returns (eval pops `to` with that label and stops).  One
 // result per cell in the grid's input (row-major) order; the commands go to pool
 // (results[i].command_offset), MR_ERR_CAPACITY if pool_cap is too small.
-extern "C" int mro_sssp_all(const mro_grid *g, const mr_params *p, mr_cell_index from, mr_result *results,
-                            mr_command *pool, uint64_t pool_cap) {
-    if (!g || !results) return MR_ERR_INVALID_ARG;
-    Query q;
-    int st = make_query(g, p, q);
-    if (st != MR_OK) return st;
-    if (!valid_input(from)) return MR_ERR_INVALID_INDEX;
-    CellIndex f = build_any(from);
-    if (!g->at(f)) return MR_ERR_INVALID_INDEX;
-    std::unordered_map<CellIndex, TotalCost, CellIndexHash> dist;
+namespace mro {
+// FindPath::eval's loop (src/pathfinder.rs:219-246) without the early exit: the final
+// dist[] label of every cell reachable from f.
+static int sssp_dist(const Query &q, const CellIndex &f,
+                     std::unordered_map<CellIndex, TotalCost, CellIndexHash> &dist) {
     auto heap_less = [&](const TotalCost &a, const TotalCost &b) { return q.cmp(a, b) > 0; };
     std::priority_queue<TotalCost, std::vector<TotalCost>, decltype(heap_less)> heap(heap_less);
     dist[f] = total_new(f);
@@ -841,6 +836,99 @@ extern "C" int mro_sssp_all(const mro_grid *g, const mr_params *p, mr_cell_index
             }
         }
     }
+    return MR_OK;
+}
+
+// The digest of a command list that tests/label_digest.py computes from mr_command
+// arrays: each 40 B command as five little-endian u64 words (reserved bytes zero),
+// h = Horner over the words with kDigestP, the list H = Horner over the commands'
+// h with kDigestQ, all mod 2^64.
+static constexpr uint64_t kDigestP = 0x9E3779B97F4A7C15ull, kDigestQ = 0xC2B2AE3D27D4EB4Full;
+static uint64_t label_digest(const TotalCost &t) {
+    uint64_t H = 0;
+    for (const Command &c : t.commands) {
+        mr_command o;
+        std::memset(&o, 0, sizeof(o));
+        o.kind = c.agg.kind;
+        o.legs = c.agg.legs;
+        o.money = c.agg.money;
+        o.fleetfoot = c.agg.fleetfoot;
+        o.time_s = c.agg.time;
+        o.from = to_mr(c.from);
+        o.to = to_mr(c.to);
+        uint64_t w[5];
+        std::memcpy(w, &o, sizeof(w));
+        uint64_t h = 0;
+        for (uint64_t x : w) h = h * kDigestP + x;
+        H = H * kDigestQ + h;
+    }
+    return H;
+}
+}  // namespace mro
+
+// Every destination of each of n sources, on `threads` host threads (test
+// infrastructure for full-size parity): per source s and row-major cell i, at
+// [s * V + i]: legs, money, time, command count, status (MR_OK / MR_NOT_FOUND) and
+// the command-list digest (label_digest above).  Any output pointer may be null.
+extern "C" int mro_sssp_digest_batch(const mro_grid *g, const mr_params *p, const mr_cell_index *sources, uint32_t n,
+                                     uint32_t threads, uint32_t *legs, uint32_t *money, int64_t *time_s,
+                                     uint32_t *n_commands, int32_t *status, uint64_t *digest) {
+    if (!g || (n && !sources)) return MR_ERR_INVALID_ARG;
+    Query q;
+    int st = make_query(g, p, q);
+    if (st != MR_OK) return st;
+    const size_t V = g->grid.size();
+    std::vector<int> res(n, MR_OK);
+    std::atomic<uint32_t> next{0};
+    auto worker = [&]() {
+        for (uint32_t s = next++; s < n; s = next++) {
+            if (!valid_input(sources[s])) {
+                res[s] = MR_ERR_INVALID_INDEX;
+                continue;
+            }
+            CellIndex f = build_any(sources[s]);
+            if (!g->at(f)) {
+                res[s] = MR_ERR_INVALID_INDEX;
+                continue;
+            }
+            std::unordered_map<CellIndex, TotalCost, CellIndexHash> dist;
+            dist.reserve(V);
+            if ((res[s] = sssp_dist(q, f, dist)) != MR_OK) continue;
+            for (size_t i = 0; i < V; ++i) {
+                const size_t o = size_t(s) * V + i;
+                auto it = dist.find(g->grid[i].index);
+                const bool ok = it != dist.end();
+                if (legs) legs[o] = ok ? it->second.legs : 0;
+                if (money) money[o] = ok ? it->second.money : 0;
+                if (time_s) time_s[o] = ok ? it->second.time : 0;
+                if (n_commands) n_commands[o] = ok ? uint32_t(it->second.commands.size()) : 0;
+                if (status) status[o] = ok ? MR_OK : MR_NOT_FOUND;
+                if (digest) digest[o] = ok ? label_digest(it->second) : 0;
+            }
+        }
+    };
+    if (threads == 0) threads = std::max(1u, std::thread::hardware_concurrency());
+    threads = std::min<uint32_t>(threads, std::max<uint32_t>(1, n));
+    std::vector<std::thread> ts;
+    for (uint32_t t = 1; t < threads; ++t) ts.emplace_back(worker);
+    worker();
+    for (auto &t : ts) t.join();
+    for (int r : res)
+        if (r != MR_OK) return r;
+    return MR_OK;
+}
+
+extern "C" int mro_sssp_all(const mro_grid *g, const mr_params *p, mr_cell_index from, mr_result *results,
+                            mr_command *pool, uint64_t pool_cap) {
+    if (!g || !results) return MR_ERR_INVALID_ARG;
+    Query q;
+    int st = make_query(g, p, q);
+    if (st != MR_OK) return st;
+    if (!valid_input(from)) return MR_ERR_INVALID_INDEX;
+    CellIndex f = build_any(from);
+    if (!g->at(f)) return MR_ERR_INVALID_INDEX;
+    std::unordered_map<CellIndex, TotalCost, CellIndexHash> dist;
+    if ((st = sssp_dist(q, f, dist)) != MR_OK) return st;
     const size_t n = g->grid.size();
     for (size_t i = 0; i < n; ++i) {
         std::memset(&results[i], 0, sizeof(mr_result));

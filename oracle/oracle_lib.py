@@ -51,6 +51,10 @@ def lib():
         L.mro_sssp_all.argtypes = [C.c_void_p, C.POINTER(mr_params), mr_cell_index, C.POINTER(mr_result),
                                    C.POINTER(mr_command), C.c_uint64]
         L.mro_sssp_all.restype = C.c_int
+        vp = C.c_void_p
+        L.mro_sssp_digest_batch.argtypes = [C.c_void_p, C.POINTER(mr_params), C.POINTER(mr_cell_index), C.c_uint32,
+                                            C.c_uint32, vp, vp, vp, vp, vp, vp]
+        L.mro_sssp_digest_batch.restype = C.c_int
         L.mro_duration_display.argtypes = [C.c_int64, C.c_char_p, C.c_uint32]
         L.mro_duration_display.restype = C.c_int
         _lib = L
@@ -127,12 +131,33 @@ class OracleGrid:
         while True:
             pool = (mr_command * cap)()
             st = lib().mro_sssp_all(self.h, C.byref(p), src.to_c(), res, pool, cap)
-            if st != -8 or cap > self.n * 4096:  # MR_ERR_CAPACITY: grow the pool
+            if st != MR_ERR_CAPACITY or cap > self.n * 4096:  # grow the pool
                 break
             cap *= 4
         if st != MR_OK:
             raise ValueError(f"oracle sssp_all failed: {st}")
         return [result_from_c(res[i], pool) for i in range(self.n)]
+
+    def sssp_digests(self, params: Params, sources, threads: int = 0) -> dict:
+        """Every cell's label from each source (the reference's Dijkstra run to
+        completion, sources spread over host threads) as numpy arrays of shape
+        (len(sources), V) in row-major cell order: legs, money, time_s, n_commands,
+        status and `digest`, the command-list digest of tests/label_digest.py."""
+        import numpy as np
+        n, V = len(sources), self.n
+        out = {"legs": np.zeros((n, V), np.uint32), "money": np.zeros((n, V), np.uint32),
+               "time_s": np.zeros((n, V), np.int64), "n_commands": np.zeros((n, V), np.uint32),
+               "status": np.zeros((n, V), np.int32), "digest": np.zeros((n, V), np.uint64)}
+        srcs = (mr_cell_index * max(n, 1))()
+        for i, s in enumerate(sources):
+            srcs[i] = s.to_c()
+        p = params.to_c()
+        st = lib().mro_sssp_digest_batch(self.h, C.byref(p), srcs, n, threads,
+                                         *(out[k].ctypes.data for k in ("legs", "money", "time_s", "n_commands",
+                                                                        "status", "digest")))
+        if st != MR_OK:
+            raise ValueError(f"oracle sssp_digests failed: {st}")
+        return out
 
 
 def duration_display(seconds: int) -> str:

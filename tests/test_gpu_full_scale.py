@@ -1,0 +1,207 @@
+"""Parity at the BASELINE sizes (configs[2], [3], [4]) through the C ABI.
+
+The oracle's Dijkstra run to completion (oracle/mr_oracle.cpp mro_sssp_digest_batch,
+the reference's FindPath::eval loop src/pathfinder.rs:219-246 without its early exit)
+gives every cell's label from a source; labels are compared whole (metrics, command
+count and a digest of the command list, tests/label_digest.py) with numpy.
+
+* configs[3] (c4): the bench's 125k uniform queries on the 1025^2 map plus 1000
+  destinations for each of 16 sources of every kind (Center, border-1 cells,
+  campfires, on-axis and random cells), one Plan as the bench runs it.  Every label
+  of the batch is property-checked; every label of the 16 sources is compared with
+  the oracle, and 32 uniform queries with the oracle's single-query eval.
+* configs[2] (c3): every one of the 1 050 625 cells of 4 sources at 1025^2 through the
+  all-destinations plan (hub + fill), two comparator orders.
+* configs[4] (c5): every one of the 16.8 M cells of 3 sources at 4097^2 (64 clustered
+  campfires per homeland, Time and Money first) through the wide hub solver's query
+  path, and a 2000-query batch.  The oracle needs minutes and ~13 GB per solve at
+  that size, so its answers are committed fixtures (tests/golden/make_full_scale.py).
+"""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import label_digest as ld
+from golden_util import as_expected
+from marshrutka_amd.abi import SORT_MONEY, SORT_TIME, CellIndex, Params
+from marshrutka_amd.mapgen import SyntheticMap, random_queries
+
+pytestmark = pytest.mark.gpu
+
+ORACLE_THREADS = 16  # the GPU box's CPU share
+C5_FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "full_scale", "c5.json")
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from marshrutka_amd import build, pathfinder
+    build.build()
+    if not pathfinder.device_available():
+        pytest.fail("no gfx950 device visible to the GPU tests")
+    for v in ("MR_ALGO", "MR_HUB_FALLBACK_ALL", "MR_HUB_SPW", "MR_HUB_WIDE", "MR_HUB_NONLIN", "MR_GRID_STATE",
+              "MR_FILL_GX", "MR_DBG_FLAGS", "MR_FILL_OVERLAP", "MR_FILL_FUSED", "MR_FILL_SLOTS"):
+        os.environ.pop(v, None)
+    return pathfinder
+
+
+@pytest.fixture(scope="module")
+def c4_map():
+    m = SyntheticMap(1025, campfires_per_homeland=4, seed=4096)  # bench.py c3/c4
+    return m, m.cells_array()
+
+
+def _sources_of_every_kind(m, rng):
+    H = m.h
+    cf = m.campfires()
+    srcs = [CellIndex.center()] + [CellIndex.border(b, 1) for b in range(4)]
+    srcs += [cf[0], cf[len(cf) // 3], cf[-1]]
+    srcs += [CellIndex.border(0, H), CellIndex.border(1, H // 2), CellIndex.border(3, 2)]  # on the axes
+    srcs += [CellIndex.homeland(2, 1, 1), CellIndex.homeland(0, H, H)]  # next to the Center, a corner
+    while len(srcs) < 16:
+        c = m.index_at(rng.randrange(m.size * m.size))
+        if c not in srcs:
+            srcs.append(c)
+    return srcs
+
+
+def test_c4_full_scale(eng, oracle_lib, c4_map):
+    m, arr = c4_map
+    V = m.size * m.size
+    keys = ld.cell_keys(arr)
+    rng = random.Random(4096)
+    uni = random_queries(m, 125_000, 4096 + 17)  # the bench's c4 batch
+    srcs = _sources_of_every_kind(m, rng)
+    extra_src, extra_dst = [], []
+    cf_cells = [m.cell_of(c) for c in m.campfires()]
+    for s in srcs:
+        d = rng.sample(range(V), 1000 - len(cf_cells) - 2) + cf_cells + [m.cell_of(CellIndex.center()), m.cell_of(s)]
+        extra_src += [m.cell_of(s)] * len(d)
+        extra_dst += d
+    uni_src = np.array([m.cell_of(a) for a, _ in uni], dtype=np.int64)
+    uni_dst = np.array([m.cell_of(b) for _, b in uni], dtype=np.int64)
+    q_src = np.concatenate([uni_src, np.array(extra_src)])
+    q_dst = np.concatenate([uni_dst, np.array(extra_dst)])
+    n = len(q_src)
+    g = eng.MapGrid.from_array(arr)
+    plan = eng.Plan(g, Params(), None, max_cmds=6, query_array=m.query_array(q_src, q_dst, arr))
+    plan.run()
+    plan.run()  # the bench's steady state: a rerun of the same plan
+    res, pool = plan.fetch_raw()
+    st = plan.stats()
+    assert st["solver"] == "hub" and st["num_sources"] >= 117_000
+    props = ld.label_properties(res, pool, n, keys[q_src], keys[q_dst])
+    assert all(v == 0 for v in props.values()), props
+    got = ld.digests(res, pool, n)
+    og = oracle_lib.OracleGrid.from_array(arr)
+    want = og.sssp_digests(Params(), srcs, threads=ORACLE_THREADS)
+    off = len(uni)
+    for i, s in enumerate(srcs):
+        sel = np.arange(off + i * 1000, off + (i + 1) * 1000)
+        bad = ld.mismatches(got, {f: want[f][i] for f in want}, idx_got=sel, idx_exp=q_dst[sel])
+        assert bad.size == 0, (str(s), len(bad), [str(m.index_at(int(q_dst[sel][j]))) for j in bad[:4]])
+    # uniform queries from random sources: the oracle's own single-query eval
+    sample = rng.sample(range(len(uni)), 32)
+    eres, epool = og.find_path_batch_raw(Params(), [uni[i] for i in sample], threads=ORACLE_THREADS)
+    ed = ld.digests(eres, epool, len(sample))
+    bad = ld.mismatches(got, ed, idx_got=np.array(sample))
+    assert bad.size == 0, [uni[sample[j]] for j in bad[:4]]
+
+
+@pytest.mark.parametrize("params", [Params(), Params(sort_by=(SORT_TIME, SORT_MONEY), route_guru=2)],
+                         ids=["legs_money", "time_money_rg2"])
+def test_c3_every_cell_1025(eng, oracle_lib, c4_map, params):
+    m, arr = c4_map
+    V = m.size * m.size
+    rng = random.Random(33)
+    srcs = [CellIndex.center(), m.campfires()[5], m.index_at(rng.randrange(V)), CellIndex.border(2, 700)]
+    g = eng.MapGrid.from_array(arr)
+    plan = eng.SSSPPlan(g, params, srcs)
+    plan.run()
+    plan.run()
+    assert plan.stats()["solver"] == "hub"
+    og = oracle_lib.OracleGrid.from_array(arr)
+    want = og.sssp_digests(params, srcs, threads=ORACLE_THREADS)
+    keys = ld.cell_keys(arr)
+    for i, s in enumerate(srcs):
+        res, pool, used = plan.labels_raw(i)
+        got = ld.digests(res, pool, V, pool_len=used)
+        bad = ld.mismatches(got, {f: want[f][i] for f in want})
+        assert bad.size == 0, (str(s), len(bad), [str(m.index_at(int(j))) for j in bad[:4]])
+        props = ld.label_properties(res, pool, V, np.full(V, keys[m.cell_of(s)]), keys)
+        assert all(v == 0 for v in props.values()), props
+
+
+@pytest.fixture(scope="module")
+def c5(eng):
+    """bench.py's c5 map and the oracle's answers on it (tests/golden/make_full_scale.py)."""
+    with open(C5_FIXTURE) as f:
+        fx = json.load(f)
+    m = SyntheticMap(**fx["map"])
+    arr = m.cells_array()
+    return m, arr, eng.MapGrid.from_array(arr), fx
+
+
+def _labels_of_source(eng, m, arr, g, params, sv, chunk=1 << 21):
+    """Every cell's label from row-major cell sv through query plans of `chunk`
+    destinations (one source, so one wave solves it and reads them all off), as
+    label_digest fields over the V cells, plus the batch's property violations."""
+    V = m.size * m.size
+    keys = ld.cell_keys(arr)
+    out = {f: [] for f in ld.FIELDS}
+    props = {}
+    for lo in range(0, V, chunk):
+        dst = np.arange(lo, min(V, lo + chunk), dtype=np.int64)
+        plan = eng.Plan(g, params, None, max_cmds=8, query_array=m.query_array(np.full(len(dst), sv), dst, arr))
+        plan.run()
+        res, pool = plan.fetch_raw()
+        assert plan.stats()["solver"] == "hub_wide"
+        d = ld.digests(res, pool, len(dst))
+        for f in ld.FIELDS:
+            out[f].append(d[f])
+        for k, v in ld.label_properties(res, pool, len(dst), np.full(len(dst), keys[sv]), keys[dst]).items():
+            props[k] = props.get(k, 0) + v
+        del plan, res, pool
+    return {f: np.concatenate(v) for f, v in out.items()}, props
+
+
+def test_c5_every_destination_4097(eng, c5):
+    """configs[4] at full size: every one of the 16.8 M cells of 3 sources (two orders)
+    through the wide hub solver's query path, against the oracle's labels of every
+    cell (one checksum per grid row, committed: tests/golden/full_scale/c5.json)."""
+    m, arr, g, fx = c5
+    assert len(fx["sources"]) >= 3
+    for src in fx["sources"]:
+        params = Params.from_json(src["params"])
+        got, props = _labels_of_source(eng, m, arr, g, params, src["cell"])
+        assert all(v == 0 for v in props.values()), (src["spec"], props)
+        rows = ld.row_checksums(got, m.size)
+        want = np.array([int(x, 16) for x in src["rows"]], dtype=np.uint64)
+        bad = np.nonzero(rows != want)[0]
+        assert bad.size == 0, (src["spec"], params.sort_by, f"{bad.size} of {m.size} rows differ", bad[:8].tolist())
+
+
+def test_c5_full_scale_sample(eng, c5):
+    """configs[4]/c5 at full size: S = 4097 (16.8 M cells), 64 clustered campfires per
+    homeland (NS = 261), Time first (SURVEY 8d option a) and Money first (option b).
+    The wide hub solver answers a 2000-query batch (2000 sources in one launch); 8 of
+    them against the oracle's FindPath::eval (committed fixture), and every label of
+    the batch against properties that hold at any size."""
+    m, arr, g, fx = c5
+    keys = ld.cell_keys(arr)
+    for run in fx["sample"]:
+        params = Params.from_json(run["params"])
+        qs = random_queries(m, *run["batch"])
+        plan = eng.Plan(g, params, qs)
+        plan.run()
+        got = plan.fetch()
+        assert plan.stats()["solver"] == "hub_wide"
+        for i, e in zip(run["index"], run["expected"]):
+            assert as_expected(got[i]) == e, (params.sort_by, qs[i])
+        res, pool = plan.fetch_raw()
+        src = np.array([m.cell_of(a) for a, _ in qs])
+        dst = np.array([m.cell_of(b) for _, b in qs])
+        props = ld.label_properties(res, pool, len(qs), keys[src], keys[dst])
+        assert all(v == 0 for v in props.values()), (params.sort_by, props)

@@ -270,36 +270,6 @@ def test_many_campfires(eng, oracle_lib, grid_state, k, clustered):
         assert st["solver"] == "hub_wide" and st["specials_per_lane"] == (2 if k == 16 else 5)
 
 
-def test_c5_full_scale_sample(eng, oracle_lib):
-    """configs[4]/c5 at full size: S = 4097 (16.8 M cells), 64 clustered campfires per
-    homeland (NS = 261), Time first (SURVEY 8d option a) and Money first (option b).
-    The wide hub solver answers a 2000-query batch; a sample is checked against the
-    oracle (one CPU Dijkstra over the 16.8 M-cell grid per query), and the whole
-    batch against properties that hold at any size: every label is a valid command
-    chain from its source to its destination with the reported metrics."""
-    m = SyntheticMap(4097, campfires_per_homeland=64, seed=4097, clustered=True)
-    arr = m.cells_array()
-    g = eng.MapGrid.from_array(arr)
-    og = oracle_lib.OracleGrid.from_array(arr)
-    qs = random_queries(m, 2000, 45)
-    for params in (Params(sort_by=(SORT_TIME, SORT_MONEY)), Params(sort_by=(SORT_MONEY, SORT_LEGS))):
-        plan = eng.Plan(g, params, qs)
-        plan.run()
-        got = plan.fetch()
-        assert plan.stats()["solver"] == "hub_wide"
-        sample = list(range(0, 2000, 250))
-        exp = og.find_path_batch(params, [qs[i] for i in sample], threads=0)
-        for i, e in zip(sample, exp):
-            assert as_expected(got[i]) == as_expected(e), (params, qs[i])
-        for (a, b), r in zip(qs, got):
-            assert r is not None
-            cmds = r.commands
-            assert cmds[0].from_ == a and cmds[-1].to == b
-            assert all(x.to == y.from_ for x, y in zip(cmds, cmds[1:]))
-            assert (r.legs, r.money, r.time_s) == (sum(c.legs for c in cmds), sum(c.money for c in cmds),
-                                                   sum(c.time_s for c in cmds))
-
-
 @pytest.mark.parametrize("max_cmds", [1, 2, 3])
 def test_overflow_pool(eng, oracle_lib, grid_state, max_cmds):
     """Labels longer than the plan's command slots go through the overflow pool

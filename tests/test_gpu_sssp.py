@@ -291,3 +291,112 @@ def test_many_sources_per_pass_match_single_source_plans(eng):
         got, exp = plan.records(i), one.records(0)
         assert np.array_equal(got, exp), (i, cells[i])
         assert got[i, 3] == 0xFFFFFFFF
+
+
+def _hip():
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    hip.hipStreamCreate.argtypes = [C.POINTER(C.c_void_p)]
+    hip.hipStreamDestroy.argtypes = [C.c_void_p]
+    hip.hipStreamSynchronize.argtypes = [C.c_void_p]
+    return hip
+
+
+def _raw_words(hip, ptr, nbytes):
+    import ctypes as C
+
+    import numpy as np
+    out = np.empty(nbytes // 4, dtype=np.uint32)
+    assert hip.hipMemcpy(out.ctypes.data, C.c_void_p(ptr), nbytes, 2) == 0  # hipMemcpyDeviceToHost
+    return out
+
+
+def test_raw_device_pointers_right_after_run(eng, monkeypatch):
+    """The device-output getters wait for the passes enqueued so far (the header's
+    contract), so a raw hipMemcpy of the returned pointer, issued right after
+    mr_plan_run with no other sync, reads finished words: an all-destinations plan
+    whose pass takes a while (512 sources on 257^2) and a query plan."""
+    import numpy as np
+    for k in ("MR_ALGO", "MR_HUB_FALLBACK_ALL", "MR_FILL_GX", "MR_DBG_FLAGS", "MR_FILL_OVERLAP", "MR_FILL_FUSED"):
+        monkeypatch.delenv(k, raising=False)
+    hip = _hip()
+    m = SyntheticMap(257, campfires_per_homeland=4, seed=257)
+    g = eng.MapGrid(m.cells())
+    cells = m.all_indices()
+    sources = random.Random(5).sample(cells, 512)
+    ref = eng.SSSPPlan(g, Params(), sources)
+    ref.run()
+    ref.records(0)  # synced
+    ptr, nbytes = ref.device_records()
+    want = _raw_words(hip, ptr, nbytes)
+    plan = eng.SSSPPlan(g, Params(), sources)
+    for passes in (1, 2):
+        for _ in range(passes):
+            plan.run()
+        ptr, nbytes = plan.device_records()  # straight after the runs
+        got = _raw_words(hip, ptr, nbytes)
+        pitch = plan.record_pitch()
+        cols = np.arange(got.size) % pitch < 257  # pad words are unspecified
+        assert np.array_equal(got[cols], want[cols]), passes
+    qs = [(random.Random(i).choice(cells), random.Random(i + 7).choice(cells)) for i in range(20000)]
+    qp = eng.Plan(g, Params(), qs)
+    qp.run()
+    want_res = [(r.legs, r.money, r.time_s) if r else None for r in qp.fetch()]
+    order = qp.record_queries()
+    qp.run()
+    d_res, rb, _, _ = qp.device_outputs()
+    words = _raw_words(hip, d_res, rb).reshape(-1, 4)
+    for k in range(0, len(qs), 97):
+        q = order[k]
+        assert (int(words[k, 0]), int(words[k, 1]), int(words[k, 2])) == want_res[q], k
+
+
+@pytest.mark.parametrize("mode", ["fused", "streams", "query"])
+def test_passes_on_alternating_streams_match_serial(eng, monkeypatch, mode):
+    """mr_plan_run on a different stream every pass: passes still run in
+    submission order (a pass on a new stream waits for the previous pass), so the
+    look-ahead tables, slots and counters they hand over are finished; the records
+    equal one serial pass's."""
+    import ctypes as C
+
+    import numpy as np
+    for k in ("MR_ALGO", "MR_HUB_FALLBACK_ALL", "MR_FILL_GX", "MR_DBG_FLAGS", "MR_FILL_OVERLAP", "MR_FILL_SLOTS"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("MR_FILL_FUSED", "0" if mode == "streams" else "1")
+    hip = _hip()
+    streams = [C.c_void_p(), C.c_void_p()]
+    for s in streams:
+        assert hip.hipStreamCreate(C.byref(s)) == 0
+    try:
+        m = SyntheticMap(193, campfires_per_homeland=5, seed=19)
+        g = eng.MapGrid(m.cells())
+        cells = m.all_indices()
+        if mode == "query":
+            qs = [(random.Random(i).choice(cells), random.Random(i + 3).choice(cells)) for i in range(30000)]
+            ref = eng.Plan(g, Params(), qs)
+            ref.run()
+            want = np.frombuffer(ref.fetch_raw()[0], dtype=np.uint32).copy()
+            plan = eng.Plan(g, Params(), qs)
+        else:
+            sources = random.Random(6).sample(cells, 256)
+            monkeypatch.setenv("MR_FILL_OVERLAP", "0")
+            ref = eng.SSSPPlan(g, Params(), sources)
+            ref.run()
+            want = [ref.records(i) for i in range(0, 256, 17)]
+            monkeypatch.delenv("MR_FILL_OVERLAP")
+            plan = eng.SSSPPlan(g, Params(), sources)
+            assert plan.stats()["fill_launch"] == mode
+        for p in range(7):
+            plan.run(streams[p % 2].value)
+        if mode == "query":
+            got = np.frombuffer(plan.fetch_raw()[0], dtype=np.uint32)
+            assert np.array_equal(got, want)
+        else:
+            for j, i in enumerate(range(0, 256, 17)):
+                assert np.array_equal(plan.records(i), want[j]), i
+        del plan, ref
+    finally:
+        for s in streams:
+            hip.hipStreamSynchronize(s)
+            hip.hipStreamDestroy(s)
