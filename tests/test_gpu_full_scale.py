@@ -116,7 +116,7 @@ def test_c3_every_cell_1025(eng, oracle_lib, c4_map, params):
     m, arr = c4_map
     V = m.size * m.size
     rng = random.Random(33)
-    srcs = [CellIndex.center(), m.campfires()[5], m.index_at(rng.randrange(V)), CellIndex.border(2, 700)]
+    srcs = [CellIndex.center(), m.campfires()[5], m.index_at(rng.randrange(V)), CellIndex.border(2, 300)]
     g = eng.MapGrid.from_array(arr)
     plan = eng.SSSPPlan(g, params, srcs)
     plan.run()
