@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MR_ABI_VERSION 4u
+#define MR_ABI_VERSION 5u
 
 /* ---- status codes ------------------------------------------------------ */
 typedef enum mr_status {
@@ -260,6 +260,8 @@ typedef struct mr_plan_stats {
     uint32_t specials_per_lane; /* hub solver: table entries each lane owns (1 = one per lane) */
     uint32_t region_boundary_cells; /* MR_SOLVER_HUB_WIDE: cells scanned for each source's region row */
     uint32_t fill_launch;       /* all-destinations hub plans: MR_FILL_* (how the fill is launched) */
+    uint32_t lane_sources;      /* hub solver: sources solved one per lane (hub_lane_kernel); the rest
+                                   (more than 32 queries each) a lane per query (ABI 5) */
 } mr_plan_stats;
 enum {
     MR_FILL_NONE = 0,    /* not an all-destinations hub plan */

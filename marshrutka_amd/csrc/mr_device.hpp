@@ -2211,7 +2211,7 @@ __device__ __forceinline__ void hub_body(const KArgs *__restrict__ a, char *smem
     // would saturate at ~88 dequeues/us, MI355X_MICROARCH.md)
     const uint32_t waves = nblocks * (kBS / 64), wid = block * (kBS / 64) + (threadIdx.x >> 6);
     for (uint32_t k = 0;; ++k) {
-        const unsigned long long base = ((unsigned long long)k * waves + wid) * SPW;
+        const unsigned long long base = a->src_off + ((unsigned long long)k * waves + wid) * SPW;
 #ifdef MR_STAMPS
         H.hmark(8);
 #endif

@@ -173,6 +173,10 @@ struct KArgs {
     // labels longer than max_cmds: their commands in this pool (bump-allocated per pass)
     OutCmd *ovf;
     uint32_t ovf_cap;
+    // hub plans: sources [0, n_lane) go to hub_lane_kernel (one source per lane, few
+    // queries each), sources [src_off, nsrc) to hub_kernel (src_off = n_lane)
+    uint32_t n_lane;
+    uint32_t src_off;
 };
 // counter words: the pass's last workgroup copies the fallback and written counts
 // to their "last" slots and zeroes the rest, so no memset precedes a pass
@@ -193,6 +197,10 @@ enum : uint32_t {
 // overflow pool: its first command slot holds {kOvfTag, offset, count}
 constexpr uint32_t kStatusOverflow = 64u, kOvfTag = 0xFFFFFFFFu;
 enum : uint32_t { kAlgoGeneric = 0, kAlgoLegs = 1 };
+// hub plans: sources with at most this many queries run on hub_lane_kernel (one source
+// per lane, its queries read off by that lane); sources with more on hub_kernel (a lane
+// per query)
+constexpr uint32_t kLaneMaxQ = 32;
 
 constexpr uint32_t kErrKOverflow = 1u, kErrMetricOverflow = 2u, kErrBucket = 4u, kErrChain = 8u;
 // KArgs::dbg_flags bit (tests only): the fill launch raises kErrChain

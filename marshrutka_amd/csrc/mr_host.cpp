@@ -38,7 +38,11 @@ uint32_t hub_wide_spl(uint32_t NS);
 hipError_t launch_hub_wide(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t blocks,
                            hipStream_t stream);
 int hub_wide_blocks_per_cu(const uint32_t perm[3], uint32_t NS, uint32_t bytes);
+uint32_t hub_lane_entries(uint32_t NS);
+hipError_t launch_hub_lane(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t n_lane,
+                           hipStream_t stream);
 }  // namespace mr
+
 
 
 using namespace mr;
@@ -714,6 +718,9 @@ struct mr_plan {
     KArgs *d_args = nullptr;
     KArgs *d_args_fb = nullptr;           // SSSP launch over the hub solver's fallback list
     KArgs *d_args_hub_last = nullptr;     // hub launch that ends the pass (fallback known to be empty)
+    KArgs *d_args_lane = nullptr;         // hub_lane_kernel launch (sources [0, n_lane))
+    KArgs *d_args_lane_last = nullptr;    // the same, ending the pass
+    uint32_t n_lane = 0;                  // sources on the lane kernel; the rest on hub_kernel
     KArgs *d_args_fill = nullptr;         // all-destinations mode: the fill launch (ends the pass)
     bool all_mode = false;
     CellWord *d_rec = nullptr;            // all-destinations outputs (KArgs::out_rec ...)
@@ -800,6 +807,7 @@ struct mr_plan {
                         (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
                         (void *)d_counter, (void *)d_args, (void *)d_dbg, (void *)d_args_fb, (void *)d_near,
                         (void *)d_fb, (void *)d_args_hub_last, (void *)d_args_fill, (void *)d_rec,
+                        (void *)d_args_lane, (void *)d_args_lane_last,
                         (void *)d_tab,
                         (void *)d_lex, (void *)d_sstate, (void *)d_near_sp, (void *)d_rb_off, (void *)d_rb_cell, (void *)d_ovf})
             if (p) (void)hipFree(p);
@@ -856,8 +864,42 @@ static int upload_args(mr_plan *pl) {
         KArgs l = k;
         l.last_launch = 1;
         if (!put(pl->all_mode ? pl->d_args_fill : pl->d_args_hub_last, l)) return MR_ERR_DEVICE;
+        if (pl->d_args_lane && (!put(pl->d_args_lane, k) || !put(pl->d_args_lane_last, l))) return MR_ERR_DEVICE;
     }
     return MR_OK;
+}
+
+// Hub plans on the lane kernel: the sources with at most kLaneMaxQ queries first (one
+// source per lane, hub_lane_kernel), the others after them (hub_kernel, a lane per
+// query); each source's records stay contiguous.  Returns the count of the first group.
+static uint32_t partition_sources(HostPlan &hp) {
+    const uint32_t ns = uint32_t(hp.src_v.size());
+    std::vector<uint32_t> order;
+    order.reserve(ns);
+    for (uint32_t i = 0; i < ns; ++i)
+        if (hp.q_begin[i + 1] - hp.q_begin[i] <= kLaneMaxQ) order.push_back(i);
+    const uint32_t n_lane = uint32_t(order.size());
+    if (n_lane == ns) return n_lane;
+    for (uint32_t i = 0; i < ns; ++i)
+        if (hp.q_begin[i + 1] - hp.q_begin[i] > kLaneMaxQ) order.push_back(i);
+    std::vector<uint32_t> src(ns), qb(ns + 1), qd(hp.q_dst.size()), qi(hp.q_id.size());
+    uint32_t off = 0;
+    for (uint32_t j = 0; j < ns; ++j) {
+        const uint32_t i = order[j];
+        src[j] = hp.src_v[i];
+        qb[j] = off;
+        for (uint32_t k = hp.q_begin[i]; k < hp.q_begin[i + 1]; ++k, ++off) {
+            qd[off] = hp.q_dst[k];
+            qi[off] = hp.q_id[k];
+            hp.q_pos[hp.q_id[k]] = off;
+        }
+    }
+    qb[ns] = off;
+    hp.src_v.swap(src);
+    hp.q_begin.swap(qb);
+    hp.q_dst.swap(qd);
+    hp.q_id.swap(qi);
+    return n_lane;
 }
 
 static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *qs, uint32_t n, uint32_t max_cmds,
@@ -875,6 +917,11 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     HostPlan &hp = pl->hp;
     // all destinations: hub_kernel + fill only, linear run times (the fill's keys)
     if (all_mode && (hp.wide || hp.nonlin)) hp.hub = hp.wide = hp.nonlin = false;
+    // query plans with a linear run time and a table that fits a lane's registers: the
+    // sources with few queries run one per lane (MR_HUB_LANE=0: all on hub_kernel)
+    const char *hl = std::getenv("MR_HUB_LANE");
+    if (hp.hub && !hp.wide && !hp.nonlin && !all_mode && hub_lane_entries(hp.p.NS) != 0 && !(hl && !std::strcmp(hl, "0")))
+        pl->n_lane = partition_sources(hp);
     auto bail = [&](int code) {
         delete pl;
         return code;
@@ -954,6 +1001,8 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     ka.fb_list = nullptr;
     ka.fb_mode = 0;
     ka.fb_all = std::getenv("MR_HUB_FALLBACK_ALL") ? 1u : 0u;  // tests cover the fallback path
+    ka.n_lane = pl->n_lane;
+    ka.src_off = pl->n_lane;
     if (const char *e = std::getenv("MR_DBG_FLAGS")) ka.dbg_flags = uint32_t(std::atoi(e));
     pl->all_mode = all_mode;
     if (all_mode) {  // per source: a record per cell, the label table, the boundary ranks
@@ -1009,15 +1058,18 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         if (hb > 160 * 1024) return bail(fail(MR_ERR_LIMIT, "hub tables exceed LDS"));
         const int hper = std::max(1, hp.wide ? hub_wide_blocks_per_cu(hp.p.perm, NS, hb)
                                              : hub_blocks_per_cu(hp.p.perm, pl->spw, hp.nonlin, hb));
-        const uint64_t per_block = 4ull * pl->spw;
-        pl->hub_blocks = uint32_t(std::min<uint64_t>((nsrc + per_block - 1) / per_block,
-                                                     uint64_t(hper) * prop.multiProcessorCount));
+        const uint64_t per_block = 4ull * pl->spw, hub_src = nsrc - pl->n_lane;
+        pl->hub_blocks = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((hub_src + per_block - 1) / per_block,
+                                                                           uint64_t(hper) * prop.multiProcessorCount)));
         if (const char *e = std::getenv("MR_HUB_BLOCKS")) pl->hub_blocks = uint32_t(std::max(1, std::atoi(e)));
         pl->fb_blocks = pl->blocks;
         pl->fill_per_cu = uint32_t(std::max(1, fill_blocks_per_cu(hp.p.perm)));
         if (hipMalloc(reinterpret_cast<void **>(&pl->d_args_fb), sizeof(KArgs)) != hipSuccess ||
             hipMalloc(reinterpret_cast<void **>(&pl->d_args_hub_last), sizeof(KArgs)) != hipSuccess ||
             hipMalloc(reinterpret_cast<void **>(&pl->d_args_fill), sizeof(KArgs)) != hipSuccess)
+            return bail(fail(MR_ERR_DEVICE, "kernel args"));
+        if (pl->n_lane && (hipMalloc(reinterpret_cast<void **>(&pl->d_args_lane), sizeof(KArgs)) != hipSuccess ||
+                           hipMalloc(reinterpret_cast<void **>(&pl->d_args_lane_last), sizeof(KArgs)) != hipSuccess))
             return bail(fail(MR_ERR_DEVICE, "kernel args"));
     }
 #ifdef MR_HUBDUMP
@@ -1225,15 +1277,19 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         if (e == hipSuccess && pl->overlap && hipEventRecord(pl->slots[pl->slot].ev_fill, s) != hipSuccess)
             e = hipErrorUnknown;
         pl->timed_fill.push_back({f0, nullptr, false});  // one per pass (f0 may be null), as in `timed`
-    } else if (pl->hp.hub && pl->fb_none) {
-        // a pass of this plan (same inputs, deterministic result) had no fallback
-        // sources: the hub launch ends the pass on its own
-        e = launch_hub_plan(pl, pl->d_args_hub_last, s);
     } else if (pl->hp.hub) {
-        // closed-form hub solve for every source, then the SSSP kernel for the
-        // sources it flagged (usually none; those workgroups exit at once)
-        e = launch_hub_plan(pl, pl->d_args, s);
-        if (e == hipSuccess)
+        // closed-form hub solve: the lane kernel for the sources with few queries, the
+        // hub kernel for the others, then the SSSP kernel for the sources they flagged
+        // (usually none; those workgroups exit at once).  Once a pass of this plan (same
+        // inputs, deterministic result) had no fallback source, the hub launches end the
+        // pass on their own.
+        const bool big = pl->ka.nsrc > pl->n_lane;
+        e = hipSuccess;
+        if (pl->n_lane)
+            e = launch_hub_lane(pl->fb_none && !big ? pl->d_args_lane_last : pl->d_args_lane, pl->ka.p.perm,
+                                pl->ka.p.NS, pl->ka.nreg, pl->n_lane, s);
+        if (e == hipSuccess && big) e = launch_hub_plan(pl, pl->fb_none ? pl->d_args_hub_last : pl->d_args, s);
+        if (e == hipSuccess && !pl->fb_none)
             e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, s);
     } else {
         e = launch_solve(pl->d_args, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->blocks, s);
@@ -1366,6 +1422,7 @@ extern "C" int mr_plan_get_stats(mr_plan *pl, mr_plan_stats *out) {
     out->sssp_workgroups = pl->blocks;
     out->specials_per_lane = !pl->hp.hub ? 0u : (pl->hp.wide ? hub_wide_spl(pl->ka.p.NS) : 1u);
     out->region_boundary_cells = pl->hp.wide && pl->hp.rb_off && !pl->hp.rb_off->empty() ? pl->hp.rb_off->back() : 0u;
+    out->lane_sources = pl->n_lane;
     out->fill_launch = !(pl->hp.hub && pl->all_mode) ? MR_FILL_NONE
                        : pl->fused                   ? MR_FILL_FUSED
                        : pl->overlap                 ? MR_FILL_STREAMS

@@ -23,13 +23,15 @@ def eng():
     return pathfinder
 
 
-@pytest.fixture(params=["auto-lds", "auto-hbm", "hub1-lds", "wide-lds", "widescan-lds", "fallback-lds", "fallback-hbm",
+@pytest.fixture(params=["auto-lds", "auto-hbm", "hub1-lds", "hub2-lds", "wide-lds", "widescan-lds", "fallback-lds", "fallback-hbm",
                         "sssp-lds", "sssp-hbm", "generic-lds", "generic-hbm"])
 def grid_state(request, monkeypatch):
     """Every solver path x both grid-state regimes:
-    auto     — hub solver when the run time is linear (two sources per wave when
-               the specials fit 32 lanes), else the SSSP solvers
-    hub1     — hub solver with one source per wave
+    auto     — hub solver when the run time is linear (one source per lane when the
+               table fits 24 entries and a source has <= 32 queries, else two
+               sources per wave when the specials fit 32 lanes), else the SSSP solvers
+    hub1     — hub solver with one source per wave (no lane kernel)
+    hub2     — hub solver with two sources per wave (no lane kernel)
     wide     — the wide hub solver (several specials per lane) even where the
                narrow one applies
     widescan — the same with each source's region row scanned from the regions'
@@ -43,6 +45,9 @@ def grid_state(request, monkeypatch):
     monkeypatch.delenv("MR_HUB_FALLBACK_ALL", raising=False)
     monkeypatch.delenv("MR_HUB_SPW", raising=False)
     monkeypatch.delenv("MR_HUB_WIDE", raising=False)
+    monkeypatch.delenv("MR_HUB_LANE", raising=False)
+    if algo in ("hub1", "hub2"):
+        monkeypatch.setenv("MR_HUB_LANE", "0")
     if algo == "wide":
         monkeypatch.setenv("MR_HUB_WIDE", "1")
     if algo == "widescan":
