@@ -75,38 +75,65 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     ap.add_argument("--queries", type=int, default=0, help="override queries per GPU")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline budget (CPU-seconds)")
+    ap.add_argument("--cpu-seconds", type=float, default=24.0,
+                    help="CPU-baseline budget (wall seconds, split between the 1-thread and all-threads legs)")
+    ap.add_argument("--e2e-reps", type=int, default=3, help="fresh batches timed end to end (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default="", help="JSON with PMC-derived HBM bytes per launch (profiles/)")
     return ap.parse_args()
 
 
+def host_cores():
+    """(cores this process may run on, threads the baseline uses).  The first is the
+    affinity mask; the second is capped by the cgroup CPU quota when one is set (a GPU
+    box's share of a 256-thread host is 16 CPUs: more threads than the quota only
+    time-slice) and by MR_CPU_THREADS."""
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    use = cores
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            use = min(use, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    if os.environ.get("MR_CPU_THREADS"):
+        use = min(use, max(1, int(os.environ["MR_CPU_THREADS"])))
+    return cores, use
+
+
 def cpu_baseline_leg(m, params, queries, gpu_results, budget_s):
     """Oracle (C++ restatement of the reference, oracle/) on host cores over a
-    bounded sample of the same workload; also checks the sample's GPU results."""
+    bounded sample of the same workload, once on one thread and once on every thread
+    the host gives this process; also checks the sample's GPU
+    results.  Each leg runs ~budget_s / 2 of wall time."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_lib
     oracle_lib.build()
     og = oracle_lib.OracleGrid.from_array(m.cells_array())
-    threads = max(1, min(16, os.cpu_count() or 1))
-    # calibrate single-threaded (up to 64 queries or ~2 s), then size the run to
-    # ~budget CPU-seconds (at least one query per thread)
+    cores, threads = host_cores()
+    leg_s = max(1.0, budget_s / 2)
+    # one thread: queries in order until the leg's time is spent
     t0 = time.perf_counter()
-    done = 0
-    while done < min(64, len(queries)) and (done == 0 or time.perf_counter() - t0 < 2.0):
-        og.find_path_batch_raw(params, queries[done:done + 1], threads=1)
-        done += 1
-    per_q = max((time.perf_counter() - t0) / done, 1e-6)
-    n = int(min(len(queries), max(min(256, 16 * threads) if per_q < 0.05 else threads, budget_s / per_q)))
+    n1 = 0
+    while n1 < len(queries) and (n1 == 0 or time.perf_counter() - t0 < leg_s):
+        og.find_path_batch_raw(params, queries[n1:n1 + 1], threads=1)
+        n1 += 1
+    wall1 = time.perf_counter() - t0
+    per_q = wall1 / n1
+    # every thread: a sample sized to ~leg_s of wall (at least one query per thread)
+    n = int(min(len(queries), max(threads, threads * leg_s / per_q)))
     sample = queries[:n]
     t0 = time.perf_counter()
     labels = og.find_path_batch(params, sample, threads=threads)
     wall = time.perf_counter() - t0
     mism = sum(1 for e, g in zip(labels, gpu_results[:n]) if as_expected(e) != as_expected(g))
     return ({"value": n / wall, "unit": "queries/s", "cores": threads, "kind": "port",
-             "sample": f"first {n} queries of the rank-0 batch, oracle/mr_oracle.cpp (binary heap of full "
-                       f"labels + hash map, as the reference) on {threads} host threads, {wall:.2f} s wall; "
-                       f"cpu model: {cpu_model()}; nproc {os.cpu_count()}"},
+             "value_all_cores": n / wall, "value_1thread": n1 / wall1, "cores_all": cores,
+             "sample": f"first {n} queries of the rank-0 batch on {threads} threads ({wall:.1f} s wall) and the first "
+                       f"{n1} on 1 thread ({wall1:.1f} s), oracle/mr_oracle.cpp (binary heap of full labels + hash map, "
+                       f"as the reference); cpu model: {cpu_model()}; {cores} cores in the affinity mask, "
+                       f"os.cpu_count() {os.cpu_count()}"},
             {"checked": n, "mismatches": mism})
 
 
@@ -119,7 +146,7 @@ def cpu_baseline_all(m, params, plan, sources, budget_s):
     import oracle_lib
     oracle_lib.build()
     og = oracle_lib.OracleGrid.from_array(m.cells_array())
-    threads = max(1, min(16, os.cpu_count() or 1))
+    cores, threads = host_cores()
     H = m.size // 2
     V = m.size * m.size
 
@@ -141,10 +168,12 @@ def cpu_baseline_all(m, params, plan, sources, budget_s):
     labels = og.find_path_batch(params, sample, threads=threads)
     wall = time.perf_counter() - t0
     mism = sum(1 for i, ((s, d), e) in enumerate(zip(sample, labels)) if as_expected(plan.label(i, d)) != as_expected(e))
-    return ({"value": n * V / wall, "unit": "queries/s", "cores": threads, "kind": "port",
+    return ({"value": n * V / wall, "unit": "queries/s", "cores": threads, "kind": "port", "cores_all": cores,
+             "value_all_cores": n * V / wall, "value_1thread": V / per,
              "sample": f"{n} single-source solves to the farthest cell (~all {V} cells settled each), "
-                       f"oracle/mr_oracle.cpp on {threads} host threads, {wall:.2f} s wall, cells/s; "
-                       f"cpu model: {cpu_model()}"},
+                       f"oracle/mr_oracle.cpp on {threads} host threads, {wall:.2f} s wall, cells/s; the 1-thread "
+                       f"figure is the first solve alone ({per:.2f} s); cpu model: {cpu_model()}; {cores} cores in "
+                       f"the affinity mask"},
             {"checked": n, "mismatches": mism})
 
 
@@ -214,6 +243,41 @@ def as_expected(label):
     if label is None:
         return None
     return (label.legs, label.money, label.time_s, tuple(c.as_tuple() for c in label.commands))
+
+
+def end_to_end(m, grid, params, qpg, seed, max_cmds, reps):
+    """Whole-call throughput of fresh batches: plan creation (host grouping by source,
+    the per-plan tables, the uploads), one pass, the device->host copy and decode of
+    every label (mr_plan_fetch), synchronised.  The queries are built as a numpy
+    mr_query array beforehand (the caller's input).  Median over `reps` batches."""
+    import random as _random
+    import numpy as np
+    import torch
+    from marshrutka_amd import pathfinder
+    V = m.size * m.size
+    rows = []
+    for r in range(reps):
+        rng = _random.Random(seed + 1000 + r)
+        src = np.array([rng.randrange(V) for _ in range(qpg)], dtype=np.int64)
+        dst = np.array([rng.randrange(V) for _ in range(qpg)], dtype=np.int64)
+        qa = m.query_array(src, dst)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        plan = pathfinder.Plan(grid, params, None, max_cmds=max_cmds, query_array=qa)
+        t1 = time.perf_counter()
+        plan.run()
+        plan.wait()
+        t2 = time.perf_counter()
+        plan.fetch_raw()
+        t3 = time.perf_counter()
+        del plan
+        rows.append((t3 - t0, t1 - t0, t2 - t1, t3 - t2))
+    rows.sort()
+    tot, cr, run, fe = rows[len(rows) // 2]
+    return {"e2e_queries_per_s": qpg / tot, "queries": qpg, "ms": tot * 1e3, "plan_create_ms": cr * 1e3,
+            "run_ms": run * 1e3, "fetch_ms": fe * 1e3, "reps": reps,
+            "what": "fresh batch: Plan create (host grouping, tables, H2D) + one pass + mr_plan_fetch (D2H and "
+                    "decode of every label), median of reps"}
 
 
 def cpu_model():
@@ -459,6 +523,8 @@ def main():
     }
     if gather_check is not None:
         out["gather_check"] = gather_check
+    if rank == 0 and not all_dst and args.e2e_reps > 0:
+        out["end_to_end"] = end_to_end(m, grid, params, qpg, wl["seed"], wl.get("max_cmds", 16), args.e2e_reps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and all_dst:
         cb, parity = cpu_baseline_all(m, params, plan, mine, args.cpu_seconds)
         out["cpu_baseline"] = cb

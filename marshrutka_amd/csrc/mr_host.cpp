@@ -869,6 +869,19 @@ static int upload_args(mr_plan *pl) {
     return MR_OK;
 }
 
+// The lane kernel adds metrics without overflow checks and keeps distances in 16
+// bits (S <= 4097): it only takes plans whose longest possible label (2 NS + 4 commands: each
+// table entry once with at most two tail commands, plus the final walk) stays below
+// 2^32 in every metric at the per-command maxima.
+static bool lane_bounds_ok(const DevParams &p) {
+    const uint64_t ncmd = 2ull * p.NS + 4, dmax = 2ull * p.S + 2;
+    const uint64_t money = std::max<uint64_t>(std::max<uint64_t>(p.soe_cost, p.shq_cost),
+                                              std::max<uint64_t>(p.sfm_cost, 5 * dmax));
+    const uint64_t time = std::max<uint64_t>(uint64_t(p.rgt) * dmax, 180 * dmax);
+    const uint64_t lim = 0xFFFFFFFFull;
+    return p.S <= 4097 && ncmd * dmax <= lim && ncmd * money <= lim && ncmd * time <= lim;
+}
+
 // Hub plans on the lane kernel: the sources with at most kLaneMaxQ queries first (one
 // source per lane, hub_lane_kernel), the others after them (hub_kernel, a lane per
 // query); each source's records stay contiguous.  Returns the count of the first group.
@@ -920,7 +933,8 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     // query plans with a linear run time and a table that fits a lane's registers: the
     // sources with few queries run one per lane (MR_HUB_LANE=0: all on hub_kernel)
     const char *hl = std::getenv("MR_HUB_LANE");
-    if (hp.hub && !hp.wide && !hp.nonlin && !all_mode && hub_lane_entries(hp.p.NS) != 0 && !(hl && !std::strcmp(hl, "0")))
+    if (hp.hub && !hp.wide && !hp.nonlin && !all_mode && hub_lane_entries(hp.p.NS) != 0 && lane_bounds_ok(hp.p) &&
+        !(hl && !std::strcmp(hl, "0")))
         pl->n_lane = partition_sources(hp);
     auto bail = [&](int code) {
         delete pl;

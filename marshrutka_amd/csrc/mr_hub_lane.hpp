@@ -13,15 +13,21 @@
 // source l of its wave and keeps ALL of that source's tentative labels in registers
 // (entries 1..TM-1, fully unrolled loops, so nothing is indexed at run time): a
 // settle is a per-lane scan, a relaxation a per-lane compare-and-select, and every
-// wave instruction advances 64 sources.  No LDS traffic beyond the specials' static
-// table, no cross-lane operation in the loop.
+// wave instruction advances 64 sources.  No cross-lane operation in the loop.
+//
+// A label is 4 registers: (c1, c2) as one 64-bit key, c3, and a meta word (length,
+// parent entry, tail count, the first tail command's kind and CentralMove count); the
+// command payloads (walk / caravan / SoE-region distances) follow from the parent's
+// and the entry's cells, so they are rebuilt where a command is written or compared.
+// The host only gives this kernel plans whose metric sums provably stay below 2^32
+// (lane_bounds_ok, mr_host.cpp), so a 64-bit add of packed deltas never carries.
 //
 // Exactness follows hub_kernel step for step:
 //   * candidates into an entry from one settled special s share chain(s), so among
-//     them (metrics, length) ties are decided by the last command's kp (= the list
-//     order); the best of them is compared with the entry's tentative label, and only
-//     an exact (metrics, length) tie there walks the command lists (cmp_list, rare,
-//     out of the unrolled code);
+//     them (metrics, length) ties are decided by the last command's kind (the list
+//     order; their kinds differ); the best of them is compared with the entry's
+//     tentative label, and only an exact (metrics, length) tie there walks the command
+//     lists (cmp_list, rare, out of the unrolled code);
 //   * blockers: a boundary special whose settled label some walk candidate tied on
 //     all three metrics (hub_kernel's note_walk).  One bit per entry keeps "a walk
 //     candidate so far has the tentative label's metrics" — every candidate is >= the
@@ -37,27 +43,52 @@ namespace mr {
 #ifndef MR_LANE_WAVES
 #define MR_LANE_WAVES 2  // waves per SIMD the register budget is cut for
 #endif
+// a scheduling fence between the unrolled entries: without it the scheduler interleaves
+// all of them and runs out of (scalar lane-mask) registers
+#ifndef MR_LANE_NOFENCE
+#define MR_LANE_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define MR_LANE_FENCE() do {} while (0)
+#endif
 
-// a label of a table entry: metrics, len | parent << 16 | (ntail - 1) << 31, and the
-// first tail command's kp.  Its tail commands are {kp, rank(parent), u} and, when
-// ntail = 2, {SoE, u, own rank}; u is the entry's own rank unless ntail = 2, when it is
-// the region cell nearest to the parent (the parent's region row at the entry's region).
-struct LLab {
-    uint32_t m0, m1, m2, lpn, kp;
-};
-__device__ __forceinline__ uint32_t ll_len(uint32_t lpn) { return lpn & 0xFFFFu; }
-__device__ __forceinline__ uint32_t ll_par(uint32_t lpn) { return (lpn >> 16) & kNone10; }
-__device__ __forceinline__ uint32_t ll_nt(uint32_t lpn) { return (lpn >> 31) + 1u; }
-__device__ __forceinline__ uint32_t ll_pack(uint32_t len, uint32_t par, uint32_t nt) {
-    return (len & 0xFFFFu) | (par << 16) | ((nt - 1u) << 31);
+// meta: kind of the first tail command (3 b) | length (8 b) << 3 | parent entry (5 b)
+// << 11 | (tail count - 1) << 16 | CentralMove count (2 b) << 17.  (meta & 0x7FF)
+// orders by (length, kind): the tie-break among candidates from one settled special.
+__device__ __forceinline__ uint32_t lm_kind(uint32_t m) { return m & 7u; }
+__device__ __forceinline__ uint32_t lm_len(uint32_t m) { return (m >> 3) & 0xFFu; }
+__device__ __forceinline__ uint32_t lm_lk(uint32_t m) { return m & 0x7FFu; }
+__device__ __forceinline__ uint32_t lm_par(uint32_t m) { return (m >> 11) & 31u; }
+__device__ __forceinline__ uint32_t lm_nt(uint32_t m) { return ((m >> 16) & 1u) + 1u; }
+__device__ __forceinline__ uint32_t lm_cj(uint32_t m) { return (m >> 17) & 3u; }
+__device__ __forceinline__ uint32_t lm_pack(uint32_t len, uint32_t par, uint32_t nt, uint32_t kind, uint32_t cj = 0) {
+    return kind | (len << 3) | (par << 11) | ((nt - 1u) << 16) | (cj << 17);
 }
-__device__ __forceinline__ LLab ll_start() { return LLab{0, 0, 0, ll_pack(1, 0, 1), kNoMove << 29}; }
+constexpr unsigned long long kInfK = ~0ull;  // a label that is not there (no metrics reach 2^32 - 1 here)
+// the pair table word of specials (s, t): walk distance | detour << 14 | SoE-region
+// distance from s into t's region << 15 (kPtNoSd: none) | t's caravan coefficient bit
+// << 29; Manhattan = walk - 2 detour
+constexpr uint32_t kPtNoSd = 0x3FFFu;
+__device__ __forceinline__ uint32_t pt_wd(uint32_t w) { return w & 0x3FFFu; }
+__device__ __forceinline__ uint32_t pt_md(uint32_t w) { return (w & 0x3FFFu) - ((w >> 13) & 2u); }
+__device__ __forceinline__ uint32_t pt_sd(uint32_t w) { return (w >> 15) & 0x3FFFu; }
+__device__ __forceinline__ uint32_t pt_c5(uint32_t w) { return (w >> 29) & 1u; }  // a caravan into t costs 5 per unit
+
+struct LLab {
+    unsigned long long K;  // c1 << 32 | c2
+    uint32_t c3, meta;
+};
+// A per-lane bit as a plain VGPR value.  Without the empty asm the compiler keeps
+// every such boolean of the unrolled loops as a 64-bit lane mask in SGPRs, runs out of
+// them and spills (hundreds of SGPRs, 60 VGPRs of spill lanes).
+__device__ __forceinline__ uint32_t vbit(bool b, uint32_t bit) {
+    uint32_t v = b ? bit : 0u;
+    asm volatile("" : "+v"(v));
+    return v;
+}
 __device__ __forceinline__ void ll_sel(bool take, LLab &d, const LLab &c) {
-    d.m0 = take ? c.m0 : d.m0;
-    d.m1 = take ? c.m1 : d.m1;
-    d.m2 = take ? c.m2 : d.m2;
-    d.lpn = take ? c.lpn : d.lpn;
-    d.kp = take ? c.kp : d.kp;
+    d.K = take ? c.K : d.K;
+    d.c3 = take ? c.c3 : d.c3;
+    d.meta = take ? c.meta : d.meta;
 }
 
 template <uint32_t PERM, uint32_t TM>
@@ -67,10 +98,12 @@ struct LaneHub {
     DevParams P;
     const SpecialStatic *spl;  // LDS copy of a->sp
     const uint2 *nearS;        // LDS: region rows of the specials, row t at t * nreg
+    const uint32_t *PT;        // LDS: the pair table, row s at s * TM
     const uint32_t *rank, *sinfo, *rank_inv;
     uint32_t *counter;
     uint32_t nreg;
-    uint32_t err = 0;
+    uint32_t hubm, c5m, regm;  // entries that are caravan hubs / cost 5 per unit to reach / region campfires
+    uint32_t validm;           // entries 1..NS
     // this lane's source
     uint32_t src = 0, src_rk = 0, ts = kNone10;
     int sx = 0, sy = 0;
@@ -79,44 +112,52 @@ struct LaneHub {
     LLab L[TM];
     uint32_t tent = 0, done = 0, wt = 0, bndm = 0, blk = 0;
 
-    template <uint32_t I>
-    __device__ __forceinline__ static uint32_t met(const LLab &x) {
-        return I == 0 ? x.m0 : (I == 1 ? x.m1 : x.m2);
+    // ---- metrics in comparator order -------------------------------------------------
+    __device__ __forceinline__ static uint32_t pick(uint32_t i, uint32_t legs, uint32_t money, uint32_t time) {
+        return i == 0 ? legs : (i == 1 ? money : time);
     }
-    // (c1, c2, c3, length) in comparator order: -1, 0, 1
+    // a (legs, money, time) delta packed as the key's (c1, c2) part
+    __device__ __forceinline__ static unsigned long long dK(uint32_t legs, uint32_t money, uint32_t time) {
+        return ((unsigned long long)pick(C1, legs, money, time) << 32) | pick(C2, legs, money, time);
+    }
+    __device__ __forceinline__ static uint32_t d3(uint32_t legs, uint32_t money, uint32_t time) {
+        return pick(C3, legs, money, time);
+    }
+    __device__ __forceinline__ static uint32_t metric(const LLab &x, uint32_t i) {  // i: 0 legs, 1 money, 2 time
+        return i == C1 ? uint32_t(x.K >> 32) : (i == C2 ? uint32_t(x.K) : x.c3);
+    }
+    __device__ __forceinline__ static LLab mk(unsigned long long K, uint32_t c3, uint32_t meta) { return LLab{K, c3, meta}; }
+    __device__ __forceinline__ static LLab start() { return LLab{0ull, 0u, lm_pack(1, 0, 1, kNoMove)}; }
+    // (c1, c2, c3, length): -1, 0, 1
     __device__ __forceinline__ static int cmp4(const LLab &x, const LLab &y) {
-        if (met<C1>(x) != met<C1>(y)) return met<C1>(x) < met<C1>(y) ? -1 : 1;
-        if (met<C2>(x) != met<C2>(y)) return met<C2>(x) < met<C2>(y) ? -1 : 1;
-        if (met<C3>(x) != met<C3>(y)) return met<C3>(x) < met<C3>(y) ? -1 : 1;
-        const uint32_t lx = ll_len(x.lpn), ly = ll_len(y.lpn);
+        if (x.K != y.K) return x.K < y.K ? -1 : 1;
+        if (x.c3 != y.c3) return x.c3 < y.c3 ? -1 : 1;
+        const uint32_t lx = lm_len(x.meta), ly = lm_len(y.meta);
         if (lx != ly) return lx < ly ? -1 : 1;
         return 0;
     }
-    __device__ __forceinline__ static bool eq3(const LLab &x, const LLab &y) {
-        return x.m0 == y.m0 && x.m1 == y.m1 && x.m2 == y.m2;
+    __device__ __forceinline__ static bool eq3(const LLab &x, const LLab &y) { return (x.K == y.K) & (x.c3 == y.c3); }
+    // the same as two flags, without branches (bitwise, so nothing short-circuits into
+    // divergent control flow in the unrolled loops)
+    struct Cmp {
+        bool lt, eq;
+    };
+    __device__ __forceinline__ static Cmp cmpx(const LLab &x, const LLab &y) {
+        const bool kl = x.K < y.K, ke = x.K == y.K, cl = x.c3 < y.c3, ce = x.c3 == y.c3;
+        const uint32_t lx = lm_len(x.meta), ly = lm_len(y.meta);
+        return Cmp{bool(kl | (ke & (cl | (ce & (lx < ly))))), bool(ke & ce & (lx == ly))};
     }
-    __device__ __forceinline__ uint32_t add32(uint32_t x, uint32_t y) {
-        const uint32_t r = x + y;
-        err |= r < x ? kErrMetricOverflow : 0u;
-        return r;
-    }
-    // a StandardMove run of k legs: 180 k s (linear run times only on this kernel)
-    __device__ __forceinline__ uint32_t run_time(uint32_t k) {
-        const unsigned long long t = 180ull * k;
-        err |= t > 0xFFFFFFFFull ? kErrMetricOverflow : 0u;
-        return uint32_t(t);
-    }
+
     __device__ __forceinline__ uint32_t rk(uint32_t e) const { return e == 0 ? src_rk : spl[e].rk; }
-    // the rank of the region cell nearest to entry p's cell in region r
-    __device__ __forceinline__ uint32_t near_rank(uint32_t p, uint32_t r) const {
-        return p == 0 ? srow[r].y : nearS[p * nreg + r].y;
+    __device__ __forceinline__ void pos(uint32_t e, int &x, int &y) const {
+        x = e == 0 ? sx : spl[e].x;
+        y = e == 0 ? sy : spl[e].y;
     }
-    __device__ __forceinline__ uint32_t u_of(const LLab &x, uint32_t own_rk, uint32_t own_rid) const {
-        return ll_nt(x.lpn) == 2 ? near_rank(ll_par(x.lpn), own_rid) : own_rk;
-    }
+    // region row entry r of entry p's cell (p = 0: the source)
+    __device__ __forceinline__ uint2 near_of(uint32_t p, uint32_t r) const { return p == 0 ? srow[r] : nearS[p * nreg + r]; }
     // entry e's label (run-time e; a select per entry: the rare paths only)
     __device__ __forceinline__ LLab get(uint32_t e) const {
-        LLab r = ll_start();
+        LLab r = start();
 #pragma unroll
         for (uint32_t t = 1; t < TM; ++t) ll_sel(e == t, r, L[t]);
         return r;
@@ -126,161 +167,174 @@ struct LaneHub {
         for (uint32_t t = 1; t < TM; ++t) ll_sel(e == t, L[t], c);
     }
 
-    // ---- label builders (TotalCost += edge, src/cost.rs:208-315) ---------------------
-    // the settled label ls of special s extended by a non-Standard edge (ext_view)
-    __device__ __forceinline__ LLab ext(const LLab &ls, uint32_t s, uint32_t kind, uint32_t payload, uint32_t dm,
-                                        uint32_t dt) {
-        const uint32_t lk = ll_nt(ls.lpn) == 2 ? kSoE : (ls.kp >> 29);
-        LLab c;
-        if (lk == kNoMove) {  // the start label: NoMove is replaced, its from kept
-            c = LLab{0, dm, dt, ll_pack(1, 0, 1), (kind << 29) | payload};
-        } else if (kind == kCentral && lk == kCentral) {  // CentralMoves merge
-            c = LLab{ls.m0, ls.m1, add32(ls.m2, dt), ll_pack(ll_len(ls.lpn), ll_par(ls.lpn), 1), ls.kp + 1u};
-        } else {
-            c = LLab{ls.m0, add32(ls.m1, dm), add32(ls.m2, dt), ll_pack(ll_len(ls.lpn) + 1u, s, 1), (kind << 29) | payload};
+    // ---- commands of a label (rare paths: list compares and output) -----------------
+    // The label x ends at a cell at (ox, oy) of rank ork, region orid (kNone10: none).
+    // Its first tail command's payload follows from its parent's cell: a walk's or a
+    // caravan's distance, the SoE-region distance, or the CentralMove count.
+    struct Own {
+        int x, y;
+        uint32_t rk, rid, c5;  // c5: a caravan into this cell costs 5 per unit
+    };
+    __device__ __forceinline__ Own own_of(uint32_t e) const {
+        int x, y;
+        pos(e, x, y);
+        return Own{x, y, rk(e), e == 0 ? kNone10 : spl[e].rid, (c5m >> e) & 1u};
+    }
+    __device__ __forceinline__ Cmd tail(uint32_t meta, const Own &o, int i) const {
+        const uint32_t p = lm_par(meta), kind = lm_kind(meta), nt = lm_nt(meta);
+        int px, py;
+        pos(p, px, py);
+        uint32_t pay = 0, u = o.rk;
+        if (nt == 2) {  // [Std{d} p -> u, SoE u -> own]: u is p's nearest cell of own's region
+            const uint2 e = near_of(p, o.rid);
+            pay = e.x;
+            u = e.y;
+        } else if (kind == kStandard) {
+            pay = walk_dist(px, py, o.x, o.y);
+        } else if (kind == kCaravan) {
+            pay = (uint32_t(abs(px - o.x) + abs(py - o.y)) << 1) | o.c5;
+        } else if (kind == kCentral) {
+            pay = lm_cj(meta);
         }
-        return c;
+        if (i == 0) return Cmd{(kind << 29) | pay, rk(p), u};
+        return Cmd{kSoE << 29, u, o.rk};
     }
-    // full(b) ++ [StandardMove{k} b -> .] from the settled special b (k > 0)
-    __device__ __forceinline__ LLab walk(const LLab &lb, uint32_t b, uint32_t k) {
-        return LLab{add32(lb.m0, k), lb.m1, add32(lb.m2, run_time(k)), ll_pack(ll_len(lb.lpn) + 1u, b, 1),
-                    (kStandard << 29) | k};
-    }
-    // ... and then its Scroll of Escape from the walk's end (ntail 2)
-    __device__ __forceinline__ LLab walk_soe(const LLab &lb, uint32_t b, uint32_t k) {
-        LLab c = walk(lb, b, k);
-        c.m1 = add32(c.m1, P.soe_cost);
-        c.lpn = ll_pack(ll_len(lb.lpn) + 2u, b, 2);
-        return c;
-    }
-
-    // ---- the command-list order (src/cost.rs:423-424), rare --------------------------
     __device__ __forceinline__ static int cmp_cmd(const Cmd &x, const Cmd &y) {
         if (x.kp != y.kp) return x.kp < y.kp ? -1 : 1;
         if (x.from != y.from) return x.from < y.from ? -1 : 1;
         if (x.to != y.to) return x.to < y.to ? -1 : 1;
         return 0;
     }
-    __device__ __forceinline__ Cmd tail(const LLab &x, uint32_t own_rk, uint32_t own_rid, int i) const {
-        const uint32_t u = u_of(x, own_rk, own_rid);
-        if (i == 0) return Cmd{x.kp, rk(ll_par(x.lpn)), u};
-        return Cmd{kSoE << 29, u, own_rk};
+    // The rare paths read the entries' meta words from a per-wave LDS copy (M: entry t of
+    // lane l at t * 64 + l), written by dump_meta() right before them, so they walk
+    // command chains with LDS reads instead of selects over the register-held table.
+    uint32_t *M;
+    __device__ __forceinline__ void dump_meta() const {
+        const uint32_t l = lane_id();
+        M[l] = start().meta;
+#pragma unroll
+        for (uint32_t t = 1; t < TM; ++t) M[t * 64u + l] = L[t].meta;
     }
-    // lexicographic compare of two equal-length command lists, walking from the last
-    // command towards the first (hub_kernel's cmp_list); xid/yid name the table entries
-    // the labels are (kOwn for built ones), so a shared prefix stops the walk
-    __device__ __forceinline__ int cmp_list(LLab x, uint32_t xid, uint32_t xrk, uint32_t xrid, LLab y, uint32_t yid, uint32_t yrk,
-                            uint32_t yrid) const {
-        int xt = int(ll_nt(x.lpn)) - 1, yt = int(ll_nt(y.lpn)) - 1;
+    __device__ __forceinline__ uint32_t meta_of(uint32_t e) const { return M[e * 64u + lane_id()]; }
+    // lexicographic compare of two equal-length command lists (metas x and y), walking
+    // from the last command towards the first (hub_kernel's cmp_list); xid/yid name the
+    // table entries the labels are (kOwn for built ones), so a shared prefix stops the walk
+    __device__ __forceinline__ int cmp_list(uint32_t x, uint32_t xid, Own xo, uint32_t y, uint32_t yid, Own yo) const {
+        int xt = int(lm_nt(x)) - 1, yt = int(lm_nt(y)) - 1;
         int res = 0;
         for (uint32_t guard = 0; guard < 4096u; ++guard) {
             if (xid != kOwn && xid == yid && xt == yt) return res;
-            const int r = cmp_cmd(tail(x, xrk, xrid, xt), tail(y, yrk, yrid, yt));
+            const int r = cmp_cmd(tail(x, xo, xt), tail(y, yo, yt));
             if (r) res = r;
             if (xt > 0) {
                 --xt;
             } else {
-                const uint32_t p = ll_par(x.lpn);
-                if (p == 0) return res;
-                xid = p;
-                x = get(p);
-                xrk = spl[p].rk;
-                xrid = spl[p].rid;
-                xt = int(ll_nt(x.lpn)) - 1;
+                const uint32_t pp = lm_par(x);
+                if (pp == 0) return res;
+                xid = pp;
+                x = meta_of(pp);
+                xo = own_of(pp);
+                xt = int(lm_nt(x)) - 1;
             }
             if (yt > 0) {
                 --yt;
             } else {
-                const uint32_t p = ll_par(y.lpn);
-                if (p == 0) return res;
-                yid = p;
-                y = get(p);
-                yrk = spl[p].rk;
-                yrid = spl[p].rid;
-                yt = int(ll_nt(y.lpn)) - 1;
+                const uint32_t pp = lm_par(y);
+                if (pp == 0) return res;
+                yid = pp;
+                y = meta_of(pp);
+                yo = own_of(pp);
+                yt = int(lm_nt(y)) - 1;
             }
         }
         atomicOr(counter + kCtrFlags, kErrChain);
         return res;
     }
 
-    // ---- candidates from one settled special s into entry t ------------------------
-    // The best of the CentralMove, caravan, SoE, walk and SoE-region candidates from s
-    // (they share chain(s): (metrics, length) ties go to the smaller last kp), and the
-    // walk candidate itself (for the blocker bit).  `live`: t is an unsettled entry.
-    struct FromS {
-        LLab c, w;
-        bool any, won;
-    };
-    __device__ __forceinline__ void consider(FromS &f, bool on, const LLab &c) const {
-        bool take = on;
-        if (on && f.any) {
-            const int r = cmp4(c, f.c);
-            take = r < 0 || (r == 0 && c.kp < f.c.kp);
-        }
-        ll_sel(take, f.c, c);
-        f.any = f.any || on;
+    // the walk of k legs from table entry b (label lb) to a plain cell
+    __device__ __forceinline__ static LLab walk_to(const LLab &lb, uint32_t b, uint32_t k) {
+        return mk(lb.K + dK(k, 0, 180u * k), lb.c3 + d3(k, 0, 180u * k), lm_pack(lm_len(lb.meta) + 1u, b, 1, kStandard));
     }
-    __device__ __forceinline__ FromS from_s(bool live, const LLab &ls, uint32_t s, const SpecialStatic &sS, bool walks,
-                                            uint32_t t, const SpecialStatic &tS) {
+
+    // ---- candidates from one settled special s into entry t ------------------------
+    // The best of the CentralMove, caravan, SoE, walk and SoE-region candidates from s;
+    // they share chain(s), so (metrics, length) ties go to the smaller last-command kind.
+    // Also the walk candidate itself (for the blocker bit).
+    // A candidate that does not apply has K = kInfK, so choosing among candidates is a
+    // plain minimum and no per-entry flag outlives its compare.
+    struct FromS {
+        LLab c, w;  // the best candidate from s; the walk candidate (for the blocker bit)
+    };
+    __device__ __forceinline__ static LLab opt(bool on, const LLab &c) { return LLab{on ? c.K : kInfK, c.c3, c.meta}; }
+    // c replaces f.c if smaller by (c1, c2, c3, length, kind)
+    __device__ __forceinline__ static void consider(LLab &f, const LLab &c) {
+        const bool lt = (c.K < f.K) | ((c.K == f.K) & ((c.c3 < f.c3) | ((c.c3 == f.c3) & (lm_lk(c.meta) < lm_lk(f.meta)))));
+        ll_sel(lt, f, c);
+    }
+    // Per-iteration context of the settled special s: its label ls; `base` = ls with an
+    // appended command (length + 1, parent s; the zero label when ls is the start label,
+    // whose NoMove is replaced); merge = ls ends in a CentralMove (one more merges).
+    // Which candidate kinds apply to which entries is a set of per-lane bit masks.
+    struct Settle {
+        LLab ls, base;
+        uint32_t s;
+        bool merge;
+        uint32_t cen, car, soe, reg, walk;  // entries a CentralMove / caravan / SoE / SoE-region / walk reaches
+    };
+    __device__ __forceinline__ FromS from_s(const Settle &z, uint32_t t, uint32_t w) const {
         const DevParams &p = P;
+        const uint32_t wd = pt_wd(w), md = pt_md(w), sd = pt_sd(w);
+        const uint32_t s = z.s, len = lm_len(z.ls.meta);
         FromS f;
-        f.any = false;
-        f.won = false;
-        f.c = ls;
-        f.w = ls;
-        if (tS.flags & (kSpCenter | kSpBorder1)) {  // CentralMove: Center <-> border-1 cells
-            const bool on = live && (((sS.flags & kSpCenter) && (tS.flags & kSpBorder1)) ||
-                                     ((sS.flags & kSpBorder1) && (tS.flags & kSpCenter)));
-            consider(f, on, ext(ls, s, kCentral, 1, 0, 10));
+        // the walk from boundary s (not into the Center)
+        f.w = opt((z.walk >> t) & 1u, mk(z.ls.K + dK(wd, 0, 180u * wd), z.ls.c3 + d3(wd, 0, 180u * wd),
+                                          lm_pack(len + 1u, s, 1, kStandard)));
+        f.c = f.w;
+        // CentralMove: the Center (entry 1) <-> the border-1 cells (entries 2..5)
+        if (t <= 5) {
+            const LLab c = z.merge ? mk(z.ls.K + dK(0, 0, 10), z.ls.c3 + d3(0, 0, 10),
+                                        lm_pack(len, lm_par(z.ls.meta), 1, kCentral, lm_cj(z.ls.meta) + 1u))
+                                   : mk(z.base.K + dK(0, 0, 10), z.base.c3 + d3(0, 0, 10),
+                                        z.base.meta | lm_pack(0, 0, 1, kCentral, 1));
+            consider(f.c, opt((z.cen >> t) & 1u, c));
         }
-        if (p.use_caravans && (tS.flags & kSpHub)) {  // caravans between hubs (src/pathfinder.rs:140-160)
-            const bool on = live && (sS.flags & kSpHub);
-            const uint32_t d = uint32_t(abs(sS.x - tS.x) + abs(sS.y - tS.y));
-            const uint32_t coef = tS.coef5 ? 5u : 2u;
-            consider(f, on, ext(ls, s, kCaravan, (d << 1) | tS.coef5, coef * d, p.rgt * d));
+        // caravans between hubs (src/pathfinder.rs:140-160, caravan_cost :251-273)
+        {
+            const uint32_t money = (2u + 3u * pt_c5(w)) * md, time = p.rgt * md;
+            consider(f.c, opt((z.car >> t) & 1u, mk(z.base.K + dK(0, money, time), z.base.c3 + d3(0, money, time),
+                                                    z.base.meta | lm_pack(0, 0, 1, kCaravan))));
         }
-        if (p.use_soe && tS.rid != kNone10) {
-            // Scroll of Escape from s to its region's campfire (src/pathfinder.rs:162-170)
-            const bool on_e = live && sS.region == t && sS.region != s;
-            consider(f, on_e, ext(ls, s, kSoE, 0, p.soe_cost, 0));
-            // ... and from the region cell nearest to boundary s: [Std{d} s -> u, SoE u -> t]
-            const uint2 e = nearS[s * nreg + tS.rid];
-            const bool on_r = live && walks && e.x != kNone32 && e.x != 0;
-            consider(f, on_r, walk_soe(ls, s, on_r ? e.x : 1u));
-        }
-        if (t != 1) {  // walks from boundary s (not into the Center)
-            const bool on = live && walks;
-            const LLab c = walk(ls, s, walk_dist(sS.x, sS.y, tS.x, tS.y));
-            consider(f, on, c);
-            f.w = c;
-            f.won = on;
-        }
+        // s's Scroll of Escape to its region's campfire (src/pathfinder.rs:162-170)
+        consider(f.c, opt((z.soe >> t) & 1u, mk(z.base.K + dK(0, p.soe_cost, 0), z.base.c3 + d3(0, p.soe_cost, 0),
+                                                z.base.meta | lm_pack(0, 0, 1, kSoE))));
+        // from the region cell nearest to boundary s: [Std{d} s -> u, SoE u -> t]
+        consider(f.c, opt(((z.reg >> t) & 1u) & (sd != kPtNoSd) & (sd != 0u),
+                          mk(z.ls.K + dK(sd, p.soe_cost, 180u * sd), z.ls.c3 + d3(sd, p.soe_cost, 180u * sd),
+                             lm_pack(len + 2u, s, 2, kStandard))));
         return f;
     }
-    // the best candidate into entry t against its tentative label: a strict win takes,
-    // an exact (metrics, length) tie is left to the list compare (bit t of *ties)
+    // the best candidate into entry t against its tentative label (K = kInfK: none):
+    // a strict win takes, an exact (metrics, length) tie is left to the list compare
+    // (bit t of *ties)
     __device__ __forceinline__ void offer(uint32_t t, const FromS &f, uint32_t &ties) {
-        if (!f.any) return;
         LLab &T = L[t];
         const uint32_t bit = 1u << t;
-        const bool have = (tent & bit) != 0;
-        const int r = have ? cmp4(f.c, T) : -1;
-        const bool same3 = have && eq3(f.c, T);
-        ll_sel(r < 0, T, f.c);
-        tent |= bit;
-        // blocker bit: a walk candidate with the (new) tentative metrics
-        const bool keep = same3 || (have && r > 0);
-        const bool wtie = f.won && eq3(f.w, T);
-        wt = (wt & ~bit) | (((keep && (wt & bit)) || wtie) ? bit : 0u);
-        ties |= r == 0 ? bit : 0u;
+        const bool any = f.c.K != kInfK;
+        const bool ke = f.c.K == T.K, ce = f.c.c3 == T.c3;
+        const uint32_t lf = lm_len(f.c.meta), lt_ = lm_len(T.meta);
+        const bool lt = any & ((f.c.K < T.K) | (ke & ((f.c.c3 < T.c3) | (ce & (lf < lt_)))));
+        const bool same3 = any & ke & ce;
+        ll_sel(lt, T, f.c);
+        tent |= vbit(lt, bit);
+        // blocker bit: a walk candidate with the (new) tentative metrics; kept while the
+        // tentative metrics stay (an unchanged label, or a win on length / commands)
+        const bool keep = !lt | same3;
+        const bool wtie = (f.w.K != kInfK) & (f.w.K == T.K) & (f.w.c3 == T.c3);
+        wt = (wt & ~bit) | vbit((keep & ((wt & bit) != 0)) | wtie, bit);
+        ties |= vbit(same3 & (lf == lt_), bit);
     }
 
     // ---- certification (hub_kernel's avail / label_avail) ----------------------------
-    __device__ __forceinline__ void bpos(uint32_t b, int &bx, int &by) const {
-        bx = b == 0 ? sx : spl[b].x;
-        by = b == 0 ? sy : spl[b].y;
-    }
     __device__ __forceinline__ bool avail(uint32_t b, int bx, int by, int vx, int vy) const {
         if (blk == 0) return true;
         const int x0 = min(bx, vx), x1 = max(bx, vx), y0 = min(by, vy), y1 = max(by, vy);
@@ -298,49 +352,51 @@ struct LaneHub {
         if (x0 <= 0 && 0 <= x1 && y0 <= 0 && 0 <= y1) return false;
         return x0 != x1 && y0 != y1;
     }
-    __device__ __forceinline__ bool label_avail(const LLab &x, uint32_t t) const {
-        if ((x.kp >> 29) != kStandard) return true;
-        const uint32_t b = ll_par(x.lpn);
+    // entry t's settled label x: its walk, or the walk to the cell its SoE is read from
+    __device__ __forceinline__ bool label_avail(uint32_t meta, uint32_t t) const {
+        if (lm_kind(meta) != kStandard) return true;
+        const uint32_t b = lm_par(meta);
         int bx, by;
-        bpos(b, bx, by);
-        if (ll_nt(x.lpn) == 1) return avail(b, bx, by, spl[t].x, spl[t].y);
-        const uint32_t u = rank_inv[near_rank(b, spl[t].rid)];
+        pos(b, bx, by);
+        if (lm_nt(meta) == 1) return avail(b, bx, by, spl[t].x, spl[t].y);
+        const uint32_t u = rank_inv[near_of(b, spl[t].rid).y];
         return avail(b, bx, by, int(u % P.S) - int(P.H), int(u / P.S) - int(P.H));
     }
 
     // ---- output (Core::emit) --------------------------------------------------------
-    __device__ __forceinline__ void emit(const LLab &x, uint32_t own_rk, uint32_t own_rid, uint32_t qi) {
+    __device__ __forceinline__ void emit(const LLab &x, uint32_t xid, const Own &xo, uint32_t qi) const {
         const DevParams &p = P;
         OutResult &o = a->out_res[qi];
         OutCmd *oc = a->out_cmd + (unsigned long long)qi * p.max_cmds;
-        const uint32_t len = ll_len(x.lpn);
+        const uint32_t len = lm_len(x.meta);
+        const uint32_t legs = metric(x, 0), money = metric(x, 1), time = metric(x, 2);
         uint32_t status = 16;
         if (len > p.max_cmds) {  // the overflow pool, else MR_ERR_CAPACITY
             const uint32_t off = atomicAdd(counter + kCtrOvf, len);
             if (p.max_cmds == 0 || off + len > a->ovf_cap || off + len < off) {
-                o = OutResult{x.m0, x.m1, x.m2, (uint32_t(16 - 4) << 16) | (len & 0xFFFFu)};
+                o = OutResult{legs, money, time, (uint32_t(16 - 4) << 16) | (len & 0xFFFFu)};
                 return;
             }
             oc[0] = OutCmd{kOvfTag, off, len, 0};
             oc = a->ovf + off;
             status = 16 + kStatusOverflow;
         }
-        int pos = int(len) - 1;
-        LLab e = x;
-        uint32_t erk = own_rk, erid = own_rid, eid = kOwn;
-        for (uint32_t guard = 0; pos >= 0 && guard <= TM + 1; ++guard) {
-            for (int j = int(ll_nt(e.lpn)) - 1; j >= 0 && pos >= 0; --j, --pos) {
-                const Cmd c = tail(e, erk, erid, j);
-                oc[pos] = OutCmd{c.kp, c.from, c.to, 0};
+        int at = int(len) - 1;
+        uint32_t e = x.meta;
+        Own eo = xo;
+        uint32_t eid = xid;
+        for (uint32_t guard = 0; at >= 0 && guard <= TM + 1; ++guard) {
+            for (int j = int(lm_nt(e)) - 1; j >= 0 && at >= 0; --j, --at) {
+                const Cmd c = tail(e, eo, j);
+                oc[at] = OutCmd{c.kp, c.from, c.to, 0};
             }
-            eid = ll_par(e.lpn);
+            eid = lm_par(e);
             if (eid == 0) break;
-            e = get(eid);
-            erk = spl[eid].rk;
-            erid = spl[eid].rid;
+            e = meta_of(eid);
+            eo = own_of(eid);
         }
-        if (pos != -1 || eid != 0) atomicOr(counter + kCtrFlags, kErrChain);
-        o = OutResult{x.m0, x.m1, x.m2, (status << 16) | (len & 0xFFFFu)};
+        if (at != -1 || eid != 0) atomicOr(counter + kCtrFlags, kErrChain);
+        o = OutResult{legs, money, time, (status << 16) | (len & 0xFFFFu)};
     }
 
     // ---- one source per lane ----------------------------------------------------------
@@ -357,108 +413,141 @@ struct LaneHub {
         // the source's own edges: its start label if it is a special, SHQ, SFm, the
         // walks from it and the SoE edges from its region rows (src/pathfinder.rs:162-178)
         const bool walks0 = have && src != p.vc;
-        const LLab st0 = ll_start();
+        const LLab st0 = start(), inf = LLab{kInfK, 0u, 0u};
 #pragma unroll
         for (uint32_t t = 1; t < TM; ++t) {
-            if (t > NS) continue;
-            const SpecialStatic tS = spl[t];
-            FromS f;
-            f.any = false;
-            f.won = false;
-            f.c = st0;
-            f.w = st0;
-            consider(f, have && t == ts, st0);
-            consider(f, have && t == p.hq_t, LLab{0, p.shq_cost, 0, ll_pack(1, 0, 1), kSHQ << 29});
-            consider(f, have && p.use_sfm && t == 1, LLab{0, p.sfm_cost, 0, ll_pack(1, 0, 1), kSFm << 29});
-            if (p.use_soe && tS.rid != kNone10) {  // [SoE src -> t], or [Std{d} src -> u, SoE u -> t]
-                const uint2 e = have ? srow[tS.rid] : make_uint2(kNone32, 0);
-                const bool on = walks0 && e.x != kNone32;
-                const LLab c = e.x == 0 ? LLab{0, p.soe_cost, 0, ll_pack(1, 0, 1), kSoE << 29}
-                                        : LLab{e.x, p.soe_cost, run_time(e.x), ll_pack(2, 0, 2), (kStandard << 29) | e.x};
-                consider(f, on, c);
+            const bool valid = have && t <= NS;
+            const SpecialStatic tS = spl[t <= NS ? t : 1u];
+            LLab c = opt(valid && t == ts, st0);
+            consider(c, opt(valid && t == p.hq_t, mk(dK(0, p.shq_cost, 0), d3(0, p.shq_cost, 0), lm_pack(1, 0, 1, kSHQ))));
+            consider(c, opt(valid && p.use_sfm && t == 1,
+                            mk(dK(0, p.sfm_cost, 0), d3(0, p.sfm_cost, 0), lm_pack(1, 0, 1, kSFm))));
+            {  // [SoE src -> t], or [Std{d} src -> u, SoE u -> t]
+                const bool reg = valid && p.use_soe && tS.rid != kNone10;
+                const uint32_t e = reg ? srow[reg ? tS.rid : 0u].x : kNone32;
+                const bool on = walks0 && reg && e != kNone32;
+                const uint32_t d = on ? e : 1u;
+                consider(c, opt(on, d == 0 ? mk(dK(0, p.soe_cost, 0), d3(0, p.soe_cost, 0), lm_pack(1, 0, 1, kSoE))
+                                           : mk(dK(d, p.soe_cost, 180u * d), d3(d, p.soe_cost, 180u * d),
+                                                lm_pack(2, 0, 2, kStandard))));
             }
+            LLab w = inf;
             if (t != 1) {
-                const bool on = walks0 && tS.v != src;
                 const uint32_t k = walk_dist(sx, sy, tS.x, tS.y);
-                const LLab c{k, 0, run_time(k), ll_pack(1, 0, 1), (kStandard << 29) | k};
-                consider(f, on, c);
-                f.w = c;
-                f.won = on;
+                w = opt(valid && walks0 && tS.v != src, mk(dK(k, 0, 180u * k), d3(k, 0, 180u * k), lm_pack(1, 0, 1, kStandard)));
+                consider(c, w);
             }
-            if (f.any) {
-                L[t] = f.c;
-                tent |= 1u << t;
-                wt |= (f.won && eq3(f.w, f.c)) ? (1u << t) : 0u;
-            } else {
-                L[t] = st0;
-            }
+            L[t] = c;
+            tent |= c.K != kInfK ? (1u << t) : 0u;
+            wt |= ((w.K != kInfK) & eq3(w, c)) ? (1u << t) : 0u;
         }
         // ---- Dijkstra over the specials, one settle per lane per iteration ----------
         for (uint32_t it = 0; it < NS; ++it) {
             const uint32_t cand = tent & ~done;
             if (!__any(cand != 0)) break;
-            // the settle candidate: least (c1, c2, c3, length)
-            LLab ls = st0;
-            uint32_t s = 0;
-            bool tie = false;
+            // the settle candidate: least (c1, c2, c3, length), two interleaved chains
+            // (odd and even entries) for the latency, then merged
+            LLab la = inf, lb = inf;
+            uint32_t sa = 0, sb = 0;
+            bool ta = false, tb = false;
 #pragma unroll
             for (uint32_t t = 1; t < TM; ++t) {
-                const bool c = (cand >> t) & 1u;
-                const int r = s == 0 ? -1 : cmp4(L[t], ls);
-                const bool take = c && r < 0;
-                tie = take ? false : (tie || (c && r == 0));
-                ll_sel(take, ls, L[t]);
-                s = take ? t : s;
+                LLab &lx = (t & 1u) ? la : lb;
+                uint32_t &sx_ = (t & 1u) ? sa : sb;
+                bool &tx = (t & 1u) ? ta : tb;
+                const LLab c = opt((cand >> t) & 1u, L[t]);
+                const bool ke = c.K == lx.K, ce = c.c3 == lx.c3;
+                const uint32_t lc = lm_len(c.meta), ll = lm_len(lx.meta);
+                const bool lt = (c.K < lx.K) | (ke & ((c.c3 < lx.c3) | (ce & (lc < ll))));
+                tx = lt ? false : (tx | ((c.K != kInfK) & ke & ce & (lc == ll)));
+                ll_sel(lt, lx, c);
+                sx_ = lt ? t : sx_;
             }
-            if (tie) {  // exact (metrics, length) ties: the command lists decide (rare)
-                for (uint32_t m = cand & ~(1u << s); m; m &= m - 1u) {
-                    const uint32_t t = uint32_t(__builtin_ctz(m));
-                    const LLab lt = get(t);
-                    if (cmp4(lt, ls) != 0) continue;
-                    if (cmp_list(lt, t, spl[t].rk, spl[t].rid, ls, s, spl[s].rk, spl[s].rid) < 0) {
-                        ls = lt;
-                        s = t;
+            Settle z;
+            z.ls = la;
+            uint32_t s = sa;
+            bool tie = ta;
+            {
+                const bool ke = lb.K == la.K, ce = lb.c3 == la.c3;
+                const uint32_t l1 = lm_len(lb.meta), l0 = lm_len(la.meta);
+                const bool lt = (lb.K < la.K) | (ke & ((lb.c3 < la.c3) | (ce & (l1 < l0))));
+                ll_sel(lt, z.ls, lb);
+                s = lt ? sb : sa;
+                tie = lt ? tb : (ta | ((lb.K != kInfK) & ke & ce & (l1 == l0)));
+            }
+            if (__any(tie)) {  // exact (metrics, length) ties: the command lists decide (rare)
+                uint32_t tied = 0;  // the entries with the winner's metrics and length
+#pragma unroll
+                for (uint32_t t = 1; t < TM; ++t)
+                    tied |= (((cand >> t) & 1u) & eq3(L[t], z.ls) & (lm_len(L[t].meta) == lm_len(z.ls.meta))) ? (1u << t)
+                                                                                                            : 0u;
+                dump_meta();
+                if (tie) {
+                    for (uint32_t m = tied & ~(1u << s); m; m &= m - 1u) {
+                        const uint32_t t = uint32_t(__builtin_ctz(m));
+                        const uint32_t mt = meta_of(t);
+                        if (cmp_list(mt, t, own_of(t), z.ls.meta, s, own_of(s)) < 0) {
+                            z.ls.meta = mt;  // (same metrics)
+                            s = t;
+                        }
                     }
                 }
             }
             const bool act = s != 0;
-            const uint32_t sc = act ? s : 1u;
-            const SpecialStatic sS = spl[sc];
+            z.s = act ? s : 1u;
             done |= act ? (1u << s) : 0u;
-            const uint32_t lk = ll_nt(ls.lpn) == 2 ? kSoE : (ls.kp >> 29);
+            const uint32_t lk = lm_nt(z.ls.meta) == 2 ? kSoE : lm_kind(z.ls.meta);
             const bool boundary = act && lk != kNoMove && lk != kStandard;
             blk |= (boundary && ((wt >> s) & 1u)) ? (1u << s) : 0u;  // a walk tied it: a blocker
             const bool walks = boundary && s != 1;                     // the Center starts no walks
             bndm |= walks ? (1u << s) : 0u;
+            const bool nomove = lk == kNoMove;  // the start label: its NoMove is replaced
+            z.base = mk(nomove ? 0ull : z.ls.K, nomove ? 0u : z.ls.c3,
+                        nomove ? lm_pack(1, 0, 1, 0) : lm_pack(lm_len(z.ls.meta) + 1u, z.s, 1, 0));
+            z.merge = lk == kCentral;
+            const uint32_t live = act ? (validm & ~done) : 0u;  // unsettled entries
+            const uint32_t rg = spl[z.s].region;
+            z.cen = live & (z.s == 1 ? 0x3Cu : ((z.s >= 2 && z.s <= 5) ? 0x2u : 0u));
+            z.car = (p.use_caravans && ((hubm >> z.s) & 1u)) ? (live & hubm) : 0u;
+            z.soe = (p.use_soe && rg != kNone10 && rg != z.s) ? (live & (1u << rg)) : 0u;
+            z.reg = (walks && p.use_soe) ? (live & regm) : 0u;
+            z.walk = walks ? (live & ~0x2u) : 0u;
+            const uint32_t *row = PT + z.s * TM;
             uint32_t ties = 0;
-            const bool any_walks = __any(walks);
 #pragma unroll
             for (uint32_t t = 1; t < TM; ++t) {
-                if (t > NS || !__any(act && !((done >> t) & 1u))) continue;  // settled in every lane
-                const SpecialStatic tS = spl[t];
-                const bool live = act && !((done >> t) & 1u);
-                FromS f;
-                if (any_walks) f = from_s(live, ls, sc, sS, walks, t, tS);
-                else f = from_s(live, ls, sc, sS, false, t, tS);
+                const FromS f = from_s(z, t, row[t]);
                 offer(t, f, ties);
+                MR_LANE_FENCE();
             }
             // exact ties with a tentative label: the candidate is rebuilt and its command
             // list compared (rare; run-time t)
-            for (; ties; ties &= ties - 1u) {
-                const uint32_t t = uint32_t(__builtin_ctz(ties));
-                const SpecialStatic tS = spl[t];
-                const FromS f = from_s(true, ls, sc, sS, walks, t, tS);
-                const LLab cur = get(t);
-                if (cmp4(f.c, cur) == 0 && cmp_list(f.c, kOwn, tS.rk, tS.rid, cur, t, tS.rk, tS.rid) < 0) put(t, f.c);
+            // (same metrics: only the meta word can change; the new ones go through LDS)
+            if (__any(ties != 0)) {
+                dump_meta();
+                uint32_t repl = 0;
+                for (; ties; ties &= ties - 1u) {
+                    const uint32_t t = uint32_t(__builtin_ctz(ties));
+                    const FromS f = from_s(z, t, row[t]);
+                    const uint32_t cur = meta_of(t);
+                    if (cmp_list(f.c.meta, kOwn, own_of(t), cur, t, own_of(t)) < 0) {
+                        M[t * 64u + lane_id()] = f.c.meta;
+                        repl |= 1u << t;
+                    }
+                }
+#pragma unroll
+                for (uint32_t t = 1; t < TM; ++t)
+                    if ((repl >> t) & 1u) L[t].meta = M[t * 64u + lane_id()];
             }
         }
         if (!have) return 0;
         // ---- certification: with blockers, every settled walk label must be certain ----
         bool unc = false;
+        dump_meta();  // (certification and the destinations' command chains)
         if (blk != 0) {
             for (uint32_t m = done; m; m &= m - 1u) {
                 const uint32_t t = uint32_t(__builtin_ctz(m));
-                if (!label_avail(get(t), t)) unc = true;
+                if (!label_avail(meta_of(t), t)) unc = true;
             }
         }
         const uint32_t qa = a->q_begin[s_idx], qb = a->q_begin[s_idx + 1];
@@ -470,42 +559,43 @@ struct LaneHub {
             const uint32_t tw = sinfo[w] & kNone10;
             const uint32_t wr = rank[w];
             if (w == src) {
-                emit(st0, src_rk, kNone10, qi);
+                emit(st0, kOwn, Own{sx, sy, src_rk, kNone10, 0u}, qi);
                 continue;
             }
             if (tw != kNone10) {
-                emit(get(tw), spl[tw].rk, spl[tw].rid, qi);
+                emit(get(tw), tw, own_of(tw), qi);
                 continue;
             }
             const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
-            LLab x = st0;
+            const Own wo{wx, wy, wr, kNone10, 0u};
+            LLab x = inf;
             uint32_t bx = kNone32;
             bool tie = false;
-            if (walk0) {
+            {
                 const uint32_t k = walk_dist(sx, sy, wx, wy);
-                x = LLab{k, 0, run_time(k), ll_pack(1, 0, 1), (kStandard << 29) | k};
-                bx = 0;
+                x = opt(walk0, mk(dK(k, 0, 180u * k), d3(k, 0, 180u * k), lm_pack(1, 0, 1, kStandard)));
+                bx = walk0 ? 0u : kNone32;
             }
 #pragma unroll
             for (uint32_t t = 2; t < TM; ++t) {
-                if (!__any((bndm >> t) & 1u)) continue;
-                const bool on = (bndm >> t) & 1u;
-                const LLab c = walk(L[t], t, walk_dist(spl[t].x, spl[t].y, wx, wy));
-                const int r = bx == kNone32 ? -1 : cmp4(c, x);
-                const bool take = on && r < 0;
-                tie = take ? false : (tie || (on && r == 0));
-                ll_sel(take, x, c);
-                bx = take ? t : bx;
+                const uint32_t k = walk_dist(spl[t].x, spl[t].y, wx, wy);
+                const LLab c = opt((bndm >> t) & 1u, walk_to(L[t], t, k));
+                const bool ke = c.K == x.K, ce = c.c3 == x.c3;
+                const uint32_t lc = lm_len(c.meta), lx = lm_len(x.meta);
+                const bool lt = (c.K < x.K) | (ke & ((c.c3 < x.c3) | (ce & (lc < lx))));
+                tie = lt ? false : (tie | ((c.K != kInfK) & ke & ce & (lc == lx)));
+                ll_sel(lt, x, c);
+                bx = lt ? t : bx;
             }
             if (tie) {  // equal metrics and length from several boundaries: the lists decide
                 for (uint32_t m = (bndm | (walk0 ? 1u : 0u)) & ~(1u << bx); m; m &= m - 1u) {
                     const uint32_t b = uint32_t(__builtin_ctz(m));
                     int px, py;
-                    bpos(b, px, py);
+                    pos(b, px, py);
                     const uint32_t k = walk_dist(px, py, wx, wy);
-                    const LLab c = b == 0 ? LLab{k, 0, run_time(k), ll_pack(1, 0, 1), (kStandard << 29) | k}
-                                          : walk(get(b), b, k);
-                    if (cmp4(c, x) == 0 && cmp_list(c, kOwn, wr, kNone10, x, kOwn, wr, kNone10) < 0) {
+                    const LLab c = b == 0 ? mk(dK(k, 0, 180u * k), d3(k, 0, 180u * k), lm_pack(1, 0, 1, kStandard))
+                                          : walk_to(get(b), b, k);
+                    if (cmp4(c, x) == 0 && cmp_list(c.meta, kOwn, wo, x.meta, kOwn, wo) < 0) {
                         x = c;
                         bx = b;
                     }
@@ -515,10 +605,10 @@ struct LaneHub {
                 a->out_res[qi] = OutResult{0, 0, 0, uint32_t(16 + 1) << 16};
                 continue;
             }
-            emit(x, wr, kNone10, qi);
+            emit(x, kOwn, wo, qi);
             if (blk != 0) {
                 int px, py;
-                bpos(bx, px, py);
+                pos(bx, px, py);
                 if (!avail(bx, px, py, wx, wy)) unc = true;
             }
         }
@@ -528,38 +618,79 @@ struct LaneHub {
     }
 };
 
+// the lane kernel's LDS: the specials' static records, their region rows and the pair table
+__host__ __device__ inline uint32_t lane_off_near(uint32_t NS) { return align16h((NS + 1) * uint32_t(sizeof(SpecialStatic))); }
+__host__ __device__ inline uint32_t lane_off_pt(uint32_t NS, uint32_t nreg) {
+    return align16h(lane_off_near(NS) + (NS + 1) * nreg * 8u);
+}
+// then the pair table (TM x TM words) and per wave the meta copy of the rare paths (TM x 64 words)
+__host__ __device__ inline uint32_t lane_off_meta(uint32_t NS, uint32_t nreg, uint32_t TM) {
+    return align16h(lane_off_pt(NS, nreg) + TM * TM * 4u);
+}
+__host__ __device__ inline uint32_t lane_lds_total(uint32_t NS, uint32_t nreg, uint32_t TM) {
+    return lane_off_meta(NS, nreg, TM) + (kBS / 64) * TM * 64u * 4u;
+}
+
 template <uint32_t PERM, uint32_t TM>
 __global__ __launch_bounds__(kBS, MR_LANE_WAVES) void hub_lane_kernel(const KArgs *__restrict__ a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint32_t NS = a->p.NS, nreg = a->nreg;
     SpecialStatic *spl = reinterpret_cast<SpecialStatic *>(smem);
-    uint2 *nearl = reinterpret_cast<uint2 *>(smem + align16h((NS + 1) * uint32_t(sizeof(SpecialStatic))));
+    uint2 *nearl = reinterpret_cast<uint2 *>(smem + lane_off_near(NS));
+    uint32_t *pt = reinterpret_cast<uint32_t *>(smem + lane_off_pt(NS, nreg));
+    const uint2 *nearg = reinterpret_cast<const uint2 *>(a->near);
     for (uint32_t t = threadIdx.x; t <= NS; t += kBS) spl[t] = a->sp[t];
     for (uint32_t i = threadIdx.x; i < NS * nreg; i += kBS) {
         const uint32_t t = 1 + i / nreg, r = i % nreg;
-        nearl[t * nreg + r] = reinterpret_cast<const uint2 *>(a->near)[(unsigned long long)a->sp[t].v * nreg + r];
+        nearl[t * nreg + r] = nearg[(unsigned long long)a->sp[t].v * nreg + r];
+    }
+    // the pair table (LaneHub::from_s): walk / Manhattan / SoE-region distances of (s, t)
+    for (uint32_t i = threadIdx.x; i < TM * TM; i += kBS) {
+        const uint32_t s = i / TM, t = i % TM;
+        uint32_t e = kPtNoSd << 15;
+        if (s >= 1 && s <= NS && t >= 1 && t <= NS) {
+            const SpecialStatic ss = a->sp[s], st = a->sp[t];
+            const uint32_t wd = walk_dist(ss.x, ss.y, st.x, st.y);
+            const uint32_t md = uint32_t(abs(ss.x - st.x) + abs(ss.y - st.y));
+            uint32_t sd = kPtNoSd;
+            if (st.rid != kNone10) {
+                const uint32_t d = nearg[(unsigned long long)ss.v * nreg + st.rid].x;
+                sd = d == kNone32 ? kPtNoSd : d;
+            }
+            e = wd | ((wd != md ? 1u : 0u) << 14) | (sd << 15) | ((st.coef5 ? 1u : 0u) << 29);
+        }
+        pt[i] = e;
     }
     __syncthreads();
     LaneHub<PERM, TM> H;
     H.a = a;
     H.P = a->p;
-    H.P.perm[0] = PERM / 9;
-    H.P.perm[1] = (PERM / 3) % 3;
-    H.P.perm[2] = PERM % 3;
     H.spl = spl;
     H.nearS = nearl;
+    H.PT = pt;
+    H.M = reinterpret_cast<uint32_t *>(smem + lane_off_meta(NS, nreg, TM)) + (threadIdx.x >> 6) * (TM * 64u);
     H.rank = a->rank;
     H.sinfo = a->sinfo;
     H.rank_inv = a->rank_inv;
     H.counter = a->counter;
     H.nreg = nreg;
+    uint32_t hubm = 0, c5m = 0, regm = 0;
+    for (uint32_t t = 1; t <= NS && t < TM; ++t) {
+        const SpecialStatic st = spl[t];
+        hubm |= (st.flags & kSpHub) ? (1u << t) : 0u;
+        c5m |= st.coef5 ? (1u << t) : 0u;
+        regm |= st.rid != kNone10 ? (1u << t) : 0u;
+    }
+    H.hubm = __builtin_amdgcn_readfirstlane(hubm);
+    H.c5m = __builtin_amdgcn_readfirstlane(c5m);
+    H.regm = __builtin_amdgcn_readfirstlane(regm);
+    H.validm = __builtin_amdgcn_readfirstlane(((2u << min(NS, TM - 1u)) - 1u) & ~1u);
     // lane l of wave w: source 64 w + l of the lane kernel's sources [0, n_lane)
     const uint32_t s_idx = (blockIdx.x * (kBS / 64) + (threadIdx.x >> 6)) * 64u + lane_id();
     const uint32_t n = a->n_lane;
     const bool have = s_idx < n;
     uint32_t written = 0;
     if (__any(have)) written = H.solve(have, have ? s_idx : (n ? n - 1 : 0));
-    if (H.err) atomicOr(a->counter + kCtrFlags, H.err);
     __shared__ uint32_t wsum;
     if (threadIdx.x == 0) wsum = 0;
     __syncthreads();

@@ -18,15 +18,16 @@ static const void *lane_fn_tm(uint32_t perm) {
 }
 
 // table entries (NS + 1) the lane kernel holds in registers; 0 = not applicable
-uint32_t hub_lane_entries(uint32_t NS) { return NS + 1 <= 24 ? 24u : 0u; }
+uint32_t hub_lane_entries(uint32_t NS) { return NS + 1 <= 22 ? 22u : (NS + 1 <= 24 ? 24u : (NS + 1 <= 32 ? 32u : 0u)); }
 
 static const void *lane_fn(const uint32_t perm[3], uint32_t NS) {
     const uint32_t k = perm[0] * 9 + perm[1] * 3 + perm[2];
-    return hub_lane_entries(NS) == 24 ? lane_fn_tm<24>(k) : nullptr;
+    const uint32_t tm = hub_lane_entries(NS);
+    return tm == 22 ? lane_fn_tm<22>(k) : (tm == 24 ? lane_fn_tm<24>(k) : (tm == 32 ? lane_fn_tm<32>(k) : nullptr));
 }
 
 uint32_t hub_lane_lds_bytes(uint32_t NS, uint32_t nreg) {
-    return align16h((NS + 1) * uint32_t(sizeof(SpecialStatic))) + (NS + 1) * nreg * 8u;
+    return lane_lds_total(NS, nreg, hub_lane_entries(NS));
 }
 
 hipError_t launch_hub_lane(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t n_lane,
