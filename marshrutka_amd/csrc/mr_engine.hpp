@@ -201,6 +201,7 @@ enum : uint32_t { kAlgoGeneric = 0, kAlgoLegs = 1 };
 // per lane, its queries read off by that lane); sources with more on hub_kernel (a lane
 // per query)
 constexpr uint32_t kLaneMaxQ = 32;
+constexpr uint32_t kLaneRegs = 6;  // hub_lane_kernel: region campfires sit in entries 6 .. 6 + kLaneRegs - 1
 
 constexpr uint32_t kErrKOverflow = 1u, kErrMetricOverflow = 2u, kErrBucket = 4u, kErrChain = 8u;
 // KArgs::dbg_flags bit (tests only): the fill launch raises kErrChain

@@ -543,6 +543,11 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
         g->find(build_border(b, 1), v);
         add(v);
     }
+    // the query homeland's campfires (the SoE regions) first: hub_lane_kernel keeps its
+    // region candidates to entries 6 .. 6 + kLaneRegs - 1 (the table order decides
+    // nothing else: equal labels are ordered by their command lists)
+    for (uint32_t v : g->campfires)
+        if (g->idx[v].kind == MR_CELL_HOMELAND && g->idx[v].sub == prm->homeland) add(v);
     for (uint32_t v : g->campfires) add(v);
     uint32_t hq_v = kNone32;
     if (prm->has_hq) {
@@ -878,8 +883,36 @@ static bool lane_bounds_ok(const DevParams &p) {
     const uint64_t money = std::max<uint64_t>(std::max<uint64_t>(p.soe_cost, p.shq_cost),
                                               std::max<uint64_t>(p.sfm_cost, 5 * dmax));
     const uint64_t time = std::max<uint64_t>(uint64_t(p.rgt) * dmax, 180 * dmax);
-    const uint64_t lim = 0xFFFFFFFFull;
+    const uint64_t lim = 0xFFFFFFFEull;  // c1 = 2^32 - 1 marks an absent label in the lane kernel
     return p.S <= 4097 && ncmd * dmax <= lim && ncmd * money <= lim && ncmd * time <= lim;
+}
+// hub_lane_kernel's fixed table layout: no caravan hub among the border-1 entries 2..5
+// and every region campfire (and so every SoE target) in entries 6 .. 6 + kLaneRegs - 1
+static bool lane_layout_ok(const HostPlan &hp) {
+    for (uint32_t t = 2; t <= 5 && t <= hp.p.NS; ++t)
+        if (hp.sp[t].flags & kSpHub) return false;
+    for (uint32_t t = 1; t <= hp.p.NS; ++t)
+        if (hp.sp[t].rid != kNone10 && (t < 6 || t >= 6 + kLaneRegs)) return false;
+    for (uint32_t t = 1; t <= hp.p.NS; ++t) {  // SoE targets: the specials' region campfires
+        const uint32_t r = hp.sp[t].region;
+        if (r != kNone10 && (r < 6 || r >= 6 + kLaneRegs || hp.sp[r].rid == kNone10)) return false;
+    }
+    return true;
+}
+
+// sources that would run on the lane kernel (at most kLaneMaxQ queries)
+static uint32_t lane_sources(const HostPlan &hp) {
+    uint32_t c = 0;
+    for (size_t i = 0; i + 1 < hp.q_begin.size(); ++i) c += hp.q_begin[i + 1] - hp.q_begin[i] <= kLaneMaxQ;
+    return c;
+}
+// half a wave per SIMD of the current device (MR_HUB_LANE_MIN overrides)
+static uint32_t lane_min_sources() {
+    if (const char *e = std::getenv("MR_HUB_LANE_MIN")) return uint32_t(std::strtoul(e, nullptr, 10));
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    return uint32_t(cus) * 4u * 32u;
 }
 
 // Hub plans on the lane kernel: the sources with at most kLaneMaxQ queries first (one
@@ -931,10 +964,14 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     // all destinations: hub_kernel + fill only, linear run times (the fill's keys)
     if (all_mode && (hp.wide || hp.nonlin)) hp.hub = hp.wide = hp.nonlin = false;
     // query plans with a linear run time and a table that fits a lane's registers: the
-    // sources with few queries run one per lane (MR_HUB_LANE=0: all on hub_kernel)
+    // sources with few queries run one per lane, when there are enough of them to give
+    // half of the SIMDs a wave (lane_min_sources); a lane-kernel wave runs a whole
+    // Dijkstra, so fewer waves than SIMDs leave it latency-bound and hub_kernel (a wave
+    // per source) is faster.  MR_HUB_LANE=0: never, =1: whenever applicable.
     const char *hl = std::getenv("MR_HUB_LANE");
-    if (hp.hub && !hp.wide && !hp.nonlin && !all_mode && hub_lane_entries(hp.p.NS) != 0 && lane_bounds_ok(hp.p) &&
-        !(hl && !std::strcmp(hl, "0")))
+    const bool lane_off = hl && !std::strcmp(hl, "0"), lane_force = hl && !std::strcmp(hl, "1");
+    if (hp.hub && !hp.wide && !hp.nonlin && !all_mode && !lane_off && hub_lane_entries(hp.p.NS) != 0 &&
+        lane_bounds_ok(hp.p) && lane_layout_ok(hp) && (lane_force || lane_sources(hp) >= lane_min_sources()))
         pl->n_lane = partition_sources(hp);
     auto bail = [&](int code) {
         delete pl;

@@ -15,19 +15,26 @@
 // settle is a per-lane scan, a relaxation a per-lane compare-and-select, and every
 // wave instruction advances 64 sources.  No cross-lane operation in the loop.
 //
-// A label is 4 registers: (c1, c2) as one 64-bit key, c3, and a meta word (length,
-// parent entry, tail count, the first tail command's kind and CentralMove count); the
-// command payloads (walk / caravan / SoE-region distances) follow from the parent's
-// and the entry's cells, so they are rebuilt where a command is written or compared.
-// The host only gives this kernel plans whose metric sums provably stay below 2^32
-// (lane_bounds_ok, mr_host.cpp), so a 64-bit add of packed deltas never carries.
+// A label is 4 registers: the metrics in comparator order (c1, c2, c3) and a meta word
+// (length in byte 0, the first tail command's kind, parent entry, tail count and
+// CentralMove count); the command payloads (walk / caravan / SoE-region distances)
+// follow from the parent's and the entry's cells, so they are rebuilt where a command
+// is written or compared.  The host only gives this kernel plans whose metric sums
+// provably stay below 2^32 - 1 (lane_bounds_ok, mr_host.cpp): c1 = 2^32 - 1 marks a
+// label that is not there, and no add carries.
+//
+// The order on (c1, c2, c3, length) is one borrow chain (ltm: byte-0 SDWA subtract,
+// three subtract-with-borrow) whose borrow becomes a 0 / ~0 VGPR mask, and every
+// selection is a bitwise select on such masks (one v_bitop3 per word): no compare
+// result lives in a 64-bit scalar lane mask, so the unrolled loops are pure VALU.
 //
 // Exactness follows hub_kernel step for step:
 //   * candidates into an entry from one settled special s share chain(s), so among
 //     them (metrics, length) ties are decided by the last command's kind (the list
-//     order; their kinds differ); the best of them is compared with the entry's
-//     tentative label, and only an exact (metrics, length) tie there walks the command
-//     lists (cmp_list, rare, out of the unrolled code);
+//     order; their kinds differ): they are visited in kind order and a later one
+//     replaces the best only when strictly smaller; the best is compared with the
+//     entry's tentative label, and only an exact (metrics, length) tie there walks the
+//     command lists (cmp_list, rare, out of the unrolled code);
 //   * blockers: a boundary special whose settled label some walk candidate tied on
 //     all three metrics (hub_kernel's note_walk).  One bit per entry keeps "a walk
 //     candidate so far has the tentative label's metrics" — every candidate is >= the
@@ -43,54 +50,94 @@ namespace mr {
 #ifndef MR_LANE_WAVES
 #define MR_LANE_WAVES 2  // waves per SIMD the register budget is cut for
 #endif
-// a scheduling fence between the unrolled entries: without it the scheduler interleaves
-// all of them and runs out of (scalar lane-mask) registers
+// a scheduling fence between the unrolled entries, so the scheduler does not
+// interleave all of them and run out of registers
 #ifndef MR_LANE_NOFENCE
 #define MR_LANE_FENCE() __builtin_amdgcn_sched_barrier(0)
 #else
 #define MR_LANE_FENCE() do {} while (0)
 #endif
 
-// meta: kind of the first tail command (3 b) | length (8 b) << 3 | parent entry (5 b)
-// << 11 | (tail count - 1) << 16 | CentralMove count (2 b) << 17.  (meta & 0x7FF)
-// orders by (length, kind): the tie-break among candidates from one settled special.
-__device__ __forceinline__ uint32_t lm_kind(uint32_t m) { return m & 7u; }
-__device__ __forceinline__ uint32_t lm_len(uint32_t m) { return (m >> 3) & 0xFFu; }
-__device__ __forceinline__ uint32_t lm_lk(uint32_t m) { return m & 0x7FFu; }
+// meta: length (8 b) | kind of the first tail command (3 b) << 8 | parent entry (5 b)
+// << 11 | (tail count - 1) << 16 | CentralMove count (2 b) << 17
+__device__ __forceinline__ uint32_t lm_len(uint32_t m) { return m & 0xFFu; }
+__device__ __forceinline__ uint32_t lm_kind(uint32_t m) { return (m >> 8) & 7u; }
 __device__ __forceinline__ uint32_t lm_par(uint32_t m) { return (m >> 11) & 31u; }
 __device__ __forceinline__ uint32_t lm_nt(uint32_t m) { return ((m >> 16) & 1u) + 1u; }
 __device__ __forceinline__ uint32_t lm_cj(uint32_t m) { return (m >> 17) & 3u; }
-__device__ __forceinline__ uint32_t lm_pack(uint32_t len, uint32_t par, uint32_t nt, uint32_t kind, uint32_t cj = 0) {
-    return kind | (len << 3) | (par << 11) | ((nt - 1u) << 16) | (cj << 17);
+__device__ __host__ __forceinline__ constexpr uint32_t lm_pack(uint32_t len, uint32_t par, uint32_t nt, uint32_t kind,
+                                                              uint32_t cj = 0) {
+    return len | (kind << 8) | (par << 11) | ((nt - 1u) << 16) | (cj << 17);
 }
-constexpr unsigned long long kInfK = ~0ull;  // a label that is not there (no metrics reach 2^32 - 1 here)
-// the pair table word of specials (s, t): walk distance | detour << 14 | SoE-region
-// distance from s into t's region << 15 (kPtNoSd: none) | t's caravan coefficient bit
-// << 29; Manhattan = walk - 2 detour
-constexpr uint32_t kPtNoSd = 0x3FFFu;
-__device__ __forceinline__ uint32_t pt_wd(uint32_t w) { return w & 0x3FFFu; }
-__device__ __forceinline__ uint32_t pt_md(uint32_t w) { return (w & 0x3FFFu) - ((w >> 13) & 2u); }
-__device__ __forceinline__ uint32_t pt_sd(uint32_t w) { return (w >> 15) & 0x3FFFu; }
-__device__ __forceinline__ uint32_t pt_c5(uint32_t w) { return (w >> 29) & 1u; }  // a caravan into t costs 5 per unit
+constexpr uint32_t kInf1 = ~0u;  // c1 of a label that is not there
 
 struct LLab {
-    unsigned long long K;  // c1 << 32 | c2
-    uint32_t c3, meta;
+    uint32_t c1, c2, c3, m;
 };
-// A per-lane bit as a plain VGPR value.  Without the empty asm the compiler keeps
-// every such boolean of the unrolled loops as a 64-bit lane mask in SGPRs, runs out of
-// them and spills (hundreds of SGPRs, 60 VGPRs of spill lanes).
-__device__ __forceinline__ uint32_t vbit(bool b, uint32_t bit) {
-    uint32_t v = b ? bit : 0u;
+
+// ---- masks: 0 / ~0 per lane, kept in VGPRs ---------------------------------------------
+// An empty asm makes the value opaque: without it the compiler turns every such mask
+// back into a 64-bit scalar lane mask (v_cmp + s_and/s_or), runs out of SGPRs and spills.
+__device__ __forceinline__ uint32_t vopaque(uint32_t v) {
+    asm("" : "+v"(v));
+    return v;
+}
+// a wave-uniform value re-read where it is used: the uniform branches of the unrolled
+// loops test bits of it, and without this the compiler hoists all their conditions out
+// of the iteration loop as 64-bit lane masks (SGPR spills)
+__device__ __forceinline__ uint32_t sopaque(uint32_t v) {
+    asm volatile("" : "+s"(v));
+    return v;
+}
+__device__ __forceinline__ uint32_t vvolatile(uint32_t v) {
     asm volatile("" : "+v"(v));
     return v;
 }
-__device__ __forceinline__ void ll_sel(bool take, LLab &d, const LLab &c) {
-    d.K = take ? c.K : d.K;
-    d.c3 = take ? c.c3 : d.c3;
-    d.meta = take ? c.meta : d.meta;
+__device__ __forceinline__ uint32_t vmask(bool b) { return vopaque(b ? ~0u : 0u); }
+// bit t of w as a mask (t is a constant in the unrolled loops: one v_bfe_i32)
+__device__ __forceinline__ uint32_t bitm(uint32_t w, uint32_t t) { return vopaque(uint32_t(int32_t(w << (31u - t)) >> 31)); }
+// k ? a : b per bit (one v_bfi_b32; written out, the compiler often makes it and/and/or/not)
+__device__ __forceinline__ uint32_t msel(uint32_t k, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(k), "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ void ll_sel(uint32_t k, LLab &d, const LLab &c) {
+    d.c1 = msel(k, c.c1, d.c1);
+    d.c2 = msel(k, c.c2, d.c2);
+    d.c3 = msel(k, c.c3, d.c3);
+    d.m = msel(k, c.m, d.m);
+}
+// x < y on (c1, c2, c3, length): the borrow of x - y, from the length byte up
+__device__ __forceinline__ uint32_t ltm(const LLab &x, const LLab &y) {
+    uint32_t t, r;
+    asm("v_sub_co_u32_sdwa %0, vcc, %2, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %4, %5, vcc\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %6, %7, vcc\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %8, %9, vcc\n\t"
+        "v_cndmask_b32_e64 %1, 0, -1, vcc"
+        : "=&v"(t), "=v"(r)
+        : "v"(x.m), "v"(y.m), "v"(x.c3), "v"(y.c3), "v"(x.c2), "v"(y.c2), "v"(x.c1), "v"(y.c1)
+        : "vcc");
+    return r;
+}
+// x < y on the metrics (c1, c2, c3) alone
+__device__ __forceinline__ uint32_t ltm3(const LLab &x, const LLab &y) {
+    uint32_t t, r;
+    asm("v_sub_co_u32_e32 %0, vcc, %2, %3\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %4, %5, vcc\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %6, %7, vcc\n\t"
+        "v_cndmask_b32_e64 %1, 0, -1, vcc"
+        : "=&v"(t), "=v"(r)
+        : "v"(x.c3), "v"(y.c3), "v"(x.c2), "v"(y.c2), "v"(x.c1), "v"(y.c1)
+        : "vcc");
+    return r;
 }
 
+// the pair table of specials (s, t), row s at s * TM: walk legs, walk time, caravan
+// money, caravan time (uint4), SoE-region distance from s into t's region and its walk
+// time (uint2; 0 where there is none), and per row s the entries t whose SoE-region
+// candidate applies (distance known and nonzero)
 template <uint32_t PERM, uint32_t TM>
 struct LaneHub {
     static constexpr uint32_t C1 = PERM / 9, C2 = (PERM / 3) % 3, C3 = PERM % 3;
@@ -98,7 +145,9 @@ struct LaneHub {
     DevParams P;
     const SpecialStatic *spl;  // LDS copy of a->sp
     const uint2 *nearS;        // LDS: region rows of the specials, row t at t * nreg
-    const uint32_t *PT;        // LDS: the pair table, row s at s * TM
+    const uint4 *PA;           // LDS: pair table, walk / caravan words
+    const uint2 *PB;           // LDS: pair table, SoE-region words
+    const uint32_t *RM;        // LDS: per row, the entries with a SoE-region candidate
     const uint32_t *rank, *sinfo, *rank_inv;
     uint32_t *counter;
     uint32_t nreg;
@@ -116,36 +165,30 @@ struct LaneHub {
     __device__ __forceinline__ static uint32_t pick(uint32_t i, uint32_t legs, uint32_t money, uint32_t time) {
         return i == 0 ? legs : (i == 1 ? money : time);
     }
-    // a (legs, money, time) delta packed as the key's (c1, c2) part
-    __device__ __forceinline__ static unsigned long long dK(uint32_t legs, uint32_t money, uint32_t time) {
-        return ((unsigned long long)pick(C1, legs, money, time) << 32) | pick(C2, legs, money, time);
+    // b + (legs, money, time), with meta word m (a zero delta folds away)
+    __device__ __forceinline__ static LLab add(const LLab &b, uint32_t legs, uint32_t money, uint32_t time, uint32_t m) {
+        return LLab{b.c1 + pick(C1, legs, money, time), b.c2 + pick(C2, legs, money, time),
+                    b.c3 + pick(C3, legs, money, time), m};
     }
-    __device__ __forceinline__ static uint32_t d3(uint32_t legs, uint32_t money, uint32_t time) {
-        return pick(C3, legs, money, time);
+    __device__ __forceinline__ static LLab mk(uint32_t legs, uint32_t money, uint32_t time, uint32_t m) {
+        return LLab{pick(C1, legs, money, time), pick(C2, legs, money, time), pick(C3, legs, money, time), m};
     }
     __device__ __forceinline__ static uint32_t metric(const LLab &x, uint32_t i) {  // i: 0 legs, 1 money, 2 time
-        return i == C1 ? uint32_t(x.K >> 32) : (i == C2 ? uint32_t(x.K) : x.c3);
+        return i == C1 ? x.c1 : (i == C2 ? x.c2 : x.c3);
     }
-    __device__ __forceinline__ static LLab mk(unsigned long long K, uint32_t c3, uint32_t meta) { return LLab{K, c3, meta}; }
-    __device__ __forceinline__ static LLab start() { return LLab{0ull, 0u, lm_pack(1, 0, 1, kNoMove)}; }
-    // (c1, c2, c3, length): -1, 0, 1
+    __device__ __forceinline__ static LLab start() { return LLab{0u, 0u, 0u, lm_pack(1, 0, 1, kNoMove)}; }
+    __device__ __forceinline__ static LLab inf() { return LLab{kInf1, 0u, 0u, 0u}; }
+    __device__ __forceinline__ static LLab opt(uint32_t on, const LLab &c) { return LLab{c.c1 | ~on, c.c2, c.c3, c.m}; }
+    // c replaces f when strictly smaller (callers visit candidates in kind order)
+    __device__ __forceinline__ static void consider(LLab &f, const LLab &c) { ll_sel(ltm(c, f), f, c); }
+    // (c1, c2, c3, length): -1, 0, 1 (rare paths)
     __device__ __forceinline__ static int cmp4(const LLab &x, const LLab &y) {
-        if (x.K != y.K) return x.K < y.K ? -1 : 1;
+        if (x.c1 != y.c1) return x.c1 < y.c1 ? -1 : 1;
+        if (x.c2 != y.c2) return x.c2 < y.c2 ? -1 : 1;
         if (x.c3 != y.c3) return x.c3 < y.c3 ? -1 : 1;
-        const uint32_t lx = lm_len(x.meta), ly = lm_len(y.meta);
+        const uint32_t lx = lm_len(x.m), ly = lm_len(y.m);
         if (lx != ly) return lx < ly ? -1 : 1;
         return 0;
-    }
-    __device__ __forceinline__ static bool eq3(const LLab &x, const LLab &y) { return (x.K == y.K) & (x.c3 == y.c3); }
-    // the same as two flags, without branches (bitwise, so nothing short-circuits into
-    // divergent control flow in the unrolled loops)
-    struct Cmp {
-        bool lt, eq;
-    };
-    __device__ __forceinline__ static Cmp cmpx(const LLab &x, const LLab &y) {
-        const bool kl = x.K < y.K, ke = x.K == y.K, cl = x.c3 < y.c3, ce = x.c3 == y.c3;
-        const uint32_t lx = lm_len(x.meta), ly = lm_len(y.meta);
-        return Cmp{bool(kl | (ke & (cl | (ce & (lx < ly))))), bool(ke & ce & (lx == ly))};
     }
 
     __device__ __forceinline__ uint32_t rk(uint32_t e) const { return e == 0 ? src_rk : spl[e].rk; }
@@ -159,12 +202,8 @@ struct LaneHub {
     __device__ __forceinline__ LLab get(uint32_t e) const {
         LLab r = start();
 #pragma unroll
-        for (uint32_t t = 1; t < TM; ++t) ll_sel(e == t, r, L[t]);
+        for (uint32_t t = 1; t < TM; ++t) ll_sel(vmask(e == t), r, L[t]);
         return r;
-    }
-    __device__ __forceinline__ void put(uint32_t e, const LLab &c) {
-#pragma unroll
-        for (uint32_t t = 1; t < TM; ++t) ll_sel(e == t, L[t], c);
     }
 
     // ---- commands of a label (rare paths: list compares and output) -----------------
@@ -211,9 +250,9 @@ struct LaneHub {
     uint32_t *M;
     __device__ __forceinline__ void dump_meta() const {
         const uint32_t l = lane_id();
-        M[l] = start().meta;
+        M[l] = start().m;
 #pragma unroll
-        for (uint32_t t = 1; t < TM; ++t) M[t * 64u + l] = L[t].meta;
+        for (uint32_t t = 1; t < TM; ++t) M[t * 64u + l] = L[t].m;
     }
     __device__ __forceinline__ uint32_t meta_of(uint32_t e) const { return M[e * 64u + lane_id()]; }
     // lexicographic compare of two equal-length command lists (metas x and y), walking
@@ -253,85 +292,74 @@ struct LaneHub {
 
     // the walk of k legs from table entry b (label lb) to a plain cell
     __device__ __forceinline__ static LLab walk_to(const LLab &lb, uint32_t b, uint32_t k) {
-        return mk(lb.K + dK(k, 0, 180u * k), lb.c3 + d3(k, 0, 180u * k), lm_pack(lm_len(lb.meta) + 1u, b, 1, kStandard));
+        return add(lb, k, 0, 180u * k, lm_pack(lm_len(lb.m) + 1u, b, 1, kStandard));
     }
 
     // ---- candidates from one settled special s into entry t ------------------------
-    // The best of the CentralMove, caravan, SoE, walk and SoE-region candidates from s;
-    // they share chain(s), so (metrics, length) ties go to the smaller last-command kind.
-    // Also the walk candidate itself (for the blocker bit).
-    // A candidate that does not apply has K = kInfK, so choosing among candidates is a
-    // plain minimum and no per-entry flag outlives its compare.
-    struct FromS {
-        LLab c, w;  // the best candidate from s; the walk candidate (for the blocker bit)
-    };
-    __device__ __forceinline__ static LLab opt(bool on, const LLab &c) { return LLab{on ? c.K : kInfK, c.c3, c.meta}; }
-    // c replaces f.c if smaller by (c1, c2, c3, length, kind)
-    __device__ __forceinline__ static void consider(LLab &f, const LLab &c) {
-        const bool lt = (c.K < f.K) | ((c.K == f.K) & ((c.c3 < f.c3) | ((c.c3 == f.c3) & (lm_lk(c.meta) < lm_lk(f.meta)))));
-        ll_sel(lt, f, c);
-    }
-    // Per-iteration context of the settled special s: its label ls; `base` = ls with an
-    // appended command (length + 1, parent s; the zero label when ls is the start label,
-    // whose NoMove is replaced); merge = ls ends in a CentralMove (one more merges).
-    // Which candidate kinds apply to which entries is a set of per-lane bit masks.
+    // Per-iteration context of the settled special s: its label ls, the meta words of the
+    // candidates from it (walk, SoE-region, caravan, SoE: length + 1 resp. + 2, parent
+    // s; a NoMove start label is replaced, not extended), the CentralMove candidate, and
+    // which entries each candidate kind reaches (bit masks).
     struct Settle {
-        LLab ls, base;
-        uint32_t s;
-        bool merge;
-        uint32_t cen, car, soe, reg, walk;  // entries a CentralMove / caravan / SoE / SoE-region / walk reaches
+        LLab ls, cen;
+        uint32_t s, mW, mR, mCar, mSoE;
+        uint32_t cenm, car, soe, reg, walk;
     };
-    __device__ __forceinline__ FromS from_s(const Settle &z, uint32_t t, uint32_t w) const {
-        const DevParams &p = P;
-        const uint32_t wd = pt_wd(w), md = pt_md(w), sd = pt_sd(w);
-        const uint32_t s = z.s, len = lm_len(z.ls.meta);
+    struct FromS {
+        LLab c, w;         // the best candidate from s; the walk candidate (for the blocker bit)
+        uint32_t any, won;  // masks: some candidate applies; the walk applies
+    };
+    // candidates in command-kind order: CentralMove, walk, caravan, then SoE or the
+    // SoE-region pair [Std{d} s -> u, SoE u -> t] (one candidate: the SoE is the d = 0
+    // case, s in t's region; the pair is one command longer than the others)
+    __device__ __forceinline__ FromS from_s(const Settle &z, uint32_t t, const uint4 A, const uint2 B) const {
         FromS f;
-        // the walk from boundary s (not into the Center)
-        f.w = opt((z.walk >> t) & 1u, mk(z.ls.K + dK(wd, 0, 180u * wd), z.ls.c3 + d3(wd, 0, 180u * wd),
-                                          lm_pack(len + 1u, s, 1, kStandard)));
+        if (t == 1) {  // no walks into the Center
+            f.w = inf();
+            f.won = 0;
+        } else {
+            f.won = bitm(z.walk, t);
+            f.w = opt(f.won, add(z.ls, A.x, 0, A.y, z.mW));
+        }
         f.c = f.w;
-        // CentralMove: the Center (entry 1) <-> the border-1 cells (entries 2..5)
-        if (t <= 5) {
-            const LLab c = z.merge ? mk(z.ls.K + dK(0, 0, 10), z.ls.c3 + d3(0, 0, 10),
-                                        lm_pack(len, lm_par(z.ls.meta), 1, kCentral, lm_cj(z.ls.meta) + 1u))
-                                   : mk(z.base.K + dK(0, 0, 10), z.base.c3 + d3(0, 0, 10),
-                                        z.base.meta | lm_pack(0, 0, 1, kCentral, 1));
-            consider(f.c, opt((z.cen >> t) & 1u, c));
+        f.any = f.won;
+        if (t <= 5) {  // CentralMove: the Center (entry 1) <-> the border-1 cells (entries 2..5)
+            const uint32_t on = bitm(z.cenm, t);
+            f.c = opt(on, z.cen);
+            if (t != 1) consider(f.c, f.w);
+            f.any |= on;
         }
-        // caravans between hubs (src/pathfinder.rs:140-160, caravan_cost :251-273)
-        {
-            const uint32_t money = (2u + 3u * pt_c5(w)) * md, time = p.rgt * md;
-            consider(f.c, opt((z.car >> t) & 1u, mk(z.base.K + dK(0, money, time), z.base.c3 + d3(0, money, time),
-                                                    z.base.meta | lm_pack(0, 0, 1, kCaravan))));
+        // Which entries are hubs / region campfires is known from the table layout the
+        // host guarantees (lane_layout_ok, mr_host.cpp): no hub among the border-1 cells
+        // 2..5, region campfires in 6 .. 6 + kLaneRegs - 1.  (Run-time branches per entry
+        // instead cost ~80 VGPRs of split live ranges in the unrolled loop.)
+        if (t == 1 || t >= 6) {  // caravans between hubs (src/pathfinder.rs:140-160, :251-273)
+            const uint32_t on = bitm(z.car, t);
+            consider(f.c, opt(on, add(z.ls, 0, A.z, A.w, z.mCar)));
+            f.any |= on;
         }
-        // s's Scroll of Escape to its region's campfire (src/pathfinder.rs:162-170)
-        consider(f.c, opt((z.soe >> t) & 1u, mk(z.base.K + dK(0, p.soe_cost, 0), z.base.c3 + d3(0, p.soe_cost, 0),
-                                                z.base.meta | lm_pack(0, 0, 1, kSoE))));
-        // from the region cell nearest to boundary s: [Std{d} s -> u, SoE u -> t]
-        consider(f.c, opt(((z.reg >> t) & 1u) & (sd != kPtNoSd) & (sd != 0u),
-                          mk(z.ls.K + dK(sd, p.soe_cost, 180u * sd), z.ls.c3 + d3(sd, p.soe_cost, 180u * sd),
-                             lm_pack(len + 2u, s, 2, kStandard))));
+        if (t >= 6 && t < 6 + kLaneRegs) {  // Scroll of Escape (src/pathfinder.rs:162-170)
+            const uint32_t so = bitm(z.soe, t), on = so | bitm(z.reg, t);
+            consider(f.c, opt(on, add(z.ls, B.x, P.soe_cost, B.y, msel(so, z.mSoE, z.mR))));
+            f.any |= on;
+        }
         return f;
     }
-    // the best candidate into entry t against its tentative label (K = kInfK: none):
-    // a strict win takes, an exact (metrics, length) tie is left to the list compare
-    // (bit t of *ties)
+    // the best candidate into entry t against its tentative label: a strict win takes,
+    // an exact (metrics, length) tie is left to the list compare (bit t of ties)
     __device__ __forceinline__ void offer(uint32_t t, const FromS &f, uint32_t &ties) {
         LLab &T = L[t];
         const uint32_t bit = 1u << t;
-        const bool any = f.c.K != kInfK;
-        const bool ke = f.c.K == T.K, ce = f.c.c3 == T.c3;
-        const uint32_t lf = lm_len(f.c.meta), lt_ = lm_len(T.meta);
-        const bool lt = any & ((f.c.K < T.K) | (ke & ((f.c.c3 < T.c3) | (ce & (lf < lt_)))));
-        const bool same3 = any & ke & ce;
+        const uint32_t lt = ltm(f.c, T) & f.any;
+        const uint32_t gt = ltm(T, f.c);
+        const uint32_t drop = ltm3(f.c, T) & f.any;  // the tentative metrics drop
         ll_sel(lt, T, f.c);
-        tent |= vbit(lt, bit);
-        // blocker bit: a walk candidate with the (new) tentative metrics; kept while the
-        // tentative metrics stay (an unchanged label, or a win on length / commands)
-        const bool keep = !lt | same3;
-        const bool wtie = (f.w.K != kInfK) & (f.w.K == T.K) & (f.w.c3 == T.c3);
-        wt = (wt & ~bit) | vbit((keep & ((wt & bit) != 0)) | wtie, bit);
-        ties |= vbit(same3 & (lf == lt_), bit);
+        tent |= lt & bit;
+        // blocker bit: a walk candidate with the (new) tentative metrics; the walk is >= the
+        // new tentative label, so it ties unless the label's metrics are strictly smaller
+        const uint32_t wtie = f.won & ~ltm3(T, f.w);
+        wt = (wt & ~(drop & bit)) | (wtie & bit);
+        ties |= f.any & ~(lt | gt) & bit;
     }
 
     // ---- certification (hub_kernel's avail / label_avail) ----------------------------
@@ -368,7 +396,7 @@ struct LaneHub {
         const DevParams &p = P;
         OutResult &o = a->out_res[qi];
         OutCmd *oc = a->out_cmd + (unsigned long long)qi * p.max_cmds;
-        const uint32_t len = lm_len(x.meta);
+        const uint32_t len = lm_len(x.m);
         const uint32_t legs = metric(x, 0), money = metric(x, 1), time = metric(x, 2);
         uint32_t status = 16;
         if (len > p.max_cmds) {  // the overflow pool, else MR_ERR_CAPACITY
@@ -382,7 +410,7 @@ struct LaneHub {
             status = 16 + kStatusOverflow;
         }
         int at = int(len) - 1;
-        uint32_t e = x.meta;
+        uint32_t e = x.m;
         Own eo = xo;
         uint32_t eid = xid;
         for (uint32_t guard = 0; at >= 0 && guard <= TM + 1; ++guard) {
@@ -410,84 +438,94 @@ struct LaneHub {
         sy = int(src / p.S) - int(p.H);
         ts = sinfo[src] & kNone10;
         srow = reinterpret_cast<const uint2 *>(a->near) + (unsigned long long)src * nreg;
-        // the source's own edges: its start label if it is a special, SHQ, SFm, the
-        // walks from it and the SoE edges from its region rows (src/pathfinder.rs:162-178)
+        // the source's own edges, in command-kind order: its start label if it is a
+        // special, the walks from it, the SoE edges from its region rows, SHQ, SFm
+        // (src/pathfinder.rs:162-178)
         const bool walks0 = have && src != p.vc;
-        const LLab st0 = start(), inf = LLab{kInfK, 0u, 0u};
+        const LLab st0 = start();
 #pragma unroll
         for (uint32_t t = 1; t < TM; ++t) {
             const bool valid = have && t <= NS;
             const SpecialStatic tS = spl[t <= NS ? t : 1u];
-            LLab c = opt(valid && t == ts, st0);
-            consider(c, opt(valid && t == p.hq_t, mk(dK(0, p.shq_cost, 0), d3(0, p.shq_cost, 0), lm_pack(1, 0, 1, kSHQ))));
-            consider(c, opt(valid && p.use_sfm && t == 1,
-                            mk(dK(0, p.sfm_cost, 0), d3(0, p.sfm_cost, 0), lm_pack(1, 0, 1, kSFm))));
+            const uint32_t m0 = vmask(valid && t == ts);
+            LLab c = opt(m0, st0);
+            uint32_t any = m0, won = 0;
+            LLab w = inf();
+            if (t != 1) {
+                const uint32_t k = walk_dist(sx, sy, tS.x, tS.y);
+                won = vmask(valid && walks0 && tS.v != src);
+                w = opt(won, mk(k, 0, 180u * k, lm_pack(1, 0, 1, kStandard)));
+                consider(c, w);
+                any |= won;
+            }
             {  // [SoE src -> t], or [Std{d} src -> u, SoE u -> t]
                 const bool reg = valid && p.use_soe && tS.rid != kNone10;
                 const uint32_t e = reg ? srow[reg ? tS.rid : 0u].x : kNone32;
                 const bool on = walks0 && reg && e != kNone32;
-                const uint32_t d = on ? e : 1u;
-                consider(c, opt(on, d == 0 ? mk(dK(0, p.soe_cost, 0), d3(0, p.soe_cost, 0), lm_pack(1, 0, 1, kSoE))
-                                           : mk(dK(d, p.soe_cost, 180u * d), d3(d, p.soe_cost, 180u * d),
-                                                lm_pack(2, 0, 2, kStandard))));
+                const uint32_t d = on ? e : 0u;
+                const uint32_t om = vmask(on);
+                consider(c, opt(om, mk(d, p.soe_cost, 180u * d,
+                                       d == 0 ? lm_pack(1, 0, 1, kSoE) : lm_pack(2, 0, 2, kStandard))));
+                any |= om;
             }
-            LLab w = inf;
-            if (t != 1) {
-                const uint32_t k = walk_dist(sx, sy, tS.x, tS.y);
-                w = opt(valid && walks0 && tS.v != src, mk(dK(k, 0, 180u * k), d3(k, 0, 180u * k), lm_pack(1, 0, 1, kStandard)));
-                consider(c, w);
+            {
+                const uint32_t om = vmask(valid && t == p.hq_t);
+                consider(c, opt(om, mk(0, p.shq_cost, 0, lm_pack(1, 0, 1, kSHQ))));
+                any |= om;
             }
-            L[t] = c;
-            tent |= c.K != kInfK ? (1u << t) : 0u;
-            wt |= ((w.K != kInfK) & eq3(w, c)) ? (1u << t) : 0u;
+            {
+                const uint32_t om = vmask(valid && p.use_sfm && t == 1);
+                consider(c, opt(om, mk(0, p.sfm_cost, 0, lm_pack(1, 0, 1, kSFm))));
+                any |= om;
+            }
+            L[t] = opt(any, c);
+            tent |= any & (1u << t);
+            wt |= won & ~ltm3(c, w) & (1u << t);
+            MR_LANE_FENCE();
         }
         // ---- Dijkstra over the specials, one settle per lane per iteration ----------
         for (uint32_t it = 0; it < NS; ++it) {
             const uint32_t cand = tent & ~done;
             if (!__any(cand != 0)) break;
             // the settle candidate: least (c1, c2, c3, length), two interleaved chains
-            // (odd and even entries) for the latency, then merged
-            LLab la = inf, lb = inf;
-            uint32_t sa = 0, sb = 0;
-            bool ta = false, tb = false;
+            // (odd and even entries) for the latency, then merged; ta / tb: the chain's
+            // best has an exact tie
+            LLab la = inf(), lb = inf();
+            uint32_t sa = 0, sb = 0, ta = 0, tb = 0;
 #pragma unroll
             for (uint32_t t = 1; t < TM; ++t) {
                 LLab &lx = (t & 1u) ? la : lb;
                 uint32_t &sx_ = (t & 1u) ? sa : sb;
-                bool &tx = (t & 1u) ? ta : tb;
-                const LLab c = opt((cand >> t) & 1u, L[t]);
-                const bool ke = c.K == lx.K, ce = c.c3 == lx.c3;
-                const uint32_t lc = lm_len(c.meta), ll = lm_len(lx.meta);
-                const bool lt = (c.K < lx.K) | (ke & ((c.c3 < lx.c3) | (ce & (lc < ll))));
-                tx = lt ? false : (tx | ((c.K != kInfK) & ke & ce & (lc == ll)));
+                uint32_t &tx = (t & 1u) ? ta : tb;
+                const uint32_t cm = bitm(cand, t);
+                const LLab c = opt(cm, L[t]);
+                const uint32_t lt = ltm(c, lx), gt = ltm(lx, c);
+                tx = ~lt & (tx | (cm & ~gt));
                 ll_sel(lt, lx, c);
-                sx_ = lt ? t : sx_;
+                sx_ = msel(lt, t, sx_);
+                MR_LANE_FENCE();
             }
             Settle z;
             z.ls = la;
-            uint32_t s = sa;
-            bool tie = ta;
+            uint32_t s, tie;
             {
-                const bool ke = lb.K == la.K, ce = lb.c3 == la.c3;
-                const uint32_t l1 = lm_len(lb.meta), l0 = lm_len(la.meta);
-                const bool lt = (lb.K < la.K) | (ke & ((lb.c3 < la.c3) | (ce & (l1 < l0))));
+                const uint32_t lt = ltm(lb, la), gt = ltm(la, lb);
                 ll_sel(lt, z.ls, lb);
-                s = lt ? sb : sa;
-                tie = lt ? tb : (ta | ((lb.K != kInfK) & ke & ce & (l1 == l0)));
+                s = msel(lt, sb, sa);
+                tie = msel(lt, tb, ta | (vmask(sb != 0) & ~gt));
             }
-            if (__any(tie)) {  // exact (metrics, length) ties: the command lists decide (rare)
+            if (__any(tie != 0)) {  // exact (metrics, length) ties: the command lists decide (rare)
                 uint32_t tied = 0;  // the entries with the winner's metrics and length
 #pragma unroll
                 for (uint32_t t = 1; t < TM; ++t)
-                    tied |= (((cand >> t) & 1u) & eq3(L[t], z.ls) & (lm_len(L[t].meta) == lm_len(z.ls.meta))) ? (1u << t)
-                                                                                                            : 0u;
+                    tied |= bitm(cand, t) & ~(ltm(L[t], z.ls) | ltm(z.ls, L[t])) & (1u << t);
                 dump_meta();
                 if (tie) {
                     for (uint32_t m = tied & ~(1u << s); m; m &= m - 1u) {
                         const uint32_t t = uint32_t(__builtin_ctz(m));
                         const uint32_t mt = meta_of(t);
-                        if (cmp_list(mt, t, own_of(t), z.ls.meta, s, own_of(s)) < 0) {
-                            z.ls.meta = mt;  // (same metrics)
+                        if (cmp_list(mt, t, own_of(t), z.ls.m, s, own_of(s)) < 0) {
+                            z.ls.m = mt;  // (same metrics and length)
                             s = t;
                         }
                     }
@@ -496,48 +534,57 @@ struct LaneHub {
             const bool act = s != 0;
             z.s = act ? s : 1u;
             done |= act ? (1u << s) : 0u;
-            const uint32_t lk = lm_nt(z.ls.meta) == 2 ? kSoE : lm_kind(z.ls.meta);
+            const uint32_t lm = z.ls.m, len = lm_len(lm);
+            const uint32_t lk = lm_nt(lm) == 2 ? kSoE : lm_kind(lm);
             const bool boundary = act && lk != kNoMove && lk != kStandard;
             blk |= (boundary && ((wt >> s) & 1u)) ? (1u << s) : 0u;  // a walk tied it: a blocker
             const bool walks = boundary && s != 1;                     // the Center starts no walks
             bndm |= walks ? (1u << s) : 0u;
-            const bool nomove = lk == kNoMove;  // the start label: its NoMove is replaced
-            z.base = mk(nomove ? 0ull : z.ls.K, nomove ? 0u : z.ls.c3,
-                        nomove ? lm_pack(1, 0, 1, 0) : lm_pack(lm_len(z.ls.meta) + 1u, z.s, 1, 0));
-            z.merge = lk == kCentral;
+            // the start label (the source's own special; metrics 0): its NoMove is replaced
+            const uint32_t bm = lk == kNoMove ? lm_pack(1, 0, 1, 0) : lm_pack(len + 1u, z.s, 1, 0);
+            z.mW = lm_pack(len + 1u, z.s, 1, kStandard);
+            z.mR = lm_pack(len + 2u, z.s, 2, kStandard);
+            z.mCar = bm | (kCaravan << 8);
+            z.mSoE = bm | (kSoE << 8);
+            // a CentralMove after a CentralMove merges into it
+            z.cen = add(z.ls, 0, 0, 10u,
+                        lk == kCentral ? lm_pack(len, lm_par(lm), 1, kCentral, lm_cj(lm) + 1u)
+                                       : (bm | lm_pack(0, 0, 1, kCentral, 1)));
             const uint32_t live = act ? (validm & ~done) : 0u;  // unsettled entries
             const uint32_t rg = spl[z.s].region;
-            z.cen = live & (z.s == 1 ? 0x3Cu : ((z.s >= 2 && z.s <= 5) ? 0x2u : 0u));
+            z.cenm = live & (z.s == 1 ? 0x3Cu : ((z.s >= 2 && z.s <= 5) ? 0x2u : 0u));
             z.car = (p.use_caravans && ((hubm >> z.s) & 1u)) ? (live & hubm) : 0u;
             z.soe = (p.use_soe && rg != kNone10 && rg != z.s) ? (live & (1u << rg)) : 0u;
-            z.reg = (walks && p.use_soe) ? (live & regm) : 0u;
+            z.reg = (walks && p.use_soe) ? (live & RM[z.s]) : 0u;
             z.walk = walks ? (live & ~0x2u) : 0u;
-            const uint32_t *row = PT + z.s * TM;
+            const uint4 *rowa = PA + z.s * TM;
+            const uint2 *rowb = PB + z.s * TM;
+            // Each step also stores into the LDS meta copy M: a settled entry's own meta
+            // (the command chains of the list compares walk settled entries only) and
+            // for the others the meta of this iteration's best candidate, which the tie
+            // path below reads instead of rebuilding the candidate.
             uint32_t ties = 0;
+            uint32_t *ml = M + lane_id();
 #pragma unroll
             for (uint32_t t = 1; t < TM; ++t) {
-                const FromS f = from_s(z, t, row[t]);
+                const FromS f = from_s(z, t, rowa[t], rowb[t]);
                 offer(t, f, ties);
+                ml[t * 64u] = msel(bitm(done, t), L[t].m, f.c.m);
                 MR_LANE_FENCE();
             }
-            // exact ties with a tentative label: the candidate is rebuilt and its command
-            // list compared (rare; run-time t)
-            // (same metrics: only the meta word can change; the new ones go through LDS)
+            // exact (metrics, length) ties with a tentative label: the command lists decide
+            // (rare; run-time t; only the meta word can change)
             if (__any(ties != 0)) {
-                dump_meta();
                 uint32_t repl = 0;
                 for (; ties; ties &= ties - 1u) {
                     const uint32_t t = uint32_t(__builtin_ctz(ties));
-                    const FromS f = from_s(z, t, row[t]);
-                    const uint32_t cur = meta_of(t);
-                    if (cmp_list(f.c.meta, kOwn, own_of(t), cur, t, own_of(t)) < 0) {
-                        M[t * 64u + lane_id()] = f.c.meta;
-                        repl |= 1u << t;
-                    }
+                    uint32_t cur = 0;  // entry t's meta
+#pragma unroll
+                    for (uint32_t e = 1; e < TM; ++e) cur = msel(vmask(e == t), L[e].m, cur);
+                    if (cmp_list(ml[t * 64u], kOwn, own_of(t), cur, t, own_of(t)) < 0) repl |= 1u << t;
                 }
 #pragma unroll
-                for (uint32_t t = 1; t < TM; ++t)
-                    if ((repl >> t) & 1u) L[t].meta = M[t * 64u + lane_id()];
+                for (uint32_t t = 1; t < TM; ++t) L[t].m = msel(bitm(repl, t), ml[t * 64u], L[t].m);
             }
         }
         if (!have) return 0;
@@ -568,34 +615,40 @@ struct LaneHub {
             }
             const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
             const Own wo{wx, wy, wr, kNone10, 0u};
-            LLab x = inf;
-            uint32_t bx = kNone32;
-            bool tie = false;
+            // Every candidate is a boundary's label plus one walk command, so they are
+            // compared on the boundary's own meta word (length - 1; the source's walk:
+            // 0) and the walk's meta is built for the winner.  The clobber and the
+            // volatile copy of bndm keep the per-entry terms inside the query loop
+            // (hoisted out of it they would hold ~170 VGPRs for the whole kernel).
+            asm volatile("" ::: "memory");
+            const uint32_t bq = vvolatile(bndm);
+            LLab x = inf();
+            uint32_t bx = walk0 ? 0u : kNone32;
+            uint32_t tie = 0;
             {
                 const uint32_t k = walk_dist(sx, sy, wx, wy);
-                x = opt(walk0, mk(dK(k, 0, 180u * k), d3(k, 0, 180u * k), lm_pack(1, 0, 1, kStandard)));
-                bx = walk0 ? 0u : kNone32;
+                ll_sel(vmask(walk0), x, mk(k, 0, 180u * k, 0u));
             }
 #pragma unroll
             for (uint32_t t = 2; t < TM; ++t) {
                 const uint32_t k = walk_dist(spl[t].x, spl[t].y, wx, wy);
-                const LLab c = opt((bndm >> t) & 1u, walk_to(L[t], t, k));
-                const bool ke = c.K == x.K, ce = c.c3 == x.c3;
-                const uint32_t lc = lm_len(c.meta), lx = lm_len(x.meta);
-                const bool lt = (c.K < x.K) | (ke & ((c.c3 < x.c3) | (ce & (lc < lx))));
-                tie = lt ? false : (tie | ((c.K != kInfK) & ke & ce & (lc == lx)));
+                const uint32_t cm = bitm(bq, t);
+                const LLab c = opt(cm, add(L[t], k, 0, 180u * k, L[t].m));
+                const uint32_t lt = ltm(c, x), gt = ltm(x, c);
+                tie = ~lt & (tie | (cm & ~gt));
                 ll_sel(lt, x, c);
-                bx = lt ? t : bx;
+                bx = msel(lt, t, bx);
+                MR_LANE_FENCE();
             }
+            x.m = lm_pack(lm_len(x.m) + 1u, bx == kNone32 ? 0u : bx, 1, kStandard);
             if (tie) {  // equal metrics and length from several boundaries: the lists decide
                 for (uint32_t m = (bndm | (walk0 ? 1u : 0u)) & ~(1u << bx); m; m &= m - 1u) {
                     const uint32_t b = uint32_t(__builtin_ctz(m));
                     int px, py;
                     pos(b, px, py);
                     const uint32_t k = walk_dist(px, py, wx, wy);
-                    const LLab c = b == 0 ? mk(dK(k, 0, 180u * k), d3(k, 0, 180u * k), lm_pack(1, 0, 1, kStandard))
-                                          : walk_to(get(b), b, k);
-                    if (cmp4(c, x) == 0 && cmp_list(c.meta, kOwn, wo, x.meta, kOwn, wo) < 0) {
+                    const LLab c = b == 0 ? mk(k, 0, 180u * k, lm_pack(1, 0, 1, kStandard)) : walk_to(get(b), b, k);
+                    if (cmp4(c, x) == 0 && cmp_list(c.m, kOwn, wo, x.m, kOwn, wo) < 0) {
                         x = c;
                         bx = b;
                     }
@@ -618,14 +671,21 @@ struct LaneHub {
     }
 };
 
-// the lane kernel's LDS: the specials' static records, their region rows and the pair table
+// the lane kernel's LDS: the specials' static records, their region rows, the pair table
+// (TM x TM uint4 + uint2), its row masks (TM words) and per wave the meta copy of the
+// rare paths (TM x 64 words)
 __host__ __device__ inline uint32_t lane_off_near(uint32_t NS) { return align16h((NS + 1) * uint32_t(sizeof(SpecialStatic))); }
 __host__ __device__ inline uint32_t lane_off_pt(uint32_t NS, uint32_t nreg) {
     return align16h(lane_off_near(NS) + (NS + 1) * nreg * 8u);
 }
-// then the pair table (TM x TM words) and per wave the meta copy of the rare paths (TM x 64 words)
+__host__ __device__ inline uint32_t lane_off_pb(uint32_t NS, uint32_t nreg, uint32_t TM) {
+    return lane_off_pt(NS, nreg) + TM * TM * 16u;
+}
+__host__ __device__ inline uint32_t lane_off_rm(uint32_t NS, uint32_t nreg, uint32_t TM) {
+    return lane_off_pb(NS, nreg, TM) + TM * TM * 8u;
+}
 __host__ __device__ inline uint32_t lane_off_meta(uint32_t NS, uint32_t nreg, uint32_t TM) {
-    return align16h(lane_off_pt(NS, nreg) + TM * TM * 4u);
+    return align16h(lane_off_rm(NS, nreg, TM) + TM * 4u);
 }
 __host__ __device__ inline uint32_t lane_lds_total(uint32_t NS, uint32_t nreg, uint32_t TM) {
     return lane_off_meta(NS, nreg, TM) + (kBS / 64) * TM * 64u * 4u;
@@ -637,29 +697,38 @@ __global__ __launch_bounds__(kBS, MR_LANE_WAVES) void hub_lane_kernel(const KArg
     const uint32_t NS = a->p.NS, nreg = a->nreg;
     SpecialStatic *spl = reinterpret_cast<SpecialStatic *>(smem);
     uint2 *nearl = reinterpret_cast<uint2 *>(smem + lane_off_near(NS));
-    uint32_t *pt = reinterpret_cast<uint32_t *>(smem + lane_off_pt(NS, nreg));
+    uint4 *pa = reinterpret_cast<uint4 *>(smem + lane_off_pt(NS, nreg));
+    uint2 *pb = reinterpret_cast<uint2 *>(smem + lane_off_pb(NS, nreg, TM));
+    uint32_t *rm = reinterpret_cast<uint32_t *>(smem + lane_off_rm(NS, nreg, TM));
     const uint2 *nearg = reinterpret_cast<const uint2 *>(a->near);
+    const uint32_t rgt = a->p.rgt;
     for (uint32_t t = threadIdx.x; t <= NS; t += kBS) spl[t] = a->sp[t];
+    for (uint32_t t = threadIdx.x; t < TM; t += kBS) rm[t] = 0;
     for (uint32_t i = threadIdx.x; i < NS * nreg; i += kBS) {
         const uint32_t t = 1 + i / nreg, r = i % nreg;
         nearl[t * nreg + r] = nearg[(unsigned long long)a->sp[t].v * nreg + r];
     }
-    // the pair table (LaneHub::from_s): walk / Manhattan / SoE-region distances of (s, t)
+    __syncthreads();
+    // the pair table (LaneHub::from_s)
     for (uint32_t i = threadIdx.x; i < TM * TM; i += kBS) {
         const uint32_t s = i / TM, t = i % TM;
-        uint32_t e = kPtNoSd << 15;
+        uint4 A = make_uint4(0, 0, 0, 0);
+        uint2 B = make_uint2(0, 0);
         if (s >= 1 && s <= NS && t >= 1 && t <= NS) {
             const SpecialStatic ss = a->sp[s], st = a->sp[t];
             const uint32_t wd = walk_dist(ss.x, ss.y, st.x, st.y);
             const uint32_t md = uint32_t(abs(ss.x - st.x) + abs(ss.y - st.y));
-            uint32_t sd = kPtNoSd;
+            A = make_uint4(wd, 180u * wd, (st.coef5 ? 5u : 2u) * md, rgt * md);
             if (st.rid != kNone10) {
                 const uint32_t d = nearg[(unsigned long long)ss.v * nreg + st.rid].x;
-                sd = d == kNone32 ? kPtNoSd : d;
+                if (d != kNone32) {
+                    B = make_uint2(d, 180u * d);
+                    if (d != 0) atomicOr(rm + s, 1u << t);
+                }
             }
-            e = wd | ((wd != md ? 1u : 0u) << 14) | (sd << 15) | ((st.coef5 ? 1u : 0u) << 29);
         }
-        pt[i] = e;
+        pa[i] = A;
+        pb[i] = B;
     }
     __syncthreads();
     LaneHub<PERM, TM> H;
@@ -667,7 +736,9 @@ __global__ __launch_bounds__(kBS, MR_LANE_WAVES) void hub_lane_kernel(const KArg
     H.P = a->p;
     H.spl = spl;
     H.nearS = nearl;
-    H.PT = pt;
+    H.PA = pa;
+    H.PB = pb;
+    H.RM = rm;
     H.M = reinterpret_cast<uint32_t *>(smem + lane_off_meta(NS, nreg, TM)) + (threadIdx.x >> 6) * (TM * 64u);
     H.rank = a->rank;
     H.sinfo = a->sinfo;

@@ -17,13 +17,15 @@ static const void *lane_fn_tm(uint32_t perm) {
     }
 }
 
-// table entries (NS + 1) the lane kernel holds in registers; 0 = not applicable
-uint32_t hub_lane_entries(uint32_t NS) { return NS + 1 <= 22 ? 22u : (NS + 1 <= 24 ? 24u : (NS + 1 <= 32 ? 32u : 0u)); }
+// table entries (NS + 1) the lane kernel holds in registers; 0 = not applicable.  One
+// size: 22 entries (Center, 4 border-1 cells, 16 campfires + HQ or 17 campfires) fit
+// the 256-VGPR budget of two waves per SIMD; a 24- or 32-entry table spills (17 /
+// 205 VGPRs with the current loop), so those plans stay on hub_kernel.
+uint32_t hub_lane_entries(uint32_t NS) { return NS + 1 <= 22 ? 22u : 0u; }
 
 static const void *lane_fn(const uint32_t perm[3], uint32_t NS) {
     const uint32_t k = perm[0] * 9 + perm[1] * 3 + perm[2];
-    const uint32_t tm = hub_lane_entries(NS);
-    return tm == 22 ? lane_fn_tm<22>(k) : (tm == 24 ? lane_fn_tm<24>(k) : (tm == 32 ? lane_fn_tm<32>(k) : nullptr));
+    return hub_lane_entries(NS) == 22 ? lane_fn_tm<22>(k) : nullptr;
 }
 
 uint32_t hub_lane_lds_bytes(uint32_t NS, uint32_t nreg) {

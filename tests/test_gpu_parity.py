@@ -23,13 +23,15 @@ def eng():
     return pathfinder
 
 
-@pytest.fixture(params=["auto-lds", "auto-hbm", "hub1-lds", "hub2-lds", "wide-lds", "widescan-lds", "fallback-lds", "fallback-hbm",
+@pytest.fixture(params=["auto-lds", "auto-hbm", "lane-lds", "hub1-lds", "hub2-lds", "wide-lds", "widescan-lds", "fallback-lds", "fallback-hbm",
                         "sssp-lds", "sssp-hbm", "generic-lds", "generic-hbm"])
 def grid_state(request, monkeypatch):
     """Every solver path x both grid-state regimes:
     auto     — hub solver when the run time is linear (one source per lane when the
-               table fits 24 entries and a source has <= 32 queries, else two
-               sources per wave when the specials fit 32 lanes), else the SSSP solvers
+               table fits 22 entries, a source has <= 32 queries and the plan has
+               enough such sources to fill the GPU, else two sources per wave when
+               the specials fit 32 lanes), else the SSSP solvers
+    lane     — auto with the lane kernel whenever it applies (MR_HUB_LANE=1)
     hub1     — hub solver with one source per wave (no lane kernel)
     hub2     — hub solver with two sources per wave (no lane kernel)
     wide     — the wide hub solver (several specials per lane) even where the
@@ -48,6 +50,8 @@ def grid_state(request, monkeypatch):
     monkeypatch.delenv("MR_HUB_LANE", raising=False)
     if algo in ("hub1", "hub2"):
         monkeypatch.setenv("MR_HUB_LANE", "0")
+    if algo == "lane":
+        monkeypatch.setenv("MR_HUB_LANE", "1")
     if algo == "wide":
         monkeypatch.setenv("MR_HUB_WIDE", "1")
     if algo == "widescan":
@@ -160,6 +164,31 @@ def test_destinations_per_source(eng, oracle_lib, grid_state, n_dst):
     qs = [(a, b) for a in srcs for b in (cells if n_dst >= len(cells) else rng.sample(cells, n_dst))]
     for params in (Params(), Params(sort_by=(SORT_TIME, SORT_LEGS)), Params(sort_by=(SORT_MONEY, SORT_TIME))):
         check(eng, oracle_lib, m, params, qs, f"n_dst={n_dst} {params}")
+
+
+def test_lane_kernel_selection(eng, oracle_lib, monkeypatch):
+    """hub_lane_kernel takes a plan's few-query sources when there are enough of them
+    to fill the GPU (MR_HUB_LANE_MIN, default half a wave per SIMD), always with
+    MR_HUB_LANE=1, never with MR_HUB_LANE=0; the table layout it needs (region
+    campfires in entries 6..11) comes from the host's special order.  Results are the
+    oracle's either way."""
+    m = SyntheticMap(33, campfires_per_homeland=4, seed=5)
+    qs = random_queries(m, 400, 6)
+    g = eng.MapGrid(m.cells())
+    lanes = {}
+    for mode, env in (("default", {}), ("force", {"MR_HUB_LANE": "1"}), ("off", {"MR_HUB_LANE": "0"}),
+                      ("min1", {"MR_HUB_LANE_MIN": "1"})):
+        monkeypatch.delenv("MR_HUB_LANE", raising=False)
+        monkeypatch.delenv("MR_HUB_LANE_MIN", raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        pl = eng.Plan(g, Params(), qs)
+        st = pl.stats()
+        lanes[mode] = st["lane_sources"]
+        check(eng, oracle_lib, m, Params(), qs, f"lane mode {mode}")
+    n_src = len({a for a, _ in qs})
+    assert lanes["default"] == 0 and lanes["off"] == 0, lanes  # 400 sources < half a wave per SIMD
+    assert lanes["force"] == n_src and lanes["min1"] == n_src, lanes
 
 
 def test_invalid_queries_report_errors(eng):
