@@ -200,7 +200,12 @@ def algorithmic_bytes(plan, stats, V):
     b = nq * (4 + 4 + 16) + 16 * n_cmds + n_src * (8 + 8 * stats["num_regions"])
     b += 8 * stats["region_boundary_cells"]  # wide solver: the regions' boundary cells, read once (L2-resident)
     b += stats["fallback_sources"] * V * BYTES_PER_VERTEX_SOLVE
-    kern = "hub_wide_kernel" if stats["solver"] == "hub_wide" else "hub_kernel"
+    if stats["solver"] == "hub_wide":
+        kern = "hub_wide_kernel"
+    elif stats.get("lane_sources", 0) == 0:
+        kern = "hub_kernel"
+    else:  # one source per lane; sources with many queries stay on hub_kernel
+        kern = "hub_lane_kernel" + (" + hub_kernel" if stats["lane_sources"] < n_src else "")
     name = kern + (" + sssp_kernel (fallback)" if stats["fallback_sources"] else "")
     return float(b), name, survey
 
@@ -515,7 +520,8 @@ def main():
                               "read) + 80 B per table entry; survey_8d_bytes_per_launch is SURVEY 8d's V x 20 B; "
                               "kernel_ms spans the fill's two launches; pass_ms is the caller-stream span of a pass (the specials' "
                               "solve runs beside the previous pass's fill, DESIGN.md 3b)" if all_dst else
-                              "hub solver: latency-bound per-source wave Dijkstra over the specials; bytes = "
+                              "hub solver: instruction-issue bound Dijkstra over the specials (one source per lane: "
+                              "hub_lane_kernel; per wave: hub_kernel; see roofline.issue); bytes = "
                               "queries in, results and command slots out, per-source region rows, plus V*20 B "
                               "per SSSP fallback source (DESIGN.md section 4)")
                      if stats["solver"] in ("hub", "hub_wide") else

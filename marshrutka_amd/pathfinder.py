@@ -293,6 +293,13 @@ class FindPath:
         return out
 
 
+def _host_array(ctype, n: int):
+    """An uninitialised ctypes array of n ctype (numpy-backed; it keeps the buffer alive)."""
+    import numpy as np
+    buf = np.empty(n * C.sizeof(ctype), dtype=np.uint8)
+    return (ctype * n).from_buffer(buf)
+
+
 def decode_records_raw(grid: MapGrid, params: Params, results, commands, n: int, max_cmds: int, overflow=None):
     """Compact device records (mr_plan_device_outputs layout: 16 B result records,
     max_cmds 16 B command slots each, an overflow pool) as host buffers — e.g. the
@@ -433,10 +440,13 @@ class Plan:
             raise EngineError(st, last_error())
 
     def fetch_raw(self):
-        """(results, command pool) as ctypes arrays, no Python label objects."""
-        res = (mr_result * max(self.n, 1))()
+        """(results, command pool) as ctypes arrays, no Python label objects.  The
+        buffers are uninitialised host memory (mr_plan_fetch writes every result and
+        the commands they point at; a zero-filled pool of n * (max_cmds + 8) commands
+        costs seconds at millions of queries)."""
+        res = _host_array(mr_result, max(self.n, 1))
         cap = self.n * self.max_cmds + max(4096, self.n * 8)  # slots + overflow pool
-        pool = (mr_command * cap)()
+        pool = _host_array(mr_command, cap)
         st = lib().mr_plan_fetch(self.handle, res, pool, cap)
         if st < 0 and st not in (abi.MR_ERR_INVALID_INDEX, MR_ERR_CAPACITY):
             raise EngineError(st, last_error())

@@ -144,17 +144,20 @@ def c5(eng):
     return m, arr, eng.MapGrid.from_array(arr), fx
 
 
-def _labels_of_source(eng, m, arr, g, params, sv, chunk=1 << 21):
+def _labels_of_source(eng, m, arr, g, params, sv, chunk=1 << 21, max_cmds=24):
     """Every cell's label from row-major cell sv through query plans of `chunk`
     destinations (one source, so one wave solves it and reads them all off), as
-    label_digest fields over the V cells, plus the batch's property violations."""
+    label_digest fields over the V cells, plus the batch's property violations.
+    max_cmds 24: c5's labels run to 22 commands (Time first), and the plan's
+    overflow pool (8 commands per query) would not hold most of them beyond 8 slots
+    (MR_ERR_CAPACITY records, the documented behaviour)."""
     V = m.size * m.size
     keys = ld.cell_keys(arr)
     out = {f: [] for f in ld.FIELDS}
     props = {}
     for lo in range(0, V, chunk):
         dst = np.arange(lo, min(V, lo + chunk), dtype=np.int64)
-        plan = eng.Plan(g, params, None, max_cmds=8, query_array=m.query_array(np.full(len(dst), sv), dst, arr))
+        plan = eng.Plan(g, params, None, max_cmds=max_cmds, query_array=m.query_array(np.full(len(dst), sv), dst, arr))
         plan.run()
         res, pool = plan.fetch_raw()
         assert plan.stats()["solver"] == "hub_wide"
@@ -176,6 +179,7 @@ def test_c5_every_destination_4097(eng, c5):
     for src in fx["sources"]:
         params = Params.from_json(src["params"])
         got, props = _labels_of_source(eng, m, arr, g, params, src["cell"])
+        assert props["not_ok"] == 0, (src["spec"], props)
         assert all(v == 0 for v in props.values()), (src["spec"], props)
         rows = ld.row_checksums(got, m.size)
         want = np.array([int(x, 16) for x in src["rows"]], dtype=np.uint64)
