@@ -309,7 +309,7 @@ def main():
     from marshrutka_amd import build, pathfinder
     from marshrutka_amd.abi import Params
     from marshrutka_amd.mapgen import SyntheticMap, random_queries
-    from marshrutka_amd.shard import PipelinedGather, shard_by_source
+    from marshrutka_amd.shard import PipelinedGather, SourceCosts, shard_by_source
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -345,6 +345,7 @@ def main():
     params = Params(sort_by=wl["sort"]) if "sort" in wl else Params()
     all_dst = bool(wl.get("all_destinations"))
     grid = pathfinder.MapGrid.from_array(m.cells_array())
+    fb_total_probe = None  # N > 1 query batches: sources the probe pass saw re-solved
     if all_dst:
         # distinct sources, a contiguous block per rank; no cross-rank data path
         cells = m.all_indices()
@@ -359,6 +360,22 @@ def main():
         keys = [(a.kind << 40) | (a.sub << 32) | (a.x << 16) | a.y for a, _ in all_q]
         shards = shard_by_source(keys, world)
         mine = [all_q[i] for i in shards[rank]]
+        if dist_on:
+            # cost-aware split (shard.SourceCosts): one untimed probe pass per rank names
+            # the sources the hub solver hands to the SSSP kernel; the batch is re-dealt
+            # with their cost, so they land one per rank and the hub work goes elsewhere
+            probe = pathfinder.Plan(grid, params, mine, max_cmds=wl.get("max_cmds", 16))
+            probe.run()
+            fb_keys = [(c.kind << 40) | (c.sub << 32) | (c.x << 16) | c.y for c in probe.fallback_sources()]
+            del probe
+            every = [None] * world
+            dist.all_gather_object(every, fb_keys)
+            costs = SourceCosts()
+            costs.observe(k for ks in every for k in ks)
+            fb_total_probe = len(costs.extra)
+            if fb_total_probe:
+                shards = shard_by_source(keys, world, costs())
+                mine = [all_q[i] for i in shards[rank]]
         counts = [len(s) for s in shards]
         # N > 1: two plans over the same shard, so the result gather of one batch
         # overlaps the solve of the next (double buffering, shard.PipelinedGather)
@@ -506,6 +523,8 @@ def main():
                    "params": "FindPath defaults: sort " + ("(Time,Money)" if wl.get("sort") == (1, 2) else
                                                            "(Legs,Money)") + ", SoE 50, caravans, skills 0, homeland Blue",
                    "solver": stats["solver"], "fallback_sources_per_step": fb_total,
+                   "cost_aware_split": None if fb_total_probe is None else
+                   {"fallback_sources_seen_by_probe": fb_total_probe},
                    "specials": stats["num_specials"],
                    "parallelism": f"sources sharded over {world} GPU(s), RCCL gather of results to rank 0 "
                                   "(double-buffered: overlaps the next batch's solve)"

@@ -240,6 +240,11 @@ int mr_decode_records(const mr_grid *grid, const mr_params *params, const void *
 int mr_plan_record_queries(const mr_plan *plan, uint32_t *query_of_record, uint32_t n);
 /* Number of unique sources (= single-source solves per pass). */
 uint32_t mr_plan_num_sources(const mr_plan *plan);
+/* The sources the last pass handed to the SSSP kernel (closed form not certain; each
+ * costs one full single-source search): up to cap source cells into out, their count
+ * in *n.  Waits for the plan's passes.  A cost signal for balancing sources over
+ * ranks (marshrutka_amd/shard.py SourceCosts); no reference counterpart. */
+int mr_plan_fallback_sources(mr_plan *plan, mr_cell_index *out, uint32_t cap, uint32_t *n);
 
 /* Which solver a plan runs and how the last pass went (diagnostics, bench). */
 enum {

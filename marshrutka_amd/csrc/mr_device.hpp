@@ -1698,10 +1698,12 @@ struct HubSolver : Core<false> {
     // distance to grow on that leg, a time gap of -1 or 0 at u that does not shrink
     // (delta >= 0), q ahead at u and b ahead at w on (gap, tail) — the tail being the
     // metric after Time, then the length (a walk from q's own cell appends a command:
-    // the flip of a blocker), the command lists undecided here.  A path through the
-    // Center is not a walk: true.
+    // the flip of a blocker), then the command lists: two walks of equal length that
+    // both append a command compare as q's and b's own lists do (`lists`, the same at
+    // every cell: their last commands end at different cells, so the lists differ);
+    // other list ties count as undecided.  A path through the Center is not a walk: true.
     __device__ __forceinline__ bool path_tie(uint32_t q, int qx, int qy, uint32_t b, int bx, int by, int vx, int vy,
-                                             bool x_first) const {
+                                             bool x_first, int lists) const {
         const DevParams &p = P;
         const bool legs_before = p.perm[0] == 0 || (p.perm[1] == 0 && p.perm[0] != 2);
         const bool money_before = p.perm[0] == 1 || (p.perm[1] == 1 && p.perm[0] != 2);
@@ -1747,7 +1749,8 @@ struct HubSolver : Core<false> {
                             if (mq != mb) return mq < mb ? -1 : 1;
                         }
                         const long long nq = dd > 0 ? nq1 : nq0, nbb = kk > 0 ? nb1 : nb0;
-                        return nq < nbb ? -1 : (nq > nbb ? 1 : 0);
+                        if (nq != nbb) return nq < nbb ? -1 : 1;
+                        return (dd > 0 && kk > 0) ? lists : 0;
                     };
                     const bool q_beats_u = gap == -1 || tail(dq, k) != 1;
                     const long long gw = gap + delta;
@@ -1776,8 +1779,15 @@ struct HubSolver : Core<false> {
         int qx, qy;
         bpos(q, sx, sy, qx, qy);
         if (!near_tie(q, qx, qy, b, bx, by, vx, vy)) return 3u;
-        return (path_tie(q, qx, qy, b, bx, by, vx, vy, true) ? 0u : 1u) |
-               (path_tie(q, qx, qy, b, bx, by, vx, vy, false) ? 0u : 2u);
+        int lists = 0;  // the order of q's and b's command lists when their walks' lengths tie
+        if (q != 0 && b != 0 && R[q].len() == R[b].len()) {
+            View xq, xb;
+            view_rec(q, xq);
+            view_rec(b, xb);
+            lists = cmp_list(xq, q, xb, b);
+        }
+        return (path_tie(q, qx, qy, b, bx, by, vx, vy, true, lists) ? 0u : 1u) |
+               (path_tie(q, qx, qy, b, bx, by, vx, vy, false, lists) ? 0u : 2u);
     }
     // Is the closed-form walk(b, d_b(v)) certain to be the reference's label of v?
     // Linear run times: always (the blocker check, avail, covers ties).  Otherwise

@@ -1457,6 +1457,22 @@ extern "C" int mr_plan_record_queries(const mr_plan *pl, uint32_t *query_of_reco
 
 extern "C" double mr_plan_fill_ms(const mr_plan *pl) { return pl ? pl->fill_ms : 0.0; }
 
+extern "C" int mr_plan_fallback_sources(mr_plan *pl, mr_cell_index *out, uint32_t cap, uint32_t *n) {
+    if (!pl || !n || (cap && !out)) return fail(MR_ERR_INVALID_ARG, "null argument");
+    *n = 0;
+    if (!plan_sync(pl)) return fail(MR_ERR_DEVICE, "sync");
+    uint32_t ctr[kCtrWords];
+    if (int st = read_counters(pl, ctr)) return st;
+    const uint32_t nf = pl->hp.hub && pl->d_fb ? std::min(ctr[kCtrLastFb], pl->ka.nsrc) : 0u;
+    std::vector<uint32_t> fb(nf);
+    if (nf && hipMemcpy(fb.data(), pl->d_fb, size_t(nf) * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(MR_ERR_DEVICE, "copy fallback list");
+    std::sort(fb.begin(), fb.end());
+    for (uint32_t k = 0; k < nf && k < cap; ++k) out[k] = pl->grid->idx[pl->hp.src_v[fb[k]]];
+    *n = nf;
+    return MR_OK;
+}
+
 extern "C" int mr_plan_get_stats(mr_plan *pl, mr_plan_stats *out) {
     if (!pl || !out) return fail(MR_ERR_INVALID_ARG, "null argument");
     std::memset(out, 0, sizeof(*out));

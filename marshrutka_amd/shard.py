@@ -3,32 +3,62 @@
 Queries are independent and the grid is read-only, so a batch shards by
 *source*: all queries of one source go to the same rank (one single-source
 solve answers all of them).  Sources are dealt to ranks by a deterministic
-longest-processing-time greedy on their query counts.  The only collective is
-the final gather of the fixed-size result records to rank 0 (RCCL over xGMI on
-MI355X; gloo in the CPU tests).
+longest-processing-time greedy on their estimated cost: the query count, plus
+what a source is known to cost beyond that (SourceCosts: a source the hub solver
+hands to the SSSP kernel costs a full single-source search, ~10^4 times a hub
+source).  The only collective is the final gather of the fixed-size result
+records to rank 0 (RCCL over xGMI on MI355X; gloo in the CPU tests).
 """
 from __future__ import annotations
 
 import heapq
-from typing import Dict, List, Sequence
+from typing import Dict, Iterable, List, Mapping, Optional, Sequence
 
 
-def shard_by_source(src_keys: Sequence[int], world: int) -> List[List[int]]:
-    """Returns, per rank, the (ascending) query indices it owns."""
+def shard_by_source(src_keys: Sequence[int], world: int,
+                    extra_cost: Optional[Mapping[int, float]] = None) -> List[List[int]]:
+    """Returns, per rank, the (ascending) query indices it owns.  A source's cost is
+    its query count plus extra_cost.get(source key, 0) (in query units)."""
     groups: Dict[int, List[int]] = {}
     for i, s in enumerate(src_keys):
         groups.setdefault(s, []).append(i)
-    # LPT: biggest groups first, ties by source key, each to the least-loaded rank
-    order = sorted(groups.items(), key=lambda kv: (-len(kv[1]), kv[0]))
-    heap = [(0, r) for r in range(world)]
+    extra = extra_cost or {}
+    cost = {k: len(v) + float(extra.get(k, 0.0)) for k, v in groups.items()}
+    # LPT: costliest sources first, ties by source key, each to the least-loaded rank
+    order = sorted(groups.items(), key=lambda kv: (-cost[kv[0]], kv[0]))
+    heap = [(0.0, r) for r in range(world)]
     out: List[List[int]] = [[] for _ in range(world)]
-    for _, idxs in order:
+    for key, idxs in order:
         load, r = heapq.heappop(heap)
         out[r].extend(idxs)
-        heapq.heappush(heap, (load + len(idxs), r))
+        heapq.heappush(heap, (load + cost[key], r))
     for r in range(world):
         out[r].sort()
     return out
+
+
+class SourceCosts:
+    """Per-source costs learned from passes, for shard_by_source's extra_cost.
+
+    observe(keys) records the sources a pass re-solved with the SSSP kernel
+    (Plan.fallback_sources(), mr_plan_fallback_sources): the closed form is not
+    certain for them, and the same source with the same parameters falls back again
+    on the next batch.  Such a source costs `fallback_cost` queries more: one full
+    search, ~16-25 ms at 1025^2 (DESIGN.md section 3a''), against ~1.8 ns per query
+    of the lane hub kernel (c4: 0.224 ms per 125k) -> ~10^7.  LPT then deals the
+    fallback sources out first, one per rank while they last, and the hub work goes
+    to the ranks without one: the ranks that pay a search get nothing else to do."""
+
+    def __init__(self, fallback_cost: float = 1e7):
+        self.fallback_cost = float(fallback_cost)
+        self.extra: Dict[int, float] = {}
+
+    def observe(self, fallback_keys: Iterable[int]) -> None:
+        for k in fallback_keys:
+            self.extra[k] = self.fallback_cost
+
+    def __call__(self) -> Dict[int, float]:
+        return dict(self.extra)
 
 
 def gather_rows_to_root(local, counts: Sequence[int], rank: int, world: int, group=None):

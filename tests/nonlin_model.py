@@ -55,7 +55,7 @@ def near_tie(mq, gq, mb, gb, gv, perm, ff) -> bool:
     return any(m != 0 and mlo <= m <= mhi and gap_hits(m) for m in range(m0 - 1, m0 + 3))
 
 
-def path_tie(mq, nq, gq, q_src, mb, nb, gb, b_src, gv, perm, ff, x_first) -> bool:
+def path_tie(mq, nq, gq, q_src, mb, nb, gb, b_src, gv, perm, ff, x_first, lists=0) -> bool:
     before = perm[:perm.index(TIME)]
     after = perm[perm.index(TIME) + 1:]
     if MONEY in before and mq[MONEY] != mb[MONEY]:
@@ -84,6 +84,8 @@ def path_tie(mq, nq, gq, q_src, mb, nb, gb, b_src, gv, perm, ff, x_first) -> boo
             continue
 
         def tail(dqq, kk):  # -1: q ahead after Time, +1: b ahead, 0: undecided (command lists)
+            # (two walks of equal length that both append a command are ordered by their
+            # boundaries' own command lists, the same at every cell: `lists`)
             for c in after:
                 a_ = mq[c] + (dqq if c == LEGS else 0)
                 b_ = mb[c] + (kk if c == LEGS else 0)
@@ -91,7 +93,9 @@ def path_tie(mq, nq, gq, q_src, mb, nb, gb, b_src, gv, perm, ff, x_first) -> boo
                     return -1 if a_ < b_ else 1
             lq = 1 if q_src else nq + (1 if dqq > 0 else 0)
             lb = 1 if b_src else nb + (1 if kk > 0 else 0)
-            return (lq > lb) - (lq < lb)
+            if lq != lb:
+                return (lq > lb) - (lq < lb)
+            return lists if (dqq > 0 and kk > 0) else 0
         q_beats_u = gap == -1 or tail(dq, k) != 1
         gw = gap + delta
         b_beats_w = gw > 0 or (gw == 0 and tail(dqn, k + 1) != -1)
@@ -114,8 +118,12 @@ def walk_certified(b, v, bnd, lab, geo, src_i, perm, ff) -> bool:
         mq, nq = metrics(lab[q]), len(lab[q].commands)
         if not near_tie(mq, geo[q], mb, geo[b], geo[v], perm, ff):
             continue
+        lists = 0  # the order of q's and b's command lists when their walks' lengths tie
+        if q != src_i and b != src_i and nq == nb:
+            kq, kb = [c.key() for c in lab[q].commands], [c.key() for c in lab[b].commands]
+            lists = (kq > kb) - (kq < kb)
         args = (mq, nq, geo[q], q == src_i, mb, nb, geo[b], b == src_i, geo[v], perm, ff)
-        clean = {x for x in clean if not path_tie(*args, x)}
+        clean = {x for x in clean if not path_tie(*args, x, lists)}
         if not clean:
             return False
     return True

@@ -32,6 +32,7 @@ from marshrutka_amd.mapgen import SyntheticMap, random_queries
 pytestmark = pytest.mark.gpu
 
 ORACLE_THREADS = 16  # the GPU box's CPU share
+FF_RATIO = {1: (50, 53), 2: (100, 109), 3: (25, 28)}  # Fleetfoot run-time ratios (src/skill.rs:65-71)
 C5_FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "full_scale", "c5.json")
 
 
@@ -108,6 +109,46 @@ def test_c4_full_scale(eng, oracle_lib, c4_map):
     ed = ld.digests(eres, epool, len(sample))
     bad = ld.mismatches(got, ed, idx_got=np.array(sample))
     assert bad.size == 0, [uni[sample[j]] for j in bad[:4]]
+
+
+@pytest.mark.parametrize("ff", [1, 3])
+def test_fleetfoot_time_first_1025(eng, oracle_lib, c4_map, ff):
+    """Non-linear run times (Fleetfoot 1, 3) with Time first at configs[3]'s size: the
+    certified hub path (DESIGN.md section 3a'') plus the SSSP kernel for the sources it
+    hands over.  A 20k-query batch property-checked in full (the time of a StandardMove
+    run through the Fleetfoot ceil), and every destination of 8 sources x 1 000 against
+    the oracle's Dijkstra from each source (mro_sssp_digest_batch)."""
+    m, arr = c4_map
+    V = m.size * m.size
+    keys = ld.cell_keys(arr)
+    rng = random.Random(ff)
+    params = Params(fleetfoot=ff, sort_by=(SORT_TIME, SORT_MONEY))
+    uni = random_queries(m, 20_000, 77 + ff)
+    srcs = _sources_of_every_kind(m, rng)[::2]
+    cf_cells = [m.cell_of(c) for c in m.campfires()]
+    extra_src, extra_dst = [], []
+    for s in srcs:
+        d = rng.sample(range(V), 1000 - len(cf_cells)) + cf_cells
+        extra_src += [m.cell_of(s)] * len(d)
+        extra_dst += d
+    q_src = np.concatenate([np.array([m.cell_of(a) for a, _ in uni]), np.array(extra_src)])
+    q_dst = np.concatenate([np.array([m.cell_of(b) for _, b in uni]), np.array(extra_dst)])
+    n = len(q_src)
+    g = eng.MapGrid.from_array(arr)
+    plan = eng.Plan(g, params, None, max_cmds=8, query_array=m.query_array(q_src, q_dst, arr))
+    plan.run()
+    res, pool = plan.fetch_raw()
+    st = plan.stats()
+    assert st["solver"] == "hub" and st["fallback_sources"] <= 8, st
+    props = ld.label_properties(res, pool, n, keys[q_src], keys[q_dst], fleetfoot_ratio=FF_RATIO[ff])
+    assert all(v == 0 for v in props.values()), props
+    got = ld.digests(res, pool, n)
+    want = oracle_lib.OracleGrid.from_array(arr).sssp_digests(params, srcs, threads=ORACLE_THREADS)
+    off = len(uni)
+    for i, s in enumerate(srcs):
+        sel = np.arange(off + i * 1000, off + (i + 1) * 1000)
+        bad = ld.mismatches(got, {f: want[f][i] for f in want}, idx_got=sel, idx_exp=q_dst[sel])
+        assert bad.size == 0, (str(s), len(bad), [str(m.index_at(int(q_dst[sel][j]))) for j in bad[:4]])
 
 
 @pytest.mark.parametrize("params", [Params(), Params(sort_by=(SORT_TIME, SORT_MONEY), route_guru=2)],

@@ -191,6 +191,25 @@ def test_lane_kernel_selection(eng, oracle_lib, monkeypatch):
     assert lanes["force"] == n_src and lanes["min1"] == n_src, lanes
 
 
+def test_fallback_sources_reported(eng, oracle_lib, monkeypatch):
+    """mr_plan_fallback_sources: the sources a pass re-solved with the SSSP kernel —
+    none on a plain hub pass, every source with MR_HUB_FALLBACK_ALL=1 (the cost signal
+    shard.SourceCosts learns from)."""
+    m = SyntheticMap(25, campfires_per_homeland=3, seed=4)
+    qs = random_queries(m, 120, 8)
+    g = eng.MapGrid(m.cells())
+    pl = eng.Plan(g, Params(), qs)
+    pl.run()
+    assert pl.stats()["solver"] == "hub" and pl.fallback_sources() == []
+    monkeypatch.setenv("MR_HUB_FALLBACK_ALL", "1")
+    pl = eng.Plan(g, Params(), qs)
+    pl.run()
+    got = pl.fallback_sources()
+    assert len(got) == pl.stats()["fallback_sources"] == pl.num_sources
+    assert set(got) == {a for a, _ in qs}
+    check(eng, oracle_lib, m, Params(), qs, "all sources re-solved")
+
+
 def test_invalid_queries_report_errors(eng):
     from marshrutka_amd.abi import MR_ERR_INVALID_INDEX, MR_OK
     m = SyntheticMap(7, campfires_per_homeland=1, seed=3)

@@ -118,3 +118,98 @@ def test_pipelined_gather_gloo_world2():
     for step, got in zip([0, 1, 2, 3, 4], seen):
         assert got[0] == [[1000 * step + j * 4 + c for c in range(4)] for j in range(2)]
         assert got[1] == [[1000 * step + 100 + j * 4 + c for c in range(4)] for j in range(3)]
+
+
+def test_cost_aware_lpt_spreads_fallback_sources():
+    """SourceCosts: the sources a pass re-solved with the SSSP kernel are dealt out
+    first, one per rank, and the hub work goes to the other ranks."""
+    from marshrutka_amd.shard import SourceCosts
+    keys = [i % 50 for i in range(1000)]
+    costs = SourceCosts()
+    costs.observe([3, 7])
+    shards = shard_by_source(keys, 4, costs())
+    owner = {keys[i]: r for r, s in enumerate(shards) for i in s}
+    assert owner[3] != owner[7]
+    heavy = {owner[3], owner[7]}
+    for r, s in enumerate(shards):
+        if r in heavy:  # only the fallback source's own queries
+            assert {keys[i] for i in s} <= {3, 7}
+    light = [len(s) for r, s in enumerate(shards) if r not in heavy]
+    assert max(light) - min(light) <= 20 and sum(light) == 960
+    assert shard_by_source(keys, 4) == shard_by_source(keys, 4, {})  # no costs: the query-count LPT
+
+
+FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "shard_records.npz")
+
+
+def _records_worker(rank, world, port, ret):
+    import json
+    import numpy as np
+    import torch.distributed as dist
+    import torch
+    from golden_util import as_expected
+    from marshrutka_amd import pathfinder
+    from marshrutka_amd.abi import Params
+    from marshrutka_amd.mapgen import SyntheticMap
+    from marshrutka_amd.shard import PipelinedGather
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        z = np.load(FIX)
+        meta = json.loads(str(z["meta"]))
+        summary = []
+        for j, run in enumerate(meta["runs"]):
+            pg = PipelinedGather([torch.from_numpy(z[f"run{j}_rank{rank}"].copy())], rank, world, host_staging=True)
+            pg.issue(0)
+            pg.drain()
+            if rank != 0:
+                continue
+            m = SyntheticMap(**meta["map"])
+            g = pathfinder.MapGrid(m.cells())
+            params = Params.from_json(run["params"])
+            rows, rw, cw, ovf_cap = run["rows"], run["rw"], run["cw"], run["ovf_cap"]
+            got = [None] * len(meta["queries"])
+            covered = 0
+            for r, buf in enumerate(pg.out[0]):
+                words = buf.numpy().view(np.uint32)
+                n = run["counts"][r]
+                res = words[: n * rw]
+                slots = words[rows * rw: rows * rw + n * cw]
+                ovf = words[rows * (rw + cw): rows * (rw + cw) + ovf_cap * 4]
+                for k, lab in enumerate(pathfinder.decode_records(g, params, res, slots, n, cw // 4, ovf)):
+                    q = meta["shards"][r][run["orders"][r][k]]
+                    got[q] = as_expected(lab)
+                    covered += 1
+            bad = sum(1 for a, b in zip(got, run["expected"]) if a != b)
+            summary.append((covered, bad))
+        if rank == 0:
+            ret.put(summary)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_engine_records_gather_gloo_world2():
+    """The N > 1 result path with real engine output: each rank's buffer holds the
+    device records of its shard as its own plan wrote them on an MI355X (fixture:
+    tests/golden/make_shard_records.py, bench.py's buffer layout: records, command
+    slots, overflow pool); rank 0 gathers both over gloo (PipelinedGather), decodes
+    them on the host (mr_decode_records) and maps record k of rank r back to its
+    query.  Every label equals the one-rank run of the whole batch, including labels
+    longer than the 3 command slots (overflow pool)."""
+    import torch.multiprocessing as mp
+    assert os.path.exists(FIX), "tests/golden/shard_records.npz (make_shard_records.py on a GPU box)"
+    ctx = mp.get_context("spawn")
+    ret = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_records_worker, args=(r, 2, port, ret)) for r in range(2)]
+    for p in procs:
+        p.start()
+    summary = ret.get(timeout=180)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert len(summary) == 2
+    for covered, bad in summary:
+        assert covered == 400 and bad == 0, summary
