@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <chrono>
 #include <thread>
 #include <string>
 #include <unordered_map>
@@ -48,6 +49,14 @@ hipError_t launch_hub_lane(const KArgs *d_args, const uint32_t perm[3], uint32_t
 using namespace mr;
 
 static thread_local std::string g_last_error;
+// MR_TIMING=1: host phase times of plan creation and fetch on stderr (diagnostics)
+static bool timing_on() {
+    static const bool on = std::getenv("MR_TIMING") != nullptr;
+    return on;
+}
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 static int fail(int code, const std::string &msg) {
     g_last_error = msg;
     return code;
@@ -143,14 +152,45 @@ struct mr_grid {
     // device copies of the region tables, uploaded on first use and shared by the
     // grid's plans (the grid outlives its plans)
     mutable uint32_t *d_near[4] = {nullptr, nullptr, nullptr, nullptr};
+    // device copies shared by the grid's plans on one device (the first plan's): the rank
+    // tables, and per (query homeland, HQ cell) the special / region word of every cell
+    // (sinfo: it depends on the special order, fixed by those two)
+    mutable int d_dev = -1;
+    mutable uint32_t *d_rank = nullptr, *d_rank_inv = nullptr;
+    struct SinfoDev {
+        uint32_t homeland, hq_v;
+        uint32_t *d;
+    };
+    mutable std::vector<SinfoDev> d_sinfo;
     ~mr_grid() {
         for (uint32_t *p : d_near)
             if (p) (void)hipFree(p);
+        for (uint32_t *p : {d_rank, d_rank_inv})
+            if (p) (void)hipFree(p);
+        for (const SinfoDev &e : d_sinfo) (void)hipFree(e.d);
     }
     int32_t gx(uint32_t v) const { return int32_t(v % S) - int32_t(H); }
     int32_t gy(uint32_t v) const { return int32_t(v / S) - int32_t(H); }
+    // The geometric layout (checked at creation): homeland cell (h, x, y) at vertex
+    // vc + x ux[h] + y uy[h], border cell (b, s) at vc + s ub[b]; find() computes the
+    // vertex and confirms it against idx[] (the hash map is the fallback).
+    bool fast = false;
+    int64_t ux[4] = {0, 0, 0, 0}, uy[4] = {0, 0, 0, 0}, ub[4] = {0, 0, 0, 0};
     bool find(const mr_cell_index &c, uint32_t &v) const {
         if (!canonical(c)) return false;
+        if (fast) {
+            int64_t w = -1;
+            if (c.kind == MR_CELL_CENTER) w = vc;
+            else if (c.kind == MR_CELL_HOMELAND && c.x <= H && c.y <= H) w = int64_t(vc) + c.x * ux[c.sub] + c.y * uy[c.sub];
+            else if (c.kind == MR_CELL_BORDER && c.x <= H) w = int64_t(vc) + c.x * ub[c.sub];
+            if (w >= 0 && w < int64_t(V)) {
+                const mr_cell_index &e = idx[size_t(w)];
+                if (e.kind == c.kind && e.sub == c.sub && e.x == c.x && e.y == c.y) {
+                    v = uint32_t(w);
+                    return true;
+                }
+            }
+        }
         auto it = index.find(ci_key(c));
         if (it == index.end()) return false;
         v = it->second;
@@ -217,6 +257,22 @@ extern "C" int mr_grid_create(const mr_cell *cells, uint32_t n, mr_grid **out) {
             delete g;
             return fail(MR_ERR_INVALID_GRID, "cell labels are not a consistent 4-grid at cell " + std::to_string(v));
         }
+    }
+    // the layout's unit steps per homeland and border (find()'s arithmetic path)
+    if (g->H >= 2) {
+        bool ok = true;
+        for (int h = 0; h < 4 && ok; ++h) {
+            uint32_t v11, v21, v12, vb;
+            ok = g->find(ci_make(MR_CELL_HOMELAND, uint8_t(h), 1, 1), v11) &&
+                 g->find(ci_make(MR_CELL_HOMELAND, uint8_t(h), 2, 1), v21) &&
+                 g->find(ci_make(MR_CELL_HOMELAND, uint8_t(h), 1, 2), v12) && g->find(build_border(h, 1), vb);
+            if (!ok) break;
+            g->ux[h] = int64_t(v21) - int64_t(v11);
+            g->uy[h] = int64_t(v12) - int64_t(v11);
+            g->ub[h] = int64_t(vb) - int64_t(vc);
+            ok = int64_t(v11) == int64_t(vc) + g->ux[h] + g->uy[h];
+        }
+        g->fast = ok;
     }
     // rank = position in the derived Ord of CellIndex (src/index.rs:41-46)
     {
@@ -459,7 +515,7 @@ namespace {
 
 struct HostPlan {
     DevParams p{};
-    std::vector<uint32_t> sinfo;
+    uint32_t homeland = 0, hq_v = 0xFFFFFFFFu;  // the key of the grid's shared sinfo (build_sinfo)
     std::vector<SpecialStatic> sp;
     std::vector<uint16_t> hubs;
     std::vector<uint32_t> src_v, q_begin, q_dst, q_id;
@@ -527,15 +583,21 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     p.use_caravans = prm->use_caravans ? 1 : 0;
     p.max_cmds = max_cmds;
     // specials: 1 Center, 2..5 border-1 cells, campfires, HQ
-    const uint32_t V = g->V;
-    std::vector<uint32_t> tix(V, kNone10);
+    std::unordered_map<uint32_t, uint32_t> tixm;  // vertex -> table entry of the specials
+    tixm.reserve(2 * g->campfires.size() + 16);
+    auto tix = [&](uint32_t v) {
+        auto it = tixm.find(v);
+        return it == tixm.end() ? kNone10 : it->second;
+    };
     std::vector<uint32_t> order;
     order.push_back(0);  // entry 0 = source (dynamic)
     auto add = [&](uint32_t v) {
-        if (tix[v] != kNone10) return tix[v];
-        tix[v] = uint32_t(order.size());
+        auto it = tixm.find(v);
+        if (it != tixm.end()) return it->second;
+        const uint32_t t = uint32_t(order.size());
+        tixm.emplace(v, t);
         order.push_back(v);
-        return tix[v];
+        return t;
     };
     add(g->vc);
     for (int b = 0; b < 4; ++b) {
@@ -557,7 +619,9 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     const uint32_t NS = uint32_t(order.size()) - 1;
     if (NS > kMaxSpecials) return fail(MR_ERR_LIMIT, "too many campfires (special table limit)");
     p.NS = NS;
-    p.hq_t = prm->has_hq ? tix[hq_v] : 0;
+    p.hq_t = prm->has_hq ? tix(hq_v) : 0;
+    hp.hq_v = hq_v;
+    hp.homeland = prm->homeland;
     const std::vector<uint32_t> &near = g->nearest[prm->homeland];
     hp.sp.assign(NS + 1, SpecialStatic{});
     hp.hubs.clear();
@@ -570,7 +634,7 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
         s.y = g->gy(v);
         bool is_cf = g->poi[v] == MR_POI_CAMPFIRE;
         s.flags = (t == 1 ? kSpCenter : 0u) | ((t >= 2 && t <= 5) ? kSpBorder1 : 0u) | ((t == 1 || is_cf) ? kSpHub : 0u);
-        s.region = near[v] == kNone32 ? kNone10 : tix[near[v]];
+        s.region = near[v] == kNone32 ? kNone10 : tix(near[v]);
         const mr_cell_index &c = g->idx[v];
         bool coef2 = c.kind == MR_CELL_CENTER || (c.kind == MR_CELL_HOMELAND && c.sub == prm->homeland);
         s.coef5 = coef2 ? 0u : 1u;
@@ -598,7 +662,7 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     const bool force_wide = fw && (!std::strcmp(fw, "1") || !std::strcmp(fw, "scan"));
     // the V x regions table (grid preprocessing, shared by the grid's plans) up to
     // 16 GB of HBM (c5: 8.6 GB); beyond it the wide kernel scans boundary cells
-    const bool table_ok = nregs <= 256 && size_t(V) * nregs * 8 <= (size_t(16) << 30) &&
+    const bool table_ok = nregs <= 256 && size_t(g->V) * nregs * 8 <= (size_t(16) << 30) &&
                           !(fw && !std::strcmp(fw, "scan"));
     const bool narrow_ok = NS <= 63 && nregs <= 63 && table_ok;
     hp.hub = hp.wide = hp.nonlin = false;
@@ -609,7 +673,7 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
         hp.hub = true;
         hp.nreg = uint32_t(regs->size());
         hp.near = &tab;
-        for (uint32_t r = 0; r < hp.nreg; ++r) hp.sp[tix[(*regs)[r]]].rid = r;
+        for (uint32_t r = 0; r < hp.nreg; ++r) hp.sp[tix((*regs)[r])].rid = r;
     } else if (linear && hub_wide_spl(NS) != 0 && nregs <= 256) {
         std::vector<uint32_t> regs;
         region_bounds(g, prm->homeland, regs, hp.rb_off, hp.rb_cell);
@@ -619,7 +683,7 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
         }
         hp.hub = hp.wide = true;
         hp.nreg = uint32_t(regs.size());
-        for (uint32_t r = 0; r < hp.nreg; ++r) hp.sp[tix[regs[r]]].rid = r;
+        for (uint32_t r = 0; r < hp.nreg; ++r) hp.sp[tix(regs[r])].rid = r;
         // the specials' rows (row 0, the source, is computed per source on the device)
         const uint32_t nr = hp.nreg;
         hp.near_sp.assign(size_t(NS + 1) * nr * 2, kNone32);
@@ -649,16 +713,17 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
             }
         }
     }
-    hp.sinfo.resize(V);
-    for (uint32_t v = 0; v < V; ++v) {
-        uint32_t r = near[v] == kNone32 ? kNone10 : tix[near[v]];
-        hp.sinfo[v] = (tix[v] & kNone10) | (r << 10);
-    }
-    // queries grouped by source (counting sort on the source vertex)
+    // queries grouped by source (counting sort on the source vertex; the V-sized
+    // counters are per-thread scratch, zero between plans)
+    const uint32_t V = g->V;
     hp.nq = n;
     hp.q_status.assign(n, MR_OK);
     std::vector<uint32_t> qs_src(n), qs_dst(n);
-    std::vector<uint32_t> count(V + 1, 0);
+    static thread_local std::vector<uint32_t> count, start;
+    if (count.size() < size_t(V) + 1) {
+        count.assign(size_t(V) + 1, 0);
+        start.assign(size_t(V) + 1, 0);
+    }
     for (uint32_t i = 0; i < n; ++i) {
         uint32_t a, b;
         if (!g->find(qs[i].from, a) || !g->find(qs[i].to, b)) {
@@ -672,7 +737,6 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     }
     hp.src_v.clear();
     hp.q_begin.clear();
-    std::vector<uint32_t> start(V, 0);
     uint32_t off = 0;
     for (uint32_t v = 0; v < V; ++v) {
         if (!count[v]) continue;
@@ -692,7 +756,60 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
         hp.q_id[k] = i;
         hp.q_pos[i] = k;  // the device writes query i's record at grouped position k
     }
+    for (uint32_t v : hp.src_v) count[v] = 0;
     return MR_OK;
+}
+
+// The special / region word of every cell for the plan's special table (sp[t].v) and
+// query homeland: sinfo[v] = table entry of v (kNone10) | entry of v's region campfire << 10.
+static std::vector<uint32_t> build_sinfo(const mr_grid *g, const HostPlan &hp) {
+    const uint32_t V = g->V;
+    std::vector<uint32_t> tix(V, kNone10), out(V);
+    for (uint32_t t = 1; t < hp.sp.size(); ++t) tix[hp.sp[t].v] = t;
+    const std::vector<uint32_t> &near = g->nearest[hp.homeland];
+    for (uint32_t v = 0; v < V; ++v) {
+        const uint32_t r = near[v] == kNone32 ? kNone10 : tix[near[v]];
+        out[v] = (tix[v] & kNone10) | (r << 10);
+    }
+    return out;
+}
+
+// The grid's shared device tables for a plan on device `dev`: rank, rank_inv and the
+// sinfo of (homeland, HQ), uploaded once; false when the grid's tables live on another
+// device (the plan then uploads its own).
+static bool grid_tables(const mr_grid *g, int dev, const HostPlan &hp, uint32_t *&rank, uint32_t *&rank_inv,
+                        uint32_t *&sinfo) {
+    std::lock_guard<std::mutex> lk(g->near_mu);
+    if (g->d_dev != -1 && g->d_dev != dev) return false;
+    auto up = [](uint32_t *&d, const std::vector<uint32_t> &h) {
+        if (hipMalloc(reinterpret_cast<void **>(&d), std::max<size_t>(h.size(), 1) * 4) != hipSuccess) return false;
+        if (!h.empty() && hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(d);
+            d = nullptr;
+            return false;
+        }
+        return true;
+    };
+    if (g->d_dev == -1) {
+        if (!up(g->d_rank, g->rank)) return false;
+        if (!up(g->d_rank_inv, g->rank_inv)) {
+            (void)hipFree(g->d_rank);
+            g->d_rank = nullptr;
+            return false;
+        }
+        g->d_dev = dev;
+    }
+    uint32_t *ds = nullptr;
+    for (const mr_grid::SinfoDev &e : g->d_sinfo)
+        if (e.homeland == hp.homeland && e.hq_v == hp.hq_v) ds = e.d;
+    if (!ds) {
+        if (g->d_sinfo.size() >= 8 || !up(ds, build_sinfo(g, hp))) return false;
+        g->d_sinfo.push_back(mr_grid::SinfoDev{hp.homeland, hp.hq_v, ds});
+    }
+    rank = g->d_rank;
+    rank_inv = g->d_rank_inv;
+    sinfo = ds;
+    return true;
 }
 
 #define HIPCHK(x)                                                                                   \
@@ -784,7 +901,8 @@ struct mr_plan {
     // streams instead)
     bool fused = false;
     uint32_t hub_lds = 0, fused_per_cu = 0;
-    uint32_t slot = 0;  // slot index of the d_* fields
+    uint32_t slot = 0;     // slot index of the d_* fields
+    bool own_tables = true;  // d_sinfo / d_rank / d_rank_inv: false = the grid's shared copies
     ~mr_plan() {
         if (!slots.empty()) {  // the d_* fields may name another slot: free each slot's once
             Slot &k = slots[0];
@@ -808,6 +926,7 @@ struct mr_plan {
                 if (e) (void)hipEventDestroy(e);
         }
         if (hub_stream) (void)hipStreamDestroy(hub_stream);
+        if (!own_tables) d_sinfo = d_rank = d_rank_inv = nullptr;  // the grid's
         for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_rank_inv, (void *)d_src, (void *)d_qb, (void *)d_qd,
                         (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
                         (void *)d_counter, (void *)d_args, (void *)d_dbg, (void *)d_args_fb, (void *)d_near,
@@ -953,9 +1072,12 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     if (!out || (n && !qs)) return fail(MR_ERR_INVALID_ARG, "null argument");
     *out = nullptr;
     if (!mr_device_available()) return fail(MR_ERR_NO_DEVICE, "no gfx950 device visible (no CPU fallback)");
+    const double tm0 = timing_on() ? now_ms() : 0.0;
+    double tm_build = 0, tm_upload = 0, tm_alloc = 0;
     auto pl = new mr_plan();
     pl->grid = g;
     int st = build_plan(g, prm, qs, n, max_cmds, pl->hp);
+    if (timing_on()) tm_build = now_ms();
     if (st != MR_OK) {
         delete pl;
         return st;
@@ -978,11 +1100,17 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         return code;
     };
     if (hipGetDevice(&pl->device) != hipSuccess) return bail(fail(MR_ERR_DEVICE, "hipGetDevice"));
-    if ((st = upload(pl->d_sinfo, hp.sinfo)) || (st = upload(pl->d_rank, g->rank)) ||
-        (st = upload(pl->d_rank_inv, g->rank_inv)) || (st = upload(pl->d_sp, hp.sp)) ||
+    if (grid_tables(g, pl->device, hp, pl->d_rank, pl->d_rank_inv, pl->d_sinfo)) {
+        pl->own_tables = false;
+    } else if ((st = upload(pl->d_sinfo, build_sinfo(g, hp))) || (st = upload(pl->d_rank, g->rank)) ||
+               (st = upload(pl->d_rank_inv, g->rank_inv))) {
+        return bail(st);
+    }
+    if ((st = upload(pl->d_sp, hp.sp)) ||
         (st = upload(pl->d_hubs, hp.hubs)) || (st = upload(pl->d_src, hp.src_v)) || (st = upload(pl->d_qb, hp.q_begin)) ||
         (st = upload(pl->d_qd, hp.q_dst)) || (st = upload(pl->d_qi, hp.q_id)))
         return bail(st);
+    if (timing_on()) tm_upload = now_ms();
     size_t nres = std::max<uint32_t>(n, 1);
     if (hipMalloc(reinterpret_cast<void **>(&pl->d_res), nres * sizeof(OutResult)) != hipSuccess ||
         hipMalloc(reinterpret_cast<void **>(&pl->d_cmd), nres * size_t(max_cmds) * sizeof(OutCmd)) != hipSuccess ||
@@ -1017,12 +1145,15 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     if (!pl->grid_in_lds) {
         const uint64_t slot_bytes = 5ull * V * 4ull;
         // HBM budget for solve slots; hub plans only solve the (few) fallback sources
-        const uint64_t budget = (hp.hub ? 8ull : 64ull) << 30;
+        // (a hub plan's slots serve the few sources its closed form cannot certify: 2 GB
+        // is ~95 slots at 1025^2 and ~6 at 4097^2, each looping over the sources)
+        const uint64_t budget = (hp.hub ? 2ull : 64ull) << 30;
         blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, budget / slot_bytes));
         if (hipMalloc(reinterpret_cast<void **>(&pl->d_ws), blocks * slot_bytes) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "hipMalloc workspace"));
     }
     pl->blocks = uint32_t(blocks);
+    if (timing_on()) tm_alloc = now_ms();
     if (hipStreamCreateWithFlags(&pl->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(MR_ERR_DEVICE, "stream"));
     KArgs &ka = pl->ka;
@@ -1192,6 +1323,9 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
             pl->fused = pl->fused_per_cu > 0;
         }
     }
+    if (timing_on())
+        std::fprintf(stderr, "MR_TIMING plan_create n=%u: build %.2f ms, upload %.2f, outputs+workspace %.2f, rest %.2f\n", n,
+                     tm_build - tm0, tm_upload - tm_build, tm_alloc - tm_upload, now_ms() - tm_alloc);
     *out = pl;
     return MR_OK;
 }
@@ -1694,17 +1828,69 @@ static int plan_collect(mr_plan *pl, std::vector<OutResult> &res, std::vector<Ou
     return MR_OK;
 }
 
+// the commands record k adds to the output pool (decode_record's `off` step)
+static uint32_t record_cmds(const OutResult &o) {
+    const int status = int(o.ncmd_status >> 16) - 16;
+    return (status == MR_OK || status == int(kStatusOverflow)) ? (o.ncmd_status & 0xFFFFu) : 0u;
+}
+
 extern "C" int mr_plan_fetch(mr_plan *pl, mr_result *results, mr_command *pool, uint64_t pool_cap) {
     if (!pl || (pl->hp.nq && !results)) return fail(MR_ERR_INVALID_ARG, "null argument");
+    const double tm0 = timing_on() ? now_ms() : 0.0;
     std::vector<OutResult> res;
     std::vector<OutCmd> cmd, ovf;
     int st = plan_collect(pl, res, cmd, ovf);
     if (st != MR_OK) return st;
+    const double tm1 = timing_on() ? now_ms() : 0.0;
     const HostPlan &hp = pl->hp;
     const CmdScale cs = cmd_scale(hp);
     const uint32_t mc = hp.p.max_cmds;
     uint64_t off = 0;
     int ret = MR_OK;
+    // Large batches decode on host threads: each query's pool offset is the prefix sum
+    // of the commands before it, so chunks write disjoint pool ranges; the first error
+    // status in query order is the one returned, as in the serial loop below.
+    const uint32_t nthr = std::min<uint32_t>(16, std::max(1u, std::thread::hardware_concurrency() / 2));
+    if (hp.nq >= 65536 && nthr > 1 && pool) {
+        std::vector<uint64_t> first(hp.nq + 1, 0);
+        for (uint32_t i = 0; i < hp.nq; ++i)
+            first[i + 1] = first[i] + (hp.q_status[i] == MR_OK ? record_cmds(res[hp.q_pos[i]]) : 0u);
+        if (first[hp.nq] <= pool_cap) {
+            std::vector<int> rets(nthr, MR_OK), errs(nthr, MR_OK);
+            std::vector<std::string> msgs(nthr);
+            std::vector<std::thread> th;
+            const uint32_t chunk = (hp.nq + nthr - 1) / nthr;
+            for (uint32_t t = 0; t < nthr; ++t)
+                th.emplace_back([&, t]() {
+                    const uint32_t a = t * chunk, b = std::min(hp.nq, a + chunk);
+                    uint64_t o = first[std::min(a, hp.nq)];
+                    for (uint32_t i = a; i < b; ++i) {
+                        mr_result &r = results[i];
+                        if (hp.q_status[i] != MR_OK) {
+                            std::memset(&r, 0, sizeof(r));
+                            r.status = hp.q_status[i];
+                            if (rets[t] == MR_OK) rets[t] = hp.q_status[i];
+                            continue;
+                        }
+                        const uint32_t k = hp.q_pos[i];
+                        if (int e = decode_record(pl->grid, cs, res[k], mc ? &cmd[size_t(k) * mc] : nullptr, mc, ovf.data(),
+                                                  ovf.size(), r, pool, pool_cap, o, rets[t])) {
+                            errs[t] = e;
+                            msgs[t] = g_last_error;  // (thread-local)
+                            return;
+                        }
+                    }
+                });
+            for (auto &x : th) x.join();
+            for (uint32_t t = 0; t < nthr; ++t)
+                if (errs[t] != MR_OK) return fail(errs[t], msgs[t]);
+            for (uint32_t t = 0; t < nthr && ret == MR_OK; ++t) ret = rets[t];
+            if (timing_on())
+                std::fprintf(stderr, "MR_TIMING fetch n=%u: collect %.2f ms, decode %.2f ms (%u threads)\n", hp.nq, tm1 - tm0,
+                             now_ms() - tm1, nthr);
+            return ret;
+        }
+    }
     for (uint32_t i = 0; i < hp.nq; ++i) {
         mr_result &r = results[i];
         if (hp.q_status[i] != MR_OK) {
