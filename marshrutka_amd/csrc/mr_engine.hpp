@@ -131,6 +131,7 @@ struct KArgs {
     const uint32_t *sinfo;       // V words: special idx (10b) | region idx << 10
     const uint32_t *rank;        // V words: position in CellIndex order
     const uint32_t *rank_inv;    // V words: vertex of each rank
+    const uint2 *cell;           // V x {sinfo, rank}: one line per random cell read (hub_lane_kernel)
     const SpecialStatic *sp;     // NS+1 entries
     const uint16_t *hubs;        // n_hubs caravan endpoints (table indices)
     const uint32_t *src_v;       // nsrc source vertices

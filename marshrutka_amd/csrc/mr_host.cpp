@@ -160,6 +160,7 @@ struct mr_grid {
     struct SinfoDev {
         uint32_t homeland, hq_v;
         uint32_t *d;
+        uint2 *cell;  // {sinfo, rank} per cell
     };
     mutable std::vector<SinfoDev> d_sinfo;
     ~mr_grid() {
@@ -167,7 +168,10 @@ struct mr_grid {
             if (p) (void)hipFree(p);
         for (uint32_t *p : {d_rank, d_rank_inv})
             if (p) (void)hipFree(p);
-        for (const SinfoDev &e : d_sinfo) (void)hipFree(e.d);
+        for (const SinfoDev &e : d_sinfo) {
+            (void)hipFree(e.d);
+            (void)hipFree(e.cell);
+        }
     }
     int32_t gx(uint32_t v) const { return int32_t(v % S) - int32_t(H); }
     int32_t gy(uint32_t v) const { return int32_t(v / S) - int32_t(H); }
@@ -777,8 +781,15 @@ static std::vector<uint32_t> build_sinfo(const mr_grid *g, const HostPlan &hp) {
 // The grid's shared device tables for a plan on device `dev`: rank, rank_inv and the
 // sinfo of (homeland, HQ), uploaded once; false when the grid's tables live on another
 // device (the plan then uploads its own).
+// {sinfo, rank} per cell (hub_lane_kernel reads both words of a cell in one line)
+static std::vector<uint2> build_cell(const mr_grid *g, const std::vector<uint32_t> &sinfo) {
+    std::vector<uint2> out(sinfo.size());
+    for (size_t v = 0; v < sinfo.size(); ++v) out[v] = make_uint2(sinfo[v], g->rank[v]);
+    return out;
+}
+
 static bool grid_tables(const mr_grid *g, int dev, const HostPlan &hp, uint32_t *&rank, uint32_t *&rank_inv,
-                        uint32_t *&sinfo) {
+                        uint32_t *&sinfo, uint2 *&cell) {
     std::lock_guard<std::mutex> lk(g->near_mu);
     if (g->d_dev != -1 && g->d_dev != dev) return false;
     auto up = [](uint32_t *&d, const std::vector<uint32_t> &h) {
@@ -800,15 +811,32 @@ static bool grid_tables(const mr_grid *g, int dev, const HostPlan &hp, uint32_t 
         g->d_dev = dev;
     }
     uint32_t *ds = nullptr;
+    uint2 *dc = nullptr;
     for (const mr_grid::SinfoDev &e : g->d_sinfo)
-        if (e.homeland == hp.homeland && e.hq_v == hp.hq_v) ds = e.d;
+        if (e.homeland == hp.homeland && e.hq_v == hp.hq_v) {
+            ds = e.d;
+            dc = e.cell;
+        }
     if (!ds) {
-        if (g->d_sinfo.size() >= 8 || !up(ds, build_sinfo(g, hp))) return false;
-        g->d_sinfo.push_back(mr_grid::SinfoDev{hp.homeland, hp.hq_v, ds});
+        if (g->d_sinfo.size() >= 8) return false;
+        const std::vector<uint32_t> si = build_sinfo(g, hp);
+        if (!up(ds, si)) return false;
+        const std::vector<uint2> ce = build_cell(g, si);
+        if (hipMalloc(reinterpret_cast<void **>(&dc), std::max<size_t>(ce.size(), 1) * sizeof(uint2)) != hipSuccess) {
+            (void)hipFree(ds);
+            return false;
+        }
+        if (!ce.empty() && hipMemcpy(dc, ce.data(), ce.size() * sizeof(uint2), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(ds);
+            (void)hipFree(dc);
+            return false;
+        }
+        g->d_sinfo.push_back(mr_grid::SinfoDev{hp.homeland, hp.hq_v, ds, dc});
     }
     rank = g->d_rank;
     rank_inv = g->d_rank_inv;
     sinfo = ds;
+    cell = dc;
     return true;
 }
 
@@ -902,7 +930,8 @@ struct mr_plan {
     bool fused = false;
     uint32_t hub_lds = 0, fused_per_cu = 0;
     uint32_t slot = 0;     // slot index of the d_* fields
-    bool own_tables = true;  // d_sinfo / d_rank / d_rank_inv: false = the grid's shared copies
+    bool own_tables = true;  // d_sinfo / d_rank / d_rank_inv / d_cell: false = the grid's shared copies
+    uint2 *d_cell = nullptr;
     ~mr_plan() {
         if (!slots.empty()) {  // the d_* fields may name another slot: free each slot's once
             Slot &k = slots[0];
@@ -926,7 +955,11 @@ struct mr_plan {
                 if (e) (void)hipEventDestroy(e);
         }
         if (hub_stream) (void)hipStreamDestroy(hub_stream);
-        if (!own_tables) d_sinfo = d_rank = d_rank_inv = nullptr;  // the grid's
+        if (!own_tables) {  // the grid's
+            d_sinfo = d_rank = d_rank_inv = nullptr;
+            d_cell = nullptr;
+        }
+        if (d_cell) (void)hipFree(d_cell);
         for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_rank_inv, (void *)d_src, (void *)d_qb, (void *)d_qd,
                         (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
                         (void *)d_counter, (void *)d_args, (void *)d_dbg, (void *)d_args_fb, (void *)d_near,
@@ -1100,11 +1133,13 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         return code;
     };
     if (hipGetDevice(&pl->device) != hipSuccess) return bail(fail(MR_ERR_DEVICE, "hipGetDevice"));
-    if (grid_tables(g, pl->device, hp, pl->d_rank, pl->d_rank_inv, pl->d_sinfo)) {
+    if (grid_tables(g, pl->device, hp, pl->d_rank, pl->d_rank_inv, pl->d_sinfo, pl->d_cell)) {
         pl->own_tables = false;
-    } else if ((st = upload(pl->d_sinfo, build_sinfo(g, hp))) || (st = upload(pl->d_rank, g->rank)) ||
-               (st = upload(pl->d_rank_inv, g->rank_inv))) {
-        return bail(st);
+    } else {
+        const std::vector<uint32_t> si = build_sinfo(g, hp);
+        if ((st = upload(pl->d_sinfo, si)) || (st = upload(pl->d_cell, build_cell(g, si))) ||
+            (st = upload(pl->d_rank, g->rank)) || (st = upload(pl->d_rank_inv, g->rank_inv)))
+            return bail(st);
     }
     if ((st = upload(pl->d_sp, hp.sp)) ||
         (st = upload(pl->d_hubs, hp.hubs)) || (st = upload(pl->d_src, hp.src_v)) || (st = upload(pl->d_qb, hp.q_begin)) ||
@@ -1161,6 +1196,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     ka.sinfo = pl->d_sinfo;
     ka.rank = pl->d_rank;
     ka.rank_inv = pl->d_rank_inv;
+    ka.cell = pl->d_cell;
     ka.sp = pl->d_sp;
     ka.hubs = pl->d_hubs;
     ka.src_v = pl->d_src;

@@ -149,6 +149,7 @@ struct LaneHub {
     const uint2 *PB;           // LDS: pair table, SoE-region words
     const uint32_t *RM;        // LDS: per row, the entries with a SoE-region candidate
     const uint32_t *rank, *sinfo, *rank_inv;
+    const uint2 *cell;  // {sinfo, rank} per cell: the source's and destinations' words in one line
     uint32_t *counter;
     uint32_t nreg;
     uint32_t hubm, c5m, regm;  // entries that are caravan hubs / cost 5 per unit to reach / region campfires
@@ -433,10 +434,11 @@ struct LaneHub {
         const DevParams &p = P;
         const uint32_t NS = p.NS;
         src = a->src_v[s_idx];
-        src_rk = rank[src];
+        const uint2 sc = cell[src];  // {sinfo, rank}
+        src_rk = sc.y;
         sx = int(src % p.S) - int(p.H);
         sy = int(src / p.S) - int(p.H);
-        ts = sinfo[src] & kNone10;
+        ts = sc.x & kNone10;
         srow = reinterpret_cast<const uint2 *>(a->near) + (unsigned long long)src * nreg;
         // the source's own edges, in command-kind order: its start label if it is a
         // special, the walks from it, the SoE edges from its region rows, SHQ, SFm
@@ -603,8 +605,9 @@ struct LaneHub {
         const bool walk0 = src != p.vc;
         for (uint32_t qi = fb_sp ? qb : qa; qi < qb; ++qi) {
             const uint32_t w = a->q_dst[qi];
-            const uint32_t tw = sinfo[w] & kNone10;
-            const uint32_t wr = rank[w];
+            const uint2 wc = cell[w];
+            const uint32_t tw = wc.x & kNone10;
+            const uint32_t wr = wc.y;
             if (w == src) {
                 emit(st0, kOwn, Own{sx, sy, src_rk, kNone10, 0u}, qi);
                 continue;
@@ -743,6 +746,7 @@ __global__ __launch_bounds__(kBS, MR_LANE_WAVES) void hub_lane_kernel(const KArg
     H.rank = a->rank;
     H.sinfo = a->sinfo;
     H.rank_inv = a->rank_inv;
+    H.cell = a->cell;
     H.counter = a->counter;
     H.nreg = nreg;
     uint32_t hubm = 0, c5m = 0, regm = 0;
