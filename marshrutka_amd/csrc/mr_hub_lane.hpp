@@ -47,9 +47,12 @@
 
 namespace mr {
 
+// waves per SIMD the register budget is cut for: two for the 22-entry table (256
+// VGPRs, no spill), one for 24 and 32 entries (256 VGPRs + AGPRs, no scratch)
 #ifndef MR_LANE_WAVES
-#define MR_LANE_WAVES 2  // waves per SIMD the register budget is cut for
+#define MR_LANE_WAVES 2
 #endif
+__host__ __device__ constexpr uint32_t lane_waves(uint32_t TM) { return TM <= 22 ? MR_LANE_WAVES : 1u; }
 // a scheduling fence between the unrolled entries, so the scheduler does not
 // interleave all of them and run out of registers
 #ifndef MR_LANE_NOFENCE
@@ -695,7 +698,7 @@ __host__ __device__ inline uint32_t lane_lds_total(uint32_t NS, uint32_t nreg, u
 }
 
 template <uint32_t PERM, uint32_t TM>
-__global__ __launch_bounds__(kBS, MR_LANE_WAVES) void hub_lane_kernel(const KArgs *__restrict__ a) {
+__global__ __launch_bounds__(kBS, lane_waves(TM)) void hub_lane_kernel(const KArgs *__restrict__ a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint32_t NS = a->p.NS, nreg = a->nreg;
     SpecialStatic *spl = reinterpret_cast<SpecialStatic *>(smem);

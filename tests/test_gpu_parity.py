@@ -191,6 +191,24 @@ def test_lane_kernel_selection(eng, oracle_lib, monkeypatch):
     assert lanes["force"] == n_src and lanes["min1"] == n_src, lanes
 
 
+@pytest.mark.parametrize("k,hq,tm", [(4, True, 24), (5, False, 32), (6, True, 32)])
+def test_lane_kernel_wide_tables(eng, oracle_lib, monkeypatch, k, hq, tm):
+    """hub_lane_kernel with the 24- and 32-entry tables (one wave per SIMD): maps with
+    k campfires per homeland (+ HQ) put NS = 5 + 4k (+1) specials in registers; every
+    comparator order, against the oracle."""
+    monkeypatch.setenv("MR_HUB_LANE", "1")
+    m = SyntheticMap(41, campfires_per_homeland=k, seed=40 + k)
+    qs = random_queries(m, 300, k)
+    g = eng.MapGrid(m.cells())
+    extra = {"hq_position": m.campfires()[-1]} if hq else {}
+    for sort_by in ((0, 2), (1, 2), (2, 0), (1, 0)):
+        params = Params(sort_by=sort_by, **extra)
+        pl = eng.Plan(g, params, qs)
+        st = pl.stats()
+        assert st["num_specials"] + 1 <= tm and st["lane_sources"] == st["num_sources"], st
+        check(eng, oracle_lib, m, params, qs, f"k={k} hq={hq} {sort_by}")
+
+
 def test_fallback_sources_reported(eng, oracle_lib, monkeypatch):
     """mr_plan_fallback_sources: the sources a pass re-solved with the SSSP kernel —
     none on a plain hub pass, every source with MR_HUB_FALLBACK_ALL=1 (the cost signal
