@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MR_ABI_VERSION 5u
+#define MR_ABI_VERSION 6u
 
 /* ---- status codes ------------------------------------------------------ */
 typedef enum mr_status {
@@ -267,6 +267,8 @@ typedef struct mr_plan_stats {
     uint32_t fill_launch;       /* all-destinations hub plans: MR_FILL_* (how the fill is launched) */
     uint32_t lane_sources;      /* hub solver: sources solved one per lane (hub_lane_kernel); the rest
                                    (more than 32 queries each) a lane per query (ABI 5) */
+    uint32_t certified_sources; /* of fallback_sources, those answered by the fixed-point certificate
+                                   in the last pass (the rest ran the SSSP kernel; ABI 6) */
 } mr_plan_stats;
 enum {
     MR_FILL_NONE = 0,    /* not an all-destinations hub plan */

@@ -79,7 +79,8 @@ class mr_plan_stats(C.Structure):
                 ("fallback_sources", C.c_uint32), ("num_specials", C.c_uint32), ("num_regions", C.c_uint32),
                 ("hub_workgroups", C.c_uint32), ("sssp_workgroups", C.c_uint32),
                 ("specials_per_lane", C.c_uint32), ("region_boundary_cells", C.c_uint32),
-                ("fill_launch", C.c_uint32), ("lane_sources", C.c_uint32)]
+                ("fill_launch", C.c_uint32), ("lane_sources", C.c_uint32),
+                ("certified_sources", C.c_uint32)]
 
 
 assert C.sizeof(mr_cell_index) == 8

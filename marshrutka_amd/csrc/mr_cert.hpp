@@ -1,0 +1,316 @@
+// mr_cert.hpp — certified fallback: the fixed-point check and the
+// sorted repair sweep over a certificate slot's cell words.
+//
+// A hub source whose closed form the hub kernel cannot certify (hub_kernel, query mode)
+// exports its label table into a slot; the fill writes every cell's closed-form word
+// (the best geodesic walk over its boundaries, any run time).  Call that assignment C.
+// The reference's labels L are the unique fixed point of L(v) = min over in-edges
+// extend(L(u), u -> v) with L(src) = start (every edge raises (metrics, length), so a
+// least discrepancy cannot exist).  The check tests, at every cell v,
+//   pull: C(v) is the extension of some in-neighbour's C (or a special's own label that
+//         the hub's exact Dijkstra over the specials built from another special), and
+//   push: no in-neighbour's extension is smaller than C(v),
+// and the slot's key is the least leading metric c1 of min(C(v), best extension) over
+// the cells that fail.  Induction on the least discrepancy w (by min(C(w), L(w))) shows
+// that every label with c1 below the key is the reference's: a discrepancy there
+// fails one of the two tests at w with a smaller key.  The in-edges of a plain cell are
+// the StandardMoves from its grid neighbours; those of a special also come from other
+// specials (built by the hub's Dijkstra, so pull and push hold by construction) and from
+// scrolls (SoE from a region, SHQ, SFm: the least extension is the region's least C, or
+// the source's, which the hub's candidates are).
+//
+// Where the closed form is wrong (Fleetfoot 1-2: the ceil makes two boundaries' time
+// gap alternate by a second, so the winner alternates cell by cell in a band, and the
+// reference settles the band in label order), the sweep recomputes the failing cells'
+// bounding box (plus a margin) in one pass in order of their leading metric, in
+// buckets of the least StandardMove increment (cells of one bucket cannot extend one
+// another): each cell from its neighbours' current words.  The check then runs again.
+#pragma once
+#include "mr_device.hpp"
+
+namespace mr {
+
+// per table entry of a slot (LDS): metrics, length, boundary rank (kNone32: not a
+// boundary), and for a walk label its boundary and run length
+struct CertEntry {
+    uint32_t m0, m1, m2, len, lex, wb, wk, pad;
+};
+// a walk label (b, k) as comparator keys: c1..c3 in comparator order, length, rank of b
+struct CertLab {
+    uint32_t c1, c2, c3, len, lex, b, k;
+};
+constexpr uint32_t kCertNoB = 0xFFFFu;
+
+__device__ __forceinline__ bool cert_less(const CertLab &x, const CertLab &y) {
+    if (x.c1 != y.c1) return x.c1 < y.c1;
+    if (x.c2 != y.c2) return x.c2 < y.c2;
+    if (x.c3 != y.c3) return x.c3 < y.c3;
+    if (x.len != y.len) return x.len < y.len;
+    return x.lex < y.lex;
+}
+__device__ __forceinline__ bool cert_same(const CertLab &x, const CertLab &y) {
+    return x.c1 == y.c1 && x.c2 == y.c2 && x.c3 == y.c3 && x.len == y.len && x.lex == y.lex;
+}
+__device__ __forceinline__ uint32_t pick(const DevParams &p, int i, uint32_t m0, uint32_t m1, uint32_t m2) {
+    const uint32_t q = p.perm[i];
+    return q == 0 ? m0 : (q == 1 ? m1 : m2);
+}
+// walk(b, k): b's label + k legs, its money, the run's time; the list is b's + one command
+__device__ __forceinline__ CertLab cert_walk(const DevParams &p, const CertEntry *E, uint32_t b, uint32_t k) {
+    const CertEntry &e = E[b];
+    const uint32_t m0 = e.m0 + k, m1 = e.m1, m2 = e.m2 + run_time_ff(k, p.ff_num, p.ff_den);
+    return CertLab{pick(p, 0, m0, m1, m2), pick(p, 1, m0, m1, m2), pick(p, 2, m0, m1, m2), b == 0 ? 1u : e.len + 1u,
+                   e.lex, b, k};
+}
+// the extension by one StandardMove of the label in cell word w (false: not a walk source)
+__device__ __forceinline__ bool cert_ext(const DevParams &p, const CertEntry *E, uint32_t w, CertLab &x) {
+    if (w == kViaSource) {
+        x = cert_walk(p, E, 0, 1);
+        return true;
+    }
+    if (w & kViaSpecial) {
+        const uint32_t t = w & kNone10;
+        if (E[t].wb != kCertNoB) {  // a walk: the run merges
+            x = cert_walk(p, E, E[t].wb, E[t].wk + 1);
+            return true;
+        }
+        if (E[t].lex == kNone32) return false;
+        x = cert_walk(p, E, t, 1);
+        return true;
+    }
+    x = cert_walk(p, E, (w >> kStBShift) & kNone10, (w & kStKMask) + 1);
+    return true;
+}
+// a slot's table into LDS (every thread of the block takes part)
+__device__ __forceinline__ void cert_load_table(const KArgs *__restrict__ a, uint32_t slot, CertEntry *E) {
+    const uint32_t T = a->p.NS + 1;
+    for (uint32_t t = threadIdx.x; t < T; t += blockDim.x) {
+        const Rec r = a->cert_tab[(unsigned long long)slot * T + t];
+        const bool walk = r.ntail() == 1 && (r.kp0 >> 29) == kStandard && t != 0;
+        E[t] = CertEntry{r.m[0], r.m[1], r.m[2], r.len(), a->cert_lex[(unsigned long long)slot * T + t],
+                         walk ? r.parent() : kCertNoB, walk ? (r.kp0 & 0x1FFFFFFFu) : 0u, 0u};
+    }
+}
+
+// the least extension of cell (x, y)'s grid neighbours (the Center has none); false when
+// a neighbour's label cannot be extended here (counted as a failure)
+template <bool ATOMIC>
+__device__ __forceinline__ bool cert_best4(const DevParams &p, const CertEntry *E, const CellWord *w, uint32_t pitch,
+                                           int x, int y, CertLab &best, bool &any) {
+    const int S = int(p.S), H = int(p.H);
+    any = false;
+    bool ok = true;
+    const int nx[4] = {x - 1, x + 1, x, x}, ny[4] = {y, y, y - 1, y + 1};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (nx[i] < 0 || nx[i] >= S || ny[i] < 0 || ny[i] >= S || (nx[i] == H && ny[i] == H)) continue;
+        const CellWord *pw = w + (size_t)ny[i] * pitch + nx[i];
+        const uint32_t wu = ATOMIC ? __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *pw;
+        CertLab c;
+        if (!cert_ext(p, E, wu, c)) {
+            ok = false;
+            continue;
+        }
+        if (!any || cert_less(c, best)) best = c;
+        any = true;
+    }
+    return ok;
+}
+
+// One launch over every slot's cells (blockIdx.y = slot): failing cells lower the slot's
+// key, count, and widen its box.
+__global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict__ a) {
+    __shared__ CertEntry E[64];
+    const uint32_t slot = blockIdx.y;
+    const uint32_t nslot = min(a->cert_cap, __hip_atomic_load(a->counter + kCtrCert, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT));
+    if (slot >= nslot) return;
+    const DevParams p = a->p;
+    cert_load_table(a, slot, E);
+    __syncthreads();
+    const uint32_t S = p.S, pitch = a->rec_pitch;
+    const CellWord *w = a->cert_rec + (unsigned long long)slot * S * pitch;
+    uint32_t key = 0xFFFFFFFFu, nf = 0, x0 = 0xFFFFFFFFu, x1 = 0, y0 = 0xFFFFFFFFu, y1 = 0;
+    for (uint32_t v = blockIdx.x * kBS + threadIdx.x; v < p.V; v += gridDim.x * kBS) {
+        const uint32_t y = v / S, x = v - y * S;
+        const uint32_t cw = w[(size_t)y * pitch + x];
+        if (cw == kViaSource || v == p.vc) continue;
+        CertLab best{};
+        bool any;
+        bool fail = !cert_best4<false>(p, E, w, pitch, int(x), int(y), best, any);
+        uint32_t own1;
+        if (cw & kViaSpecial) {
+            const uint32_t t = cw & kNone10;
+            const CertEntry &e = E[t];
+            if (e.wb != kCertNoB) {  // a walk into a special: supported by a neighbour, beaten by none
+                const CertLab o = cert_walk(p, E, e.wb, e.wk);
+                own1 = o.c1;
+                fail = fail || !any || !cert_same(o, best);
+            } else {  // built over the specials: no neighbour's walk may reach it first (a tie on
+                      // metrics and length would need the command lists: counted as a failure)
+                const uint32_t o1 = pick(p, 0, e.m0, e.m1, e.m2), o2 = pick(p, 1, e.m0, e.m1, e.m2),
+                               o3 = pick(p, 2, e.m0, e.m1, e.m2);
+                own1 = o1;
+                const bool below = o1 != best.c1 ? o1 < best.c1
+                                                 : (o2 != best.c2 ? o2 < best.c2 : (o3 != best.c3 ? o3 < best.c3 : e.len < best.len));
+                fail = fail || (any && !below);
+            }
+        } else {  // a plain cell: exactly its neighbours' least extension
+            const CertLab o = cert_walk(p, E, (cw >> kStBShift) & kNone10, cw & kStKMask);
+            own1 = o.c1;
+            fail = fail || !any || !cert_same(o, best);
+        }
+        if (fail) {
+            key = min(key, any ? min(own1, best.c1) : own1);
+            ++nf;
+            x0 = min(x0, x);
+            x1 = max(x1, x);
+            y0 = min(y0, y);
+            y1 = max(y1, y);
+        }
+    }
+    // one atomic per wave and field
+    if (__any(nf != 0)) {
+        key = wave_min_u32(key);
+        x0 = wave_min_u32(x0);
+        y0 = wave_min_u32(y0);
+        x1 = ~wave_min_u32(~x1);
+        y1 = ~wave_min_u32(~y1);
+        uint32_t n = nf;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) n += uint32_t(__shfl_xor(int(n), o));
+        if (lane_id() == 0) {
+            uint32_t *st = a->cert_st + slot * kCertSt;
+            atomicMin(st + kCertKey, key);
+            atomicAdd(st + kCertFails, n);
+            atomicMin(st + kCertX0, x0);
+            atomicMax(st + kCertX1, x1);
+            atomicMin(st + kCertY0, y0);
+            atomicMax(st + kCertY1, y1);
+        }
+    }
+}
+
+constexpr uint32_t kSweepBS = 1024;      // threads of the sweep's one workgroup per slot
+constexpr uint32_t kSweepBuckets = 16384;  // leading-metric buckets a window may span
+constexpr int kSweepMargin = 2;            // cells added round the failing cells' box
+
+// One workgroup per slot: the failing box (+ margin) in order of the leading metric of its
+// current words, bucket by bucket, each cell from its neighbours; then the slot's check
+// state is reset for the next check.  Words are read past L1 (agent-scope loads) so a
+// bucket sees the previous one's stores.
+__global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__restrict__ a) {
+    __shared__ CertEntry E[64];
+    __shared__ uint32_t off[kSweepBuckets];
+    __shared__ uint32_t red[2];
+    const uint32_t slot = blockIdx.x, tid = threadIdx.x;
+    const uint32_t nslot = min(a->cert_cap, __hip_atomic_load(a->counter + kCtrCert, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT));
+    if (slot >= nslot) return;
+    uint32_t *st = a->cert_st + slot * kCertSt;
+    if (st[kCertFails] == 0) return;  // certified as it stands
+    const DevParams p = a->p;
+    cert_load_table(a, slot, E);
+    if (tid == 0) {
+        red[0] = 0xFFFFFFFFu;
+        red[1] = 0;
+    }
+    const int S = int(p.S);
+    const int bx0 = max(0, int(st[kCertX0]) - kSweepMargin), bx1 = min(S - 1, int(st[kCertX1]) + kSweepMargin);
+    const int by0 = max(0, int(st[kCertY0]) - kSweepMargin), by1 = min(S - 1, int(st[kCertY1]) + kSweepMargin);
+    const uint32_t bw = uint32_t(bx1 - bx0 + 1), area = bw * uint32_t(by1 - by0 + 1);
+    const uint32_t pitch = a->rec_pitch;
+    CellWord *w = a->cert_rec + (unsigned long long)slot * p.S * pitch;
+    uint32_t *list = a->cert_aux + (unsigned long long)slot * p.V;
+    // the leading metric: the first in comparator order that grows along a walk; its least
+    // StandardMove increment is the bucket width
+    const uint32_t L = p.perm[0] != 1u ? p.perm[0] : p.perm[1];
+    const uint32_t W = L == 0 ? 1u : max(1u, p.W);
+    auto lead_of = [&](uint32_t cw) {
+        const uint32_t b = (cw >> kStBShift) & kNone10, k = cw & kStKMask;
+        return L == 0 ? E[b].m0 + k : E[b].m2 + run_time_ff(k, p.ff_num, p.ff_den);
+    };
+    auto plain_word = [&](uint32_t cw) { return cw != kViaSource && !(cw & kViaSpecial); };
+    __syncthreads();
+    // the window's key range
+    uint32_t kmin = 0xFFFFFFFFu, kmax = 0;
+    for (uint32_t i = tid; i < area; i += kSweepBS) {
+        const uint32_t y = uint32_t(by0) + i / bw, x = uint32_t(bx0) + i % bw;
+        const uint32_t cw = w[(size_t)y * pitch + x];
+        if (!plain_word(cw)) continue;
+        const uint32_t kk = lead_of(cw) / W;
+        kmin = min(kmin, kk);
+        kmax = max(kmax, kk);
+    }
+    kmin = wave_min_u32(kmin);
+    kmax = ~wave_min_u32(~kmax);
+    if (lane_id() == 0) {
+        atomicMin(&red[0], kmin);
+        atomicMax(&red[1], kmax);
+    }
+    __syncthreads();
+    kmin = red[0];
+    kmax = red[1];
+    const uint32_t nb = kmax >= kmin ? kmax - kmin + 1 : 0;
+    if (nb == 0 || nb > kSweepBuckets) return;  // nothing to sweep / too wide: left to the SSSP kernel
+    for (uint32_t j = tid; j < nb; j += kSweepBS) off[j] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < area; i += kSweepBS) {
+        const uint32_t y = uint32_t(by0) + i / bw, x = uint32_t(bx0) + i % bw;
+        const uint32_t cw = w[(size_t)y * pitch + x];
+        if (plain_word(cw)) atomicAdd(&off[lead_of(cw) / W - kmin], 1u);
+    }
+    __syncthreads();
+    // exclusive prefix sum of the counts (each thread a run of buckets, then the runs)
+    {
+        const uint32_t per = (nb + kSweepBS - 1) / kSweepBS, j0 = tid * per, j1 = min(nb, j0 + per);
+        uint32_t sum = 0;
+        for (uint32_t j = j0; j < j1; ++j) sum += off[j];
+        // block scan of the run sums through LDS (the histogram's tail is free past nb;
+        // a second small array avoids aliasing it)
+        __shared__ uint32_t runs[kSweepBS];
+        runs[tid] = sum;
+        __syncthreads();
+        for (uint32_t d = 1; d < kSweepBS; d <<= 1) {
+            const uint32_t v = tid >= d ? runs[tid - d] : 0u;
+            __syncthreads();
+            runs[tid] += v;
+            __syncthreads();
+        }
+        uint32_t acc = runs[tid] - sum;
+        for (uint32_t j = j0; j < j1; ++j) {
+            const uint32_t c = off[j];
+            off[j] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < area; i += kSweepBS) {
+        const uint32_t y = uint32_t(by0) + i / bw, x = uint32_t(bx0) + i % bw;
+        const uint32_t cw = w[(size_t)y * pitch + x];
+        if (plain_word(cw)) list[atomicAdd(&off[lead_of(cw) / W - kmin], 1u)] = y * p.S + x;
+    }
+    __syncthreads();
+    // off[j] now ends bucket j.  Bucket by bucket: each cell takes its neighbours' least
+    // extension (a cell of this bucket never extends another of it).
+    for (uint32_t j = 0; j < nb; ++j) {
+        const uint32_t beg = j ? off[j - 1] : 0u, end = off[j];
+        if (beg == end) continue;
+        for (uint32_t i = beg + tid; i < end; i += kSweepBS) {
+            const uint32_t v = list[i], y = v / p.S, x = v - y * p.S;
+            CertLab best{};
+            bool any;
+            cert_best4<true>(p, E, w, pitch, int(x), int(y), best, any);
+            if (!any) continue;
+            CellWord *pw = w + (size_t)y * pitch + x;
+            const uint32_t nw = (best.b << kStBShift) | best.k;
+            if (__hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != nw)
+                __hip_atomic_store(pw, nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+    }
+    // the next check starts from an empty state
+    if (tid < kCertSt) st[tid] = (tid == kCertKey || tid == kCertX0 || tid == kCertY0) ? 0xFFFFFFFFu : 0u;
+}
+
+}  // namespace mr

@@ -50,6 +50,7 @@ struct Shared {
     uint32_t lb;            // generic: list rotation base / legs: current frontier buffer
     uint32_t nd;            // generic: dirty count
     uint32_t sidx;
+    uint32_t sslot;         // fallback launch: the source's certificate slot (kNone32: none)
     uint32_t done;
     uint32_t L;             // legs: current level
     uint32_t nbnd;          // legs: number of boundaries
@@ -849,6 +850,44 @@ struct Core {
         }
         if (threadIdx.x == 0) a->src_state[s_idx] = 2;
     }
+    // Certified fallback: the label of vertex d from certificate
+    // slot words w (the cell words of a fill, repaired by the sweep) and the slot's table in R
+    __device__ __forceinline__ void cert_view(const CellWord *w, uint32_t d, View &x) const {
+        const DevParams &p = P;
+        const uint32_t y = d / p.S, cw = w[(unsigned long long)y * a->rec_pitch + (d - y * p.S)];
+        if (cw == kViaSource) view_start(x);
+        else if (cw & kViaSpecial) view_rec(cw & kNone10, x);
+        else view_walk((cw >> kStBShift) & kNone10, cw & kStKMask, rank[d], x);
+    }
+    // Source s_idx's records from certificate slot k when the leading metric of each of
+    // its labels lies below the slot's failure key (those labels are the reference's:
+    // the fixed-point argument of section 3d); false, with nothing written, otherwise
+    __device__ __forceinline__ bool cert_emit(uint32_t s_idx, uint32_t k) {
+        const DevParams &p = P;
+        const uint32_t T = p.NS + 1;
+        for (uint32_t t = threadIdx.x; t < T; t += kBS) R[t] = a->cert_tab[(unsigned long long)k * T + t];
+        src = a->src_v[s_idx];
+        src_rk = rank[src];
+        const uint32_t key = a->cert_st[k * kCertSt + kCertKey];
+        const CellWord *w = a->cert_rec + (unsigned long long)k * p.S * a->rec_pitch;
+        __syncthreads();
+        const uint32_t q0 = a->q_begin[s_idx], q1 = a->q_begin[s_idx + 1];
+        int ok = 1;
+        for (uint32_t i = q0 + threadIdx.x; i < q1; i += kBS) {
+            View x;
+            cert_view(w, a->q_dst[i], x);
+            const uint32_t c1 = p.perm[0] == 0 ? x.m0 : (p.perm[0] == 1 ? x.m1 : x.m2);
+            ok &= c1 < key ? 1 : 0;
+        }
+        if (!__syncthreads_and(ok)) return false;
+        for (uint32_t i = q0 + threadIdx.x; i < q1; i += kBS) {
+            View x;
+            cert_view(w, a->q_dst[i], x);
+            emit(x, i);
+        }
+        __syncthreads();
+        return true;
+    }
     // 1 if every destination of this source (when <= early_exit_max) is settled
     __device__ __forceinline__ uint32_t dsts_done() const {
         const uint32_t lane = lane_id();
@@ -1372,14 +1411,26 @@ __device__ __forceinline__ void finish_launch(const KArgs *__restrict__ a, uint3
         c[kCtrLastFb] = fb;
         c[kCtrLastWritten] = wr;
         c[kCtrLastOvf] = ov;
+        c[kCtrLastCert] = atomicAdd(c + kCtrCertDone, 0u);
+        c[kCtrCertDone] = 0;
         c[kCtrOvf] = 0;
         c[kCtrDequeue] = 0;
         c[kCtrFbCount] = 0;
         c[kCtrFbDequeue] = 0;
+        c[kCtrCert] = 0;
         c[kCtrWritten] = 0;
         c[kCtrDone] = 0;
         __threadfence();
     }
+}
+
+// A source handed to the SSSP launch: fallback entry i, with its certificate slot
+// (kNone32: none, the SSSP kernel solves it)
+__device__ __forceinline__ void push_fallback(const KArgs *__restrict__ a, uint32_t *counter, uint32_t s_idx,
+                                              uint32_t slot) {
+    const uint32_t i = atomicAdd(counter + kCtrFbCount, 1u);
+    a->fb_list[i] = s_idx;
+    if (a->fb_cert) a->fb_cert[i] = slot;
 }
 
 // ===================================================================================
@@ -1987,6 +2038,47 @@ struct HubSolver : Core<false> {
         wave_sync();
     }
 
+    // Certified fallback: the same ranks and table into certificate slot `slot`, with
+    // the source's vertex and the slot's failure key reset (the check lowers it)
+    __device__ __forceinline__ void export_cert(bool go, uint32_t slot, uint32_t nb) const {
+        const DevParams &p = P;
+        const uint32_t t = seg_lane();
+        if (t <= p.NS) lexs[t] = kNone32;
+        wave_sync();
+        if (go && t < nb) {
+            const uint32_t bj = bnd[t];
+            uint32_t r = 0;
+            for (uint32_t i = 0; i < nb; ++i) {
+                const uint32_t bi = bnd[i];
+                if (bi == bj) continue;
+                bool less;
+                if (bi == 0 || bj == 0) {
+                    less = bi == 0;
+                } else if (R[bi].len() != R[bj].len()) {
+                    less = R[bi].len() < R[bj].len();
+                } else {
+                    View xi, xj;
+                    view_rec(bi, xi);
+                    view_rec(bj, xj);
+                    less = cmp_list(xi, bi, xj, bj) < 0;
+                }
+                r += less ? 1u : 0u;
+            }
+            lexs[bj] = r;
+        }
+        wave_sync();
+        if (go && t <= p.NS) {
+            const unsigned long long tb = (unsigned long long)slot * (p.NS + 1);
+            a->cert_tab[tb + t] = R[t];
+            a->cert_lex[tb + t] = lexs[t];
+        }
+        if (go && t < kCertSt) {  // key none, no failing cell, an empty box
+            a->cert_st[slot * kCertSt + t] = (t == kCertKey || t == kCertX0 || t == kCertY0) ? 0xFFFFFFFFu : 0u;
+            if (t == 0) a->cert_src[slot] = src;
+        }
+        wave_sync();
+    }
+
     // Segment h solves source base + h (none past the end).
     __device__ __forceinline__ void solve(uint32_t base) {
         const DevParams &p = P;
@@ -2128,7 +2220,17 @@ struct HubSolver : Core<false> {
             fallback = fallback || (have && seg_bits<LPS>(__ballot(unc_q)) != 0);
             if (t == 0 && have && !fallback) written += qb - qa;
         }
-        if (fallback && t == 0) a->fb_list[atomicAdd(counter + kCtrFbCount, 1u)] = s_idx;
+        // A query-mode fallback source takes a certificate slot while they last: its
+        // label table and boundary ranks go there, and the fill + check launches decide
+        // whether the SSSP kernel is needed at all
+        uint32_t slot = kNone32;
+        if (fallback && t == 0 && !a->all_mode && a->cert_cap) {
+            slot = atomicAdd(counter + kCtrCert, 1u);
+            if (slot >= a->cert_cap) slot = kNone32;
+        }
+        slot = uint32_t(__shfl(int(slot), int(lane_id() & ~(LPS - 1u))));  // segment lane 0's
+        if (__any(fallback && slot != kNone32)) export_cert(fallback && slot != kNone32, slot, nb);
+        if (fallback && t == 0) push_fallback(a, counter, s_idx, slot);
         MR_HSTAMP(7);
     }
 };
@@ -2609,7 +2711,7 @@ struct HubWide : HubSolver<1> {
         const uint32_t qa = a->q_begin[s_idx], qb = fallback ? qa : a->q_begin[s_idx + 1];
         fallback = __ballot(emit_wide(qa, qb, nb, nbk, sx, sy, st0)) != 0 || fallback;
         if (j == 0 && !fallback) written += qb - qa;
-        if (fallback && j == 0) a->fb_list[atomicAdd(counter + kCtrFbCount, 1u)] = s_idx;
+        if (fallback && j == 0) push_fallback(a, counter, s_idx, kNone32);
     }
 };
 
@@ -2718,9 +2820,16 @@ __device__ __forceinline__ uint32_t bit_width64(unsigned long long x) { return x
 
 // the fill kernel's rare path: a tile whose source's keys do not fit 32 bits.  Row
 // by row, each cell's walk distance in full and the three-metric compare.
+// AggregatedCost::time of a StandardMove run of d legs at Fleetfoot ratio fn/fd (the
+// ceil of src/skill.rs:21-30; fn == fd: linear)
+__device__ __forceinline__ uint32_t run_time_ff(uint32_t d, uint32_t fn, uint32_t fd) {
+    return fn == fd ? 180u * d : uint32_t((180ull * d * fn + fd - 1) / fd);
+}
+
 template <uint32_t PERM>
 __device__ __forceinline__ void fill_tile_rows(const uint32_t (*B)[64], unsigned long long live, int wx,
-                                                      int y0, int ty0, int cx, uint32_t S, uint32_t pitch, CellWord *outs) {
+                                                      int y0, int ty0, int cx, uint32_t S, uint32_t pitch, CellWord *outs,
+                                                      uint32_t fn, uint32_t fd) {
     constexpr uint32_t q0 = PERM / 9, q1 = (PERM / 3) % 3, q2 = PERM % 3;
 #pragma unroll 1
     for (int i = 0; i < int(kFillTH); ++i) {
@@ -2729,7 +2838,7 @@ __device__ __forceinline__ void fill_tile_rows(const uint32_t (*B)[64], unsigned
             const uint32_t rr = uint32_t(__ffsll((long long)m) - 1);
             const uint32_t d = walk_dist(int(B[0][rr]), int(B[1][rr]), wx, y0 + i);
             const uint32_t b0 = B[2][rr], b1 = B[3][rr], b2 = B[4][rr];
-            const uint32_t mm0 = b0 + d, mm2 = b2 + 180u * d;
+            const uint32_t mm0 = b0 + d, mm2 = b2 + run_time_ff(d, fn, fd);
             const uint32_t c1 = q0 == 0 ? mm0 : (q0 == 1 ? b1 : mm2);
             const uint32_t c2 = q1 == 0 ? mm0 : (q1 == 1 ? b1 : mm2);
             const uint32_t c3 = q2 == 0 ? mm0 : (q2 == 1 ? b1 : mm2);
@@ -2768,7 +2877,13 @@ __device__ __forceinline__ void fill_body(const KArgs *__restrict__ a, uint32_t 
     const uint32_t lane = threadIdx.x & 63u, wv = uint32_t(__builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)));
     uint32_t(*B)[64] = btab[wv];
     uint32_t(*P)[64] = btab[wv] + 8;
-    const uint32_t NS = a->p.NS, T = NS + 1, S = a->p.S, nsrc = a->nsrc, pitch = a->rec_pitch;
+    // (certificate slots: as many sources as the hub kernel exported this pass)
+    const uint32_t NS = a->p.NS, T = NS + 1, S = a->p.S, pitch = a->rec_pitch;
+    const uint32_t nsrc = a->nsrc_dev ? min(a->nsrc, *a->nsrc_dev) : a->nsrc;
+    // Fleetfoot 1..3 (certificate slots only): walk times through the ceil, so the
+    // full-compare path, and prune bounds from run_time_ff
+    const uint32_t fn = a->p.ff_num, fd = a->p.ff_den;
+    const bool nonlin = fn != fd;
     const int H = int(a->p.H);
     const uint32_t tpx = (S + kTW - 1) / kTW, tpy = (S + kTH - 1) / kTH, ntile = tpx * tpy;
     const bool no_prune = (a->dbg_flags & 1u) != 0, no_pack = (a->dbg_flags & 2u) != 0;
@@ -2856,7 +2971,7 @@ __device__ __forceinline__ void fill_body(const KArgs *__restrict__ a, uint32_t 
         const uint32_t rbs = max(1u, bit_width64(nk - 1));
         const uint32_t wL = uint32_t(__builtin_amdgcn_readfirstlane(int(max(1u, bit_width64(mxL)))));
         // keys wider than 32 bits (or MR_DBG_FLAGS bit 1): the rare full-compare path
-        const bool packable = !no_pack && wL + rbs <= 32u;
+        const bool packable = !no_pack && !nonlin && wL + rbs <= 32u;
         const uint32_t stepL = packable ? sL << rbs : 0u, maskr = (1u << rbs) - 1u;
         if (packable) {
             if (isb) B[6][r] = kept ? uint32_t(em[L] << rbs) | srank : 0xFFFFFFFFu;  // by rank
@@ -2926,8 +3041,9 @@ __device__ __forceinline__ void fill_body(const KArgs *__restrict__ a, uint32_t 
             } else {
                 unsigned long long lo = ~0ull, hi = ~0ull;
                 if (cnd) {
-                    lo = pb_l + sP * uint64_t(dx + dy);
-                    hi = pb_l + sP * uint64_t(fx + fy + 2);
+                    const bool tl = PL == 2u;  // a time lead grows by the run time
+                    lo = pb_l + (tl ? uint64_t(run_time_ff(uint32_t(dx + dy), fn, fd)) : sP * uint64_t(dx + dy));
+                    hi = pb_l + (tl ? uint64_t(run_time_ff(uint32_t(fx + fy + 2), fn, fd)) : sP * uint64_t(fx + fy + 2));
                 }
 #pragma unroll
                 for (int o = 32; o > 0; o >>= 1) {
@@ -3054,7 +3170,7 @@ __device__ __forceinline__ void fill_body(const KArgs *__restrict__ a, uint32_t 
             } else {
                 for (int k = 0; k < kCPL; ++k) {  // keys too wide for 32 bits
                     const int cx = tx0 + 64 * k + int(lane);
-                    fill_tile_rows<PERM>(B, live, x0 + 64 * k + int(lane), y0, ty0, cx, S, pitch, outs);
+                    fill_tile_rows<PERM>(B, live, x0 + 64 * k + int(lane), y0, ty0, cx, S, pitch, outs, fn, fd);
                 }
             }
             // specials' cells hold their own labels, the source's cell (last: it may also
@@ -3142,11 +3258,14 @@ __host__ __device__ inline LdsLayout lds_layout(uint32_t NS, uint32_t V, bool gr
 
 // next source index for a workgroup: every source in order, or (fallback launch
 // after the hub solver) the sources it listed
-__device__ __forceinline__ uint32_t next_source(const KArgs *__restrict__ a) {
+__device__ __forceinline__ uint32_t next_source(const KArgs *__restrict__ a, uint32_t &slot) {
+    slot = kNone32;
     if (a->fb_mode) {
         const uint32_t n = __hip_atomic_load(a->counter + kCtrFbCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t i = atomicAdd(a->counter + kCtrFbDequeue, 1u);
-        return i < n ? a->fb_list[i] : kNone32;
+        if (i >= n) return kNone32;
+        if (a->fb_cert) slot = a->fb_cert[i];
+        return a->fb_list[i];
     }
     const uint32_t i = atomicAdd(a->counter + kCtrDequeue, 1u);
     return i < a->nsrc ? i : kNone32;
@@ -3215,12 +3334,16 @@ __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a)
         S.stamps = &stamps;
         uint32_t nsolved = 0;
         for (;;) {
-            if (threadIdx.x == 0) sh->sidx = next_source(a);
+            if (threadIdx.x == 0) sh->sidx = next_source(a, sh->sslot);
             __syncthreads();
-            const uint32_t s = sh->sidx;
+            const uint32_t s = sh->sidx, slot = sh->sslot;
             __syncthreads();
             if (s == kNone32) break;
-            S.solve(s);
+            if (slot != kNone32 && S.cert_emit(s, slot)) {
+                if (threadIdx.x == 0) atomicAdd(a->counter + kCtrCertDone, 1u);
+            } else {
+                S.solve(s);
+            }
             written += a->q_begin[s + 1] - a->q_begin[s];
             ++nsolved;
         }
@@ -3254,12 +3377,16 @@ __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a)
         S.best = reinterpret_cast<uint32_t *>(smem + L.off_b);
         S.fired = reinterpret_cast<uint32_t *>(smem + L.off_d);
         for (;;) {
-            if (threadIdx.x == 0) sh->sidx = next_source(a);
+            if (threadIdx.x == 0) sh->sidx = next_source(a, sh->sslot);
             __syncthreads();
-            const uint32_t s = sh->sidx;
+            const uint32_t s = sh->sidx, slot = sh->sslot;
             __syncthreads();
             if (s == kNone32) break;
-            S.solve(s);
+            if (slot != kNone32 && S.cert_emit(s, slot)) {
+                if (threadIdx.x == 0) atomicAdd(a->counter + kCtrCertDone, 1u);
+            } else {
+                S.solve(s);
+            }
             written += a->q_begin[s + 1] - a->q_begin[s];
         }
         S.flush_err();

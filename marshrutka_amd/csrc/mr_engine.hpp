@@ -178,6 +178,22 @@ struct KArgs {
     // queries each), sources [src_off, nsrc) to hub_kernel (src_off = n_lane)
     uint32_t n_lane;
     uint32_t src_off;
+    // Certified fallback: the hub kernel exports the label table
+    // of up to cert_cap flagged sources into slots (cert_tab / cert_lex / cert_src; the
+    // slot of fallback entry i in fb_cert[i], kNone32 for none), the fill writes every
+    // cell's closed-form word into cert_rec (rec_pitch words a row), the check kernel
+    // the least leading metric of a cell that fails the fixed-point test into
+    // cert_key[slot], and the SSSP launch emits a source's labels from its slot when
+    // every one of them lies below that key.
+    uint32_t cert_cap;
+    Rec *cert_tab;
+    uint32_t *cert_lex;
+    uint32_t *cert_src;
+    CellWord *cert_rec;
+    uint32_t *cert_st;           // per slot kCertSt words (kCert* below)
+    uint32_t *cert_aux;          // per slot V words: the repair sweep's cells by bucket
+    uint32_t *fb_cert;
+    const uint32_t *nsrc_dev;    // fill launches over cert slots: sources = min(nsrc, *nsrc_dev)
 };
 // counter words: the pass's last workgroup copies the fallback and written counts
 // to their "last" slots and zeroes the rest, so no memset precedes a pass
@@ -192,8 +208,14 @@ enum : uint32_t {
     kCtrWritten = 7,      // result records written               64-bit counter with this)
     kCtrOvf = 8,          // command-overflow pool: commands allocated in this pass
     kCtrLastOvf = 9,      // kCtrOvf of the last completed pass
-    kCtrWords = 10
+    kCtrCert = 10,        // certified-fallback slots taken in this pass
+    kCtrCertDone = 11,    // fallback sources the certificate answered in this pass
+    kCtrLastCert = 12,    // kCtrCertDone of the last completed pass
+    kCtrWords = 13
 };
+// per certificate slot: the least leading metric of a failing cell (the check lowers it;
+// labels below it are exact), failing cells, their bounding box (grid coordinates)
+enum : uint32_t { kCertKey = 0, kCertFails = 1, kCertX0 = 2, kCertX1 = 3, kCertY0 = 4, kCertY1 = 5, kCertSt = 8 };
 // result status (OutResult high half - 16) of a label whose commands went to the
 // overflow pool: its first command slot holds {kOvfTag, offset, count}
 constexpr uint32_t kStatusOverflow = 64u, kOvfTag = 0xFFFFFFFFu;

@@ -42,6 +42,8 @@ int hub_wide_blocks_per_cu(const uint32_t perm[3], uint32_t NS, uint32_t bytes);
 uint32_t hub_lane_entries(uint32_t NS);
 hipError_t launch_hub_lane(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t n_lane,
                            hipStream_t stream);
+hipError_t launch_cert_check(const KArgs *d_args, uint32_t gx, uint32_t slots, hipStream_t stream);
+hipError_t launch_cert_sweep(const KArgs *d_args, uint32_t slots, hipStream_t stream);
 }  // namespace mr
 
 
@@ -932,6 +934,15 @@ struct mr_plan {
     uint32_t slot = 0;     // slot index of the d_* fields
     bool own_tables = true;  // d_sinfo / d_rank / d_rank_inv / d_cell: false = the grid's shared copies
     uint2 *d_cell = nullptr;
+    // certified fallback (query hub plans): per slot a label table,
+    // boundary ranks, source, cell words, check state and sweep list; the fill's
+    // argument block over the slots
+    uint32_t cert_cap = 0, cert_fill_gx = 1, cert_check_gx = 1;
+    Rec *d_cert_tab = nullptr;
+    uint32_t *d_cert_lex = nullptr, *d_cert_src = nullptr, *d_cert_st = nullptr, *d_cert_aux = nullptr,
+             *d_fb_cert = nullptr, *d_cert_ones = nullptr;
+    CellWord *d_cert_rec = nullptr;
+    KArgs *d_args_cert = nullptr;
     ~mr_plan() {
         if (!slots.empty()) {  // the d_* fields may name another slot: free each slot's once
             Slot &k = slots[0];
@@ -960,6 +971,10 @@ struct mr_plan {
             d_cell = nullptr;
         }
         if (d_cell) (void)hipFree(d_cell);
+        for (void *p : {(void *)d_cert_tab, (void *)d_cert_lex, (void *)d_cert_src, (void *)d_cert_st,
+                        (void *)d_cert_aux, (void *)d_fb_cert, (void *)d_cert_ones, (void *)d_cert_rec,
+                        (void *)d_args_cert})
+            if (p) (void)hipFree(p);
         for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_rank_inv, (void *)d_src, (void *)d_qb, (void *)d_qd,
                         (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
                         (void *)d_counter, (void *)d_args, (void *)d_dbg, (void *)d_args_fb, (void *)d_near,
@@ -1021,6 +1036,17 @@ static int upload_args(mr_plan *pl) {
         KArgs l = k;
         l.last_launch = 1;
         if (!put(pl->all_mode ? pl->d_args_fill : pl->d_args_hub_last, l)) return MR_ERR_DEVICE;
+        if (pl->d_args_cert) {  // the fill over the certificate slots the hub kernel exported
+            KArgs c = k;
+            c.nsrc = pl->cert_cap;
+            c.nsrc_dev = pl->d_counter + kCtrCert;
+            c.src_v = pl->d_cert_src;
+            c.src_state = pl->d_cert_ones;
+            c.out_tab = pl->d_cert_tab;
+            c.out_lex = pl->d_cert_lex;
+            c.out_rec = pl->d_cert_rec;
+            if (!put(pl->d_args_cert, c)) return MR_ERR_DEVICE;
+        }
         if (pl->d_args_lane && (!put(pl->d_args_lane, k) || !put(pl->d_args_lane_last, l))) return MR_ERR_DEVICE;
     }
     return MR_OK;
@@ -1286,6 +1312,43 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
             hipMalloc(reinterpret_cast<void **>(&pl->d_args_hub_last), sizeof(KArgs)) != hipSuccess ||
             hipMalloc(reinterpret_cast<void **>(&pl->d_args_fill), sizeof(KArgs)) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "kernel args"));
+        // Certified fallback for query plans on hub_kernel (MR_CERT=0: off; MR_CERT_SLOTS:
+        // slots per pass, default 8): a flagged source's table goes to a slot, the fill
+        // writes its closed form over every cell, the check and one repair sweep decide
+        // whether its labels need the SSSP kernel at all.
+        const char *ce = std::getenv("MR_CERT");
+        if (!all_mode && !hp.wide && !(ce && !std::strcmp(ce, "0"))) {
+            uint32_t cap = 8;
+            if (const char *e = std::getenv("MR_CERT_SLOTS")) cap = uint32_t(std::min(64, std::max(1, std::atoi(e))));
+            const size_t T = size_t(NS) + 1;
+            const uint32_t pitch = (hp.p.S + 31) / 32 * 32;
+            std::vector<uint32_t> ones(cap, 1u);
+            if (hipMalloc(reinterpret_cast<void **>(&pl->d_cert_tab), cap * T * sizeof(Rec)) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void **>(&pl->d_cert_lex), cap * T * 4) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void **>(&pl->d_cert_src), cap * 4) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void **>(&pl->d_cert_st), cap * kCertSt * 4) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void **>(&pl->d_cert_aux), size_t(cap) * V * 4) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void **>(&pl->d_cert_rec), size_t(cap) * hp.p.S * pitch * 4) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void **>(&pl->d_fb_cert), std::max<size_t>(nsrc, 1) * 4) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void **>(&pl->d_args_cert), sizeof(KArgs)) != hipSuccess ||
+                upload(pl->d_cert_ones, ones) != MR_OK)
+                return bail(fail(MR_ERR_DEVICE, "certificate slots"));
+            pl->cert_cap = cap;
+            ka.cert_cap = cap;
+            ka.cert_tab = pl->d_cert_tab;
+            ka.cert_lex = pl->d_cert_lex;
+            ka.cert_src = pl->d_cert_src;
+            ka.cert_st = pl->d_cert_st;
+            ka.cert_aux = pl->d_cert_aux;
+            ka.cert_rec = pl->d_cert_rec;
+            ka.fb_cert = pl->d_fb_cert;
+            ka.rec_pitch = pitch;
+            const uint64_t tiles = uint64_t((hp.p.S + kFillTW - 1) / kFillTW) * ((hp.p.S + kFillTH - 1) / kFillTH);
+            pl->cert_fill_gx = uint32_t(std::max<uint64_t>(
+                1, std::min<uint64_t>((tiles + 3) / 4, uint64_t(pl->fill_per_cu) * prop.multiProcessorCount)));
+            pl->cert_check_gx = uint32_t(std::max<uint64_t>(
+                1, std::min<uint64_t>((uint64_t(V) + 4 * 256 - 1) / (4 * 256), 4ull * prop.multiProcessorCount)));
+        }
         if (pl->n_lane && (hipMalloc(reinterpret_cast<void **>(&pl->d_args_lane), sizeof(KArgs)) != hipSuccess ||
                            hipMalloc(reinterpret_cast<void **>(&pl->d_args_lane_last), sizeof(KArgs)) != hipSuccess))
             return bail(fail(MR_ERR_DEVICE, "kernel args"));
@@ -1510,6 +1573,15 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
             e = launch_hub_lane(pl->fb_none && !big ? pl->d_args_lane_last : pl->d_args_lane, pl->ka.p.perm,
                                 pl->ka.p.NS, pl->ka.nreg, pl->n_lane, s);
         if (e == hipSuccess && big) e = launch_hub_plan(pl, pl->fb_none ? pl->d_args_hub_last : pl->d_args, s);
+        // certified fallback: the slots' closed forms, the check, one repair sweep, the
+        // check again (each exits at once without exported slots); the SSSP launch then
+        // emits every certified source from its slot and solves the rest
+        if (e == hipSuccess && !pl->fb_none && pl->cert_cap) {
+            e = launch_fill(pl->d_args_cert, pl->ka.p.perm, pl->cert_fill_gx, 1, s);
+            if (e == hipSuccess) e = launch_cert_check(pl->d_args, pl->cert_check_gx, pl->cert_cap, s);
+            if (e == hipSuccess) e = launch_cert_sweep(pl->d_args, pl->cert_cap, s);
+            if (e == hipSuccess) e = launch_cert_check(pl->d_args, pl->cert_check_gx, pl->cert_cap, s);
+        }
         if (e == hipSuccess && !pl->fb_none)
             e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, s);
     } else {
@@ -1660,6 +1732,7 @@ extern "C" int mr_plan_get_stats(mr_plan *pl, mr_plan_stats *out) {
     out->specials_per_lane = !pl->hp.hub ? 0u : (pl->hp.wide ? hub_wide_spl(pl->ka.p.NS) : 1u);
     out->region_boundary_cells = pl->hp.wide && pl->hp.rb_off && !pl->hp.rb_off->empty() ? pl->hp.rb_off->back() : 0u;
     out->lane_sources = pl->n_lane;
+    out->certified_sources = ctr[kCtrLastCert];
     out->fill_launch = !(pl->hp.hub && pl->all_mode) ? MR_FILL_NONE
                        : pl->fused                   ? MR_FILL_FUSED
                        : pl->overlap                 ? MR_FILL_STREAMS

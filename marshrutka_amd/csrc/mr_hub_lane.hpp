@@ -672,7 +672,7 @@ struct LaneHub {
             }
         }
         const bool fallback = fb_sp || unc;
-        if (fallback) a->fb_list[atomicAdd(counter + kCtrFbCount, 1u)] = s_idx;
+        if (fallback) push_fallback(a, counter, s_idx, kNone32);
         return fallback ? 0u : qb - qa;
     }
 };

@@ -1,0 +1,19 @@
+// mr_k_cert.hip — certified fallback kernels (cert_check_kernel, cert_sweep_kernel)
+// (host-side launch helpers called from mr_host.cpp; device code in mr_cert.hpp)
+#include "mr_cert.hpp"
+
+namespace mr {
+
+// the check over every slot's cells: gx workgroups per slot, `slots` slots
+hipError_t launch_cert_check(const KArgs *d_args, uint32_t gx, uint32_t slots, hipStream_t stream) {
+    void *args[] = {const_cast<KArgs **>(&d_args)};
+    return hipLaunchKernel((const void *)&cert_check_kernel, dim3(gx, slots), dim3(kBS), args, 0, stream);
+}
+
+// the repair sweep: one workgroup per slot
+hipError_t launch_cert_sweep(const KArgs *d_args, uint32_t slots, hipStream_t stream) {
+    void *args[] = {const_cast<KArgs **>(&d_args)};
+    return hipLaunchKernel((const void *)&cert_sweep_kernel, dim3(slots), dim3(kSweepBS), args, 0, stream);
+}
+
+}  // namespace mr

@@ -23,7 +23,7 @@ def eng():
     return pathfinder
 
 
-@pytest.fixture(params=["auto-lds", "auto-hbm", "lane-lds", "hub1-lds", "hub2-lds", "wide-lds", "widescan-lds", "fallback-lds", "fallback-hbm",
+@pytest.fixture(params=["auto-lds", "auto-hbm", "lane-lds", "hub1-lds", "hub2-lds", "wide-lds", "widescan-lds", "fallback-lds", "fallback-hbm", "fbsssp-lds",
                         "sssp-lds", "sssp-hbm", "generic-lds", "generic-hbm"])
 def grid_state(request, monkeypatch):
     """Every solver path x both grid-state regimes:
@@ -38,7 +38,10 @@ def grid_state(request, monkeypatch):
                narrow one applies
     widescan — the same with each source's region row scanned from the regions'
                boundary cells instead of read from the grid's region table
-    fallback — hub solver handing every source to the SSSP kernel
+    fallback — hub solver handing every source over: 64 a pass through the
+               certificate (fill, check, repair sweep), the
+               rest (and any the certificate cannot answer) to the SSSP kernel
+    fbsssp   — the same with the certificate off: every source on the SSSP kernel
     sssp     — no hub solver (level-synchronous solver for Legs-first orders)
     generic  — the bucketed solver for every order."""
     algo, state = request.param.split("-")
@@ -48,6 +51,8 @@ def grid_state(request, monkeypatch):
     monkeypatch.delenv("MR_HUB_SPW", raising=False)
     monkeypatch.delenv("MR_HUB_WIDE", raising=False)
     monkeypatch.delenv("MR_HUB_LANE", raising=False)
+    monkeypatch.delenv("MR_CERT", raising=False)
+    monkeypatch.delenv("MR_CERT_SLOTS", raising=False)
     if algo in ("hub1", "hub2"):
         monkeypatch.setenv("MR_HUB_LANE", "0")
     if algo == "lane":
@@ -60,8 +65,12 @@ def grid_state(request, monkeypatch):
         monkeypatch.setenv("MR_HUB_SPW", "1")
     if algo in ("sssp", "generic"):
         monkeypatch.setenv("MR_ALGO", algo)
-    if algo == "fallback":
+    if algo in ("fallback", "fbsssp"):
         monkeypatch.setenv("MR_HUB_FALLBACK_ALL", "1")
+    if algo == "fallback":
+        monkeypatch.setenv("MR_CERT_SLOTS", "64")
+    if algo == "fbsssp":
+        monkeypatch.setenv("MR_CERT", "0")
     return request.param
 
 
