@@ -55,30 +55,33 @@ __device__ __forceinline__ uint32_t pick(const DevParams &p, int i, uint32_t m0,
     const uint32_t q = p.perm[i];
     return q == 0 ? m0 : (q == 1 ? m1 : m2);
 }
-// walk(b, k): b's label + k legs, its money, the run's time; the list is b's + one command
-__device__ __forceinline__ CertLab cert_walk(const DevParams &p, const CertEntry *E, uint32_t b, uint32_t k) {
+// walk(b, k): b's label + k legs, its money, the run's time (from the table FT of nft
+// run times when given); the list is b's + one command
+__device__ __forceinline__ CertLab cert_walk(const DevParams &p, const CertEntry *E, uint32_t b, uint32_t k,
+                                             const uint32_t *FT = nullptr, uint32_t nft = 0) {
     const CertEntry &e = E[b];
-    const uint32_t m0 = e.m0 + k, m1 = e.m1, m2 = e.m2 + run_time_ff(k, p.ff_num, p.ff_den);
+    const uint32_t m0 = e.m0 + k, m1 = e.m1, m2 = e.m2 + (k < nft ? FT[k] : run_time_ff(k, p.ff_num, p.ff_den));
     return CertLab{pick(p, 0, m0, m1, m2), pick(p, 1, m0, m1, m2), pick(p, 2, m0, m1, m2), b == 0 ? 1u : e.len + 1u,
                    e.lex, b, k};
 }
 // the extension by one StandardMove of the label in cell word w (false: not a walk source)
-__device__ __forceinline__ bool cert_ext(const DevParams &p, const CertEntry *E, uint32_t w, CertLab &x) {
+__device__ __forceinline__ bool cert_ext(const DevParams &p, const CertEntry *E, uint32_t w, CertLab &x,
+                                         const uint32_t *FT = nullptr, uint32_t nft = 0) {
     if (w == kViaSource) {
-        x = cert_walk(p, E, 0, 1);
+        x = cert_walk(p, E, 0, 1, FT, nft);
         return true;
     }
     if (w & kViaSpecial) {
         const uint32_t t = w & kNone10;
         if (E[t].wb != kCertNoB) {  // a walk: the run merges
-            x = cert_walk(p, E, E[t].wb, E[t].wk + 1);
+            x = cert_walk(p, E, E[t].wb, E[t].wk + 1, FT, nft);
             return true;
         }
         if (E[t].lex == kNone32) return false;
-        x = cert_walk(p, E, t, 1);
+        x = cert_walk(p, E, t, 1, FT, nft);
         return true;
     }
-    x = cert_walk(p, E, (w >> kStBShift) & kNone10, (w & kStKMask) + 1);
+    x = cert_walk(p, E, (w >> kStBShift) & kNone10, (w & kStKMask) + 1, FT, nft);
     return true;
 }
 // a slot's table into LDS (every thread of the block takes part)
@@ -96,7 +99,8 @@ __device__ __forceinline__ void cert_load_table(const KArgs *__restrict__ a, uin
 // a neighbour's label cannot be extended here (counted as a failure)
 template <bool ATOMIC>
 __device__ __forceinline__ bool cert_best4(const DevParams &p, const CertEntry *E, const CellWord *w, uint32_t pitch,
-                                           int x, int y, CertLab &best, bool &any) {
+                                           int x, int y, CertLab &best, bool &any, const uint32_t *FT = nullptr,
+                                           uint32_t nft = 0) {
     const int S = int(p.S), H = int(p.H);
     any = false;
     bool ok = true;
@@ -105,9 +109,9 @@ __device__ __forceinline__ bool cert_best4(const DevParams &p, const CertEntry *
     for (int i = 0; i < 4; ++i) {
         if (nx[i] < 0 || nx[i] >= S || ny[i] < 0 || ny[i] >= S || (nx[i] == H && ny[i] == H)) continue;
         const CellWord *pw = w + (size_t)ny[i] * pitch + nx[i];
-        const uint32_t wu = ATOMIC ? __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *pw;
+        const uint32_t wu = ATOMIC ? __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : *pw;
         CertLab c;
-        if (!cert_ext(p, E, wu, c)) {
+        if (!cert_ext(p, E, wu, c, FT, nft)) {
             ok = false;
             continue;
         }
@@ -169,7 +173,11 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
             y1 = max(y1, y);
         }
     }
-    // one atomic per wave and field
+    // the workgroup's partial state (plain stores: a consumer reduces the workgroups')
+    __shared__ uint32_t red[kCertSt];
+    if (threadIdx.x < kCertSt) red[threadIdx.x] = (threadIdx.x == kCertKey || threadIdx.x == kCertX0 ||
+                                                   threadIdx.x == kCertY0) ? 0xFFFFFFFFu : 0u;
+    __syncthreads();
     if (__any(nf != 0)) {
         key = wave_min_u32(key);
         x0 = wave_min_u32(x0);
@@ -180,37 +188,56 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) n += uint32_t(__shfl_xor(int(n), o));
         if (lane_id() == 0) {
-            uint32_t *st = a->cert_st + slot * kCertSt;
-            atomicMin(st + kCertKey, key);
-            atomicAdd(st + kCertFails, n);
-            atomicMin(st + kCertX0, x0);
-            atomicMax(st + kCertX1, x1);
-            atomicMin(st + kCertY0, y0);
-            atomicMax(st + kCertY1, y1);
+            atomicMin(red + kCertKey, key);
+            atomicAdd(red + kCertFails, n);
+            atomicMin(red + kCertX0, x0);
+            atomicMax(red + kCertX1, x1);
+            atomicMin(red + kCertY0, y0);
+            atomicMax(red + kCertY1, y1);
         }
     }
+    __syncthreads();
+    if (threadIdx.x < kCertSt) a->cert_st[((unsigned long long)slot * a->cert_parts + blockIdx.x) * kCertSt + threadIdx.x] = red[threadIdx.x];
 }
 
 constexpr uint32_t kSweepBS = 1024;      // threads of the sweep's one workgroup per slot
 constexpr uint32_t kSweepBuckets = 16384;  // leading-metric buckets a window may span
 constexpr int kSweepMargin = 2;            // cells added round the failing cells' box
+constexpr uint32_t kSweepRunTimes = 8200;  // run-time table (walks of up to 2 S + 3 legs at S = 4097)
 
 // One workgroup per slot: the failing box (+ margin) in order of the leading metric of its
 // current words, bucket by bucket, each cell from its neighbours; then the slot's check
-// state is reset for the next check.  Words are read past L1 (agent-scope loads) so a
-// bucket sees the previous one's stores.
+// state is reset for the next check.  One workgroup (one CU) owns the slot's words during
+// the sweep, so workgroup-scope accesses and the barrier order the buckets (agent scope
+// would take every load past the XCD's L2).
 __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__restrict__ a) {
     __shared__ CertEntry E[64];
     __shared__ uint32_t off[kSweepBuckets];
+    __shared__ uint32_t FT[kSweepRunTimes];  // run times of 0 .. kSweepRunTimes - 1 legs
     __shared__ uint32_t red[2];
     const uint32_t slot = blockIdx.x, tid = threadIdx.x;
     const uint32_t nslot = min(a->cert_cap, __hip_atomic_load(a->counter + kCtrCert, __ATOMIC_RELAXED,
                                                                __HIP_MEMORY_SCOPE_AGENT));
     if (slot >= nslot) return;
-    uint32_t *st = a->cert_st + slot * kCertSt;
+    // the check's state: the least / greatest over its workgroups' partials
+    __shared__ uint32_t st[kCertSt];
+    if (tid < kCertSt) st[tid] = (tid == kCertKey || tid == kCertX0 || tid == kCertY0) ? 0xFFFFFFFFu : 0u;
+    __syncthreads();
+    for (uint32_t j = tid; j < a->cert_parts; j += kSweepBS) {
+        const uint32_t *ps = a->cert_st + ((unsigned long long)slot * a->cert_parts + j) * kCertSt;
+        if (ps[kCertFails] == 0) continue;
+        atomicAdd(st + kCertFails, ps[kCertFails]);
+        atomicMin(st + kCertX0, ps[kCertX0]);
+        atomicMax(st + kCertX1, ps[kCertX1]);
+        atomicMin(st + kCertY0, ps[kCertY0]);
+        atomicMax(st + kCertY1, ps[kCertY1]);
+    }
+    __syncthreads();
     if (st[kCertFails] == 0) return;  // certified as it stands
     const DevParams p = a->p;
     cert_load_table(a, slot, E);
+    const uint32_t nft = min(kSweepRunTimes, 2u * p.S + 4u);
+    for (uint32_t k = tid; k < nft; k += kSweepBS) FT[k] = run_time_ff(k, p.ff_num, p.ff_den);
     if (tid == 0) {
         red[0] = 0xFFFFFFFFu;
         red[1] = 0;
@@ -228,7 +255,7 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
     const uint32_t W = L == 0 ? 1u : max(1u, p.W);
     auto lead_of = [&](uint32_t cw) {
         const uint32_t b = (cw >> kStBShift) & kNone10, k = cw & kStKMask;
-        return L == 0 ? E[b].m0 + k : E[b].m2 + run_time_ff(k, p.ff_num, p.ff_den);
+        return L == 0 ? E[b].m0 + k : E[b].m2 + (k < nft ? FT[k] : run_time_ff(k, p.ff_num, p.ff_den));
     };
     auto plain_word = [&](uint32_t cw) { return cw != kViaSource && !(cw & kViaSpecial); };
     __syncthreads();
@@ -288,7 +315,7 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
     for (uint32_t i = tid; i < area; i += kSweepBS) {
         const uint32_t y = uint32_t(by0) + i / bw, x = uint32_t(bx0) + i % bw;
         const uint32_t cw = w[(size_t)y * pitch + x];
-        if (plain_word(cw)) list[atomicAdd(&off[lead_of(cw) / W - kmin], 1u)] = y * p.S + x;
+        if (plain_word(cw)) list[atomicAdd(&off[lead_of(cw) / W - kmin], 1u)] = y << 16 | x;
     }
     __syncthreads();
     // off[j] now ends bucket j.  Bucket by bucket: each cell takes its neighbours' least
@@ -297,20 +324,18 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
         const uint32_t beg = j ? off[j - 1] : 0u, end = off[j];
         if (beg == end) continue;
         for (uint32_t i = beg + tid; i < end; i += kSweepBS) {
-            const uint32_t v = list[i], y = v / p.S, x = v - y * p.S;
+            const uint32_t v = list[i], y = v >> 16, x = v & 0xFFFFu;
             CertLab best{};
             bool any;
-            cert_best4<true>(p, E, w, pitch, int(x), int(y), best, any);
+            cert_best4<true>(p, E, w, pitch, int(x), int(y), best, any, FT, nft);
             if (!any) continue;
             CellWord *pw = w + (size_t)y * pitch + x;
             const uint32_t nw = (best.b << kStBShift) | best.k;
-            if (__hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != nw)
-                __hip_atomic_store(pw, nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != nw)
+                __hip_atomic_store(pw, nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         __syncthreads();
     }
-    // the next check starts from an empty state
-    if (tid < kCertSt) st[tid] = (tid == kCertKey || tid == kCertX0 || tid == kCertY0) ? 0xFFFFFFFFu : 0u;
 }
 
 }  // namespace mr

@@ -61,6 +61,18 @@ struct Shared {
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
+// Exact floor(x / d) for 0 < d < 2^31 and |x| < 2^50 without an integer division (a
+// 64-bit divide expands to ~150 VALU instructions on gfx950; the non-linear hub's
+// certification divides per path cell): the correctly rounded double quotient is
+// within one of the result, and one remainder step corrects it.
+__device__ __forceinline__ long long floor_div(long long x, long long d) {
+    long long q = (long long)floor(double(x) / double(d));
+    const long long r = x - q * d;
+    q += r >= d ? 1 : 0;
+    q -= r < 0 ? 1 : 0;
+    return q;
+}
+
 // Diagnostic phase stamps (build with -DMR_STAMPS; never in the product build):
 // thread 0 of each workgroup accumulates shader cycles per phase.
 #ifdef MR_STAMPS
@@ -251,7 +263,7 @@ struct Core {
     __device__ __forceinline__ uint32_t run_time(uint32_t k) const {
         const DevParams &p = P;
         unsigned long long t = 180ull * k;
-        if (p.ff_num != p.ff_den) t = (t * p.ff_num + p.ff_den - 1) / p.ff_den;
+        if (p.ff_num != p.ff_den) t = (unsigned long long)floor_div((long long)(t * p.ff_num + p.ff_den - 1), p.ff_den);
         err |= t > 0xFFFFFFFFull ? kErrMetricOverflow : 0u;
         return uint32_t(t);
     }
@@ -868,9 +880,17 @@ struct Core {
         for (uint32_t t = threadIdx.x; t < T; t += kBS) R[t] = a->cert_tab[(unsigned long long)k * T + t];
         src = a->src_v[s_idx];
         src_rk = rank[src];
-        const uint32_t key = a->cert_st[k * kCertSt + kCertKey];
+        // the slot's key: the least over the check's workgroups
+        uint32_t key = 0xFFFFFFFFu;
+        for (uint32_t j = threadIdx.x; j < a->cert_parts; j += kBS)
+            key = min(key, a->cert_st[((unsigned long long)k * a->cert_parts + j) * kCertSt + kCertKey]);
+        key = wave_min_u32(key);
+        if (threadIdx.x == 0) sh->done = 0xFFFFFFFFu;
+        __syncthreads();
+        if (lane_id() == 0) atomicMin(&sh->done, key);
         const CellWord *w = a->cert_rec + (unsigned long long)k * p.S * a->rec_pitch;
         __syncthreads();
+        key = sh->done;
         const uint32_t q0 = a->q_begin[s_idx], q1 = a->q_begin[s_idx + 1];
         int ok = 1;
         for (uint32_t i = q0 + threadIdx.x; i < q1; i += kBS) {
@@ -1712,7 +1732,7 @@ struct HubSolver : Core<false> {
     // the gap f(k + m) - f(k) takes one of {lo, hi} for every k (cm = 180 m num / den)
     __device__ __forceinline__ bool gap_hits(long long d0, long long m) const {
         const long long a = 180ll * (long long)P.ff_num * (m < 0 ? -m : m), den = (long long)P.ff_den;
-        long long lo = a / den, hi = (a + den - 1) / den;
+        long long lo = floor_div(a, den), hi = floor_div(a + den - 1, den);
         if (m < 0) {
             const long long t = lo;
             lo = -hi;
@@ -1738,7 +1758,7 @@ struct HubSolver : Core<false> {
         }
         // d0 + 180 m num / den within (-2, 1): m next to -d0 den / (180 num)
         const long long c = 180ll * (long long)p.ff_num, num = (-2 - d0) * (long long)p.ff_den;
-        const long long m0 = num >= 0 ? num / c : -((-num + c - 1) / c);
+        const long long m0 = floor_div(num, c);
         for (long long m = m0 - 1; m <= m0 + 2; ++m)
             if (m != 0 && m >= mlo && m <= mhi && gap_hits(d0, m)) return true;
         return false;
@@ -2072,10 +2092,7 @@ struct HubSolver : Core<false> {
             a->cert_tab[tb + t] = R[t];
             a->cert_lex[tb + t] = lexs[t];
         }
-        if (go && t < kCertSt) {  // key none, no failing cell, an empty box
-            a->cert_st[slot * kCertSt + t] = (t == kCertKey || t == kCertX0 || t == kCertY0) ? 0xFFFFFFFFu : 0u;
-            if (t == 0) a->cert_src[slot] = src;
-        }
+        if (go && t == 0) a->cert_src[slot] = src;
         wave_sync();
     }
 
@@ -2823,7 +2840,7 @@ __device__ __forceinline__ uint32_t bit_width64(unsigned long long x) { return x
 // AggregatedCost::time of a StandardMove run of d legs at Fleetfoot ratio fn/fd (the
 // ceil of src/skill.rs:21-30; fn == fd: linear)
 __device__ __forceinline__ uint32_t run_time_ff(uint32_t d, uint32_t fn, uint32_t fd) {
-    return fn == fd ? 180u * d : uint32_t((180ull * d * fn + fd - 1) / fd);
+    return fn == fd ? 180u * d : uint32_t(floor_div(180ll * d * fn + fd - 1, fd));
 }
 
 template <uint32_t PERM>

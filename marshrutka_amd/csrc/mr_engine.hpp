@@ -190,7 +190,8 @@ struct KArgs {
     uint32_t *cert_lex;
     uint32_t *cert_src;
     CellWord *cert_rec;
-    uint32_t *cert_st;           // per slot kCertSt words (kCert* below)
+    uint32_t *cert_st;           // per slot and check workgroup kCertSt words (kCert* below)
+    uint32_t cert_parts;         // check workgroups per slot (partial states a consumer reduces)
     uint32_t *cert_aux;          // per slot V words: the repair sweep's cells by bucket
     uint32_t *fb_cert;
     const uint32_t *nsrc_dev;    // fill launches over cert slots: sources = min(nsrc, *nsrc_dev)
@@ -213,8 +214,9 @@ enum : uint32_t {
     kCtrLastCert = 12,    // kCtrCertDone of the last completed pass
     kCtrWords = 13
 };
-// per certificate slot: the least leading metric of a failing cell (the check lowers it;
-// labels below it are exact), failing cells, their bounding box (grid coordinates)
+// per certificate slot and check workgroup: the least leading metric of a failing cell
+// (labels below the least over the workgroups are exact), failing cells, their bounding
+// box (grid coordinates)
 enum : uint32_t { kCertKey = 0, kCertFails = 1, kCertX0 = 2, kCertX1 = 3, kCertY0 = 4, kCertY1 = 5, kCertSt = 8 };
 // result status (OutResult high half - 16) of a label whose commands went to the
 // overflow pool: its first command slot holds {kOvfTag, offset, count}

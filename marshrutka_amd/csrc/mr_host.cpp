@@ -1326,7 +1326,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
             if (hipMalloc(reinterpret_cast<void **>(&pl->d_cert_tab), cap * T * sizeof(Rec)) != hipSuccess ||
                 hipMalloc(reinterpret_cast<void **>(&pl->d_cert_lex), cap * T * 4) != hipSuccess ||
                 hipMalloc(reinterpret_cast<void **>(&pl->d_cert_src), cap * 4) != hipSuccess ||
-                hipMalloc(reinterpret_cast<void **>(&pl->d_cert_st), cap * kCertSt * 4) != hipSuccess ||
+
                 hipMalloc(reinterpret_cast<void **>(&pl->d_cert_aux), size_t(cap) * V * 4) != hipSuccess ||
                 hipMalloc(reinterpret_cast<void **>(&pl->d_cert_rec), size_t(cap) * hp.p.S * pitch * 4) != hipSuccess ||
                 hipMalloc(reinterpret_cast<void **>(&pl->d_fb_cert), std::max<size_t>(nsrc, 1) * 4) != hipSuccess ||
@@ -1348,6 +1348,12 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
                 1, std::min<uint64_t>((tiles + 3) / 4, uint64_t(pl->fill_per_cu) * prop.multiProcessorCount)));
             pl->cert_check_gx = uint32_t(std::max<uint64_t>(
                 1, std::min<uint64_t>((uint64_t(V) + 4 * 256 - 1) / (4 * 256), 4ull * prop.multiProcessorCount)));
+            // the check's state: one partial per slot and check workgroup, reduced by its readers
+            if (hipMalloc(reinterpret_cast<void **>(&pl->d_cert_st), size_t(cap) * pl->cert_check_gx * kCertSt * 4) !=
+                hipSuccess)
+                return bail(fail(MR_ERR_DEVICE, "certificate slots"));
+            ka.cert_st = pl->d_cert_st;
+            ka.cert_parts = pl->cert_check_gx;
         }
         if (pl->n_lane && (hipMalloc(reinterpret_cast<void **>(&pl->d_args_lane), sizeof(KArgs)) != hipSuccess ||
                            hipMalloc(reinterpret_cast<void **>(&pl->d_args_lane_last), sizeof(KArgs)) != hipSuccess))
