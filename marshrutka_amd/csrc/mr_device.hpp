@@ -35,9 +35,30 @@
 
 #include "mr_engine.hpp"
 
+#include <map>
+#include <mutex>
+#include <tuple>
+
 namespace mr {
 
 constexpr int kBS = 256;
+
+// hipOccupancyMaxActiveBlocksPerMultiprocessor, once per (kernel, block size, LDS bytes)
+// and device: plan creation asks for several, and the query is not free
+inline int occupancy_cached(const void *fn, int bs, size_t lds) {
+    static std::mutex mu;
+    static std::map<std::tuple<const void *, int, size_t, int>, int> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const auto key = std::make_tuple(fn, bs, lds, dev);
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int n = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, bs, lds);
+    cache.emplace(key, n);
+    return n;
+}
 constexpr uint32_t kOwn = 0xFFFFu;
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
 constexpr unsigned long long kInf64 = ~0ull;

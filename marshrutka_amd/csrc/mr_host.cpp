@@ -44,6 +44,12 @@ hipError_t launch_hub_lane(const KArgs *d_args, const uint32_t perm[3], uint32_t
                            hipStream_t stream);
 hipError_t launch_cert_check(const KArgs *d_args, uint32_t gx, uint32_t slots, hipStream_t stream);
 hipError_t launch_cert_sweep(const KArgs *d_args, uint32_t slots, hipStream_t stream);
+hipError_t decode_records_device(const OutResult *res, const OutCmd *slots, const OutCmd *ovf, uint32_t novf,
+                                 const uint32_t *q_id, uint32_t nrec, uint32_t nq, uint32_t mc,
+                                 const mr_cell_index *idx_rank, uint32_t V, uint32_t rgt, uint32_t soe, uint32_t shq,
+                                 uint32_t sfm, uint32_t ff, uint32_t *cnt, uint32_t *off, void *temp, size_t *temp_bytes,
+                                 mr_result *out, mr_command *pool, unsigned long long pool_cap, uint32_t *err,
+                                 hipStream_t stream);
 }  // namespace mr
 
 
@@ -165,7 +171,9 @@ struct mr_grid {
         uint2 *cell;  // {sinfo, rank} per cell
     };
     mutable std::vector<SinfoDev> d_sinfo;
+    mutable mr_cell_index *d_idx_rank = nullptr;  // device fetch: the CellIndex of every rank
     ~mr_grid() {
+        if (d_idx_rank) (void)hipFree(d_idx_rank);
         for (uint32_t *p : d_near)
             if (p) (void)hipFree(p);
         for (uint32_t *p : {d_rank, d_rank_inv})
@@ -366,14 +374,27 @@ extern "C" void mr_params_default(mr_params *p) {
 extern "C" uint32_t mr_abi_version(void) { return MR_ABI_VERSION; }
 extern "C" const char *mr_last_error(void) { return g_last_error.c_str(); }
 
+// Device properties, queried once per device (hipGetDeviceProperties costs far more
+// than the rest of a small plan's creation)
+static const hipDeviceProp_t *device_props(int dev) {
+    static std::mutex mu;
+    static std::unordered_map<int, hipDeviceProp_t> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(dev);
+    if (it != cache.end()) return &it->second;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return nullptr;
+    return &cache.emplace(dev, prop).first->second;
+}
+
 extern "C" int mr_device_available(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return 0;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
-    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+    const hipDeviceProp_t *prop = device_props(dev);
+    if (!prop) return 0;
+    return std::strncmp(prop->gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
 }
 
 // Region tables for the hub solver (built lazily, once per grid and homeland).
@@ -842,6 +863,122 @@ static bool grid_tables(const mr_grid *g, int dev, const HostPlan &hp, uint32_t 
     return true;
 }
 
+// Plan buffers come from a cache of freed device blocks (size classes per device: powers
+// of two up to 64 MiB, 64 MiB steps above): a plan for each fresh batch then costs no
+// hipMalloc / hipFree (tens of microseconds each, milliseconds for large blocks).  A
+// block returns to the cache when its plan is destroyed, after mr_plan_destroy has
+// waited for the plan's work; the cache keeps up to 16 GiB and is emptied before a
+// hipMalloc that would otherwise fail.
+struct BlockCache {
+    std::mutex mu;
+    std::unordered_map<void *, std::pair<int, size_t>> live;  // block -> (device, class bytes)
+    std::unordered_map<uint64_t, std::vector<void *>> free;   // (device, class) -> blocks
+    size_t cached = 0;
+};
+static BlockCache &block_cache() {
+    static BlockCache *c = new BlockCache();  // never destroyed: plans may outlive static destructors
+    return *c;
+}
+static size_t size_class(size_t b) {
+    constexpr size_t kBig = size_t(64) << 20;
+    if (b > kBig) return (b + kBig - 1) / kBig * kBig;
+    size_t c = 256;
+    while (c < b) c <<= 1;
+    return c;
+}
+static uint64_t cache_key(int dev, size_t cls) { return (uint64_t(cls) << 8) | uint64_t(dev & 0xFF); }
+static void trim_cache(int dev) {  // hipFree every cached block of `dev` (caller holds the lock)
+    BlockCache &c = block_cache();
+    for (auto it = c.free.begin(); it != c.free.end(); ++it) {
+        if (int(it->first & 0xFF) != (dev & 0xFF)) continue;
+        for (void *q : it->second) {
+            (void)hipFree(q);
+            c.cached -= size_t(it->first >> 8);
+        }
+        it->second.clear();
+    }
+}
+static hipError_t pmalloc(void **p, size_t bytes) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const size_t cls = size_class(std::max<size_t>(bytes, 1));
+    BlockCache &c = block_cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto it = c.free.find(cache_key(dev, cls));
+    if (it != c.free.end() && !it->second.empty()) {
+        *p = it->second.back();
+        it->second.pop_back();
+        c.cached -= cls;
+        c.live[*p] = {dev, cls};
+        return hipSuccess;
+    }
+    hipError_t e = hipMalloc(p, cls);
+    if (e == hipErrorOutOfMemory) {
+        (void)hipGetLastError();
+        trim_cache(dev);
+        e = hipMalloc(p, cls);
+    }
+    if (e == hipSuccess) c.live[*p] = {dev, cls};
+    return e;
+}
+static void pfree(void *p) {
+    if (!p) return;
+    BlockCache &c = block_cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto it = c.live.find(p);
+    if (it == c.live.end()) {
+        (void)hipFree(p);
+        return;
+    }
+    const int dev = it->second.first;
+    const size_t cls = it->second.second;
+    c.live.erase(it);
+    if (c.cached + cls > (size_t(16) << 30)) {
+        (void)hipFree(p);
+        return;
+    }
+    c.free[cache_key(dev, cls)].push_back(p);
+    c.cached += cls;
+}
+
+// Plan streams come from a per-device pool as well: a destroyed plan (which waited for
+// its work) returns its streams, and the next plan takes them without hipStreamCreate.
+struct StreamPool {
+    std::mutex mu;
+    std::vector<std::pair<int, hipStream_t>> free;
+};
+static StreamPool &stream_pool() {
+    static StreamPool *p = new StreamPool();
+    return *p;
+}
+static hipError_t pstream_create(hipStream_t *s) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    {
+        StreamPool &p = stream_pool();
+        std::lock_guard<std::mutex> lk(p.mu);
+        for (size_t i = p.free.size(); i-- > 0;)
+            if (p.free[i].first == dev) {
+                *s = p.free[i].second;
+                p.free.erase(p.free.begin() + long(i));
+                return hipSuccess;
+            }
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+static void pstream_release(hipStream_t s) {
+    if (!s) return;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    StreamPool &p = stream_pool();
+    std::lock_guard<std::mutex> lk(p.mu);
+    if (p.free.size() >= 64) {
+        (void)hipStreamDestroy(s);
+        return;
+    }
+    p.free.emplace_back(dev, s);
+}
+
 #define HIPCHK(x)                                                                                   \
     do {                                                                                            \
         hipError_t e_ = (x);                                                                        \
@@ -852,7 +989,7 @@ template <class T>
 static int upload(T *&dptr, const std::vector<T> &h) {
     dptr = nullptr;
     size_t bytes = std::max<size_t>(h.size(), 1) * sizeof(T);
-    HIPCHK(hipMalloc(reinterpret_cast<void **>(&dptr), bytes));
+    HIPCHK(pmalloc(reinterpret_cast<void **>(&dptr), bytes));
     if (!h.empty()) HIPCHK(hipMemcpy(dptr, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
     return MR_OK;
 }
@@ -961,20 +1098,20 @@ struct mr_plan {
         for (Slot &k : slots) {
             for (void *p : {(void *)k.tab, (void *)k.lex, (void *)k.sstate, (void *)k.fb, (void *)k.counter,
                             (void *)k.args, (void *)k.args_fb, (void *)k.args_fill})
-                if (p) (void)hipFree(p);
+                if (p) (void)pfree(p);
             for (hipEvent_t e : {k.ev_hub, k.ev_fill})
                 if (e) (void)hipEventDestroy(e);
         }
-        if (hub_stream) (void)hipStreamDestroy(hub_stream);
+        pstream_release(hub_stream);
         if (!own_tables) {  // the grid's
             d_sinfo = d_rank = d_rank_inv = nullptr;
             d_cell = nullptr;
         }
-        if (d_cell) (void)hipFree(d_cell);
+        if (d_cell) (void)pfree(d_cell);
         for (void *p : {(void *)d_cert_tab, (void *)d_cert_lex, (void *)d_cert_src, (void *)d_cert_st,
                         (void *)d_cert_aux, (void *)d_fb_cert, (void *)d_cert_ones, (void *)d_cert_rec,
                         (void *)d_args_cert})
-            if (p) (void)hipFree(p);
+            if (p) (void)pfree(p);
         for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_rank_inv, (void *)d_src, (void *)d_qb, (void *)d_qd,
                         (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
                         (void *)d_counter, (void *)d_args, (void *)d_dbg, (void *)d_args_fb, (void *)d_near,
@@ -982,7 +1119,7 @@ struct mr_plan {
                         (void *)d_args_lane, (void *)d_args_lane_last,
                         (void *)d_tab,
                         (void *)d_lex, (void *)d_sstate, (void *)d_near_sp, (void *)d_rb_off, (void *)d_rb_cell, (void *)d_ovf})
-            if (p) (void)hipFree(p);
+            if (p) (void)pfree(p);
         if (ev_last && ev_last_orphan) (void)hipEventDestroy(ev_last);
         for (auto &e : timed) {
             (void)hipEventDestroy(e.first);
@@ -990,7 +1127,7 @@ struct mr_plan {
         }
         for (auto &f : timed_fill)  // its end event is the pass's, destroyed above
             if (f.first) (void)hipEventDestroy(f.first);
-        if (stream) (void)hipStreamDestroy(stream);
+        pstream_release(stream);
     }
 };
 
@@ -1173,11 +1310,11 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         return bail(st);
     if (timing_on()) tm_upload = now_ms();
     size_t nres = std::max<uint32_t>(n, 1);
-    if (hipMalloc(reinterpret_cast<void **>(&pl->d_res), nres * sizeof(OutResult)) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void **>(&pl->d_cmd), nres * size_t(max_cmds) * sizeof(OutCmd)) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void **>(&pl->d_ovf), std::max<size_t>(4096, size_t(n) * 8) * sizeof(OutCmd)) !=
+    if (pmalloc(reinterpret_cast<void **>(&pl->d_res), nres * sizeof(OutResult)) != hipSuccess ||
+        pmalloc(reinterpret_cast<void **>(&pl->d_cmd), nres * size_t(max_cmds) * sizeof(OutCmd)) != hipSuccess ||
+        pmalloc(reinterpret_cast<void **>(&pl->d_ovf), std::max<size_t>(4096, size_t(n) * 8) * sizeof(OutCmd)) !=
             hipSuccess ||
-        hipMalloc(reinterpret_cast<void **>(&pl->d_counter), kCtrWords * 4) != hipSuccess ||
+        pmalloc(reinterpret_cast<void **>(&pl->d_counter), kCtrWords * 4) != hipSuccess ||
         hipMemset(pl->d_counter, 0, kCtrWords * 4) != hipSuccess)
         return bail(fail(MR_ERR_DEVICE, "hipMalloc outputs"));
     // algorithm: level-synchronous when the comparator leads with Legs (MR_ALGO=generic forces the
@@ -1196,8 +1333,9 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     }
     uint32_t bytes = lds_bytes(NS, V, pl->grid_in_lds, pl->algo);
     if (bytes > 160 * 1024) return bail(fail(MR_ERR_LIMIT, "special table exceeds LDS"));
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, pl->device) != hipSuccess) return bail(fail(MR_ERR_DEVICE, "props"));
+    const hipDeviceProp_t *propp = device_props(pl->device);
+    if (!propp) return bail(fail(MR_ERR_DEVICE, "props"));
+    const hipDeviceProp_t &prop = *propp;
     pl->cus = uint32_t(prop.multiProcessorCount);
     int per_cu = std::max(1, max_blocks_per_cu(pl->grid_in_lds, pl->algo, bytes));
     uint64_t resident = uint64_t(per_cu) * uint64_t(prop.multiProcessorCount);
@@ -1210,12 +1348,12 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         // is ~95 slots at 1025^2 and ~6 at 4097^2, each looping over the sources)
         const uint64_t budget = (hp.hub ? 2ull : 64ull) << 30;
         blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, budget / slot_bytes));
-        if (hipMalloc(reinterpret_cast<void **>(&pl->d_ws), blocks * slot_bytes) != hipSuccess)
+        if (pmalloc(reinterpret_cast<void **>(&pl->d_ws), blocks * slot_bytes) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "hipMalloc workspace"));
     }
     pl->blocks = uint32_t(blocks);
     if (timing_on()) tm_alloc = now_ms();
-    if (hipStreamCreateWithFlags(&pl->stream, hipStreamNonBlocking) != hipSuccess)
+    if (pstream_create(&pl->stream) != hipSuccess)
         return bail(fail(MR_ERR_DEVICE, "stream"));
     KArgs &ka = pl->ka;
     ka.p = hp.p;
@@ -1258,11 +1396,11 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
             if (std::atoi(e) == 64) align = 64;
         const uint32_t pitch = (hp.p.S + align - 1) / align * align;
         ka.rec_pitch = pitch;
-        if (hipMalloc(reinterpret_cast<void **>(&pl->d_rec),
+        if (pmalloc(reinterpret_cast<void **>(&pl->d_rec),
                       std::max<size_t>(nsrc, 1) * hp.p.S * pitch * sizeof(CellWord)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&pl->d_tab), std::max<size_t>(nsrc, 1) * T * sizeof(Rec)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&pl->d_lex), std::max<size_t>(nsrc, 1) * T * 4) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&pl->d_sstate), std::max<size_t>(nsrc, 1) * 4) != hipSuccess)
+            pmalloc(reinterpret_cast<void **>(&pl->d_tab), std::max<size_t>(nsrc, 1) * T * sizeof(Rec)) != hipSuccess ||
+            pmalloc(reinterpret_cast<void **>(&pl->d_lex), std::max<size_t>(nsrc, 1) * T * 4) != hipSuccess ||
+            pmalloc(reinterpret_cast<void **>(&pl->d_sstate), std::max<size_t>(nsrc, 1) * 4) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "hipMalloc all-destinations outputs"));
         ka.all_mode = 1;
         ka.out_rec = pl->d_rec;
@@ -1275,7 +1413,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
             for (uint32_t k = hp.q_begin[si]; k < hp.q_begin[si + 1]; ++k) pl->src_of_input[hp.q_id[k]] = si;
     }
     if (hp.hub) {
-        if (hipMalloc(reinterpret_cast<void **>(&pl->d_fb), std::max<size_t>(nsrc, 1) * 4) != hipSuccess)
+        if (pmalloc(reinterpret_cast<void **>(&pl->d_fb), std::max<size_t>(nsrc, 1) * 4) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "hub tables"));
         if (hp.near) {
             ka.near = region_table_device(g, prm->homeland, *hp.near);
@@ -1308,9 +1446,9 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         if (const char *e = std::getenv("MR_HUB_BLOCKS")) pl->hub_blocks = uint32_t(std::max(1, std::atoi(e)));
         pl->fb_blocks = pl->blocks;
         pl->fill_per_cu = uint32_t(std::max(1, fill_blocks_per_cu(hp.p.perm)));
-        if (hipMalloc(reinterpret_cast<void **>(&pl->d_args_fb), sizeof(KArgs)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&pl->d_args_hub_last), sizeof(KArgs)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&pl->d_args_fill), sizeof(KArgs)) != hipSuccess)
+        if (pmalloc(reinterpret_cast<void **>(&pl->d_args_fb), sizeof(KArgs)) != hipSuccess ||
+            pmalloc(reinterpret_cast<void **>(&pl->d_args_hub_last), sizeof(KArgs)) != hipSuccess ||
+            pmalloc(reinterpret_cast<void **>(&pl->d_args_fill), sizeof(KArgs)) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "kernel args"));
         // Certified fallback for query plans on hub_kernel (MR_CERT=0: off; MR_CERT_SLOTS:
         // slots per pass, default 8): a flagged source's table goes to a slot, the fill
@@ -1323,14 +1461,14 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
             const size_t T = size_t(NS) + 1;
             const uint32_t pitch = (hp.p.S + 31) / 32 * 32;
             std::vector<uint32_t> ones(cap, 1u);
-            if (hipMalloc(reinterpret_cast<void **>(&pl->d_cert_tab), cap * T * sizeof(Rec)) != hipSuccess ||
-                hipMalloc(reinterpret_cast<void **>(&pl->d_cert_lex), cap * T * 4) != hipSuccess ||
-                hipMalloc(reinterpret_cast<void **>(&pl->d_cert_src), cap * 4) != hipSuccess ||
+            if (pmalloc(reinterpret_cast<void **>(&pl->d_cert_tab), cap * T * sizeof(Rec)) != hipSuccess ||
+                pmalloc(reinterpret_cast<void **>(&pl->d_cert_lex), cap * T * 4) != hipSuccess ||
+                pmalloc(reinterpret_cast<void **>(&pl->d_cert_src), cap * 4) != hipSuccess ||
 
-                hipMalloc(reinterpret_cast<void **>(&pl->d_cert_aux), size_t(cap) * V * 4) != hipSuccess ||
-                hipMalloc(reinterpret_cast<void **>(&pl->d_cert_rec), size_t(cap) * hp.p.S * pitch * 4) != hipSuccess ||
-                hipMalloc(reinterpret_cast<void **>(&pl->d_fb_cert), std::max<size_t>(nsrc, 1) * 4) != hipSuccess ||
-                hipMalloc(reinterpret_cast<void **>(&pl->d_args_cert), sizeof(KArgs)) != hipSuccess ||
+                pmalloc(reinterpret_cast<void **>(&pl->d_cert_aux), size_t(cap) * V * 4) != hipSuccess ||
+                pmalloc(reinterpret_cast<void **>(&pl->d_cert_rec), size_t(cap) * hp.p.S * pitch * 4) != hipSuccess ||
+                pmalloc(reinterpret_cast<void **>(&pl->d_fb_cert), std::max<size_t>(nsrc, 1) * 4) != hipSuccess ||
+                pmalloc(reinterpret_cast<void **>(&pl->d_args_cert), sizeof(KArgs)) != hipSuccess ||
                 upload(pl->d_cert_ones, ones) != MR_OK)
                 return bail(fail(MR_ERR_DEVICE, "certificate slots"));
             pl->cert_cap = cap;
@@ -1349,32 +1487,32 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
             pl->cert_check_gx = uint32_t(std::max<uint64_t>(
                 1, std::min<uint64_t>((uint64_t(V) + 4 * 256 - 1) / (4 * 256), 4ull * prop.multiProcessorCount)));
             // the check's state: one partial per slot and check workgroup, reduced by its readers
-            if (hipMalloc(reinterpret_cast<void **>(&pl->d_cert_st), size_t(cap) * pl->cert_check_gx * kCertSt * 4) !=
+            if (pmalloc(reinterpret_cast<void **>(&pl->d_cert_st), size_t(cap) * pl->cert_check_gx * kCertSt * 4) !=
                 hipSuccess)
                 return bail(fail(MR_ERR_DEVICE, "certificate slots"));
             ka.cert_st = pl->d_cert_st;
             ka.cert_parts = pl->cert_check_gx;
         }
-        if (pl->n_lane && (hipMalloc(reinterpret_cast<void **>(&pl->d_args_lane), sizeof(KArgs)) != hipSuccess ||
-                           hipMalloc(reinterpret_cast<void **>(&pl->d_args_lane_last), sizeof(KArgs)) != hipSuccess))
+        if (pl->n_lane && (pmalloc(reinterpret_cast<void **>(&pl->d_args_lane), sizeof(KArgs)) != hipSuccess ||
+                           pmalloc(reinterpret_cast<void **>(&pl->d_args_lane_last), sizeof(KArgs)) != hipSuccess))
             return bail(fail(MR_ERR_DEVICE, "kernel args"));
     }
 #ifdef MR_HUBDUMP
     if (const char *e = std::getenv("MR_DEBUG_SRC"))
-        if (hipMalloc(reinterpret_cast<void **>(&pl->d_dbg), 64 * 16 * 4) == hipSuccess) {
+        if (pmalloc(reinterpret_cast<void **>(&pl->d_dbg), 64 * 16 * 4) == hipSuccess) {
             (void)hipMemset(pl->d_dbg, 0, 64 * 16 * 4);
             ka.dbg = pl->d_dbg;
             ka.dbg_blocks = uint32_t(std::atoi(e));
         }
 #endif
 #ifdef MR_STAMPS
-    if (hipMalloc(reinterpret_cast<void **>(&pl->d_dbg), (size_t(pl->blocks) * 10 + 16) * 8) == hipSuccess) {
+    if (pmalloc(reinterpret_cast<void **>(&pl->d_dbg), (size_t(pl->blocks) * 10 + 16) * 8) == hipSuccess) {
         (void)hipMemset(pl->d_dbg, 0, (size_t(pl->blocks) * 10 + 16) * 8);
         ka.dbg = pl->d_dbg;
         ka.dbg_blocks = pl->blocks;
     }
 #endif
-    if (hipMalloc(reinterpret_cast<void **>(&pl->d_args), sizeof(KArgs)) != hipSuccess || upload_args(pl) != MR_OK)
+    if (pmalloc(reinterpret_cast<void **>(&pl->d_args), sizeof(KArgs)) != hipSuccess || upload_args(pl) != MR_OK)
         return bail(fail(MR_ERR_DEVICE, "kernel args"));
     // all destinations with the hub: slots of per-pass buffers, so that the specials'
     // solves of the next passes overlap this pass's fill (MR_FILL_OVERLAP=0: off;
@@ -1398,15 +1536,15 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         for (uint32_t i = 0; i < nslots; ++i) {
             mr_plan::Slot &k = pl->slots[i];
             if (i > 0 &&
-                (hipMalloc(reinterpret_cast<void **>(&k.tab), ns * T * sizeof(Rec)) != hipSuccess ||
-                 hipMalloc(reinterpret_cast<void **>(&k.lex), ns * T * 4) != hipSuccess ||
-                 hipMalloc(reinterpret_cast<void **>(&k.sstate), ns * 4) != hipSuccess ||
-                 hipMalloc(reinterpret_cast<void **>(&k.fb), ns * 4) != hipSuccess ||
-                 hipMalloc(reinterpret_cast<void **>(&k.counter), kCtrWords * 4) != hipSuccess ||
+                (pmalloc(reinterpret_cast<void **>(&k.tab), ns * T * sizeof(Rec)) != hipSuccess ||
+                 pmalloc(reinterpret_cast<void **>(&k.lex), ns * T * 4) != hipSuccess ||
+                 pmalloc(reinterpret_cast<void **>(&k.sstate), ns * 4) != hipSuccess ||
+                 pmalloc(reinterpret_cast<void **>(&k.fb), ns * 4) != hipSuccess ||
+                 pmalloc(reinterpret_cast<void **>(&k.counter), kCtrWords * 4) != hipSuccess ||
                  hipMemset(k.counter, 0, kCtrWords * 4) != hipSuccess ||
-                 hipMalloc(reinterpret_cast<void **>(&k.args), sizeof(KArgs)) != hipSuccess ||
-                 hipMalloc(reinterpret_cast<void **>(&k.args_fb), sizeof(KArgs)) != hipSuccess ||
-                 hipMalloc(reinterpret_cast<void **>(&k.args_fill), sizeof(KArgs)) != hipSuccess))
+                 pmalloc(reinterpret_cast<void **>(&k.args), sizeof(KArgs)) != hipSuccess ||
+                 pmalloc(reinterpret_cast<void **>(&k.args_fb), sizeof(KArgs)) != hipSuccess ||
+                 pmalloc(reinterpret_cast<void **>(&k.args_fill), sizeof(KArgs)) != hipSuccess))
                 return bail(fail(MR_ERR_DEVICE, "all-destinations slots"));
             if (hipEventCreateWithFlags(&k.ev_hub, hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&k.ev_fill, hipEventDisableTiming) != hipSuccess)
@@ -1418,7 +1556,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
                 if (ua != MR_OK) return bail(fail(MR_ERR_DEVICE, "kernel args"));
             }
         }
-        if (hipStreamCreateWithFlags(&pl->hub_stream, hipStreamNonBlocking) != hipSuccess)
+        if (pstream_create(&pl->hub_stream) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "hub stream"));
         pl->overlap = true;
         const char *fz = std::getenv("MR_FILL_FUSED");
@@ -1949,8 +2087,105 @@ static uint32_t record_cmds(const OutResult &o) {
     return (status == MR_OK || status == int(kStatusOverflow)) ? (o.ncmd_status & 0xFFFFu) : 0u;
 }
 
+// the grid's CellIndex-by-rank table on the plan's device (uploaded once)
+static const mr_cell_index *grid_idx_rank(const mr_grid *g, int dev) {
+    std::lock_guard<std::mutex> lk(g->near_mu);
+    if (g->d_dev != dev) return nullptr;
+    if (!g->d_idx_rank) {
+        std::vector<mr_cell_index> t(g->V);
+        for (uint32_t r = 0; r < g->V; ++r) t[r] = g->idx[g->rank_inv[r]];
+        mr_cell_index *d = nullptr;
+        if (hipMalloc(reinterpret_cast<void **>(&d), std::max<size_t>(t.size(), 1) * sizeof(mr_cell_index)) != hipSuccess)
+            return nullptr;
+        if (!t.empty() && hipMemcpy(d, t.data(), t.size() * sizeof(mr_cell_index), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(d);
+            return nullptr;
+        }
+        g->d_idx_rank = d;
+    }
+    return g->d_idx_rank;
+}
+
+// mr_plan_fetch with the records expanded on the device (mr_k_decode.hip) into the ABI
+// layout, then one copy of the results and one of the commands; the host only marks the
+// queries that had no record (invalid indices) and finds the status to return.  Returns
+// false (nothing written) when the device path does not apply (the host decoder runs).
+static bool plan_fetch_device(mr_plan *pl, mr_result *results, mr_command *pool, uint64_t pool_cap, int &ret) {
+    const HostPlan &hp = pl->hp;
+    const uint32_t nq = hp.nq, nrec = uint32_t(hp.q_id.size()), mc = hp.p.max_cmds;
+    if (const char *e = std::getenv("MR_HOST_DECODE"))
+        if (!std::strcmp(e, "1")) return false;
+    if (!pool || !nq || pl->all_mode) return false;
+    const mr_cell_index *idx_rank = grid_idx_rank(pl->grid, pl->device);
+    if (!idx_rank) return false;
+    const double tm0 = timing_on() ? now_ms() : 0.0;
+    if (!plan_sync(pl)) return (ret = fail(MR_ERR_DEVICE, "sync")), true;
+    uint32_t flags = 0;
+    if ((ret = check_device_errors(pl, flags)) != MR_OK) return true;
+    uint32_t ctr[kCtrWords];
+    if ((ret = read_counters(pl, ctr)) != MR_OK) return true;
+    const uint32_t nov = std::min(ctr[kCtrLastOvf], pl->ka.ovf_cap);
+    const uint64_t bound = uint64_t(nrec) * mc + nov, pcap = std::min<uint64_t>(pool_cap, std::max<uint64_t>(bound, 1));
+    const CmdScale cs = cmd_scale(hp);
+    size_t temp_bytes = 0;
+    (void)decode_records_device(nullptr, nullptr, nullptr, 0, nullptr, 0, nq, mc, nullptr, 0, 0, 0, 0, 0, 0, nullptr,
+                                nullptr, nullptr, &temp_bytes, nullptr, nullptr, 0, nullptr, pl->stream);
+    void *scratch = nullptr, *d_out = nullptr, *d_pool = nullptr;
+    const size_t cnt_b = (size_t(nq) * 4 + 255) / 256 * 256, tail = 256;
+    if (pmalloc(&scratch, 2 * cnt_b + temp_bytes + tail) != hipSuccess ||
+        pmalloc(&d_out, size_t(nq) * sizeof(mr_result)) != hipSuccess ||
+        pmalloc(&d_pool, size_t(pcap) * sizeof(mr_command)) != hipSuccess) {
+        pfree(scratch);
+        pfree(d_out);
+        return false;  // the host decoder needs no device memory
+    }
+    uint32_t *cnt = static_cast<uint32_t *>(scratch), *off = reinterpret_cast<uint32_t *>(static_cast<char *>(scratch) + cnt_b);
+    uint32_t *err = reinterpret_cast<uint32_t *>(static_cast<char *>(scratch) + 2 * cnt_b);
+    void *temp = static_cast<char *>(scratch) + 2 * cnt_b + tail;
+    hipError_t e = decode_records_device(pl->ka.out_res, pl->ka.out_cmd, pl->ka.ovf, nov, pl->d_qi, nrec, nq, mc, idx_rank,
+                                         pl->grid->V, cs.rgt, cs.soe, cs.shq, cs.sfm, cs.ff, cnt, off, temp, &temp_bytes,
+                                         static_cast<mr_result *>(d_out), static_cast<mr_command *>(d_pool), pcap, err,
+                                         pl->stream);
+    uint32_t tailw[3] = {0, 0, 0};  // err, off and count of the last query: the commands written
+    if (e == hipSuccess) e = hipMemcpyAsync(&tailw[0], err, 4, hipMemcpyDeviceToHost, pl->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(&tailw[1], off + (nq - 1), 4, hipMemcpyDeviceToHost, pl->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(&tailw[2], cnt + (nq - 1), 4, hipMemcpyDeviceToHost, pl->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(results, d_out, size_t(nq) * sizeof(mr_result), hipMemcpyDeviceToHost, pl->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(pl->stream);
+    const uint64_t total = uint64_t(tailw[1]) + tailw[2], ncopy = std::min<uint64_t>(total, pcap);
+    if (e == hipSuccess && ncopy)
+        e = hipMemcpy(pool, d_pool, size_t(ncopy) * sizeof(mr_command), hipMemcpyDeviceToHost);
+    pfree(scratch);
+    pfree(d_out);
+    pfree(d_pool);
+    const double tm1 = timing_on() ? now_ms() : 0.0;
+    if (e != hipSuccess) return (ret = fail(MR_ERR_DEVICE, std::string("device fetch: ") + hipGetErrorString(e))), true;
+    if (tailw[0] & 1u) return (ret = fail(MR_ERR_DEVICE, "malformed record (overflow tag or cell rank)")), true;
+    // queries without a record (an invalid index), and the first error in query order
+    // (a label whose commands did not fit the caller's pool counts as MR_ERR_CAPACITY)
+    ret = MR_OK;
+    for (uint32_t i = 0; i < nq; ++i) {
+        mr_result &r = results[i];
+        if (hp.q_status[i] != MR_OK) {
+            std::memset(&r, 0, sizeof(r));
+            r.status = hp.q_status[i];
+        }
+        if (ret != MR_OK) continue;
+        if (r.status != MR_OK) ret = r.status;
+        else if (uint64_t(r.command_offset) + r.n_commands > pool_cap) ret = MR_ERR_CAPACITY;
+    }
+    if (timing_on())
+        std::fprintf(stderr, "MR_TIMING fetch n=%u (device decode): kernels + copies %.2f ms, host %.2f ms\n", nq,
+                     tm1 - tm0, now_ms() - tm1);
+    return true;
+}
+
 extern "C" int mr_plan_fetch(mr_plan *pl, mr_result *results, mr_command *pool, uint64_t pool_cap) {
     if (!pl || (pl->hp.nq && !results)) return fail(MR_ERR_INVALID_ARG, "null argument");
+    {
+        int ret = MR_OK;
+        if (plan_fetch_device(pl, results, pool, pool_cap, ret)) return ret;
+    }
     const double tm0 = timing_on() ? now_ms() : 0.0;
     std::vector<OutResult> res;
     std::vector<OutCmd> cmd, ovf;

@@ -1,0 +1,131 @@
+// mr_k_decode.hip — mr_plan_fetch on the device: the compact records a pass wrote
+// (OutResult + command slots / overflow pool, grouped by source) expanded into the ABI's
+// mr_result (query order) and mr_command pool, the layout the host decoder writes
+// (mr_host.cpp decode_record): query i's commands at the exclusive prefix sum of the
+// command counts of queries 0 .. i-1.  The host then copies both arrays once.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "../../include/marshrutka_pf.h"
+#include "mr_engine.hpp"
+
+namespace mr {
+
+// the record's command count as the pool counts it (0: no commands to write)
+__device__ __forceinline__ uint32_t rec_cmds(const OutResult &o) {
+    const int st = int(o.ncmd_status >> 16) - 16;
+    return (st == MR_OK || st == int(kStatusOverflow)) ? (o.ncmd_status & 0xFFFFu) : 0u;
+}
+
+__global__ void decode_count_kernel(const OutResult *__restrict__ res, const uint32_t *__restrict__ q_id, uint32_t nrec,
+                                    uint32_t *__restrict__ cnt) {
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nrec; k += gridDim.x * blockDim.x)
+        cnt[q_id[k]] = rec_cmds(res[k]);
+}
+
+struct DecodeScale {
+    uint32_t rgt, soe, shq, sfm, ff;
+};
+
+// one thread per record: its mr_result at its query, its commands at the query's offset
+// when they fit pool_cap (else the capacity flag); err bit 0: a malformed record
+__global__ void decode_write_kernel(const OutResult *__restrict__ res, const OutCmd *__restrict__ slots,
+                                    const OutCmd *__restrict__ ovf, uint32_t novf, const uint32_t *__restrict__ q_id,
+                                    uint32_t nrec, uint32_t mc, const uint32_t *__restrict__ off,
+                                    const mr_cell_index *__restrict__ idx_rank, uint32_t V, DecodeScale cs,
+                                    mr_result *__restrict__ out, mr_command *__restrict__ pool, unsigned long long pool_cap,
+                                    uint32_t *__restrict__ err) {
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nrec; k += gridDim.x * blockDim.x) {
+        const OutResult o = res[k];
+        const uint32_t q = q_id[k];
+        int status = int(o.ncmd_status >> 16) - 16;
+        mr_result r;
+        r.legs = o.legs;
+        r.money = o.money;
+        r.time_s = int64_t(o.time);
+        r.n_commands = o.ncmd_status & 0xFFFFu;
+        r.command_offset = off[q];
+        r.reserved = 0;
+        const OutCmd *src = slots + (unsigned long long)k * mc;
+        if (status == MR_NOT_FOUND) r.n_commands = 0;
+        if (status == int(kStatusOverflow)) {  // its commands in the overflow pool at {offset, count}
+            const OutCmd tag = src[0];
+            if (!mc || tag.kp != kOvfTag || tag.to != r.n_commands || (unsigned long long)tag.from + tag.to > novf) {
+                atomicOr(err, 1u);
+                r.n_commands = 0;
+            }
+            src = ovf + tag.from;
+            status = MR_OK;
+        } else if (status == MR_OK && r.n_commands > mc) {
+            atomicOr(err, 1u);
+        }
+        r.status = status;
+        out[q] = r;
+        if (status != MR_OK) continue;
+        if ((unsigned long long)r.command_offset + r.n_commands > pool_cap) {
+            atomicOr(err, 2u);
+            continue;
+        }
+        for (uint32_t j = 0; j < r.n_commands; ++j) {
+            const OutCmd c = src[j];
+            const uint32_t kind = c.kp >> 29, pay = c.kp & 0x1FFFFFFFu;
+            mr_command m;
+            m.kind = uint8_t(kind);
+            m.reserved[0] = m.reserved[1] = m.reserved[2] = 0;
+            m.legs = 0;
+            m.money = 0;
+            m.fleetfoot = 0;
+            m.time_s = 0;
+            switch (kind) {
+                case kCentral: m.time_s = int64_t(10) * pay; break;
+                case kStandard:
+                    m.legs = pay;
+                    m.time_s = int64_t(180) * pay;
+                    m.fleetfoot = cs.ff;
+                    break;
+                case kCaravan:
+                    m.time_s = int64_t(cs.rgt) * (pay >> 1);
+                    m.money = (pay >> 1) * ((pay & 1u) ? 5u : 2u);
+                    break;
+                case kSoE: m.money = cs.soe; break;
+                case kSHQ: m.money = cs.shq; break;
+                case kSFm: m.money = cs.sfm; break;
+                default: break;
+            }
+            if (kind > kSFm || c.from >= V || c.to >= V) {
+                atomicOr(err, 1u);
+                continue;
+            }
+            m.from = idx_rank[c.from];  // device commands name cells by rank
+            m.to = idx_rank[c.to];
+            pool[(unsigned long long)r.command_offset + j] = m;
+        }
+    }
+}
+
+// Device decode of a plan's records into out (n_queries results) and pool; cnt / off
+// are n_queries words of scratch (cnt zeroed here), temp scan scratch of *temp_bytes
+// (a null temp returns the size needed).  err: one word.
+hipError_t decode_records_device(const OutResult *res, const OutCmd *slots, const OutCmd *ovf, uint32_t novf,
+                                 const uint32_t *q_id, uint32_t nrec, uint32_t nq, uint32_t mc,
+                                 const mr_cell_index *idx_rank, uint32_t V, uint32_t rgt, uint32_t soe, uint32_t shq,
+                                 uint32_t sfm, uint32_t ff, uint32_t *cnt, uint32_t *off, void *temp, size_t *temp_bytes,
+                                 mr_result *out, mr_command *pool, unsigned long long pool_cap, uint32_t *err,
+                                 hipStream_t stream) {
+    if (!temp) return hipcub::DeviceScan::ExclusiveSum(nullptr, *temp_bytes, cnt, off, int(nq), stream);
+    hipError_t e = hipMemsetAsync(cnt, 0, size_t(nq) * 4, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(err, 0, 4, stream);
+    const uint32_t blocks = std::max(1u, std::min(4096u, (nrec + 255) / 256));
+    if (e == hipSuccess && nrec)
+        hipLaunchKernelGGL(decode_count_kernel, dim3(blocks), dim3(256), 0, stream, res, q_id, nrec, cnt);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, cnt, off, int(nq), stream);
+    const DecodeScale cs{rgt, soe, shq, sfm, ff};
+    if (e == hipSuccess && nrec)
+        hipLaunchKernelGGL(decode_write_kernel, dim3(blocks), dim3(256), 0, stream, res, slots, ovf, novf, q_id, nrec, mc,
+                           off, idx_rank, V, cs, out, pool, pool_cap, err);
+    if (e == hipSuccess) e = hipGetLastError();
+    return e;
+}
+
+}  // namespace mr

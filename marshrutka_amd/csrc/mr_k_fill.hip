@@ -28,7 +28,7 @@ hipError_t launch_fill(const KArgs *d_args, const uint32_t perm[3], uint32_t gx,
 int fill_blocks_per_cu(const uint32_t perm[3]) {
     const void *fn = fill_fn(perm);
     int n = 0;
-    if (fn) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kBS, 0);
+    if (fn) n = occupancy_cached(fn, kBS, 0);
     return n;
 }
 
@@ -62,7 +62,7 @@ hipError_t launch_hub_fill(const KArgs *hub_args, const KArgs *fill_args, const 
 int hub_fill_blocks_per_cu(const uint32_t perm[3], uint32_t spw, uint32_t lds_bytes) {
     const void *fn = hub_fill_fn(perm, spw);
     int n = 0;
-    if (fn) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kBS, lds_bytes);
+    if (fn) n = occupancy_cached(fn, kBS, lds_bytes);
     return n;
 }
 

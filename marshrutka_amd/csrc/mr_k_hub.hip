@@ -27,7 +27,7 @@ hipError_t launch_hub(const KArgs *d_args, const uint32_t perm[3], uint32_t spw,
 int hub_blocks_per_cu(const uint32_t perm[3], uint32_t spw, bool nonlin, uint32_t bytes) {
     int n = 0;
     const void *fn = hub_fn(perm, spw, nonlin);
-    if (fn) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kBS, bytes);
+    if (fn) n = occupancy_cached(fn, kBS, bytes);
     return n;
 }
 

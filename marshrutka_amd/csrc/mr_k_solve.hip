@@ -29,7 +29,7 @@ hipError_t launch_solve(const KArgs *d_args, bool grid_in_lds, uint32_t algo, ui
 
 int max_blocks_per_cu(bool grid_in_lds, uint32_t algo, uint32_t bytes) {
     int n = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, select_kernel(grid_in_lds, algo), kBS, bytes);
+    n = occupancy_cached(select_kernel(grid_in_lds, algo), kBS, bytes);
     return n;
 }
 

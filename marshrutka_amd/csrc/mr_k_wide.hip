@@ -37,7 +37,7 @@ hipError_t launch_hub_wide(const KArgs *d_args, const uint32_t perm[3], uint32_t
 int hub_wide_blocks_per_cu(const uint32_t perm[3], uint32_t NS, uint32_t bytes) {
     int n = 0;
     const void *fn = wide_fn(perm, NS);
-    if (fn) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kBS, bytes);
+    if (fn) n = occupancy_cached(fn, kBS, bytes);
     return n;
 }
 

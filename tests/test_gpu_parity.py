@@ -430,3 +430,39 @@ def _device_words(ptr: int, nbytes: int):
     out = np.empty(nbytes // 4, dtype=np.uint32)
     assert hip.hipMemcpy(out.ctypes.data, C.c_void_p(ptr), nbytes, 2) == 0  # hipMemcpyDeviceToHost
     return out
+
+
+@pytest.mark.parametrize("max_cmds", [1, 3, 16])
+def test_device_fetch_matches_host_decode(eng, monkeypatch, max_cmds):
+    """mr_plan_fetch expands the records on the device (mr_k_decode.hip) and copies the
+    ABI arrays once; MR_HOST_DECODE=1 keeps the host decoder.  Both must write the same
+    bytes: invalid queries, labels in the overflow pool (few command slots), Time-first
+    Fleetfoot labels, and a caller pool too short for every label (MR_ERR_CAPACITY)."""
+    import ctypes as C
+    from marshrutka_amd.abi import MR_ERR_CAPACITY, mr_command, mr_query, mr_result
+    from marshrutka_amd import pathfinder as pf
+    m = SyntheticMap(65, campfires_per_homeland=5, seed=11)
+    g = eng.MapGrid(m.cells())
+    qs = random_queries(m, 3000, 12)
+    qs[5] = (CellIndex(1, 0, 999, 999), qs[5][1])  # not a cell of the grid
+    qs[77] = (qs[77][0], CellIndex(2, 1, 999, 0))
+    for params in (Params(), Params(fleetfoot=2, sort_by=(SORT_TIME, SORT_MONEY), use_sfm=True)):
+        out = {}
+        for mode in ("device", "host"):
+            if mode == "host":
+                monkeypatch.setenv("MR_HOST_DECODE", "1")
+            else:
+                monkeypatch.delenv("MR_HOST_DECODE", raising=False)
+            plan = eng.Plan(g, params, qs, max_cmds=max_cmds)
+            plan.run()
+            for cap in (len(qs) * 24, 500):
+                res = (mr_result * len(qs))()
+                pool = (mr_command * cap)()
+                st = pf.lib().mr_plan_fetch(plan.handle, res, pool, cap)
+                out[(mode, cap)] = (st, bytes(res), bytes(pool))
+        for cap in (len(qs) * 24, 500):
+            d, h = out[("device", cap)], out[("host", cap)]
+            assert d[0] == h[0], (cap, d[0], h[0])
+            assert d[1] == h[1], cap
+            assert d[2] == h[2], cap
+        assert out[("device", 500)][0] == MR_ERR_CAPACITY or out[("device", 500)][0] < 0
