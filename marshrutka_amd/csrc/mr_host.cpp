@@ -187,8 +187,10 @@ struct mr_grid {
     int32_t gy(uint32_t v) const { return int32_t(v / S) - int32_t(H); }
     // The geometric layout (checked at creation): homeland cell (h, x, y) at vertex
     // vc + x ux[h] + y uy[h], border cell (b, s) at vc + s ub[b]; find() computes the
-    // vertex and confirms it against idx[] (the hash map is the fallback).
-    bool fast = false;
+    // vertex and confirms it against idx[] (the hash map is the fallback).  When the
+    // formula was verified for every cell at creation (`exact`), the confirmation is
+    // skipped: a query batch's lookups then touch no per-cell table.
+    bool fast = false, exact = false;
     int64_t ux[4] = {0, 0, 0, 0}, uy[4] = {0, 0, 0, 0}, ub[4] = {0, 0, 0, 0};
     bool find(const mr_cell_index &c, uint32_t &v) const {
         if (!canonical(c)) return false;
@@ -198,6 +200,10 @@ struct mr_grid {
             else if (c.kind == MR_CELL_HOMELAND && c.x <= H && c.y <= H) w = int64_t(vc) + c.x * ux[c.sub] + c.y * uy[c.sub];
             else if (c.kind == MR_CELL_BORDER && c.x <= H) w = int64_t(vc) + c.x * ub[c.sub];
             if (w >= 0 && w < int64_t(V)) {
+                if (exact) {
+                    v = uint32_t(w);
+                    return true;
+                }
                 const mr_cell_index &e = idx[size_t(w)];
                 if (e.kind == c.kind && e.sub == c.sub && e.x == c.x && e.y == c.y) {
                     v = uint32_t(w);
@@ -287,6 +293,17 @@ extern "C" int mr_grid_create(const mr_cell *cells, uint32_t n, mr_grid **out) {
             ok = int64_t(v11) == int64_t(vc) + g->ux[h] + g->uy[h];
         }
         g->fast = ok;
+        // every cell where the formula puts it: find() may then trust the formula
+        bool all = ok;
+        for (uint32_t v = 0; v < n && all; ++v) {
+            const mr_cell_index &c = g->idx[v];
+            int64_t w = -1;
+            if (c.kind == MR_CELL_CENTER) w = vc;
+            else if (c.kind == MR_CELL_HOMELAND) w = int64_t(vc) + c.x * g->ux[c.sub] + c.y * g->uy[c.sub];
+            else if (c.kind == MR_CELL_BORDER) w = int64_t(vc) + c.x * g->ub[c.sub];
+            all = w == int64_t(v);
+        }
+        g->exact = all;
     }
     // rank = position in the derived Ord of CellIndex (src/index.rs:41-46)
     {
@@ -1071,6 +1088,7 @@ struct mr_plan {
     uint32_t slot = 0;     // slot index of the d_* fields
     bool own_tables = true;  // d_sinfo / d_rank / d_rank_inv / d_cell: false = the grid's shared copies
     uint2 *d_cell = nullptr;
+    uint32_t *d_qblock = nullptr;  // the per-batch arrays (d_src, d_qb, d_qd, d_qi point into it)
     // certified fallback (query hub plans): per slot a label table,
     // boundary ranks, source, cell words, check state and sweep list; the fill's
     // argument block over the slots
@@ -1103,6 +1121,8 @@ struct mr_plan {
                 if (e) (void)hipEventDestroy(e);
         }
         pstream_release(hub_stream);
+        d_src = d_qb = d_qd = d_qi = nullptr;  // inside d_qblock
+        pfree(d_qblock);
         if (!own_tables) {  // the grid's
             d_sinfo = d_rank = d_rank_inv = nullptr;
             d_cell = nullptr;
@@ -1304,10 +1324,22 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
             (st = upload(pl->d_rank, g->rank)) || (st = upload(pl->d_rank_inv, g->rank_inv)))
             return bail(st);
     }
-    if ((st = upload(pl->d_sp, hp.sp)) ||
-        (st = upload(pl->d_hubs, hp.hubs)) || (st = upload(pl->d_src, hp.src_v)) || (st = upload(pl->d_qb, hp.q_begin)) ||
-        (st = upload(pl->d_qd, hp.q_dst)) || (st = upload(pl->d_qi, hp.q_id)))
+    if ((st = upload(pl->d_sp, hp.sp)) || (st = upload(pl->d_hubs, hp.hubs)))
         return bail(st);
+    {  // the per-batch arrays in one device block and one copy (sources, offsets, destinations, query ids)
+        const size_t a0 = 0, a1 = a0 + (hp.src_v.size() + 63) / 64 * 64, a2 = a1 + (hp.q_begin.size() + 63) / 64 * 64,
+                     a3 = a2 + (hp.q_dst.size() + 63) / 64 * 64, a4 = a3 + (hp.q_id.size() + 63) / 64 * 64;
+        std::vector<uint32_t> pack(std::max<size_t>(a4, 1));
+        std::copy(hp.src_v.begin(), hp.src_v.end(), pack.begin() + long(a0));
+        std::copy(hp.q_begin.begin(), hp.q_begin.end(), pack.begin() + long(a1));
+        std::copy(hp.q_dst.begin(), hp.q_dst.end(), pack.begin() + long(a2));
+        std::copy(hp.q_id.begin(), hp.q_id.end(), pack.begin() + long(a3));
+        if ((st = upload(pl->d_qblock, pack))) return bail(st);
+        pl->d_src = pl->d_qblock + a0;
+        pl->d_qb = pl->d_qblock + a1;
+        pl->d_qd = pl->d_qblock + a2;
+        pl->d_qi = pl->d_qblock + a3;
+    }
     if (timing_on()) tm_upload = now_ms();
     size_t nres = std::max<uint32_t>(n, 1);
     if (pmalloc(reinterpret_cast<void **>(&pl->d_res), nres * sizeof(OutResult)) != hipSuccess ||
@@ -2152,8 +2184,28 @@ static bool plan_fetch_device(mr_plan *pl, mr_result *results, mr_command *pool,
     if (e == hipSuccess) e = hipMemcpyAsync(&tailw[2], cnt + (nq - 1), 4, hipMemcpyDeviceToHost, pl->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(results, d_out, size_t(nq) * sizeof(mr_result), hipMemcpyDeviceToHost, pl->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(pl->stream);
-    const uint64_t total = uint64_t(tailw[1]) + tailw[2], ncopy = std::min<uint64_t>(total, pcap);
-    if (e == hipSuccess && ncopy)
+    // queries without a record (an invalid index), and the status to return: the first
+    // error in query order, or MR_ERR_CAPACITY once a label's commands do not fit the
+    // caller's pool (written up to the first such label), as the host decoder does
+    const uint64_t total = uint64_t(tailw[1]) + tailw[2];
+    uint64_t end = total;
+    ret = MR_OK;
+    if (e == hipSuccess && !(tailw[0] & 1u))
+        for (uint32_t i = 0; i < nq; ++i) {
+            mr_result &r = results[i];
+            if (hp.q_status[i] != MR_OK) {
+                std::memset(&r, 0, sizeof(r));
+                r.status = hp.q_status[i];
+            }
+            if (r.status == MR_OK && uint64_t(r.command_offset) + r.n_commands > pool_cap) {
+                end = std::min<uint64_t>(end, r.command_offset);
+                ret = MR_ERR_CAPACITY;  // (the host decoder's rule: a short pool wins over other errors)
+            } else if (ret == MR_OK && r.status != MR_OK) {
+                ret = r.status;
+            }
+        }
+    const uint64_t ncopy = std::min<uint64_t>(end, pcap);
+    if (e == hipSuccess && ncopy && !(tailw[0] & 1u))
         e = hipMemcpy(pool, d_pool, size_t(ncopy) * sizeof(mr_command), hipMemcpyDeviceToHost);
     pfree(scratch);
     pfree(d_out);
@@ -2161,19 +2213,6 @@ static bool plan_fetch_device(mr_plan *pl, mr_result *results, mr_command *pool,
     const double tm1 = timing_on() ? now_ms() : 0.0;
     if (e != hipSuccess) return (ret = fail(MR_ERR_DEVICE, std::string("device fetch: ") + hipGetErrorString(e))), true;
     if (tailw[0] & 1u) return (ret = fail(MR_ERR_DEVICE, "malformed record (overflow tag or cell rank)")), true;
-    // queries without a record (an invalid index), and the first error in query order
-    // (a label whose commands did not fit the caller's pool counts as MR_ERR_CAPACITY)
-    ret = MR_OK;
-    for (uint32_t i = 0; i < nq; ++i) {
-        mr_result &r = results[i];
-        if (hp.q_status[i] != MR_OK) {
-            std::memset(&r, 0, sizeof(r));
-            r.status = hp.q_status[i];
-        }
-        if (ret != MR_OK) continue;
-        if (r.status != MR_OK) ret = r.status;
-        else if (uint64_t(r.command_offset) + r.n_commands > pool_cap) ret = MR_ERR_CAPACITY;
-    }
     if (timing_on())
         std::fprintf(stderr, "MR_TIMING fetch n=%u (device decode): kernels + copies %.2f ms, host %.2f ms\n", nq,
                      tm1 - tm0, now_ms() - tm1);
