@@ -34,6 +34,7 @@ namespace mr {
 // boundary), and for a walk label its boundary and run length
 struct CertEntry {
     uint32_t m0, m1, m2, len, lex, wb, wk, pad;
+    uint32_t sb, sk, su, pad2;  // a Scroll-of-Escape-region label: its walk (b, k) and the cell (rank) it ends at
 };
 // a walk label (b, k) as comparator keys: c1..c3 in comparator order, length, rank of b
 struct CertLab {
@@ -90,8 +91,10 @@ __device__ __forceinline__ void cert_load_table(const KArgs *__restrict__ a, uin
     for (uint32_t t = threadIdx.x; t < T; t += blockDim.x) {
         const Rec r = a->cert_tab[(unsigned long long)slot * T + t];
         const bool walk = r.ntail() == 1 && (r.kp0 >> 29) == kStandard && t != 0;
+        const bool soe = r.ntail() == 2 && (r.kp0 >> 29) == kStandard && t != 0;  // walk, then SoE from its end
         E[t] = CertEntry{r.m[0], r.m[1], r.m[2], r.len(), a->cert_lex[(unsigned long long)slot * T + t],
-                         walk ? r.parent() : kCertNoB, walk ? (r.kp0 & 0x1FFFFFFFu) : 0u, 0u};
+                         walk ? r.parent() : kCertNoB, walk ? (r.kp0 & 0x1FFFFFFFu) : 0u, 0u,
+                         soe ? r.parent() : kCertNoB, soe ? (r.kp0 & 0x1FFFFFFFu) : 0u, soe ? r.u : kNone32, 0u};
     }
 }
 
@@ -160,9 +163,37 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
                 fail = fail || (any && !below);
             }
         } else {  // a plain cell: exactly its neighbours' least extension
-            const CertLab o = cert_walk(p, E, (cw >> kStBShift) & kNone10, cw & kStKMask);
+            const uint32_t b = (cw >> kStBShift) & kNone10, k = cw & kStKMask;
+            const CertLab o = cert_walk(p, E, b, k);
             own1 = o.c1;
             fail = fail || !any || !cert_same(o, best);
+            // Its Scroll of Escape into its region's campfire c (the repair sweep may have
+            // changed the cell after the hub built c's label from the closed form): c's
+            // SoE-region label must start from this cell's word when it names this cell
+            // (pull), and no other cell's SoE may reach c first (push; a tie on metrics and
+            // length would need the command lists: counted as a failure).
+            const uint32_t rc = p.use_soe ? (a->sinfo[v] >> 10) & kNone10 : kNone10;
+            if (rc != kNone10) {
+                const CertEntry &e = E[rc];
+                const CertLab &w = o;
+                // metrics of the walk, then + the scroll's money
+                const uint32_t wm0 = E[b].m0 + k, wm1 = E[b].m1 + p.soe_cost,
+                               wm2 = E[b].m2 + run_time_ff(k, p.ff_num, p.ff_den);
+                const uint32_t x1 = pick(p, 0, wm0, wm1, wm2), x2 = pick(p, 1, wm0, wm1, wm2), x3 = pick(p, 2, wm0, wm1, wm2),
+                               xl = w.len + 1u;
+                const uint32_t c1 = pick(p, 0, e.m0, e.m1, e.m2), c2 = pick(p, 1, e.m0, e.m1, e.m2),
+                               c3 = pick(p, 2, e.m0, e.m1, e.m2);
+                bool bad;
+                if (e.su == a->rank[v]) {
+                    bad = e.sb != b || e.sk != k;
+                } else {  // c strictly first
+                    bad = !(c1 != x1 ? c1 < x1 : (c2 != x2 ? c2 < x2 : (c3 != x3 ? c3 < x3 : e.len < xl)));
+                }
+                if (bad) {
+                    own1 = min(own1, min(c1, x1));
+                    fail = true;
+                }
+            }
         }
         if (fail) {
             key = min(key, any ? min(own1, best.c1) : own1);
