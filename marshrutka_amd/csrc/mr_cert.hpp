@@ -184,10 +184,18 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
                 const uint32_t c1 = pick(p, 0, e.m0, e.m1, e.m2), c2 = pick(p, 1, e.m0, e.m1, e.m2),
                                c3 = pick(p, 2, e.m0, e.m1, e.m2);
                 bool bad;
-                if (e.su == a->rank[v]) {
+                const uint32_t rv = a->rank[v];
+                if (e.su == rv) {
                     bad = e.sb != b || e.sk != k;
-                } else {  // c strictly first
+                } else if (c1 != x1 || c2 != x2 || c3 != x3 || e.len != xl) {  // c strictly first
                     bad = !(c1 != x1 ? c1 < x1 : (c2 != x2 ? c2 < x2 : (c3 != x3 ? c3 < x3 : e.len < xl)));
+                } else if (e.sb != kCertNoB) {
+                    // equal metrics and length against c's own SoE-region label full(sb) ++
+                    // [Std sb -> su] ++ [SoE su -> c]: the lists differ inside the boundaries'
+                    // labels (their ranks decide) or, from one boundary, in the walk's end cell
+                    bad = b != e.sb ? E[b].lex < E[e.sb].lex : rv < e.su;
+                } else {
+                    bad = true;  // a tie with another kind of label: the lists would decide
                 }
                 if (bad) {
                     own1 = min(own1, min(c1, x1));
