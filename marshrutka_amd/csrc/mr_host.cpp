@@ -757,50 +757,61 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
             }
         }
     }
-    // queries grouped by source (counting sort on the source vertex; the V-sized
-    // counters are per-thread scratch, zero between plans)
+    // Queries grouped by source vertex, sources ascending, each source's queries in
+    // input order: a stable sort of the valid queries by source, 13-bit LSD radix passes
+    // over the batch (two while V < 2^26).  The counting sort it replaces touched two
+    // V-sized arrays at random (5.5 ms at 125k queries on 1025^2).
     const uint32_t V = g->V;
     hp.nq = n;
     hp.q_status.assign(n, MR_OK);
-    std::vector<uint32_t> qs_src(n), qs_dst(n);
-    static thread_local std::vector<uint32_t> count, start;
-    if (count.size() < size_t(V) + 1) {
-        count.assign(size_t(V) + 1, 0);
-        start.assign(size_t(V) + 1, 0);
-    }
+    std::vector<uint64_t> kv, tmp;  // source << 32 | query index
+    kv.reserve(n);
+    std::vector<uint32_t> qs_dst(n);
     for (uint32_t i = 0; i < n; ++i) {
         uint32_t a, b;
         if (!g->find(qs[i].from, a) || !g->find(qs[i].to, b)) {
             hp.q_status[i] = MR_ERR_INVALID_INDEX;
-            qs_src[i] = kNone32;
             continue;
         }
-        qs_src[i] = a;
         qs_dst[i] = b;
-        count[a]++;
+        kv.push_back((uint64_t(a) << 32) | i);
+    }
+    const uint32_t m = uint32_t(kv.size());
+    tmp.resize(m);
+    constexpr uint32_t kBits = 13, kB = 1u << kBits;
+    const uint32_t passes = V <= (1u << (2 * kBits)) ? 2u : 3u;
+    std::vector<uint32_t> hist(kB);
+    for (uint32_t pass = 0; pass < passes; ++pass) {
+        const uint32_t sh = 32 + kBits * pass;
+        std::fill(hist.begin(), hist.end(), 0u);
+        for (uint32_t k = 0; k < m; ++k) ++hist[uint32_t(kv[k] >> sh) & (kB - 1)];
+        uint32_t acc = 0;
+        for (uint32_t j = 0; j < kB; ++j) {
+            const uint32_t c = hist[j];
+            hist[j] = acc;
+            acc += c;
+        }
+        for (uint32_t k = 0; k < m; ++k) tmp[hist[uint32_t(kv[k] >> sh) & (kB - 1)]++] = kv[k];
+        kv.swap(tmp);
     }
     hp.src_v.clear();
     hp.q_begin.clear();
-    uint32_t off = 0;
-    for (uint32_t v = 0; v < V; ++v) {
-        if (!count[v]) continue;
-        hp.src_v.push_back(v);
-        hp.q_begin.push_back(off);
-        start[v] = off;
-        off += count[v];
-    }
-    hp.q_begin.push_back(off);
-    hp.q_dst.resize(off);
-    hp.q_id.resize(off);
+    hp.q_dst.resize(m);
+    hp.q_id.resize(m);
     hp.q_pos.assign(n, kNone32);
-    for (uint32_t i = 0; i < n; ++i) {
-        if (qs_src[i] == kNone32) continue;
-        uint32_t k = start[qs_src[i]]++;
+    uint32_t prev = kNone32;
+    for (uint32_t k = 0; k < m; ++k) {
+        const uint32_t a = uint32_t(kv[k] >> 32), i = uint32_t(kv[k]);
+        if (a != prev) {
+            hp.src_v.push_back(a);
+            hp.q_begin.push_back(k);
+            prev = a;
+        }
         hp.q_dst[k] = qs_dst[i];
         hp.q_id[k] = i;
         hp.q_pos[i] = k;  // the device writes query i's record at grouped position k
     }
-    for (uint32_t v : hp.src_v) count[v] = 0;
+    hp.q_begin.push_back(m);
     return MR_OK;
 }
 
