@@ -12,9 +12,10 @@ before the timed region starts.
 Workloads (BASELINE.json configs; odd sides per SURVEY.md §8a A14):
   c1           one query on a 15x15 game-like map (configs[0]: plumbing; latency of
                one query through the device path)
-  c4 (default) the 1025x1025 map with 1M/8 = 125k uniform queries per GPU
-               (configs[3] shard; weak scaling up to the 1M batch at N=8: the
-               north-star target, >= 1e6 q/s on a 1024x1024 grid at 8 GPUs)
+  c4 (default) configs[3]: one batch of 1M uniform queries on the 1025x1025 map,
+               its sources sharded over the N ranks (1M on one GPU, 125k per rank
+               at N=8; strong scaling: the north-star target, >= 1e6 q/s on a
+               1024x1024 grid at 8 GPUs, is quoted on this batch)
   c2           10k uniform (src,dst) queries per GPU on a 65x65 synthetic map
                (configs[1]: "10k random (src,dst) batch on 64x64")
   c3           1024 sources per GPU, every destination of each on 1025x1025
@@ -58,9 +59,11 @@ WORKLOADS = {
     "c3": dict(size=1025, queries_per_gpu=1024, campfires=4, seed=4096, all_destinations=True,
                desc="configs[2]: single source -> all 1 050 625 cells of the 1025x1025 synthetic map, 1024 "
                     "sources per GPU per pass; a step answers V queries per source (SURVEY 8d c3)"),
-    "c4": dict(size=1025, queries_per_gpu=125_000, campfires=4, seed=4096, max_cmds=6,
-               desc="configs[3] shard: 125k uniform (src,dst) per GPU on a 1025x1025 synthetic map "
-                    "(1024 -> odd 1025), default FindPath params; N=8 is the 1M batch"),
+    # c4: one 1M-query batch for the whole job (strong scaling), split by source over
+    # the ranks: N = 1 answers all of configs[3] on one GPU
+    "c4": dict(size=1025, queries_total=1_000_000, campfires=4, seed=4096, max_cmds=6,
+               desc="configs[3]: one batch of 1M uniform (src,dst) queries on a 1025x1025 synthetic map "
+                    "(1024 -> odd 1025), default FindPath params, its sources sharded over the GPUs"),
     "c5": dict(size=4097, queries_per_gpu=10_000, campfires=64, clustered=True, seed=4097, sort=(1, 2), max_cmds=16,
                desc="configs[4]: 10k uniform (src,dst) per GPU on a 4097x4097 synthetic map (4096 -> odd 4097) "
                     "with 64 clustered campfires per homeland (261 specials); sort_by (Time, Money), so caravan "
@@ -74,7 +77,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
-    ap.add_argument("--queries", type=int, default=0, help="override queries per GPU")
+    ap.add_argument("--queries", type=int, default=0,
+                    help="override queries per GPU (c4: the whole batch is this x N)")
     ap.add_argument("--cpu-seconds", type=float, default=24.0,
                     help="CPU-baseline budget (wall seconds, split between the 1-thread and all-threads legs)")
     ap.add_argument("--e2e-reps", type=int, default=3, help="fresh batches timed end to end (0: skip)")
@@ -255,16 +259,15 @@ def end_to_end(m, grid, params, qpg, seed, max_cmds, reps):
     the per-plan tables, the uploads), one pass, the device->host copy and decode of
     every label (mr_plan_fetch), synchronised.  The queries are built as a numpy
     mr_query array beforehand (the caller's input).  Median over `reps` batches."""
-    import random as _random
     import numpy as np
     import torch
     from marshrutka_amd import pathfinder
     V = m.size * m.size
     rows = []
     for r in range(reps):
-        rng = _random.Random(seed + 1000 + r)
-        src = np.array([rng.randrange(V) for _ in range(qpg)], dtype=np.int64)
-        dst = np.array([rng.randrange(V) for _ in range(qpg)], dtype=np.int64)
+        rng = np.random.default_rng(seed + 1000 + r)
+        src = rng.integers(0, V, qpg, dtype=np.int64)
+        dst = rng.integers(0, V, qpg, dtype=np.int64)
         qa = m.query_array(src, dst)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -308,7 +311,7 @@ def main():
 
     from marshrutka_amd import build, pathfinder
     from marshrutka_amd.abi import Params
-    from marshrutka_amd.mapgen import SyntheticMap, random_queries
+    from marshrutka_amd.mapgen import SyntheticMap, random_queries, random_query_cells
     from marshrutka_amd.shard import PipelinedGather, SourceCosts, shard_by_source
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -338,7 +341,10 @@ def main():
         raise SystemExit("no gfx950 device visible: the engine has no CPU fallback")
 
     wl = dict(WORKLOADS[args.workload])
-    qpg = args.queries or wl["queries_per_gpu"]
+    # strong-scaling workloads (c4) split one batch of queries_total over the ranks
+    strong = "queries_total" in wl and not args.queries
+    qpg = args.queries or (-(-wl["queries_total"] // world) if strong else wl["queries_per_gpu"])
+    total_q = wl["queries_total"] if strong else qpg * world
     m = SyntheticMap(wl["size"], campfires_per_homeland=wl["campfires"], seed=wl["seed"],
                      clustered=bool(wl.get("clustered")))
     # the app's defaults (src/app.rs:782-811), with the workload's sort order
@@ -356,17 +362,26 @@ def main():
         plan = pathfinder.SSSPPlan(grid, params, mine)
         n_src = plan.num_sources
     else:
-        all_q = random_queries(m, qpg * world, wl["seed"] + 17)
-        keys = [(a.kind << 40) | (a.sub << 32) | (a.x << 16) | a.y for a, _ in all_q]
+        import numpy as np
+        # the batch as row-major cells (random_queries' stream, vectorised: 1M queries
+        # need no Python object each); a source's key is its cell
+        q_src, q_dst = random_query_cells(m, total_q, wl["seed"] + 17)
+        cells_arr = m.cells_array()
+        keys = q_src.tolist()
         shards = shard_by_source(keys, world)
-        mine = [all_q[i] for i in shards[rank]]
+
+        def my_queries(sh):
+            idx = np.asarray(sh, dtype=np.int64)
+            return m.query_array(q_src[idx], q_dst[idx], cells_arr)
+
+        mine = my_queries(shards[rank])
         if dist_on:
             # cost-aware split (shard.SourceCosts): one untimed probe pass per rank names
             # the sources the hub solver hands to the SSSP kernel; the batch is re-dealt
             # with their cost, so they land one per rank and the hub work goes elsewhere
-            probe = pathfinder.Plan(grid, params, mine, max_cmds=wl.get("max_cmds", 16))
+            probe = pathfinder.Plan(grid, params, None, max_cmds=wl.get("max_cmds", 16), query_array=mine)
             probe.run()
-            fb_keys = [(c.kind << 40) | (c.sub << 32) | (c.x << 16) | c.y for c in probe.fallback_sources()]
+            fb_keys = [m.cell_of(c) for c in probe.fallback_sources()]
             del probe
             every = [None] * world
             dist.all_gather_object(every, fb_keys)
@@ -375,12 +390,13 @@ def main():
             fb_total_probe = len(costs.extra)
             if fb_total_probe:
                 shards = shard_by_source(keys, world, costs())
-                mine = [all_q[i] for i in shards[rank]]
+                mine = my_queries(shards[rank])
         counts = [len(s) for s in shards]
         # N > 1: two plans over the same shard, so the result gather of one batch
         # overlaps the solve of the next (double buffering, shard.PipelinedGather)
         depth = 2 if dist_on else 1
-        plans = [pathfinder.Plan(grid, params, mine, max_cmds=wl.get("max_cmds", 16)) for _ in range(depth)]
+        plans = [pathfinder.Plan(grid, params, None, max_cmds=wl.get("max_cmds", 16), query_array=mine)
+                 for _ in range(depth)]
         plan = plans[0]
         n_src = plan.num_sources
         _, rbytes, _, cbytes = plan.device_outputs()
@@ -507,7 +523,11 @@ def main():
     if os.path.exists(sq_path) and kms > 0:
         try:
             with open(sq_path) as f:
-                sq = json.load(f)["per_launch"]
+                sqf = json.load(f)
+            # counters of another batch size describe another launch: not this one's
+            if sqf.get("workload") != args.workload or sqf.get("queries_per_gpu") != qpg:
+                raise ValueError("SQ counters of another workload or batch size")
+            sq = sqf["per_launch"]
             busy = sq["SQ_INSTS_VALU"] * 2.0 / (1024 * kms * 1e-3 * 2.4e9)
             issue = {"valu_per_launch": sq["SQ_INSTS_VALU"], "salu_per_launch": sq["SQ_INSTS_SALU"],
                      "lds_per_launch": sq["SQ_INSTS_LDS"], "valu_busy_frac_at_2_4GHz": busy,
@@ -517,8 +537,9 @@ def main():
     out = {
         "metric": METRIC, "value": value, "unit": "queries/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
         "config": {"workload": wl["desc"], "grid": f"{wl['size']}x{wl['size']}", "queries_per_gpu": qpg,
+                   "queries_per_step": sum(counts),
                    "campfires_per_homeland": wl["campfires"], "unique_sources_per_step": tot_src,
                    "params": "FindPath defaults: sort " + ("(Time,Money)" if wl.get("sort") == (1, 2) else
                                                            "(Legs,Money)") + ", SoE 50, caravans, skills 0, homeland Blue",
@@ -555,8 +576,17 @@ def main():
         out["cpu_baseline"] = cb
         out["parity"] = parity
     elif rank == 0 and world == 1 and not args.no_cpu_baseline:
-        gpu_res = plan.fetch()
-        cb, parity = cpu_baseline_leg(m, params, mine, gpu_res, args.cpu_seconds)
+        # the oracle's sample is a prefix of the batch (a few hundred queries at 1025^2):
+        # only that prefix becomes Python objects
+        from marshrutka_amd.abi import CellIndex, result_from_c
+        head = min(len(mine), 50_000)
+        qs = mine[:head]
+        pairs = [(CellIndex(int(a["kind"]), int(a["sub"]), int(a["x"]), int(a["y"])),
+                  CellIndex(int(b["kind"]), int(b["sub"]), int(b["x"]), int(b["y"])))
+                 for a, b in zip(qs["from"], qs["to"])]
+        res, pool = plan.fetch_raw()
+        gpu_res = [result_from_c(res[i], pool) for i in range(head)]
+        cb, parity = cpu_baseline_leg(m, params, pairs, gpu_res, args.cpu_seconds)
         out["cpu_baseline"] = cb
         out["parity"] = parity
     elif rank == 0:

@@ -240,10 +240,12 @@ int mr_decode_records(const mr_grid *grid, const mr_params *params, const void *
 int mr_plan_record_queries(const mr_plan *plan, uint32_t *query_of_record, uint32_t n);
 /* Number of unique sources (= single-source solves per pass). */
 uint32_t mr_plan_num_sources(const mr_plan *plan);
-/* The sources the last pass handed to the SSSP kernel (closed form not certain; each
- * costs one full single-source search): up to cap source cells into out, their count
- * in *n.  Waits for the plan's passes.  A cost signal for balancing sources over
- * ranks (marshrutka_amd/shard.py SourceCosts); no reference counterpart. */
+/* The sources the last pass solved with the SSSP kernel (closed form not certain and
+ * not certified from a certificate slot; each costs one full single-source search), in
+ * source order: up to cap source cells into out, their count in *n.  Sources the
+ * certificate answered are left out (they cost no search; mr_plan_stats counts them).
+ * Waits for the plan's passes.  A cost signal for balancing sources over ranks
+ * (marshrutka_amd/shard.py SourceCosts); no reference counterpart. */
 int mr_plan_fallback_sources(mr_plan *plan, mr_cell_index *out, uint32_t cap, uint32_t *n);
 
 /* Which solver a plan runs and how the last pass went (diagnostics, bench). */
@@ -282,6 +284,15 @@ int mr_plan_get_stats(mr_plan *plan, mr_plan_stats *out);
  * mr_plan_run calls since the previous call to this function, measured with
  * HIP events on the stream the kernel is launched on. */
 double mr_plan_kernel_ms(mr_plan *plan, uint32_t *n_launches);
+/* Frees the device blocks the engine keeps for reuse by later plans (plan buffers go
+ * back to a per-device cache of up to 16 GiB when a plan is destroyed, so creating the
+ * next plan needs no hipMalloc).  Blocks of live plans are untouched; safe at any time.
+ * mr_grid_destroy trims too, and a failing device allocation trims and retries once. */
+void mr_cache_trim(void);
+/* Waits for the plan's passes and frees it.  Device pointers the plan handed out
+ * (mr_plan_device_outputs, mr_sssp_device_records / _tables) are invalid afterwards:
+ * their memory may back the next plan's buffers, so a reader on another stream must
+ * have finished before this call (mr_plan_wait orders it). */
 void mr_plan_destroy(mr_plan *plan);
 
 /* ---- all destinations (single source -> every cell) ------- */

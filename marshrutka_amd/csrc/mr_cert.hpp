@@ -239,6 +239,49 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
     if (threadIdx.x < kCertSt) a->cert_st[((unsigned long long)slot * a->cert_parts + blockIdx.x) * kCertSt + threadIdx.x] = red[threadIdx.x];
 }
 
+// One workgroup, after the hub launches: the certificate slots go to the staged fallback
+// entries in source order (the cert_cap least source indices), and their staged tables
+// are copied into the slots; every other entry gets none.  A pass with more fallback
+// entries than the staging holds gives no slots (which entries were staged then
+// depended on arrival order).  Sets kCtrCert, which the slot kernels read.
+constexpr uint32_t kSelectBS = 1024;
+__global__ __launch_bounds__(kSelectBS) void cert_select_kernel(const KArgs *__restrict__ a) {
+    __shared__ uint32_t key[kCertStageMax], slot_of[kCertStageMax];
+    __shared__ uint32_t nstaged;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t n = __hip_atomic_load(a->counter + kCtrFbCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t cap = min(a->cert_stage_cap, kCertStageMax);
+    if (n > cap) {
+        for (uint32_t i = tid; i < n; i += kSelectBS) a->fb_cert[i] = kNone32;
+        if (tid == 0) a->counter[kCtrCert] = 0;
+        return;
+    }
+    if (tid == 0) nstaged = 0;
+    for (uint32_t i = tid; i < n; i += kSelectBS) key[i] = a->fb_cert[i] == kFbStaged ? a->fb_list[i] : kNone32;
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kSelectBS) {
+        uint32_t slot = kNone32;
+        if (key[i] != kNone32) {
+            uint32_t r = 0;  // staged entries of a smaller source (sources are distinct)
+            for (uint32_t j = 0; j < n; ++j) r += key[j] < key[i] ? 1u : 0u;
+            if (r < a->cert_cap) slot = r;
+            atomicAdd(&nstaged, 1u);
+        }
+        slot_of[i] = slot;
+        a->fb_cert[i] = slot;
+    }
+    __syncthreads();
+    const uint32_t T = a->p.NS + 1;
+    for (uint32_t k = tid; k < n * T; k += kSelectBS) {
+        const uint32_t i = k / T, t = k - i * T, slot = slot_of[i];
+        if (slot == kNone32) continue;
+        a->cert_tab[(unsigned long long)slot * T + t] = a->cert_stage_tab[(unsigned long long)i * T + t];
+        a->cert_lex[(unsigned long long)slot * T + t] = a->cert_stage_lex[(unsigned long long)i * T + t];
+        if (t == 0) a->cert_src[slot] = a->cert_stage_src[i];
+    }
+    if (tid == 0) a->counter[kCtrCert] = min(nstaged, a->cert_cap);
+}
+
 constexpr uint32_t kSweepBS = 1024;      // threads of the sweep's one workgroup per slot
 constexpr uint32_t kSweepBuckets = 16384;  // leading-metric buckets a window may span
 constexpr int kSweepMargin = 2;            // cells added round the failing cells' box

@@ -72,6 +72,7 @@ struct Shared {
     uint32_t nd;            // generic: dirty count
     uint32_t sidx;
     uint32_t sslot;         // fallback launch: the source's certificate slot (kNone32: none)
+    uint32_t sentry;        // fallback launch: the source's fallback entry
     uint32_t done;
     uint32_t L;             // legs: current level
     uint32_t nbnd;          // legs: number of boundaries
@@ -1467,11 +1468,14 @@ __device__ __forceinline__ void finish_launch(const KArgs *__restrict__ a, uint3
 
 // A source handed to the SSSP launch: fallback entry i, with its certificate slot
 // (kNone32: none, the SSSP kernel solves it)
-__device__ __forceinline__ void push_fallback(const KArgs *__restrict__ a, uint32_t *counter, uint32_t s_idx,
-                                              uint32_t slot) {
+// (kNone32: none, the SSSP kernel solves it; kFbStaged: its table is staged for
+// cert_select_kernel).  Returns i.
+__device__ __forceinline__ uint32_t push_fallback(const KArgs *__restrict__ a, uint32_t *counter, uint32_t s_idx,
+                                                  uint32_t slot) {
     const uint32_t i = atomicAdd(counter + kCtrFbCount, 1u);
     a->fb_list[i] = s_idx;
     if (a->fb_cert) a->fb_cert[i] = slot;
+    return i;
 }
 
 // ===================================================================================
@@ -2079,8 +2083,8 @@ struct HubSolver : Core<false> {
         wave_sync();
     }
 
-    // Certified fallback: the same ranks and table into certificate slot `slot`, with
-    // the source's vertex and the slot's failure key reset (the check lowers it)
+    // Certified fallback: the same ranks and table into staging entry `slot` (the
+    // source's fallback entry), with the source's vertex
     __device__ __forceinline__ void export_cert(bool go, uint32_t slot, uint32_t nb) const {
         const DevParams &p = P;
         const uint32_t t = seg_lane();
@@ -2110,10 +2114,10 @@ struct HubSolver : Core<false> {
         wave_sync();
         if (go && t <= p.NS) {
             const unsigned long long tb = (unsigned long long)slot * (p.NS + 1);
-            a->cert_tab[tb + t] = R[t];
-            a->cert_lex[tb + t] = lexs[t];
+            a->cert_stage_tab[tb + t] = R[t];
+            a->cert_stage_lex[tb + t] = lexs[t];
         }
-        if (go && t == 0) a->cert_src[slot] = src;
+        if (go && t == 0) a->cert_stage_src[slot] = src;
         wave_sync();
     }
 
@@ -2258,17 +2262,16 @@ struct HubSolver : Core<false> {
             fallback = fallback || (have && seg_bits<LPS>(__ballot(unc_q)) != 0);
             if (t == 0 && have && !fallback) written += qb - qa;
         }
-        // A query-mode fallback source takes a certificate slot while they last: its
-        // label table and boundary ranks go there, and the fill + check launches decide
-        // whether the SSSP kernel is needed at all
-        uint32_t slot = kNone32;
-        if (fallback && t == 0 && !a->all_mode && a->cert_cap) {
-            slot = atomicAdd(counter + kCtrCert, 1u);
-            if (slot >= a->cert_cap) slot = kNone32;
-        }
-        slot = uint32_t(__shfl(int(slot), int(lane_id() & ~(LPS - 1u))));  // segment lane 0's
-        if (__any(fallback && slot != kNone32)) export_cert(fallback && slot != kNone32, slot, nb);
-        if (fallback && t == 0) push_fallback(a, counter, s_idx, slot);
+        // A query-mode fallback source stages its label table and boundary ranks under
+        // its fallback entry; cert_select_kernel then gives the certificate slots to the
+        // staged sources in source order, and the fill + check launches decide whether
+        // the SSSP kernel is needed at all
+        uint32_t entry = kNone32;
+        if (fallback && t == 0) entry = push_fallback(a, counter, s_idx, kNone32);
+        entry = uint32_t(__shfl(int(entry), int(lane_id() & ~(LPS - 1u))));  // segment lane 0's
+        const bool stage = fallback && !a->all_mode && a->cert_cap && entry < a->cert_stage_cap;
+        if (__any(stage)) export_cert(stage, entry, nb);
+        if (stage && t == 0) a->fb_cert[entry] = kFbStaged;
         MR_HSTAMP(7);
     }
 };
@@ -3296,14 +3299,17 @@ __host__ __device__ inline LdsLayout lds_layout(uint32_t NS, uint32_t V, bool gr
 
 // next source index for a workgroup: every source in order, or (fallback launch
 // after the hub solver) the sources it listed
-__device__ __forceinline__ uint32_t next_source(const KArgs *__restrict__ a, uint32_t &slot) {
+__device__ __forceinline__ uint32_t next_source(const KArgs *__restrict__ a, uint32_t &slot, uint32_t &entry) {
     slot = kNone32;
+    entry = kNone32;
     if (a->fb_mode) {
         const uint32_t n = __hip_atomic_load(a->counter + kCtrFbCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t i = atomicAdd(a->counter + kCtrFbDequeue, 1u);
         if (i >= n) return kNone32;
         if (a->fb_cert) slot = a->fb_cert[i];
-        return a->fb_list[i];
+        if (slot >= a->cert_cap) slot = kNone32;  // none, or staged without a slot
+        entry = i;
+        return a->fb_list[i] & ~kFbCertified;
     }
     const uint32_t i = atomicAdd(a->counter + kCtrDequeue, 1u);
     return i < a->nsrc ? i : kNone32;
@@ -3372,13 +3378,16 @@ __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a)
         S.stamps = &stamps;
         uint32_t nsolved = 0;
         for (;;) {
-            if (threadIdx.x == 0) sh->sidx = next_source(a, sh->sslot);
+            if (threadIdx.x == 0) sh->sidx = next_source(a, sh->sslot, sh->sentry);
             __syncthreads();
             const uint32_t s = sh->sidx, slot = sh->sslot;
             __syncthreads();
             if (s == kNone32) break;
             if (slot != kNone32 && S.cert_emit(s, slot)) {
-                if (threadIdx.x == 0) atomicAdd(a->counter + kCtrCertDone, 1u);
+                if (threadIdx.x == 0) {
+                    atomicAdd(a->counter + kCtrCertDone, 1u);
+                    a->fb_list[sh->sentry] |= kFbCertified;  // answered without a search
+                }
             } else {
                 S.solve(s);
             }
@@ -3415,13 +3424,16 @@ __global__ __launch_bounds__(kBS) void solve_kernel(const KArgs *__restrict__ a)
         S.best = reinterpret_cast<uint32_t *>(smem + L.off_b);
         S.fired = reinterpret_cast<uint32_t *>(smem + L.off_d);
         for (;;) {
-            if (threadIdx.x == 0) sh->sidx = next_source(a, sh->sslot);
+            if (threadIdx.x == 0) sh->sidx = next_source(a, sh->sslot, sh->sentry);
             __syncthreads();
             const uint32_t s = sh->sidx, slot = sh->sslot;
             __syncthreads();
             if (s == kNone32) break;
             if (slot != kNone32 && S.cert_emit(s, slot)) {
-                if (threadIdx.x == 0) atomicAdd(a->counter + kCtrCertDone, 1u);
+                if (threadIdx.x == 0) {
+                    atomicAdd(a->counter + kCtrCertDone, 1u);
+                    a->fb_list[sh->sentry] |= kFbCertified;  // answered without a search
+                }
             } else {
                 S.solve(s);
             }

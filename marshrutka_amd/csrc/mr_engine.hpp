@@ -195,7 +195,23 @@ struct KArgs {
     uint32_t *cert_aux;          // per slot V words: the repair sweep's cells by bucket
     uint32_t *fb_cert;
     const uint32_t *nsrc_dev;    // fill launches over cert slots: sources = min(nsrc, *nsrc_dev)
+    // Slots are given deterministically: the hub kernel stages the table of fallback
+    // entry i (while i < cert_stage_cap) and tags fb_cert[i] = kFbStaged; then
+    // cert_select_kernel gives the slots to the staged sources in source order (the
+    // cert_cap least source indices) and copies their tables into them.  A pass with
+    // more fallback entries than cert_stage_cap stages nothing usable: no slots.  So
+    // which sources the certificate answers never depends on the order of arrival.
+    Rec *cert_stage_tab;         // cert_stage_cap * (NS+1)
+    uint32_t *cert_stage_lex;    // cert_stage_cap * (NS+1)
+    uint32_t *cert_stage_src;    // cert_stage_cap
+    uint32_t cert_stage_cap;
 };
+// fb_cert[i] of a staged entry before cert_select_kernel gives it a slot (or none)
+constexpr uint32_t kFbStaged = 0xFFFFFFFEu;
+// fb_list[i] | kFbCertified: the SSSP launch emitted entry i from its certificate slot
+// (mr_plan_fallback_sources leaves such sources out: they cost no search)
+constexpr uint32_t kFbCertified = 0x80000000u;
+constexpr uint32_t kCertStageMax = 4096u;  // cert_select_kernel's LDS arrays (32 KB)
 // counter words: the pass's last workgroup copies the fallback and written counts
 // to their "last" slots and zeroes the rest, so no memset precedes a pass
 enum : uint32_t {
@@ -209,7 +225,7 @@ enum : uint32_t {
     kCtrWritten = 7,      // result records written               64-bit counter with this)
     kCtrOvf = 8,          // command-overflow pool: commands allocated in this pass
     kCtrLastOvf = 9,      // kCtrOvf of the last completed pass
-    kCtrCert = 10,        // certified-fallback slots taken in this pass
+    kCtrCert = 10,        // certified-fallback slots given in this pass (cert_select_kernel)
     kCtrCertDone = 11,    // fallback sources the certificate answered in this pass
     kCtrLastCert = 12,    // kCtrCertDone of the last completed pass
     kCtrWords = 13

@@ -20,6 +20,10 @@
 #include "../../include/marshrutka_pf.h"
 #include "mr_engine.hpp"
 
+// hipMalloc for the grid's long-lived device tables: on out-of-memory the plan block
+// cache (below) is trimmed and the allocation retried once
+static hipError_t dev_malloc(void **p, size_t bytes);
+
 namespace mr {
 uint32_t lds_bytes(uint32_t NS, uint32_t V, bool grid_in_lds, uint32_t algo);
 hipError_t launch_solve(const KArgs *d_args, bool grid_in_lds, uint32_t algo, uint32_t NS, uint32_t V,
@@ -42,6 +46,7 @@ int hub_wide_blocks_per_cu(const uint32_t perm[3], uint32_t NS, uint32_t bytes);
 uint32_t hub_lane_entries(uint32_t NS);
 hipError_t launch_hub_lane(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t n_lane,
                            hipStream_t stream);
+hipError_t launch_cert_select(const KArgs *d_args, hipStream_t stream);
 hipError_t launch_cert_check(const KArgs *d_args, uint32_t gx, uint32_t slots, hipStream_t stream);
 hipError_t launch_cert_sweep(const KArgs *d_args, uint32_t slots, hipStream_t stream);
 hipError_t decode_records_device(const OutResult *res, const OutCmd *slots, const OutCmd *ovf, uint32_t novf,
@@ -368,7 +373,12 @@ extern "C" int mr_grid_create(const mr_cell *cells, uint32_t n, mr_grid **out) {
     return MR_OK;
 }
 
-extern "C" void mr_grid_destroy(mr_grid *g) { delete g; }
+extern "C" void mr_grid_destroy(mr_grid *g) {
+    delete g;
+    // the grid's plans are gone (a plan must not outlive its grid): hand the blocks they
+    // cached back to the device
+    mr_cache_trim();
+}
 extern "C" uint32_t mr_grid_square_size(const mr_grid *g) { return g ? g->S : 0; }
 
 extern "C" void mr_params_default(mr_params *p) {
@@ -489,7 +499,7 @@ static const uint32_t *region_table_device(const mr_grid *g, int h, const std::v
     if (!g->d_near[h]) {
         uint32_t *d = nullptr;
         const size_t bytes = std::max<size_t>(tab.size(), 1) * 4;
-        if (hipMalloc(reinterpret_cast<void **>(&d), bytes) != hipSuccess) return nullptr;
+        if (dev_malloc(reinterpret_cast<void **>(&d), bytes) != hipSuccess) return nullptr;
         if (!tab.empty() && hipMemcpy(d, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
             (void)hipFree(d);
             return nullptr;
@@ -555,6 +565,7 @@ static void region_bounds(const mr_grid *g, int h, std::vector<uint32_t> &regs, 
 }
 
 // ------------------------------------------------------------------ planning
+
 namespace {
 
 struct HostPlan {
@@ -844,7 +855,7 @@ static bool grid_tables(const mr_grid *g, int dev, const HostPlan &hp, uint32_t 
     std::lock_guard<std::mutex> lk(g->near_mu);
     if (g->d_dev != -1 && g->d_dev != dev) return false;
     auto up = [](uint32_t *&d, const std::vector<uint32_t> &h) {
-        if (hipMalloc(reinterpret_cast<void **>(&d), std::max<size_t>(h.size(), 1) * 4) != hipSuccess) return false;
+        if (dev_malloc(reinterpret_cast<void **>(&d), std::max<size_t>(h.size(), 1) * 4) != hipSuccess) return false;
         if (!h.empty() && hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
             (void)hipFree(d);
             d = nullptr;
@@ -873,7 +884,7 @@ static bool grid_tables(const mr_grid *g, int dev, const HostPlan &hp, uint32_t 
         const std::vector<uint32_t> si = build_sinfo(g, hp);
         if (!up(ds, si)) return false;
         const std::vector<uint2> ce = build_cell(g, si);
-        if (hipMalloc(reinterpret_cast<void **>(&dc), std::max<size_t>(ce.size(), 1) * sizeof(uint2)) != hipSuccess) {
+        if (dev_malloc(reinterpret_cast<void **>(&dc), std::max<size_t>(ce.size(), 1) * sizeof(uint2)) != hipSuccess) {
             (void)hipFree(ds);
             return false;
         }
@@ -968,6 +979,17 @@ static void pfree(void *p) {
     c.free[cache_key(dev, cls)].push_back(p);
     c.cached += cls;
 }
+static void trim_cache_all() {
+    BlockCache &c = block_cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    for (auto &kv : c.free) {
+        for (void *q : kv.second) {
+            (void)hipFree(q);
+            c.cached -= size_t(kv.first >> 8);
+        }
+        kv.second.clear();
+    }
+}
 
 // Plan streams come from a per-device pool as well: a destroyed plan (which waited for
 // its work) returns its streams, and the next plan takes them without hipStreamCreate.
@@ -1023,6 +1045,18 @@ static int upload(T *&dptr, const std::vector<T> &h) {
 }
 
 }  // namespace
+
+static hipError_t dev_malloc(void **p, size_t bytes) {
+    hipError_t e = hipMalloc(p, bytes);
+    if (e == hipErrorOutOfMemory) {
+        (void)hipGetLastError();
+        trim_cache_all();
+        e = hipMalloc(p, bytes);
+    }
+    return e;
+}
+
+extern "C" void mr_cache_trim(void) { trim_cache_all(); }
 
 struct mr_plan {
     const mr_grid *grid = nullptr;
@@ -1109,6 +1143,8 @@ struct mr_plan {
              *d_fb_cert = nullptr, *d_cert_ones = nullptr;
     CellWord *d_cert_rec = nullptr;
     KArgs *d_args_cert = nullptr;
+    Rec *d_cert_stage_tab = nullptr;
+    uint32_t *d_cert_stage_lex = nullptr, *d_cert_stage_src = nullptr;
     ~mr_plan() {
         if (!slots.empty()) {  // the d_* fields may name another slot: free each slot's once
             Slot &k = slots[0];
@@ -1141,7 +1177,8 @@ struct mr_plan {
         if (d_cell) (void)pfree(d_cell);
         for (void *p : {(void *)d_cert_tab, (void *)d_cert_lex, (void *)d_cert_src, (void *)d_cert_st,
                         (void *)d_cert_aux, (void *)d_fb_cert, (void *)d_cert_ones, (void *)d_cert_rec,
-                        (void *)d_args_cert})
+                        (void *)d_args_cert, (void *)d_cert_stage_tab, (void *)d_cert_stage_lex,
+                        (void *)d_cert_stage_src})
             if (p) (void)pfree(p);
         for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_rank_inv, (void *)d_src, (void *)d_qb, (void *)d_qd,
                         (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
@@ -1504,7 +1541,13 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
             const size_t T = size_t(NS) + 1;
             const uint32_t pitch = (hp.p.S + 31) / 32 * 32;
             std::vector<uint32_t> ones(cap, 1u);
-            if (pmalloc(reinterpret_cast<void **>(&pl->d_cert_tab), cap * T * sizeof(Rec)) != hipSuccess ||
+            // staging for every fallback entry up to kCertStageMax (mr_engine.hpp): a
+            // pass with more hands nothing to the certificate
+            const uint32_t stage = uint32_t(std::min<size_t>(kCertStageMax, std::max<size_t>(nsrc, 1)));
+            if (pmalloc(reinterpret_cast<void **>(&pl->d_cert_stage_tab), stage * T * sizeof(Rec)) != hipSuccess ||
+                pmalloc(reinterpret_cast<void **>(&pl->d_cert_stage_lex), stage * T * 4) != hipSuccess ||
+                pmalloc(reinterpret_cast<void **>(&pl->d_cert_stage_src), stage * 4) != hipSuccess ||
+                pmalloc(reinterpret_cast<void **>(&pl->d_cert_tab), cap * T * sizeof(Rec)) != hipSuccess ||
                 pmalloc(reinterpret_cast<void **>(&pl->d_cert_lex), cap * T * 4) != hipSuccess ||
                 pmalloc(reinterpret_cast<void **>(&pl->d_cert_src), cap * 4) != hipSuccess ||
 
@@ -1516,6 +1559,10 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
                 return bail(fail(MR_ERR_DEVICE, "certificate slots"));
             pl->cert_cap = cap;
             ka.cert_cap = cap;
+            ka.cert_stage_cap = stage;
+            ka.cert_stage_tab = pl->d_cert_stage_tab;
+            ka.cert_stage_lex = pl->d_cert_stage_lex;
+            ka.cert_stage_src = pl->d_cert_stage_src;
             ka.cert_tab = pl->d_cert_tab;
             ka.cert_lex = pl->d_cert_lex;
             ka.cert_src = pl->d_cert_src;
@@ -1760,11 +1807,13 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
             e = launch_hub_lane(pl->fb_none && !big ? pl->d_args_lane_last : pl->d_args_lane, pl->ka.p.perm,
                                 pl->ka.p.NS, pl->ka.nreg, pl->n_lane, s);
         if (e == hipSuccess && big) e = launch_hub_plan(pl, pl->fb_none ? pl->d_args_hub_last : pl->d_args, s);
-        // certified fallback: the slots' closed forms, the check, one repair sweep, the
-        // check again (each exits at once without exported slots); the SSSP launch then
+        // certified fallback: the slots given to the staged sources in source order,
+        // their closed forms, the check, one repair sweep, the check again (each exits at
+        // once without slots); the SSSP launch then
         // emits every certified source from its slot and solves the rest
         if (e == hipSuccess && !pl->fb_none && pl->cert_cap) {
-            e = launch_fill(pl->d_args_cert, pl->ka.p.perm, pl->cert_fill_gx, 1, s);
+            e = launch_cert_select(pl->d_args, s);
+            if (e == hipSuccess) e = launch_fill(pl->d_args_cert, pl->ka.p.perm, pl->cert_fill_gx, 1, s);
             if (e == hipSuccess) e = launch_cert_check(pl->d_args, pl->cert_check_gx, pl->cert_cap, s);
             if (e == hipSuccess) e = launch_cert_sweep(pl->d_args, pl->cert_cap, s);
             if (e == hipSuccess) e = launch_cert_check(pl->d_args, pl->cert_check_gx, pl->cert_cap, s);
@@ -1896,9 +1945,11 @@ extern "C" int mr_plan_fallback_sources(mr_plan *pl, mr_cell_index *out, uint32_
     std::vector<uint32_t> fb(nf);
     if (nf && hipMemcpy(fb.data(), pl->d_fb, size_t(nf) * 4, hipMemcpyDeviceToHost) != hipSuccess)
         return fail(MR_ERR_DEVICE, "copy fallback list");
+    // entries the certificate answered carry kFbCertified: no search was run for them
+    fb.erase(std::remove_if(fb.begin(), fb.end(), [](uint32_t s) { return (s & kFbCertified) != 0; }), fb.end());
     std::sort(fb.begin(), fb.end());
-    for (uint32_t k = 0; k < nf && k < cap; ++k) out[k] = pl->grid->idx[pl->hp.src_v[fb[k]]];
-    *n = nf;
+    for (uint32_t k = 0; k < fb.size() && k < cap; ++k) out[k] = pl->grid->idx[pl->hp.src_v[fb[k]]];
+    *n = uint32_t(fb.size());
     return MR_OK;
 }
 
@@ -2086,7 +2137,7 @@ static int check_device_errors(mr_plan *pl, uint32_t &flags) {
             std::vector<uint32_t> fb(ctr[kCtrLastFb]);
             (void)hipMemcpy(fb.data(), pl->d_fb, fb.size() * 4, hipMemcpyDeviceToHost);
             std::fprintf(stderr, "MR_DEBUG fallback sources (vertex):");
-            for (uint32_t s : fb) std::fprintf(stderr, " %u", pl->hp.src_v[s]);
+            for (uint32_t s : fb) std::fprintf(stderr, " %u%s", pl->hp.src_v[s & ~kFbCertified], (s & kFbCertified) ? "c" : "");
             std::fprintf(stderr, "\n");
         }
     }
@@ -2138,7 +2189,7 @@ static const mr_cell_index *grid_idx_rank(const mr_grid *g, int dev) {
         std::vector<mr_cell_index> t(g->V);
         for (uint32_t r = 0; r < g->V; ++r) t[r] = g->idx[g->rank_inv[r]];
         mr_cell_index *d = nullptr;
-        if (hipMalloc(reinterpret_cast<void **>(&d), std::max<size_t>(t.size(), 1) * sizeof(mr_cell_index)) != hipSuccess)
+        if (dev_malloc(reinterpret_cast<void **>(&d), std::max<size_t>(t.size(), 1) * sizeof(mr_cell_index)) != hipSuccess)
             return nullptr;
         if (!t.empty() && hipMemcpy(d, t.data(), t.size() * sizeof(mr_cell_index), hipMemcpyHostToDevice) != hipSuccess) {
             (void)hipFree(d);
@@ -2218,6 +2269,9 @@ static bool plan_fetch_device(mr_plan *pl, mr_result *results, mr_command *pool,
     const uint64_t ncopy = std::min<uint64_t>(end, pcap);
     if (e == hipSuccess && ncopy && !(tailw[0] & 1u))
         e = hipMemcpy(pool, d_pool, size_t(ncopy) * sizeof(mr_command), hipMemcpyDeviceToHost);
+    // the blocks go back to the cache, which hands them out with no implicit sync: on
+    // every path (a failed enqueue included) the work queued on them must be done first
+    (void)hipStreamSynchronize(pl->stream);
     pfree(scratch);
     pfree(d_out);
     pfree(d_pool);

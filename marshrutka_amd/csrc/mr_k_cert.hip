@@ -1,8 +1,14 @@
-// mr_k_cert.hip — certified fallback kernels (cert_check_kernel, cert_sweep_kernel)
+// mr_k_cert.hip — certified fallback kernels (cert_select_kernel, cert_check_kernel, cert_sweep_kernel)
 // (host-side launch helpers called from mr_host.cpp; device code in mr_cert.hpp)
 #include "mr_cert.hpp"
 
 namespace mr {
+
+// the slots' deterministic assignment (one workgroup)
+hipError_t launch_cert_select(const KArgs *d_args, hipStream_t stream) {
+    void *args[] = {const_cast<KArgs **>(&d_args)};
+    return hipLaunchKernel((const void *)&cert_select_kernel, dim3(1), dim3(kSelectBS), args, 0, stream);
+}
 
 // the check over every slot's cells: gx workgroups per slot, `slots` slots
 hipError_t launch_cert_check(const KArgs *d_args, uint32_t gx, uint32_t slots, hipStream_t stream) {

@@ -58,6 +58,7 @@ __global__ void decode_write_kernel(const OutResult *__restrict__ res, const Out
             status = MR_OK;
         } else if (status == MR_OK && r.n_commands > mc) {
             atomicOr(err, 1u);
+            r.n_commands = 0;  // its slots hold no more than mc commands: read none (decode_record)
         }
         r.status = status;
         out[q] = r;

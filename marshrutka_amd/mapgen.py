@@ -223,6 +223,22 @@ def random_queries(m: SyntheticMap, n: int, seed: int) -> List[Tuple[CellIndex, 
     return [(m.index_at(rng.below(V)), m.index_at(rng.below(V))) for _ in range(n)]
 
 
+def random_query_cells(m: SyntheticMap, n: int, seed: int):
+    """random_queries as row-major cell numbers, vectorised: (src, dst) int64 arrays
+    with src[i] / dst[i] the cells of random_queries(m, n, seed)[i] (the same
+    splitmix64 stream: draw 2i is the source, 2i + 1 the destination)."""
+    import numpy as np
+    V = m.size * m.size
+    with np.errstate(over="ignore"):
+        s0 = np.uint64((seed ^ 0x5DEECE66D) & MASK64)
+        z = s0 + np.arange(1, 2 * n + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    cell = (z % np.uint64(V)).astype(np.int64)
+    return cell[0::2], cell[1::2]
+
+
 def random_sources_queries(m: SyntheticMap, n: int, n_sources: int, seed: int):
     """Queries drawn from a fixed pool of n_sources sources (SSSP-style batches)."""
     rng = SplitMix64(seed ^ 0x2545F4914F6CDD1D)

@@ -5,11 +5,12 @@ the reference's FindPath::eval loop src/pathfinder.rs:219-246 without its early 
 gives every cell's label from a source; labels are compared whole (metrics, command
 count and a digest of the command list, tests/label_digest.py) with numpy.
 
-* configs[3] (c4): the bench's 125k uniform queries on the 1025^2 map plus 1000
-  destinations for each of 16 sources of every kind (Center, border-1 cells,
-  campfires, on-axis and random cells), one Plan as the bench runs it.  Every label
-  of the batch is property-checked; every label of the 16 sources is compared with
-  the oracle, and 32 uniform queries with the oracle's single-query eval.
+* configs[3] (c4): the bench's whole 1M-query batch on the 1025^2 map plus 1000
+  destinations for each of 32 sources (16 of every kind: Center, border-1 cells,
+  campfires, on-axis and random cells; 16 of the batch's own), one Plan as the bench
+  runs it.  Every label of the batch is property-checked; every label of the 32
+  sources is compared with the oracle, and 64 batch queries with the oracle's
+  single-query eval.
 * configs[2] (c3): every one of the 1 050 625 cells of 4 sources at 1025^2 through the
   all-destinations plan (hub + fill), two comparator orders.
 * configs[4] (c5): every one of the 16.8 M cells of 3 sources at 4097^2 (64 clustered
@@ -27,7 +28,7 @@ import pytest
 import label_digest as ld
 from golden_util import as_expected
 from marshrutka_amd.abi import SORT_MONEY, SORT_TIME, CellIndex, Params
-from marshrutka_amd.mapgen import SyntheticMap, random_queries
+from marshrutka_amd.mapgen import SyntheticMap, random_queries, random_query_cells
 
 pytestmark = pytest.mark.gpu
 
@@ -69,20 +70,32 @@ def _sources_of_every_kind(m, rng):
 
 
 def test_c4_full_scale(eng, oracle_lib, c4_map):
+    """configs[3] at its stated size: the bench's whole 1M-query batch on one GPU (645k
+    unique sources), every label property-checked, plus 1 000 destinations for each of
+    32 sources against the oracle's Dijkstra from each source: 16 of every kind (Center,
+    border-1 cells, campfires, on-axis, random) and the 16 batch sources with the most
+    queries (whose batch queries are checked too), and 64 batch queries against the
+    oracle's single-query eval."""
     m, arr = c4_map
     V = m.size * m.size
     keys = ld.cell_keys(arr)
     rng = random.Random(4096)
-    uni = random_queries(m, 125_000, 4096 + 17)  # the bench's c4 batch
+    uni_src, uni_dst = random_query_cells(m, 1_000_000, 4096 + 17)  # bench.py's c4 batch
+    nb = len(uni_src)
     srcs = _sources_of_every_kind(m, rng)
+    cnt = np.bincount(uni_src, minlength=V)
+    for c in np.argsort(-cnt, kind="stable"):
+        if len(srcs) == 32:
+            break
+        ci = m.index_at(int(c))
+        if ci not in srcs:
+            srcs.append(ci)
     extra_src, extra_dst = [], []
     cf_cells = [m.cell_of(c) for c in m.campfires()]
     for s in srcs:
         d = rng.sample(range(V), 1000 - len(cf_cells) - 2) + cf_cells + [m.cell_of(CellIndex.center()), m.cell_of(s)]
         extra_src += [m.cell_of(s)] * len(d)
         extra_dst += d
-    uni_src = np.array([m.cell_of(a) for a, _ in uni], dtype=np.int64)
-    uni_dst = np.array([m.cell_of(b) for _, b in uni], dtype=np.int64)
     q_src = np.concatenate([uni_src, np.array(extra_src)])
     q_dst = np.concatenate([uni_dst, np.array(extra_dst)])
     n = len(q_src)
@@ -92,23 +105,27 @@ def test_c4_full_scale(eng, oracle_lib, c4_map):
     plan.run()  # the bench's steady state: a rerun of the same plan
     res, pool = plan.fetch_raw()
     st = plan.stats()
-    assert st["solver"] == "hub" and st["num_sources"] >= 117_000
+    assert st["solver"] == "hub" and st["num_sources"] >= 645_000, st
     props = ld.label_properties(res, pool, n, keys[q_src], keys[q_dst])
     assert all(v == 0 for v in props.values()), props
     got = ld.digests(res, pool, n)
     og = oracle_lib.OracleGrid.from_array(arr)
     want = og.sssp_digests(Params(), srcs, threads=ORACLE_THREADS)
-    off = len(uni)
     for i, s in enumerate(srcs):
-        sel = np.arange(off + i * 1000, off + (i + 1) * 1000)
+        sel = np.arange(nb + i * 1000, nb + (i + 1) * 1000)
         bad = ld.mismatches(got, {f: want[f][i] for f in want}, idx_got=sel, idx_exp=q_dst[sel])
         assert bad.size == 0, (str(s), len(bad), [str(m.index_at(int(q_dst[sel][j]))) for j in bad[:4]])
-    # uniform queries from random sources: the oracle's own single-query eval
-    sample = rng.sample(range(len(uni)), 32)
-    eres, epool = og.find_path_batch_raw(Params(), [uni[i] for i in sample], threads=ORACLE_THREADS)
+        mine = np.nonzero(uni_src[:nb] == m.cell_of(s))[0]  # the source's own queries of the batch
+        if mine.size:
+            bad = ld.mismatches(got, {f: want[f][i] for f in want}, idx_got=mine, idx_exp=q_dst[mine])
+            assert bad.size == 0, (str(s), "batch queries", len(bad))
+    # uniform batch queries from random sources: the oracle's own single-query eval
+    sample = rng.sample(range(nb), 64)
+    pairs = [(m.index_at(int(uni_src[i])), m.index_at(int(uni_dst[i]))) for i in sample]
+    eres, epool = og.find_path_batch_raw(Params(), pairs, threads=ORACLE_THREADS)
     ed = ld.digests(eres, epool, len(sample))
     bad = ld.mismatches(got, ed, idx_got=np.array(sample))
-    assert bad.size == 0, [uni[sample[j]] for j in bad[:4]]
+    assert bad.size == 0, [pairs[j] for j in bad[:4]]
 
 
 @pytest.mark.parametrize("ff", [1, 3])

@@ -142,6 +142,67 @@ def test_default_params_c2_sample(eng, oracle_lib):
     check(eng, oracle_lib, m, Params(), random_queries(m, 400, 7), "c2 sample")
 
 
+def test_c2_full_batch(eng, oracle_lib):
+    """configs[1] at its stated size: bench.py's whole c2 batch (10 000 uniform queries
+    on the 65x65 map, default parameters) through one plan, every label against the
+    oracle's FindPath::eval (src/pathfinder.rs:199-248)."""
+    m = SyntheticMap(65, campfires_per_homeland=4, seed=2024)  # bench.py c2
+    qs = random_queries(m, 10_000, 2024 + 17)
+    check(eng, oracle_lib, m, Params(), qs, "c2 full batch")
+
+
+@pytest.mark.parametrize("max_cmds", [1, 3, 16])
+def test_certificate_sfm_fleetfoot_vs_oracle(eng, oracle_lib, monkeypatch, max_cmds):
+    """The scenario whose two plans once disagreed (tools/plan_diff.py; DESIGN.md
+    section 3d): 65x65, 5 campfires per homeland, Fleetfoot 2, (Time, Money), the
+    Scroll of the Forum, few command slots.  Every source is handed to the certificate
+    (MR_HUB_FALLBACK_ALL, 64 slots), in plans of at most 64 sources so that each one
+    goes through a slot, and every label is compared with the oracle (SoE / SFm
+    src/pathfinder.rs:162-178, the Fleetfoot ceil per run src/cost.rs:122-124).  A
+    second run of each plan must give the same bytes (slots are given in source
+    order, never by arrival)."""
+    import ctypes as C
+    from marshrutka_amd.abi import mr_command, mr_result, result_from_c
+    from marshrutka_amd import pathfinder as pf
+    monkeypatch.setenv("MR_HUB_FALLBACK_ALL", "1")
+    monkeypatch.setenv("MR_CERT_SLOTS", "64")
+    monkeypatch.delenv("MR_CERT", raising=False)
+    monkeypatch.delenv("MR_HUB_LANE", raising=False)
+    m = SyntheticMap(65, campfires_per_homeland=5, seed=11)
+    g = eng.MapGrid(m.cells())
+    og = oracle_lib.OracleGrid(m.cells())
+    params = Params(fleetfoot=2, sort_by=(SORT_TIME, SORT_MONEY), use_sfm=True)
+    qs = random_queries(m, 3000, 12)
+    exp = og.find_path_batch(params, qs, threads=0)
+    by_src = {}
+    for i, (a, _) in enumerate(qs):
+        by_src.setdefault(a, []).append(i)
+    groups = list(by_src.values())
+    certified = 0
+    for lo in range(0, len(groups), 64):
+        idx = [i for grp in groups[lo:lo + 64] for i in grp]
+        sub = [qs[i] for i in idx]
+        plan = eng.Plan(g, params, sub, max_cmds=max_cmds)
+        outs = []
+        for _ in range(2):
+            plan.run()
+            cap = len(sub) * 24
+            res, pool = (mr_result * len(sub))(), (mr_command * cap)()
+            st = pf.lib().mr_plan_fetch(plan.handle, res, pool, cap)
+            assert st == 0, st
+            outs.append((bytes(res), bytes(pool)))
+        assert outs[0] == outs[1], "two runs of one plan differ"
+        stats = plan.stats()
+        certified += stats["certified_sources"]
+        assert stats["fallback_sources"] == len(groups[lo:lo + 64])
+        # the sources left to the SSSP kernel: the ones the certificate did not answer
+        assert len(plan.fallback_sources()) == stats["fallback_sources"] - stats["certified_sources"]
+        got = [result_from_c(res[k], pool) for k in range(len(sub))]
+        bad = [(sub[k], exp[i]) for k, i in enumerate(idx) if as_expected(got[k]) != as_expected(exp[i])]
+        assert not bad, f"max_cmds={max_cmds}: {len(bad)}/{len(sub)} mismatches; first {bad[0]}"
+    assert certified > 0
+
+
 def test_hbm_regime_mid_grid(eng, oracle_lib):
     m = SyntheticMap(129, campfires_per_homeland=4, seed=77)
     for params in (Params(), Params(fleetfoot=3, sort_by=(SORT_TIME, SORT_MONEY)),

@@ -9,8 +9,8 @@ O=gpurun_out/prof_$TAG
 mkdir -p $O
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-steps() { case $1 in c5) echo 3;; c4) echo 10;; *) echo 20;; esac; }
-qpg() { case $1 in c2) echo 10000;; c3) echo 1024;; c4) echo 125000;; c5) echo 10000;; esac; }
+steps() { case $1 in c5) echo 3;; *) echo 20;; esac; }
+qpg() { case $1 in c2) echo 10000;; c3) echo 1024;; c4) echo 1000000;; c5) echo 10000;; esac; }
 for W in $WLS; do
   ST=$(steps $W)
   timeout -k 10 300 python3 "$R/bench.py" --workload $W --steps $ST --warmup 2 > $O/bench_$W.json 2> $O/bench_$W.err || exit 1
@@ -24,6 +24,6 @@ for W in $WLS; do
   python3 "$R/tools/pmc_summary.py" $K --workload $W --queries $(qpg $W) --fetch $O/pmc_FETCH_SIZE_$W --write $O/pmc_WRITE_SIZE_$W --out $O/pmc_$W.json > /dev/null || exit 1
   echo "$W pmc ok"
   K2=hub_kernel; [ $W = c4 ] && K2=hub_lane_kernel; [ $W = c3 ] && K2=hub_fill_kernel; [ $W = c5 ] && K2=hub_wide_kernel
-  bash "$R/tools/gpu_sq.sh" $W $O/sq_$W && python3 "$R/tools/sq_summary.py" --workload $W --kernel $K2 --sq $O/sq_$W --out $O/sq_$W.json > /dev/null || exit 1
+  bash "$R/tools/gpu_sq.sh" $W $O/sq_$W && python3 "$R/tools/sq_summary.py" --workload $W --kernel $K2 --sq $O/sq_$W --queries $(qpg $W) --out $O/sq_$W.json > /dev/null || exit 1
   echo "$W sq ok"
 done

@@ -4,7 +4,7 @@ per launch of the workload's dominant kernel, the instruction counts the SQ repo
 (SQ_INSTS_VALU / SALU / LDS / VMEM_RD / VMEM_WR, summed over the chip) and the waves.
 bench.py turns them into the issue side of the roofline.
 
-    python tools/sq_summary.py --workload c4 --kernel hub_kernel --sq gpurun_out/diag/sq --out profiles/sq_c4.json
+    python tools/sq_summary.py --workload c4 --kernel hub_kernel --sq gpurun_out/diag/sq --queries 125000 --out profiles/sq_c4.json
 """
 from __future__ import annotations
 
@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--kernel", required=True, help="kernel family, e.g. hub_kernel, fill_kernel")
     ap.add_argument("--sq", required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--queries", type=int, required=True, help="queries per GPU of the profiled run (bench.py checks it)")
     a = ap.parse_args()
     files = glob.glob(os.path.join(a.sq, "**", "*counter_collection.csv"), recursive=True)
     vals = defaultdict(list)
@@ -34,7 +35,7 @@ def main():
     if not vals:
         raise SystemExit(f"no {a.kernel} rows under {a.sq}")
     per = {k: sum(v) / len(v) for k, v in vals.items()}
-    out = {"workload": a.workload, "kernel": a.kernel, "per_launch": per,
+    out = {"workload": a.workload, "queries_per_gpu": a.queries, "kernel": a.kernel, "per_launch": per,
            "launches": max(len(v) for v in vals.values()),
            "method": "rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD "
                      "SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-trace --stats (tools/gpu_sq.sh); mean per "
