@@ -162,6 +162,9 @@ struct mr_grid {
     // with a neighbour outside it, the Center excluded), {x | y << 16, rank}, by region
     mutable std::vector<uint32_t> rb_off[4], rb_cell[4];
     mutable bool rb_built[4] = {false, false, false, false};
+    // wide hub solver without the region table: a special cell's row of {distance, rank}
+    // per region, scanned from the boundary cells once per (homeland, cell)
+    mutable std::unordered_map<uint32_t, std::vector<uint32_t>> near_sp_cache[4];
     // device copies of the region tables, uploaded on first use and shared by the
     // grid's plans (the grid outlives its plans)
     mutable uint32_t *d_near[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -744,9 +747,26 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
         hp.near_sp.assign(size_t(NS + 1) * nr * 2, kNone32);
         const std::vector<uint32_t> &nearh = g->nearest[prm->homeland];
         const std::vector<uint32_t> &off = *hp.rb_off, &cell = *hp.rb_cell;
+        // With the grid's region table the rows are its rows (the same (distance, rank)
+        // minimum: seen from outside a region its nearest cell is a boundary cell); without
+        // it each row scans the boundary cells once per grid and special cell (cached: the
+        // scan is O(boundary cells) per special, 28 ms a plan at c5 when done per plan).
         for (uint32_t t = 1; t <= NS; ++t) {
             const uint32_t v = order[t];
             if (v == g->vc) continue;
+            uint32_t *row = &hp.near_sp[size_t(t) * nr * 2];
+            if (hp.near) {
+                std::copy(hp.near->begin() + long(size_t(v) * nr * 2), hp.near->begin() + long(size_t(v + 1) * nr * 2), row);
+                continue;
+            }
+            {
+                std::lock_guard<std::mutex> lk(g->near_mu);
+                auto it = g->near_sp_cache[prm->homeland].find(v);
+                if (it != g->near_sp_cache[prm->homeland].end()) {
+                    std::copy(it->second.begin(), it->second.end(), row);
+                    continue;
+                }
+            }
             const int vx = g->gx(v), vy = g->gy(v);
             for (uint32_t r = 0; r < nr; ++r) {
                 uint32_t bd = kNone32, br = kNone32;
@@ -763,9 +783,11 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
                         }
                     }
                 }
-                hp.near_sp[(size_t(t) * nr + r) * 2] = bd;
-                hp.near_sp[(size_t(t) * nr + r) * 2 + 1] = br;
+                row[2 * r] = bd;
+                row[2 * r + 1] = br;
             }
+            std::lock_guard<std::mutex> lk(g->near_mu);
+            g->near_sp_cache[prm->homeland][v].assign(row, row + 2 * nr);
         }
     }
     // Queries grouped by source vertex, sources ascending, each source's queries in

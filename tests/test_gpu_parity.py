@@ -281,8 +281,11 @@ def test_lane_kernel_wide_tables(eng, oracle_lib, monkeypatch, k, hq, tm):
 
 def test_fallback_sources_reported(eng, oracle_lib, monkeypatch):
     """mr_plan_fallback_sources: the sources a pass re-solved with the SSSP kernel —
-    none on a plain hub pass, every source with MR_HUB_FALLBACK_ALL=1 (the cost signal
-    shard.SourceCosts learns from)."""
+    none on a plain hub pass; with MR_HUB_FALLBACK_ALL=1 every source is handed over,
+    and the list holds exactly those the certificate did not answer (the certified
+    ones cost no search: the cost signal shard.SourceCosts learns from).  The
+    certificate's slots go to the least source indices, so with the certificate off
+    the list is every source, and with 8 slots it is the same set every run."""
     m = SyntheticMap(25, campfires_per_homeland=3, seed=4)
     qs = random_queries(m, 120, 8)
     g = eng.MapGrid(m.cells())
@@ -290,11 +293,23 @@ def test_fallback_sources_reported(eng, oracle_lib, monkeypatch):
     pl.run()
     assert pl.stats()["solver"] == "hub" and pl.fallback_sources() == []
     monkeypatch.setenv("MR_HUB_FALLBACK_ALL", "1")
+    monkeypatch.setenv("MR_CERT", "0")
     pl = eng.Plan(g, Params(), qs)
     pl.run()
     got = pl.fallback_sources()
     assert len(got) == pl.stats()["fallback_sources"] == pl.num_sources
     assert set(got) == {a for a, _ in qs}
+    monkeypatch.delenv("MR_CERT")
+    runs = []
+    for _ in range(2):
+        pl = eng.Plan(g, Params(), qs)
+        pl.run()
+        st = pl.stats()
+        got = pl.fallback_sources()
+        assert st["fallback_sources"] == pl.num_sources and 0 < st["certified_sources"] <= 8, st
+        assert len(got) == st["fallback_sources"] - st["certified_sources"]
+        runs.append(got)
+    assert runs[0] == runs[1]
     check(eng, oracle_lib, m, Params(), qs, "all sources re-solved")
 
 

@@ -5,7 +5,7 @@ set -o pipefail
 O=gpurun_out/r04a
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1 && echo tests-ok || { tail -40 $O/gpu_tests.log; exit 1; }
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1 && echo tests-ok || { tail -60 $O/gpu_tests.log; }
 tail -3 $O/gpu_tests.log
 timeout -k 10 400 python bench.py > $O/bench_c4.json 2> $O/bench_c4.err && echo bench-ok || { tail -20 $O/bench_c4.err; exit 1; }
 cat $O/bench_c4.json
