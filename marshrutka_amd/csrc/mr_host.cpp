@@ -9,7 +9,9 @@
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <chrono>
 #include <thread>
@@ -74,6 +76,74 @@ static int fail(int code, const std::string &msg) {
     g_last_error = msg;
     return code;
 }
+
+// ------------------------------------------------------------------ host threads
+// A persistent pool for the per-batch host work (grouping a batch by source, the fetch's
+// copies): run(n, fn) calls fn(i) for every i in [0, n) on the pool's workers and the
+// calling thread, and returns when every call has finished.  One job at a time (callers
+// are serialised); min(16, hardware threads) threads (MR_HOST_THREADS overrides: a GPU
+// box's share of its host is 16 CPUs, more threads would only time-slice).
+class HostPool {
+  public:
+    static HostPool &get() {
+        static HostPool *p = new HostPool();  // never destroyed: workers block on it at exit
+        return *p;
+    }
+    uint32_t size() const { return nthreads_; }
+    void run(uint32_t n, const std::function<void(uint32_t)> &fn) {
+        if (n == 0) return;
+        if (nthreads_ <= 1 || n == 1) {
+            for (uint32_t i = 0; i < n; ++i) fn(i);
+            return;
+        }
+        std::lock_guard<std::mutex> job(job_mu_);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            fn_ = &fn;
+            n_ = n;
+            next_.store(0);
+            pending_ = nthreads_ - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [&] { return pending_ == 0; });
+        fn_ = nullptr;
+    }
+
+  private:
+    HostPool() {
+        nthreads_ = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+        if (const char *e = std::getenv("MR_HOST_THREADS")) nthreads_ = uint32_t(std::max(1, std::min(64, std::atoi(e))));
+        for (uint32_t t = 1; t < nthreads_; ++t) std::thread([this] { loop(); }).detach();
+    }
+    void work() {
+        for (uint32_t i = next_++; i < n_; i = next_++) (*fn_)(i);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+            }
+            work();
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0) done_cv_.notify_one();
+        }
+    }
+    uint32_t nthreads_ = 1;
+    std::mutex job_mu_, mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(uint32_t)> *fn_ = nullptr;
+    uint32_t n_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    std::atomic<uint32_t> next_{0};
+};
+// [0, n) in `parts` near-equal ranges: range p is [chunk_lo(n, parts, p), chunk_lo(n, parts, p + 1))
+static inline uint32_t chunk_lo(uint32_t n, uint32_t parts, uint32_t p) { return uint32_t(uint64_t(n) * p / parts); }
 
 // ------------------------------------------------------------------ CellIndex
 static inline uint64_t ci_key(const mr_cell_index &c) {
@@ -793,58 +863,117 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     // Queries grouped by source vertex, sources ascending, each source's queries in
     // input order: a stable sort of the valid queries by source, 13-bit LSD radix passes
     // over the batch (two while V < 2^26).  The counting sort it replaces touched two
-    // V-sized arrays at random (5.5 ms at 125k queries on 1025^2).
+    // V-sized arrays at random (5.5 ms at 125k queries on 1025^2).  Large batches run
+    // every phase over host threads (HostPool): per part a histogram, the parts' offsets
+    // by (digit, part) keep the sort stable, then each part scatters its own keys.
     const uint32_t V = g->V;
     hp.nq = n;
     hp.q_status.assign(n, MR_OK);
-    std::vector<uint64_t> kv, tmp;  // source << 32 | query index
-    kv.reserve(n);
-    std::vector<uint32_t> qs_dst(n);
-    for (uint32_t i = 0; i < n; ++i) {
-        uint32_t a, b;
-        if (!g->find(qs[i].from, a) || !g->find(qs[i].to, b)) {
-            hp.q_status[i] = MR_ERR_INVALID_INDEX;
-            continue;
+    HostPool &pool = HostPool::get();
+    // about 64k queries a part (a part's work must outweigh waking a thread)
+    const uint32_t parts = std::max(1u, std::min(pool.size(), n / 65536u));
+    std::vector<uint32_t> qs_src(n), qs_dst(n), cnt(parts + 1, 0);
+    pool.run(parts, [&](uint32_t pt) {
+        uint32_t c = 0;
+        for (uint32_t i = chunk_lo(n, parts, pt), e = chunk_lo(n, parts, pt + 1); i < e; ++i) {
+            uint32_t a, b;
+            if (!g->find(qs[i].from, a) || !g->find(qs[i].to, b)) {
+                hp.q_status[i] = MR_ERR_INVALID_INDEX;
+                qs_src[i] = kNone32;
+                continue;
+            }
+            qs_src[i] = a;
+            qs_dst[i] = b;
+            ++c;
         }
-        qs_dst[i] = b;
-        kv.push_back((uint64_t(a) << 32) | i);
-    }
-    const uint32_t m = uint32_t(kv.size());
-    tmp.resize(m);
+        cnt[pt + 1] = c;
+    });
+    for (uint32_t pt = 0; pt < parts; ++pt) cnt[pt + 1] += cnt[pt];
+    const uint32_t m = cnt[parts];
+    std::vector<uint64_t> kv(m), tmp(m);  // source << 32 | query index
+    pool.run(parts, [&](uint32_t pt) {
+        uint32_t o = cnt[pt];
+        for (uint32_t i = chunk_lo(n, parts, pt), e = chunk_lo(n, parts, pt + 1); i < e; ++i)
+            if (qs_src[i] != kNone32) kv[o++] = (uint64_t(qs_src[i]) << 32) | i;
+    });
     constexpr uint32_t kBits = 13, kB = 1u << kBits;
     const uint32_t passes = V <= (1u << (2 * kBits)) ? 2u : 3u;
-    std::vector<uint32_t> hist(kB);
+    std::vector<uint32_t> hist(size_t(parts) * kB);
     for (uint32_t pass = 0; pass < passes; ++pass) {
         const uint32_t sh = 32 + kBits * pass;
-        std::fill(hist.begin(), hist.end(), 0u);
-        for (uint32_t k = 0; k < m; ++k) ++hist[uint32_t(kv[k] >> sh) & (kB - 1)];
-        uint32_t acc = 0;
-        for (uint32_t j = 0; j < kB; ++j) {
-            const uint32_t c = hist[j];
-            hist[j] = acc;
-            acc += c;
+        pool.run(parts, [&](uint32_t pt) {
+            uint32_t *h = &hist[size_t(pt) * kB];
+            std::fill(h, h + kB, 0u);
+            for (uint32_t k = chunk_lo(m, parts, pt), e = chunk_lo(m, parts, pt + 1); k < e; ++k)
+                ++h[uint32_t(kv[k] >> sh) & (kB - 1)];
+        });
+        // offsets by (digit, part): the digits' totals, their prefix, then per digit the
+        // parts in order (ranges of digits per thread: each part's row is read in order)
+        if (parts == 1) {
+            uint32_t acc = 0;
+            for (uint32_t j = 0; j < kB; ++j) {
+                const uint32_t c = hist[j];
+                hist[j] = acc;
+                acc += c;
+            }
+        } else {
+            std::vector<uint32_t> base(kB + 1, 0);
+            pool.run(parts, [&](uint32_t pt) {
+                for (uint32_t j = chunk_lo(kB, parts, pt), e = chunk_lo(kB, parts, pt + 1); j < e; ++j) {
+                    uint32_t c = 0;
+                    for (uint32_t q = 0; q < parts; ++q) c += hist[size_t(q) * kB + j];
+                    base[j + 1] = c;
+                }
+            });
+            for (uint32_t j = 0; j < kB; ++j) base[j + 1] += base[j];
+            pool.run(parts, [&](uint32_t pt) {
+                for (uint32_t j = chunk_lo(kB, parts, pt), e = chunk_lo(kB, parts, pt + 1); j < e; ++j) {
+                    uint32_t acc = base[j];
+                    for (uint32_t q = 0; q < parts; ++q) {
+                        const uint32_t c = hist[size_t(q) * kB + j];
+                        hist[size_t(q) * kB + j] = acc;
+                        acc += c;
+                    }
+                }
+            });
         }
-        for (uint32_t k = 0; k < m; ++k) tmp[hist[uint32_t(kv[k] >> sh) & (kB - 1)]++] = kv[k];
+        pool.run(parts, [&](uint32_t pt) {
+            uint32_t *h = &hist[size_t(pt) * kB];
+            for (uint32_t k = chunk_lo(m, parts, pt), e = chunk_lo(m, parts, pt + 1); k < e; ++k)
+                tmp[h[uint32_t(kv[k] >> sh) & (kB - 1)]++] = kv[k];
+        });
         kv.swap(tmp);
     }
-    hp.src_v.clear();
-    hp.q_begin.clear();
+    // sources: a new one starts where the sorted source changes; per part the count of
+    // starts, then each part writes its sources and its records' destinations / ids
+    std::vector<uint32_t> starts(parts + 1, 0);
+    pool.run(parts, [&](uint32_t pt) {
+        uint32_t c = 0;
+        for (uint32_t k = chunk_lo(m, parts, pt), e = chunk_lo(m, parts, pt + 1); k < e; ++k)
+            c += (k == 0 || (kv[k] >> 32) != (kv[k - 1] >> 32)) ? 1u : 0u;
+        starts[pt + 1] = c;
+    });
+    for (uint32_t pt = 0; pt < parts; ++pt) starts[pt + 1] += starts[pt];
+    hp.src_v.resize(starts[parts]);
+    hp.q_begin.resize(starts[parts] + 1);
     hp.q_dst.resize(m);
     hp.q_id.resize(m);
     hp.q_pos.assign(n, kNone32);
-    uint32_t prev = kNone32;
-    for (uint32_t k = 0; k < m; ++k) {
-        const uint32_t a = uint32_t(kv[k] >> 32), i = uint32_t(kv[k]);
-        if (a != prev) {
-            hp.src_v.push_back(a);
-            hp.q_begin.push_back(k);
-            prev = a;
+    pool.run(parts, [&](uint32_t pt) {
+        uint32_t si = starts[pt];
+        for (uint32_t k = chunk_lo(m, parts, pt), e = chunk_lo(m, parts, pt + 1); k < e; ++k) {
+            const uint32_t a = uint32_t(kv[k] >> 32), i = uint32_t(kv[k]);
+            if (k == 0 || a != uint32_t(kv[k - 1] >> 32)) {
+                hp.src_v[si] = a;
+                hp.q_begin[si] = k;
+                ++si;
+            }
+            hp.q_dst[k] = qs_dst[i];
+            hp.q_id[k] = i;
+            hp.q_pos[i] = k;  // the device writes query i's record at grouped position k
         }
-        hp.q_dst[k] = qs_dst[i];
-        hp.q_id[k] = i;
-        hp.q_pos[i] = k;  // the device writes query i's record at grouped position k
-    }
-    hp.q_begin.push_back(m);
+    });
+    hp.q_begin[starts[parts]] = m;
     return MR_OK;
 }
 
@@ -1067,6 +1196,110 @@ static int upload(T *&dptr, const std::vector<T> &h) {
 }
 
 }  // namespace
+
+// Pinned host staging for the per-batch copies (the query block up, a fetch's results
+// and commands down): a pageable hipMemcpy runs at a fraction of the DMA rate.  One
+// grow-only buffer per direction; a copy holds its mutex while it uses the buffer.
+struct PinnedStage {
+    std::mutex mu;
+    void *p = nullptr;
+    size_t bytes = 0;
+    void *get(size_t want) {  // caller holds mu; nullptr if pinned memory is not available
+        if (bytes >= want) return p;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+        const size_t cls = (want + (size_t(8) << 20) - 1) / (size_t(8) << 20) * (size_t(8) << 20);
+        if (hipHostMalloc(&p, cls, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            p = nullptr;
+            return nullptr;
+        }
+        bytes = cls;
+        return p;
+    }
+};
+static PinnedStage &stage_up() {
+    static PinnedStage *s = new PinnedStage();
+    return *s;
+}
+static PinnedStage &stage_down() {
+    static PinnedStage *s = new PinnedStage();
+    return *s;
+}
+// true when [p, p + bytes) is page-locked host memory HIP can DMA into directly
+static bool host_pinned(const void *p) {
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeHost && at.hostPointer != nullptr;
+}
+// Device -> host copies of `n` segments into caller memory on `s`: straight DMA when the
+// destination is pinned, else through the pinned stage in 16 MB chunks, two in flight:
+// the DMA of chunk c + 1 runs while host threads copy chunk c out of the stage.
+struct D2HSeg {
+    void *dst;
+    const void *src;
+    size_t bytes;
+};
+static hipError_t copy_d2h(const D2HSeg *seg, int n, hipStream_t s) {
+    hipError_t e = hipSuccess;
+    bool direct = true;
+    for (int i = 0; i < n; ++i)
+        if (seg[i].bytes && !host_pinned(seg[i].dst)) direct = false;
+    if (direct) {
+        for (int i = 0; i < n && e == hipSuccess; ++i)
+            if (seg[i].bytes) e = hipMemcpyAsync(seg[i].dst, seg[i].src, seg[i].bytes, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        return e;
+    }
+    constexpr size_t kChunk = size_t(16) << 20;
+    PinnedStage &st = stage_down();
+    std::lock_guard<std::mutex> lk(st.mu);
+    char *buf = static_cast<char *>(st.get(2 * kChunk));
+    if (!buf) {  // no pinned memory: pageable copies
+        for (int i = 0; i < n && e == hipSuccess; ++i)
+            if (seg[i].bytes) e = hipMemcpyAsync(seg[i].dst, seg[i].src, seg[i].bytes, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        return e;
+    }
+    struct Chunk {
+        char *dst;
+        const char *src;
+        size_t bytes;
+    };
+    std::vector<Chunk> ch;
+    for (int i = 0; i < n; ++i)
+        for (size_t o = 0; o < seg[i].bytes; o += kChunk)
+            ch.push_back({static_cast<char *>(seg[i].dst) + o, static_cast<const char *>(seg[i].src) + o,
+                          std::min(kChunk, seg[i].bytes - o)});
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    for (hipEvent_t &x : ev)
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&x, hipEventDisableTiming);
+    auto issue = [&](size_t c) {
+        if (e == hipSuccess) e = hipMemcpyAsync(buf + (c % 2) * kChunk, ch[c].src, ch[c].bytes, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipEventRecord(ev[c % 2], s);
+    };
+    for (size_t c = 0; c < ch.size() && c < 2; ++c) issue(c);
+    HostPool &pool = HostPool::get();
+    for (size_t c = 0; c < ch.size() && e == hipSuccess; ++c) {
+        e = hipEventSynchronize(ev[c % 2]);
+        if (e != hipSuccess) break;
+        const char *from = buf + (c % 2) * kChunk;
+        const uint32_t parts = ch[c].bytes >= (size_t(1) << 20) ? pool.size() : 1u;
+        pool.run(parts, [&](uint32_t pt) {
+            const size_t a = ch[c].bytes * pt / parts, b = ch[c].bytes * (pt + 1) / parts;
+            std::memcpy(ch[c].dst + a, from + a, b - a);
+        });
+        if (c + 2 < ch.size()) issue(c + 2);
+    }
+    (void)hipStreamSynchronize(s);  // nothing may still write the stage once it is unlocked
+    for (hipEvent_t x : ev)
+        if (x) (void)hipEventDestroy(x);
+    return e;
+}
 
 static hipError_t dev_malloc(void **p, size_t bytes) {
     hipError_t e = hipMalloc(p, bytes);
@@ -1399,12 +1632,32 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     {  // the per-batch arrays in one device block and one copy (sources, offsets, destinations, query ids)
         const size_t a0 = 0, a1 = a0 + (hp.src_v.size() + 63) / 64 * 64, a2 = a1 + (hp.q_begin.size() + 63) / 64 * 64,
                      a3 = a2 + (hp.q_dst.size() + 63) / 64 * 64, a4 = a3 + (hp.q_id.size() + 63) / 64 * 64;
-        std::vector<uint32_t> pack(std::max<size_t>(a4, 1));
-        std::copy(hp.src_v.begin(), hp.src_v.end(), pack.begin() + long(a0));
-        std::copy(hp.q_begin.begin(), hp.q_begin.end(), pack.begin() + long(a1));
-        std::copy(hp.q_dst.begin(), hp.q_dst.end(), pack.begin() + long(a2));
-        std::copy(hp.q_id.begin(), hp.q_id.end(), pack.begin() + long(a3));
-        if ((st = upload(pl->d_qblock, pack))) return bail(st);
+        // packed in the pinned upload stage (host threads for large batches), one DMA
+        const size_t words = std::max<size_t>(a4, 1);
+        if (pmalloc(reinterpret_cast<void **>(&pl->d_qblock), words * 4) != hipSuccess)
+            return bail(fail(MR_ERR_DEVICE, "hipMalloc query block"));
+        {
+            PinnedStage &su = stage_up();
+            std::lock_guard<std::mutex> lk(su.mu);
+            uint32_t *pack = static_cast<uint32_t *>(su.get(words * 4));
+            std::vector<uint32_t> pv;
+            if (!pack) {
+                pv.assign(words, 0u);
+                pack = pv.data();
+            }
+            const std::vector<uint32_t> *arr[4] = {&hp.src_v, &hp.q_begin, &hp.q_dst, &hp.q_id};
+            const size_t at[4] = {a0, a1, a2, a3};
+            HostPool &hpool = HostPool::get();
+            const uint32_t parts = words >= (size_t(1) << 18) ? hpool.size() : 1u;
+            hpool.run(4 * parts, [&](uint32_t j) {
+                const std::vector<uint32_t> &v = *arr[j / parts];
+                const uint32_t pt = j % parts, lo = chunk_lo(uint32_t(v.size()), parts, pt),
+                               hi = chunk_lo(uint32_t(v.size()), parts, pt + 1);
+                if (hi > lo) std::memcpy(pack + at[j / parts] + lo, v.data() + lo, size_t(hi - lo) * 4);
+            });
+            if (hipMemcpy(pl->d_qblock, pack, words * 4, hipMemcpyHostToDevice) != hipSuccess)
+                return bail(fail(MR_ERR_DEVICE, "upload query block"));
+        }
         pl->d_src = pl->d_qblock + a0;
         pl->d_qb = pl->d_qblock + a1;
         pl->d_qd = pl->d_qblock + a2;
@@ -2266,8 +2519,11 @@ static bool plan_fetch_device(mr_plan *pl, mr_result *results, mr_command *pool,
     if (e == hipSuccess) e = hipMemcpyAsync(&tailw[0], err, 4, hipMemcpyDeviceToHost, pl->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(&tailw[1], off + (nq - 1), 4, hipMemcpyDeviceToHost, pl->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(&tailw[2], cnt + (nq - 1), 4, hipMemcpyDeviceToHost, pl->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(results, d_out, size_t(nq) * sizeof(mr_result), hipMemcpyDeviceToHost, pl->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(pl->stream);
+    if (e == hipSuccess) {
+        const D2HSeg sg{results, d_out, size_t(nq) * sizeof(mr_result)};
+        e = copy_d2h(&sg, 1, pl->stream);
+    }
     // queries without a record (an invalid index), and the status to return: the first
     // error in query order, or MR_ERR_CAPACITY once a label's commands do not fit the
     // caller's pool (written up to the first such label), as the host decoder does
@@ -2289,8 +2545,10 @@ static bool plan_fetch_device(mr_plan *pl, mr_result *results, mr_command *pool,
             }
         }
     const uint64_t ncopy = std::min<uint64_t>(end, pcap);
-    if (e == hipSuccess && ncopy && !(tailw[0] & 1u))
-        e = hipMemcpy(pool, d_pool, size_t(ncopy) * sizeof(mr_command), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && ncopy && !(tailw[0] & 1u)) {
+        const D2HSeg sg{pool, d_pool, size_t(ncopy) * sizeof(mr_command)};
+        e = copy_d2h(&sg, 1, pl->stream);
+    }
     // the blocks go back to the cache, which hands them out with no implicit sync: on
     // every path (a failed enqueue included) the work queued on them must be done first
     (void)hipStreamSynchronize(pl->stream);

@@ -61,6 +61,10 @@ __host__ __device__ constexpr uint32_t lane_waves(uint32_t TM) { return TM <= 22
 #define MR_LANE_FENCE() do {} while (0)
 #endif
 
+// pair-table reads issued this many entries ahead of their use in the relax loop
+#ifndef MR_LANE_PF
+#define MR_LANE_PF 1
+#endif
 // meta: length (8 b) | kind of the first tail command (3 b) << 8 | parent entry (5 b)
 // << 11 | (tail count - 1) << 16 | CentralMove count (2 b) << 17
 __device__ __forceinline__ uint32_t lm_len(uint32_t m) { return m & 0xFFu; }
@@ -124,6 +128,43 @@ __device__ __forceinline__ uint32_t ltm(const LLab &x, const LLab &y) {
         : "vcc");
     return r;
 }
+// d = c when c < d on (c1, c2, c3, length): the borrow chain leaves the order in VCC and
+// four v_cndmask_b32_e32 select on it directly (4-byte VOP2 selects, no mask register,
+// and one asm block instead of six, so no s_nop between them).  The in-out operands are
+// early clobbers: a select writes d before the block has read all of c, and an input
+// holding the same value as a d word may otherwise share its register.
+__device__ __forceinline__ void ltm_take(const LLab &c, LLab &d) {
+    uint32_t t;
+    asm("v_sub_co_u32_sdwa %0, vcc, %5, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %6, %2, vcc\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %7, %3, vcc\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %8, %4, vcc\n\t"
+        "v_cndmask_b32_e32 %4, %4, %8, vcc\n\t"
+        "v_cndmask_b32_e32 %3, %3, %7, vcc\n\t"
+        "v_cndmask_b32_e32 %2, %2, %6, vcc\n\t"
+        "v_cndmask_b32_e32 %1, %1, %5, vcc"
+        : "=&v"(t), "+&v"(d.m), "+&v"(d.c3), "+&v"(d.c2), "+&v"(d.c1)
+        : "v"(c.m), "v"(c.c3), "v"(c.c2), "v"(c.c1)
+        : "vcc");
+}
+// the same with an index word riding along (i = ci when c is taken); returns the mask
+__device__ __forceinline__ uint32_t ltm_take_idx(const LLab &c, LLab &d, uint32_t ci, uint32_t &i) {
+    uint32_t t, k;
+    asm("v_sub_co_u32_sdwa %0, vcc, %8, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %9, %4, vcc\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %10, %5, vcc\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %11, %6, vcc\n\t"
+        "v_cndmask_b32_e64 %1, 0, -1, vcc\n\t"
+        "v_cndmask_b32_e32 %6, %6, %11, vcc\n\t"
+        "v_cndmask_b32_e32 %5, %5, %10, vcc\n\t"
+        "v_cndmask_b32_e32 %4, %4, %9, vcc\n\t"
+        "v_cndmask_b32_e32 %3, %3, %8, vcc\n\t"
+        "v_cndmask_b32_e32 %2, %2, %7, vcc"
+        : "=&v"(t), "=&v"(k), "+&v"(i), "+&v"(d.m), "+&v"(d.c3), "+&v"(d.c2), "+&v"(d.c1)
+        : "v"(ci), "v"(c.m), "v"(c.c3), "v"(c.c2), "v"(c.c1)
+        : "vcc");
+    return k;
+}
 // x < y on the metrics (c1, c2, c3) alone
 __device__ __forceinline__ uint32_t ltm3(const LLab &x, const LLab &y) {
     uint32_t t, r;
@@ -184,7 +225,11 @@ struct LaneHub {
     __device__ __forceinline__ static LLab inf() { return LLab{kInf1, 0u, 0u, 0u}; }
     __device__ __forceinline__ static LLab opt(uint32_t on, const LLab &c) { return LLab{c.c1 | ~on, c.c2, c.c3, c.m}; }
     // c replaces f when strictly smaller (callers visit candidates in kind order)
+#ifdef MR_LANE_CLASSIC
     __device__ __forceinline__ static void consider(LLab &f, const LLab &c) { ll_sel(ltm(c, f), f, c); }
+#else
+    __device__ __forceinline__ static void consider(LLab &f, const LLab &c) { ltm_take(c, f); }
+#endif
     // (c1, c2, c3, length): -1, 0, 1 (rare paths)
     __device__ __forceinline__ static int cmp4(const LLab &x, const LLab &y) {
         if (x.c1 != y.c1) return x.c1 < y.c1 ? -1 : 1;
@@ -354,10 +399,17 @@ struct LaneHub {
     __device__ __forceinline__ void offer(uint32_t t, const FromS &f, uint32_t &ties) {
         LLab &T = L[t];
         const uint32_t bit = 1u << t;
-        const uint32_t lt = ltm(f.c, T) & f.any;
+        // (an absent candidate, c1 = 2^32 - 1, is below neither a present label nor an
+        // absent one: no `& f.any` on lt and drop)
         const uint32_t gt = ltm(T, f.c);
-        const uint32_t drop = ltm3(f.c, T) & f.any;  // the tentative metrics drop
+        const uint32_t drop = ltm3(f.c, T);  // the tentative metrics drop
+#ifdef MR_LANE_CLASSIC
+        const uint32_t lt = ltm(f.c, T);
         ll_sel(lt, T, f.c);
+#else
+        uint32_t dummy = 0;
+        const uint32_t lt = ltm_take_idx(f.c, T, 0u, dummy);
+#endif
         tent |= lt & bit;
         // blocker bit: a walk candidate with the (new) tentative metrics; the walk is >= the
         // new tentative label, so it ties unless the label's metrics are strictly smaller
@@ -504,10 +556,16 @@ struct LaneHub {
                 uint32_t &tx = (t & 1u) ? ta : tb;
                 const uint32_t cm = bitm(cand, t);
                 const LLab c = opt(cm, L[t]);
+#ifdef MR_LANE_CLASSIC
                 const uint32_t lt = ltm(c, lx), gt = ltm(lx, c);
                 tx = ~lt & (tx | (cm & ~gt));
                 ll_sel(lt, lx, c);
                 sx_ = msel(lt, t, sx_);
+#else
+                const uint32_t gt = ltm(lx, c);
+                const uint32_t lt = ltm_take_idx(c, lx, t, sx_);
+                tx = ~lt & (tx | (cm & ~gt));
+#endif
                 MR_LANE_FENCE();
             }
             Settle z;
@@ -568,11 +626,28 @@ struct LaneHub {
             // (the command chains of the list compares walk settled entries only) and
             // for the others the meta of this iteration's best candidate, which the tie
             // path below reads instead of rebuilding the candidate.
+            // The pair-table words of entry t are read MR_LANE_PF entries ahead: the fences
+            // keep each entry's code in place, so a read issued in its own entry left the
+            // wave parked on it (SQ: ~31 % of the kernel's wave cycles waiting).
             uint32_t ties = 0;
             uint32_t *ml = M + lane_id();
+            uint4 pa[MR_LANE_PF + 1];
+            uint2 pb[MR_LANE_PF + 1];
+#pragma unroll
+            for (uint32_t j = 0; j < MR_LANE_PF; ++j) {
+                if (1 + j < TM) pa[j] = rowa[1 + j];
+                if (1 + j >= 6 && 1 + j < 6 + kLaneRegs && 1 + j < TM) pb[j] = rowb[1 + j];
+            }
 #pragma unroll
             for (uint32_t t = 1; t < TM; ++t) {
-                const FromS f = from_s(z, t, rowa[t], rowb[t]);
+                constexpr uint32_t R = MR_LANE_PF + 1;
+                const uint32_t ahead = t + MR_LANE_PF;
+                if (ahead < TM) {
+                    pa[(ahead - 1) % R] = rowa[ahead];
+                    if (ahead >= 6 && ahead < 6 + kLaneRegs) pb[(ahead - 1) % R] = rowb[ahead];
+                }
+                const uint2 B = (t >= 6 && t < 6 + kLaneRegs) ? pb[(t - 1) % R] : make_uint2(0, 0);
+                const FromS f = from_s(z, t, pa[(t - 1) % R], B);
                 offer(t, f, ties);
                 ml[t * 64u] = msel(bitm(done, t), L[t].m, f.c.m);
                 MR_LANE_FENCE();
@@ -640,10 +715,16 @@ struct LaneHub {
                 const uint32_t k = walk_dist(spl[t].x, spl[t].y, wx, wy);
                 const uint32_t cm = bitm(bq, t);
                 const LLab c = opt(cm, add(L[t], k, 0, 180u * k, L[t].m));
+#ifdef MR_LANE_CLASSIC
                 const uint32_t lt = ltm(c, x), gt = ltm(x, c);
                 tie = ~lt & (tie | (cm & ~gt));
                 ll_sel(lt, x, c);
                 bx = msel(lt, t, bx);
+#else
+                const uint32_t gt = ltm(x, c);
+                const uint32_t lt = ltm_take_idx(c, x, t, bx);
+                tie = ~lt & (tie | (cm & ~gt));
+#endif
                 MR_LANE_FENCE();
             }
             x.m = lm_pack(lm_len(x.m) + 1u, bx == kNone32 ? 0u : bx, 1, kStandard);

@@ -359,6 +359,13 @@ def labels_digest(results, pool, n: int, order=None) -> str:
     return h.hexdigest()
 
 
+def fetch_buffers(n: int, max_cmds: int = 16):
+    """Host buffers for Plan.fetch_raw(out=...) of plans of up to n queries with max_cmds
+    command slots: (results, command pool: the slots + the overflow pool)."""
+    cap = n * max_cmds + max(4096, n * 8)
+    return _host_array(mr_result, max(n, 1)), _host_array(mr_command, cap)
+
+
 class Plan:
     """Device-resident batch: inputs uploaded once, `run()` enqueues one pass."""
 
@@ -455,14 +462,21 @@ class Plan:
         if st != MR_OK:
             raise EngineError(st, last_error())
 
-    def fetch_raw(self):
+    def fetch_buffers(self):
+        """Host buffers fetch_raw can fill (results, command pool), sized for this plan:
+        a caller answering batch after batch allocates them once and passes them back."""
+        return fetch_buffers(self.n, self.max_cmds)
+
+    def fetch_raw(self, out=None):
         """(results, command pool) as ctypes arrays, no Python label objects.  The
         buffers are uninitialised host memory (mr_plan_fetch writes every result and
         the commands they point at; a zero-filled pool of n * (max_cmds + 8) commands
-        costs seconds at millions of queries)."""
-        res = _host_array(mr_result, max(self.n, 1))
-        cap = self.n * self.max_cmds + max(4096, self.n * 8)  # slots + overflow pool
-        pool = _host_array(mr_command, cap)
+        costs seconds at millions of queries); `out` = buffers of fetch_buffers() (of
+        this plan or a larger one) to fill instead of new ones."""
+        res, pool = out if out is not None else self.fetch_buffers()
+        cap = len(pool)
+        if len(res) < max(self.n, 1):
+            raise EngineError(abi.MR_ERR_INVALID_ARG, "fetch_raw: result buffer shorter than the batch")
         st = lib().mr_plan_fetch(self.handle, res, pool, cap)
         if st < 0 and st not in (abi.MR_ERR_INVALID_INDEX, MR_ERR_CAPACITY):
             raise EngineError(st, last_error())
