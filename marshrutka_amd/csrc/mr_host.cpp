@@ -680,6 +680,7 @@ static uint32_t caravan_unit_time(uint32_t route_guru) {
 
 static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs, uint32_t n, uint32_t max_cmds,
                       HostPlan &hp) {
+    const double tbs = timing_on() ? now_ms() : 0.0;
     if (!g || !prm) return fail(MR_ERR_INVALID_ARG, "null grid or params");
     if (prm->sort_by[0] > 2 || prm->sort_by[1] > 2 || prm->homeland > 3)
         return fail(MR_ERR_INVALID_ARG, "invalid sort_by or homeland");
@@ -861,52 +862,72 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
         }
     }
     // Queries grouped by source vertex, sources ascending, each source's queries in
-    // input order: a stable sort of the valid queries by source, 13-bit LSD radix passes
-    // over the batch (two while V < 2^26).  The counting sort it replaces touched two
+    // input order: a stable sort of the queries by source, 13-bit LSD radix passes over
+    // the batch (two while V < 2^26).  The counting sort it replaces touched two
     // V-sized arrays at random (5.5 ms at 125k queries on 1025^2).  Large batches run
     // every phase over host threads (HostPool): per part a histogram, the parts' offsets
     // by (digit, part) keep the sort stable, then each part scatters its own keys.
     const uint32_t V = g->V;
     hp.nq = n;
-    hp.q_status.assign(n, MR_OK);
+    const double tb0 = timing_on() ? now_ms() : 0.0;
     HostPool &pool = HostPool::get();
     // about 64k queries a part (a part's work must outweigh waking a thread)
     const uint32_t parts = std::max(1u, std::min(pool.size(), n / 65536u));
-    std::vector<uint32_t> qs_src(n), qs_dst(n), cnt(parts + 1, 0);
+    constexpr uint32_t kBits = 13, kB = 1u << kBits;
+    // An invalid query gets the source key 2^32 - 1: its low bits are all ones, so with
+    // enough passes to cover every vertex id (two while V < 2^26) it sorts after every
+    // valid query, and the grouping stops at the first one.
+    const uint32_t passes = V < (1u << (2 * kBits)) ? 2u : 3u;
+    // scratch reused across plans of this thread (no fresh pages per batch); the pool's
+    // workers reach it through these references (a thread_local named inside a lambda
+    // would be the worker's own)
+    static thread_local std::vector<uint64_t> kv_s, tmp_s;  // source << 32 | query index
+    static thread_local std::vector<uint32_t> hist_s, dst_s;
+    std::vector<uint64_t> &kv = kv_s, &tmp = tmp_s;
+    std::vector<uint32_t> &hist = hist_s, &qs_dst = dst_s;
+    kv.resize(n);
+    tmp.resize(n);
+    qs_dst.resize(n);
+    hist.resize(size_t(parts) * kB);
+    hp.q_status.resize(n);
+    hp.q_pos.resize(n);
+    std::vector<uint32_t> bad(parts + 1, 0);
+    // lookups, fused with the first pass's histogram
     pool.run(parts, [&](uint32_t pt) {
+        uint32_t *h = &hist[size_t(pt) * kB];
+        std::fill(h, h + kB, 0u);
         uint32_t c = 0;
         for (uint32_t i = chunk_lo(n, parts, pt), e = chunk_lo(n, parts, pt + 1); i < e; ++i) {
             uint32_t a, b;
+            uint64_t key;
             if (!g->find(qs[i].from, a) || !g->find(qs[i].to, b)) {
                 hp.q_status[i] = MR_ERR_INVALID_INDEX;
-                qs_src[i] = kNone32;
-                continue;
+                hp.q_pos[i] = kNone32;
+                key = (uint64_t(kNone32) << 32) | i;
+                ++c;
+            } else {
+                hp.q_status[i] = MR_OK;
+                qs_dst[i] = b;
+                key = (uint64_t(a) << 32) | i;
             }
-            qs_src[i] = a;
-            qs_dst[i] = b;
-            ++c;
+            kv[i] = key;
+            ++h[uint32_t(key >> 32) & (kB - 1)];
         }
-        cnt[pt + 1] = c;
+        bad[pt + 1] = c;
     });
-    for (uint32_t pt = 0; pt < parts; ++pt) cnt[pt + 1] += cnt[pt];
-    const uint32_t m = cnt[parts];
-    std::vector<uint64_t> kv(m), tmp(m);  // source << 32 | query index
-    pool.run(parts, [&](uint32_t pt) {
-        uint32_t o = cnt[pt];
-        for (uint32_t i = chunk_lo(n, parts, pt), e = chunk_lo(n, parts, pt + 1); i < e; ++i)
-            if (qs_src[i] != kNone32) kv[o++] = (uint64_t(qs_src[i]) << 32) | i;
-    });
-    constexpr uint32_t kBits = 13, kB = 1u << kBits;
-    const uint32_t passes = V <= (1u << (2 * kBits)) ? 2u : 3u;
-    std::vector<uint32_t> hist(size_t(parts) * kB);
+    uint32_t nbad = 0;
+    for (uint32_t pt = 0; pt < parts; ++pt) nbad += bad[pt + 1];
+    const uint32_t m = n - nbad;
+    const double tb1 = timing_on() ? now_ms() : 0.0;
     for (uint32_t pass = 0; pass < passes; ++pass) {
         const uint32_t sh = 32 + kBits * pass;
-        pool.run(parts, [&](uint32_t pt) {
-            uint32_t *h = &hist[size_t(pt) * kB];
-            std::fill(h, h + kB, 0u);
-            for (uint32_t k = chunk_lo(m, parts, pt), e = chunk_lo(m, parts, pt + 1); k < e; ++k)
-                ++h[uint32_t(kv[k] >> sh) & (kB - 1)];
-        });
+        if (pass > 0)
+            pool.run(parts, [&](uint32_t pt) {
+                uint32_t *h = &hist[size_t(pt) * kB];
+                std::fill(h, h + kB, 0u);
+                for (uint32_t k = chunk_lo(n, parts, pt), e = chunk_lo(n, parts, pt + 1); k < e; ++k)
+                    ++h[uint32_t(kv[k] >> sh) & (kB - 1)];
+            });
         // offsets by (digit, part): the digits' totals, their prefix, then per digit the
         // parts in order (ranges of digits per thread: each part's row is read in order)
         if (parts == 1) {
@@ -939,11 +960,12 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
         }
         pool.run(parts, [&](uint32_t pt) {
             uint32_t *h = &hist[size_t(pt) * kB];
-            for (uint32_t k = chunk_lo(m, parts, pt), e = chunk_lo(m, parts, pt + 1); k < e; ++k)
+            for (uint32_t k = chunk_lo(n, parts, pt), e = chunk_lo(n, parts, pt + 1); k < e; ++k)
                 tmp[h[uint32_t(kv[k] >> sh) & (kB - 1)]++] = kv[k];
         });
         kv.swap(tmp);
     }
+    const double tb2 = timing_on() ? now_ms() : 0.0;
     // sources: a new one starts where the sorted source changes; per part the count of
     // starts, then each part writes its sources and its records' destinations / ids
     std::vector<uint32_t> starts(parts + 1, 0);
@@ -958,7 +980,6 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     hp.q_begin.resize(starts[parts] + 1);
     hp.q_dst.resize(m);
     hp.q_id.resize(m);
-    hp.q_pos.assign(n, kNone32);
     pool.run(parts, [&](uint32_t pt) {
         uint32_t si = starts[pt];
         for (uint32_t k = chunk_lo(m, parts, pt), e = chunk_lo(m, parts, pt + 1); k < e; ++k) {
@@ -974,6 +995,9 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
         }
     });
     hp.q_begin[starts[parts]] = m;
+    if (timing_on())
+        std::fprintf(stderr, "MR_TIMING build_plan n=%u parts=%u: specials %.2f ms, lookups %.2f, radix %.2f, grouping %.2f\n", n,
+                     parts, tb0 - tbs, tb1 - tb0, tb2 - tb1, now_ms() - tb2);
     return MR_OK;
 }
 
