@@ -1822,10 +1822,17 @@ struct HubSolver : Core<false> {
                 ux = k < ky ? bx : bx + sx * (k - ky);
             }
         };
-        int ux, uy;
+        // Periodic skip: on a run of steps where q moves away from the path (its distance
+        // grows by one a step, no axis crossed) every quantity below is constant or
+        // periodic in k with period den (run_time(k + den) = run_time(k) + 180 num), so
+        // once den consecutive steps of a run are checked the rest of the run is skipped
+        // and the scan resumes at the first step that leaves it (tests/test_path_tie_skip.py
+        // restates this loop and checks it against the cell-by-cell scan).
+        const int den = int(p.ff_den);
+        int ux, uy, run = 0;
         cell(0, ux, uy);
         uint32_t dq = walk_dist(qx, qy, ux, uy);
-        for (int k = 0; k < K; ++k) {
+        for (int k = 0; k < K;) {
             if (ux == 0 && uy == 0) return true;
             int wx, wy;
             cell(k + 1, wx, wy);
@@ -1854,6 +1861,25 @@ struct HubSolver : Core<false> {
                     if (q_beats_u && b_beats_w) return true;
                 }
             }
+            const bool along_x = x_first ? k < kx : k >= ky;
+            const bool plain = k >= 1 && (along_x ? (ux != 0 && wx != 0 && sx * (ux - qx) >= 0)
+                                                  : (uy != 0 && wy != 0 && sy * (uy - qy) >= 0));
+            run = plain ? run + 1 : 0;
+            if (run >= den) {
+                // the next step that is not plain: the segment's end, or the step before
+                // the one whose cell lies on the axis being crossed
+                int j = along_x ? (x_first ? kx : K) : (x_first ? K : ky);
+                const int c0 = along_x ? ux : uy, sd = along_x ? sx : sy;
+                if (c0 * sd < 0) j = min(j, k + abs(c0) - 1);
+                if (j > k + 1) {
+                    k = j;
+                    run = 0;
+                    cell(k, ux, uy);
+                    dq = walk_dist(qx, qy, ux, uy);
+                    continue;
+                }
+            }
+            ++k;
             ux = wx;
             uy = wy;
             dq = dqn;

@@ -86,7 +86,7 @@ static int fail(int code, const std::string &msg) {
 class HostPool {
   public:
     static HostPool &get() {
-        static HostPool *p = new HostPool();  // never destroyed: workers block on it at exit
+        static HostPool *p = new HostPool();  // never destroyed: workers wait on it at exit
         return *p;
     }
     uint32_t size() const { return nthreads_; }
@@ -97,19 +97,17 @@ class HostPool {
             return;
         }
         std::lock_guard<std::mutex> job(job_mu_);
-        {
+        fn_ = &fn;
+        n_ = n;
+        done_.store(0, std::memory_order_relaxed);
+        const uint64_t g = (ticket_.load(std::memory_order_relaxed) >> 32) + 1;
+        ticket_.store(g << 32, std::memory_order_release);  // publishes fn_ and n_ with the new job
+        if (sleepers_.load(std::memory_order_acquire) > 0) {
             std::lock_guard<std::mutex> lk(mu_);
-            fn_ = &fn;
-            n_ = n;
-            next_.store(0);
-            pending_ = nthreads_ - 1;
-            ++gen_;
+            cv_.notify_all();
         }
-        cv_.notify_all();
-        work();
-        std::unique_lock<std::mutex> lk(mu_);
-        done_cv_.wait(lk, [&] { return pending_ == 0; });
-        fn_ = nullptr;
+        work(g);
+        while (done_.load(std::memory_order_acquire) < n) __builtin_ia32_pause();
     }
 
   private:
@@ -118,29 +116,45 @@ class HostPool {
         if (const char *e = std::getenv("MR_HOST_THREADS")) nthreads_ = uint32_t(std::max(1, std::min(64, std::atoi(e))));
         for (uint32_t t = 1; t < nthreads_; ++t) std::thread([this] { loop(); }).detach();
     }
-    void work() {
-        for (uint32_t i = next_++; i < n_; i = next_++) (*fn_)(i);
+    // Items are claimed by compare-and-swap on {job, next item}: a worker still in an
+    // old job can never take (and lose) an item of the next one.
+    void work(uint64_t g) {
+        for (;;) {
+            uint64_t v = ticket_.load(std::memory_order_acquire);
+            if ((v >> 32) != g || uint32_t(v) >= n_) return;
+            if (!ticket_.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel)) continue;
+            (*fn_)(uint32_t(v));
+            done_.fetch_add(1, std::memory_order_release);
+        }
     }
     void loop() {
         uint64_t seen = 0;
         for (;;) {
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return gen_ != seen; });
-                seen = gen_;
+            uint64_t g = ticket_.load(std::memory_order_acquire) >> 32;
+            // spin a little for the next job (a batch's phases come back to back), then sleep
+            for (int k = 0; g == seen && k < 20000; ++k) {
+                __builtin_ia32_pause();
+                g = ticket_.load(std::memory_order_acquire) >> 32;
             }
-            work();
-            std::lock_guard<std::mutex> lk(mu_);
-            if (--pending_ == 0) done_cv_.notify_one();
+            if (g == seen) {
+                std::unique_lock<std::mutex> lk(mu_);
+                sleepers_.fetch_add(1, std::memory_order_acq_rel);
+                cv_.wait(lk, [&] { return (ticket_.load(std::memory_order_acquire) >> 32) != seen; });
+                sleepers_.fetch_sub(1, std::memory_order_acq_rel);
+                g = ticket_.load(std::memory_order_acquire) >> 32;
+            }
+            seen = g;
+            work(g);
         }
     }
     uint32_t nthreads_ = 1;
     std::mutex job_mu_, mu_;
-    std::condition_variable cv_, done_cv_;
+    std::condition_variable cv_;
     const std::function<void(uint32_t)> *fn_ = nullptr;
-    uint32_t n_ = 0, pending_ = 0;
-    uint64_t gen_ = 0;
-    std::atomic<uint32_t> next_{0};
+    uint32_t n_ = 0;
+    std::atomic<uint64_t> ticket_{0};  // job << 32 | next item
+    std::atomic<uint32_t> done_{0};
+    std::atomic<int> sleepers_{0};
 };
 // [0, n) in `parts` near-equal ranges: range p is [chunk_lo(n, parts, p), chunk_lo(n, parts, p + 1))
 static inline uint32_t chunk_lo(uint32_t n, uint32_t parts, uint32_t p) { return uint32_t(uint64_t(n) * p / parts); }
@@ -871,8 +885,8 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     hp.nq = n;
     const double tb0 = timing_on() ? now_ms() : 0.0;
     HostPool &pool = HostPool::get();
-    // about 64k queries a part (a part's work must outweigh waking a thread)
-    const uint32_t parts = std::max(1u, std::min(pool.size(), n / 65536u));
+    // at least 32k queries a part (a part's work must outweigh waking a thread)
+    const uint32_t parts = std::max(1u, std::min(pool.size(), n / 32768u));
     constexpr uint32_t kBits = 13, kB = 1u << kBits;
     // An invalid query gets the source key 2^32 - 1: its low bits are all ones, so with
     // enough passes to cover every vertex id (two while V < 2^26) it sorts after every

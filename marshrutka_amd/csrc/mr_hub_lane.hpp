@@ -53,13 +53,17 @@ namespace mr {
 #define MR_LANE_WAVES 2
 #endif
 __host__ __device__ constexpr uint32_t lane_waves(uint32_t TM) { return TM <= 22 ? MR_LANE_WAVES : 1u; }
-// a scheduling fence between the unrolled entries, so the scheduler does not
-// interleave all of them and run out of registers
-#ifndef MR_LANE_NOFENCE
-#define MR_LANE_FENCE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define MR_LANE_FENCE() do {} while (0)
+// a scheduling fence after every MR_LANE_FENCE_EVERY unrolled entries (0: none), so the
+// scheduler does not interleave all of them and run out of registers
+#ifndef MR_LANE_FENCE_EVERY
+#define MR_LANE_FENCE_EVERY 1
 #endif
+#define MR_LANE_FENCE_AT(t)                                                              \
+    do {                                                                                 \
+        if (MR_LANE_FENCE_EVERY > 0 && ((t) % (MR_LANE_FENCE_EVERY > 0 ? MR_LANE_FENCE_EVERY : 1)) == 0) \
+            __builtin_amdgcn_sched_barrier(0);                                           \
+    } while (0)
+#define MR_LANE_FENCE() MR_LANE_FENCE_AT(t)
 
 // pair-table reads issued this many entries ahead of their use in the relax loop
 #ifndef MR_LANE_PF
