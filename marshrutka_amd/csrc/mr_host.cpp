@@ -2128,8 +2128,12 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
             e = launch_cert_select(pl->d_args, s);
             if (e == hipSuccess) e = launch_fill(pl->d_args_cert, pl->ka.p.perm, pl->cert_fill_gx, 1, s);
             if (e == hipSuccess) e = launch_cert_check(pl->d_args, pl->cert_check_gx, pl->cert_cap, s);
-            if (e == hipSuccess) e = launch_cert_sweep(pl->d_args, pl->cert_cap, s);
-            if (e == hipSuccess) e = launch_cert_check(pl->d_args, pl->cert_check_gx, pl->cert_cap, s);
+            // (MR_CERT_NOSWEEP=1: diagnostics, the first check's state stays for MR_CERT_DEBUG)
+            static const bool nosweep = std::getenv("MR_CERT_NOSWEEP") != nullptr;
+            if (!nosweep) {
+                if (e == hipSuccess) e = launch_cert_sweep(pl->d_args, pl->cert_cap, s);
+                if (e == hipSuccess) e = launch_cert_check(pl->d_args, pl->cert_check_gx, pl->cert_cap, s);
+            }
         }
         if (e == hipSuccess && !pl->fb_none)
             e = launch_solve(pl->d_args_fb, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->fb_blocks, s);
@@ -2271,6 +2275,29 @@ extern "C" int mr_plan_get_stats(mr_plan *pl, mr_plan_stats *out) {
     std::memset(out, 0, sizeof(*out));
     uint32_t ctr[kCtrWords];
     if (int st = read_counters(pl, ctr)) return st;
+    if (std::getenv("MR_CERT_DEBUG") && pl->cert_cap) {  // diagnostics: each slot's last check
+        const size_t parts = pl->cert_check_gx, n = size_t(pl->cert_cap) * parts * kCertSt;
+        std::vector<uint32_t> cs(n), src(pl->cert_cap);
+        if (hipMemcpy(cs.data(), pl->d_cert_st, n * 4, hipMemcpyDeviceToHost) == hipSuccess &&
+            hipMemcpy(src.data(), pl->d_cert_src, src.size() * 4, hipMemcpyDeviceToHost) == hipSuccess)
+            for (uint32_t k = 0; k < pl->cert_cap; ++k) {
+                uint32_t key = kNone32, fails = 0, x0 = kNone32, x1 = 0, y0 = kNone32, y1 = 0;
+                for (size_t j = 0; j < parts; ++j) {
+                    const uint32_t *q = &cs[(k * parts + j) * kCertSt];
+                    if (!q[kCertFails]) continue;
+                    key = std::min(key, q[kCertKey]);
+                    fails += q[kCertFails];
+                    x0 = std::min(x0, q[kCertX0]);
+                    x1 = std::max(x1, q[kCertX1]);
+                    y0 = std::min(y0, q[kCertY0]);
+                    y1 = std::max(y1, q[kCertY1]);
+                }
+                const uint32_t v = src[k] < pl->grid->V ? src[k] : 0;
+                std::fprintf(stderr, "MR_CERT_DEBUG slot %u src (%d,%d): fails %u key %u box x %d..%d y %d..%d\n", k,
+                             pl->grid->gx(v), pl->grid->gy(v), fails, key, int(x0) - int(pl->grid->H),
+                             int(x1) - int(pl->grid->H), int(y0) - int(pl->grid->H), int(y1) - int(pl->grid->H));
+            }
+    }
     out->solver = pl->hp.hub ? (pl->hp.wide ? MR_SOLVER_HUB_WIDE : MR_SOLVER_HUB)
                              : (pl->algo == kAlgoLegs ? MR_SOLVER_LEVELS : MR_SOLVER_BUCKETED);
     out->grid_state_in_lds = pl->grid_in_lds ? 1u : 0u;

@@ -56,7 +56,7 @@ __host__ __device__ constexpr uint32_t lane_waves(uint32_t TM) { return TM <= 22
 // a scheduling fence after every MR_LANE_FENCE_EVERY unrolled entries (0: none), so the
 // scheduler does not interleave all of them and run out of registers
 #ifndef MR_LANE_FENCE_EVERY
-#define MR_LANE_FENCE_EVERY 1
+#define MR_LANE_FENCE_EVERY 0  // none: c4 0.975 ms against 1.033 with a fence after every entry (r04 A/B)
 #endif
 #define MR_LANE_FENCE_AT(t)                                                              \
     do {                                                                                 \
