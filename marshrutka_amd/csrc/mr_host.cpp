@@ -131,8 +131,9 @@ class HostPool {
         uint64_t seen = 0;
         for (;;) {
             uint64_t g = ticket_.load(std::memory_order_acquire) >> 32;
-            // spin a little for the next job (a batch's phases come back to back), then sleep
-            for (int k = 0; g == seen && k < 20000; ++k) {
+            // spin briefly for the next job (a batch's phases come back to back), then sleep: a
+            // longer spin burns the CPU quota a GPU box gives the process (cgroup cpu.max)
+            for (int k = 0; g == seen && k < 2000; ++k) {
                 __builtin_ia32_pause();
                 g = ticket_.load(std::memory_order_acquire) >> 32;
             }
