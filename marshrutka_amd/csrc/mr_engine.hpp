@@ -205,6 +205,9 @@ struct KArgs {
     uint32_t *cert_stage_lex;    // cert_stage_cap * (NS+1)
     uint32_t *cert_stage_src;    // cert_stage_cap
     uint32_t cert_stage_cap;
+    // 1: every cell's rank is std_rank of its position (mr_hub_lane.hpp; checked at grid
+    // creation), so the lane kernel reads no per-cell record
+    uint32_t rank_std;
 };
 // fb_cert[i] of a staged entry before cert_select_kernel gives it a slot (or none)
 constexpr uint32_t kFbStaged = 0xFFFFFFFEu;
@@ -243,6 +246,21 @@ enum : uint32_t { kAlgoGeneric = 0, kAlgoLegs = 1 };
 // per query)
 constexpr uint32_t kLaneMaxQ = 32;
 constexpr uint32_t kLaneRegs = 6;  // hub_lane_kernel: region campfires sit in entries 6 .. 6 + kLaneRegs - 1
+
+// CellIndex rank of the cell at (x, y) in the standard layout (Blue x<0 y<0, Red x<0 y>0,
+// Green x>0 y>0, Yellow x>0 y<0; borders BR y=0 x<0, RG x=0 y>0, GY y=0 x>0, YB x=0 y<0):
+// the derived Ord Center < Homeland{h, (|x|, |y|)} < Border{b, shift} (src/index.rs:41-46)
+// over a complete grid of homeland size H.  mr_grid_create checks it for every cell.
+__host__ __device__ inline uint32_t std_rank(int x, int y, uint32_t H) {
+    const uint32_t ax = uint32_t(x < 0 ? -x : x), ay = uint32_t(y < 0 ? -y : y);
+    if (x == 0 && y == 0) return 0u;
+    if (y == 0 || x == 0) {
+        const uint32_t b = y == 0 ? (x < 0 ? 0u : 2u) : (y > 0 ? 1u : 3u);
+        return 1u + 4u * H * H + b * H + (ax + ay - 1u);
+    }
+    const uint32_t h = x < 0 ? (y < 0 ? 0u : 1u) : (y > 0 ? 2u : 3u);
+    return 1u + h * H * H + (ax - 1u) * H + (ay - 1u);
+}
 
 constexpr uint32_t kErrKOverflow = 1u, kErrMetricOverflow = 2u, kErrBucket = 4u, kErrChain = 8u;
 // KArgs::dbg_flags bit (tests only): the fill launch raises kErrChain

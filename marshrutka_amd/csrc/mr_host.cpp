@@ -284,6 +284,7 @@ struct mr_grid {
     // formula was verified for every cell at creation (`exact`), the confirmation is
     // skipped: a query batch's lookups then touch no per-cell table.
     bool fast = false, exact = false;
+    bool rank_std = false;  // rank[v] = std_rank(position of v) for every cell (mr_hub_lane.hpp)
     int64_t ux[4] = {0, 0, 0, 0}, uy[4] = {0, 0, 0, 0}, ub[4] = {0, 0, 0, 0};
     bool find(const mr_cell_index &c, uint32_t &v) const {
         if (!canonical(c)) return false;
@@ -411,6 +412,9 @@ extern "C" int mr_grid_create(const mr_cell *cells, uint32_t n, mr_grid **out) {
         }
         for (uint32_t r = 0; r < n; ++r)
             if (g->poi[keys[r].second] == MR_POI_CAMPFIRE) g->campfires.push_back(keys[r].second);
+        bool std_ok = true;
+        for (uint32_t v = 0; v < n && std_ok; ++v) std_ok = g->rank[v] == std_rank(g->gx(v), g->gy(v), g->H);
+        g->rank_std = std_ok && !std::getenv("MR_RANK_TABLE");  // (tests: force the table)
     }
     // nearest campfire per homeland (src/grid.rs:134-230, 297-325): the argmin
     // of (manhattan distance, |x|!=|y|, |x|+|y|, |x|, |y|) over the homeland's
@@ -1778,6 +1782,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     ka.fb_mode = 0;
     ka.fb_all = std::getenv("MR_HUB_FALLBACK_ALL") ? 1u : 0u;  // tests cover the fallback path
     ka.n_lane = pl->n_lane;
+    ka.rank_std = g->rank_std ? 1u : 0u;
     ka.src_off = pl->n_lane;
     if (const char *e = std::getenv("MR_DBG_FLAGS")) ka.dbg_flags = uint32_t(std::atoi(e));
     pl->all_mode = all_mode;

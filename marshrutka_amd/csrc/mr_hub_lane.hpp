@@ -81,10 +81,14 @@ __device__ __host__ __forceinline__ constexpr uint32_t lm_pack(uint32_t len, uin
     return len | (kind << 8) | (par << 11) | ((nt - 1u) << 16) | (cj << 17);
 }
 constexpr uint32_t kInf1 = ~0u;  // c1 of a label that is not there
+// the specials' cells by hash (kLaneHash slots of {vertex, entry}, linear probing)
+constexpr uint32_t kLaneHash = 64;
+__device__ __forceinline__ uint32_t lane_hash(uint32_t v) { return (v * 0x9E3779B1u) >> 26; }
 
 struct LLab {
     uint32_t c1, c2, c3, m;
 };
+
 
 // ---- masks: 0 / ~0 per lane, kept in VGPRs ---------------------------------------------
 // An empty asm makes the value opaque: without it the compiler turns every such mask
@@ -301,6 +305,8 @@ struct LaneHub {
     // lane l at t * 64 + l), written by dump_meta() right before them, so they walk
     // command chains with LDS reads instead of selects over the register-held table.
     uint32_t *M;
+    const uint2 *HT;     // LDS: the specials' cells by hash (lane_hash)
+    uint32_t ht_probes;  // the longest probe sequence in HT
     __device__ __forceinline__ void dump_meta() const {
         const uint32_t l = lane_id();
         M[l] = start().m;
@@ -487,17 +493,36 @@ struct LaneHub {
         o = OutResult{legs, money, time, (status << 16) | (len & 0xFFFFu)};
     }
 
+    // A cell's special entry (kNone10: plain) and CellIndex rank.  On a grid in the
+    // standard layout (mr_grid rank_std: every cell's rank is the closed form of its
+    // position) the rank is arithmetic and the entry a scan of the specials' cells in
+    // LDS, so a source or destination costs no random HBM line; else the grid's
+    // {sinfo, rank} record.
+    __device__ __forceinline__ void cell_word(uint32_t v, int x, int y, uint32_t &t, uint32_t &r) const {
+        if (a->rank_std) {
+            r = std_rank(x, y, P.H);
+            t = kNone10;
+            const uint32_t h = lane_hash(v);
+            for (uint32_t k = 0; k < ht_probes; ++k) {  // (uniform bound)
+                const uint2 e = HT[(h + k) & (kLaneHash - 1u)];
+                t = e.x == v ? e.y : t;
+            }
+        } else {
+            const uint2 c = cell[v];  // {sinfo, rank}
+            t = c.x & kNone10;
+            r = c.y;
+        }
+    }
+
     // ---- one source per lane ----------------------------------------------------------
     // returns the records this lane wrote (0 when the source went to the SSSP kernel)
     __device__ __forceinline__ uint32_t solve(bool have, uint32_t s_idx) {
         const DevParams &p = P;
         const uint32_t NS = p.NS;
         src = a->src_v[s_idx];
-        const uint2 sc = cell[src];  // {sinfo, rank}
-        src_rk = sc.y;
         sx = int(src % p.S) - int(p.H);
         sy = int(src / p.S) - int(p.H);
-        ts = sc.x & kNone10;
+        cell_word(src, sx, sy, ts, src_rk);
         srow = reinterpret_cast<const uint2 *>(a->near) + (unsigned long long)src * nreg;
         // the source's own edges, in command-kind order: its start label if it is a
         // special, the walks from it, the SoE edges from its region rows, SHQ, SFm
@@ -687,9 +712,9 @@ struct LaneHub {
         const bool walk0 = src != p.vc;
         for (uint32_t qi = fb_sp ? qb : qa; qi < qb; ++qi) {
             const uint32_t w = a->q_dst[qi];
-            const uint2 wc = cell[w];
-            const uint32_t tw = wc.x & kNone10;
-            const uint32_t wr = wc.y;
+            const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
+            uint32_t tw, wr;
+            cell_word(w, wx, wy, tw, wr);
             if (w == src) {
                 emit(st0, kOwn, Own{sx, sy, src_rk, kNone10, 0u}, qi);
                 continue;
@@ -698,7 +723,6 @@ struct LaneHub {
                 emit(get(tw), tw, own_of(tw), qi);
                 continue;
             }
-            const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
             const Own wo{wx, wy, wr, kNone10, 0u};
             // Every candidate is a boundary's label plus one walk command, so they are
             // compared on the boundary's own meta word (length - 1; the source's walk:
@@ -778,8 +802,11 @@ __host__ __device__ inline uint32_t lane_off_rm(uint32_t NS, uint32_t nreg, uint
 __host__ __device__ inline uint32_t lane_off_meta(uint32_t NS, uint32_t nreg, uint32_t TM) {
     return align16h(lane_off_rm(NS, nreg, TM) + TM * 4u);
 }
-__host__ __device__ inline uint32_t lane_lds_total(uint32_t NS, uint32_t nreg, uint32_t TM) {
+__host__ __device__ inline uint32_t lane_off_hash(uint32_t NS, uint32_t nreg, uint32_t TM) {
     return lane_off_meta(NS, nreg, TM) + (kBS / 64) * TM * 64u * 4u;
+}
+__host__ __device__ inline uint32_t lane_lds_total(uint32_t NS, uint32_t nreg, uint32_t TM) {
+    return lane_off_hash(NS, nreg, TM) + kLaneHash * 8u + 16u;
 }
 
 template <uint32_t PERM, uint32_t TM>
@@ -821,6 +848,23 @@ __global__ __launch_bounds__(kBS, lane_waves(TM)) void hub_lane_kernel(const KAr
         pa[i] = A;
         pb[i] = B;
     }
+    // the specials' cells by hash: thread 0 inserts them (linear probing) and records the
+    // longest probe sequence, which bounds every lookup
+    if (threadIdx.x == 0) {
+        uint2 *ht = reinterpret_cast<uint2 *>(smem + lane_off_hash(NS, nreg, TM));
+        for (uint32_t h = 0; h < kLaneHash; ++h) ht[h] = make_uint2(kNone32, kNone10);
+        uint32_t probes = 1;
+        for (uint32_t t = 1; t <= NS && t < TM; ++t) {
+            uint32_t h = lane_hash(spl[t].v), k = 1;
+            while (ht[h].x != kNone32) {
+                h = (h + 1u) & (kLaneHash - 1u);
+                ++k;
+            }
+            ht[h] = make_uint2(spl[t].v, t);
+            probes = max(probes, k);
+        }
+        *reinterpret_cast<uint32_t *>(smem + lane_off_hash(NS, nreg, TM) + kLaneHash * 8u) = probes;
+    }
     __syncthreads();
     LaneHub<PERM, TM> H;
     H.a = a;
@@ -831,6 +875,9 @@ __global__ __launch_bounds__(kBS, lane_waves(TM)) void hub_lane_kernel(const KAr
     H.PB = pb;
     H.RM = rm;
     H.M = reinterpret_cast<uint32_t *>(smem + lane_off_meta(NS, nreg, TM)) + (threadIdx.x >> 6) * (TM * 64u);
+    H.HT = reinterpret_cast<const uint2 *>(smem + lane_off_hash(NS, nreg, TM));
+    H.ht_probes = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t *>(smem + lane_off_hash(NS, nreg, TM) +
+                                                                                    kLaneHash * 8u));
     H.rank = a->rank;
     H.sinfo = a->sinfo;
     H.rank_inv = a->rank_inv;

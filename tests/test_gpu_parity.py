@@ -23,7 +23,7 @@ def eng():
     return pathfinder
 
 
-@pytest.fixture(params=["auto-lds", "auto-hbm", "lane-lds", "hub1-lds", "hub2-lds", "wide-lds", "widescan-lds", "fallback-lds", "fallback-hbm", "fbsssp-lds",
+@pytest.fixture(params=["auto-lds", "auto-hbm", "lane-lds", "lanetab-lds", "hub1-lds", "hub2-lds", "wide-lds", "widescan-lds", "fallback-lds", "fallback-hbm", "fbsssp-lds",
                         "sssp-lds", "sssp-hbm", "generic-lds", "generic-hbm"])
 def grid_state(request, monkeypatch):
     """Every solver path x both grid-state regimes:
@@ -31,7 +31,9 @@ def grid_state(request, monkeypatch):
                table fits 22 entries, a source has <= 32 queries and the plan has
                enough such sources to fill the GPU, else two sources per wave when
                the specials fit 32 lanes), else the SSSP solvers
-    lane     — auto with the lane kernel whenever it applies (MR_HUB_LANE=1)
+    lane     — auto with the lane kernel whenever it applies (MR_HUB_LANE=1); on the
+               standard layout it computes ranks and looks up specials itself
+    lanetab  — the same reading every cell's {sinfo, rank} record (MR_RANK_TABLE=1)
     hub1     — hub solver with one source per wave (no lane kernel)
     hub2     — hub solver with two sources per wave (no lane kernel)
     wide     — the wide hub solver (several specials per lane) even where the
@@ -53,6 +55,10 @@ def grid_state(request, monkeypatch):
     monkeypatch.delenv("MR_HUB_LANE", raising=False)
     monkeypatch.delenv("MR_CERT", raising=False)
     monkeypatch.delenv("MR_CERT_SLOTS", raising=False)
+    monkeypatch.delenv("MR_RANK_TABLE", raising=False)
+    if algo == "lanetab":
+        monkeypatch.setenv("MR_RANK_TABLE", "1")
+        algo = "lane"
     if algo in ("hub1", "hub2"):
         monkeypatch.setenv("MR_HUB_LANE", "0")
     if algo == "lane":
