@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MR_ABI_VERSION 6u
+#define MR_ABI_VERSION 7u
 
 /* ---- status codes ------------------------------------------------------ */
 typedef enum mr_status {
@@ -271,6 +271,9 @@ typedef struct mr_plan_stats {
                                    (more than 32 queries each) a lane per query (ABI 5) */
     uint32_t certified_sources; /* of fallback_sources, those answered by the fixed-point certificate
                                    in the last pass (the rest ran the SSSP kernel; ABI 6) */
+    uint32_t lanes_per_source;  /* hub solver: lanes that share one source's Dijkstra over the
+                                   specials: 1 hub_lane_kernel, 8 or 16 hub_group_kernel, 0 hub_kernel
+                                   and the others (ABI 7) */
 } mr_plan_stats;
 enum {
     MR_FILL_NONE = 0,    /* not an all-destinations hub plan */

@@ -1,4 +1,4 @@
-//! Raw bindings of `include/marshrutka_pf.h` (MR_ABI_VERSION 6) for the reference
+//! Raw bindings of `include/marshrutka_pf.h` (MR_ABI_VERSION 7) for the reference
 //! crate (maratik123/marshrutka).  Every `#[repr(C)]` struct here has the header's
 //! field order, sizes and offsets; `tests/test_rust_shim.py` checks that against the
 //! header compiled by a C compiler (this image has no Rust toolchain, so this file is
@@ -11,7 +11,7 @@
 
 use std::os::raw::{c_char, c_int, c_void};
 
-pub const MR_ABI_VERSION: u32 = 6;
+pub const MR_ABI_VERSION: u32 = 7;
 
 // mr_status
 pub const MR_OK: c_int = 0;
@@ -133,6 +133,7 @@ pub struct mr_plan_stats {
     pub fill_launch: u32,
     pub lane_sources: u32,
     pub certified_sources: u32,
+    pub lanes_per_source: u32,
 }
 
 #[repr(C)]

@@ -80,7 +80,7 @@ class mr_plan_stats(C.Structure):
                 ("hub_workgroups", C.c_uint32), ("sssp_workgroups", C.c_uint32),
                 ("specials_per_lane", C.c_uint32), ("region_boundary_cells", C.c_uint32),
                 ("fill_launch", C.c_uint32), ("lane_sources", C.c_uint32),
-                ("certified_sources", C.c_uint32)]
+                ("certified_sources", C.c_uint32), ("lanes_per_source", C.c_uint32)]
 
 
 assert C.sizeof(mr_cell_index) == 8

@@ -265,5 +265,8 @@ __host__ __device__ inline uint32_t std_rank(int x, int y, uint32_t H) {
 constexpr uint32_t kErrKOverflow = 1u, kErrMetricOverflow = 2u, kErrBucket = 4u, kErrChain = 8u;
 // KArgs::dbg_flags bit (tests only): the fill launch raises kErrChain
 constexpr uint32_t kDbgInjectFlag = 16u;
+// KArgs::dbg_flags bits (timing experiments only, results are not valid): hub_group_kernel
+// skips its Dijkstra / its destinations
+constexpr uint32_t kDbgGroupNoSolve = 32u, kDbgGroupNoReadoff = 64u;
 
 }  // namespace mr

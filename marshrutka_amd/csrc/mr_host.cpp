@@ -48,6 +48,10 @@ int hub_wide_blocks_per_cu(const uint32_t perm[3], uint32_t NS, uint32_t bytes);
 uint32_t hub_lane_entries(uint32_t NS);
 hipError_t launch_hub_lane(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t n_lane,
                            hipStream_t stream);
+uint32_t hub_group_slots(uint32_t NS, uint32_t G);
+uint32_t hub_group_lds_bytes(uint32_t NS, uint32_t nreg, uint32_t G);
+hipError_t launch_hub_group(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t n,
+                            uint32_t G, hipStream_t stream);
 hipError_t launch_cert_select(const KArgs *d_args, hipStream_t stream);
 hipError_t launch_cert_check(const KArgs *d_args, uint32_t gx, uint32_t slots, hipStream_t stream);
 hipError_t launch_cert_sweep(const KArgs *d_args, uint32_t slots, hipStream_t stream);
@@ -1370,6 +1374,7 @@ struct mr_plan {
     KArgs *d_args_lane = nullptr;         // hub_lane_kernel launch (sources [0, n_lane))
     KArgs *d_args_lane_last = nullptr;    // the same, ending the pass
     uint32_t n_lane = 0;                  // sources on the lane kernel; the rest on hub_kernel
+    uint32_t lane_g = 0;                  // > 0: the n_lane sources run G lanes each (hub_group_kernel)
     KArgs *d_args_fill = nullptr;         // all-destinations mode: the fill launch (ends the pass)
     bool all_mode = false;
     CellWord *d_rec = nullptr;            // all-destinations outputs (KArgs::out_rec ...)
@@ -1654,9 +1659,26 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     // per source) is faster.  MR_HUB_LANE=0: never, =1: whenever applicable.
     const char *hl = std::getenv("MR_HUB_LANE");
     const bool lane_off = hl && !std::strcmp(hl, "0"), lane_force = hl && !std::strcmp(hl, "1");
-    if (hp.hub && !hp.wide && !hp.nonlin && !all_mode && !lane_off && hub_lane_entries(hp.p.NS) != 0 &&
-        lane_bounds_ok(hp.p) && lane_layout_ok(hp) && (lane_force || lane_sources(hp) >= lane_min_sources()))
+    // Plans the lane kernel does not take (too few sources to fill the GPU, or a table
+    // layout it does not hold) run one source per group of G lanes when the table fits 32
+    // entries: a source's Dijkstra is then ~G times shorter in wave instructions, which
+    // is what a small plan's pass time is (hub_group_kernel).  MR_HUB_GROUP=0: never,
+    // =8 / =16: the group size (default 8); MR_HUB_GROUP_FORCE=1: even where the lane
+    // kernel applies.  The certificate's table export is hub_kernel's, so
+    // MR_HUB_FALLBACK_ALL keeps hub_kernel.
+    const char *hg = std::getenv("MR_HUB_GROUP");
+    const uint32_t hgv = hg ? uint32_t(std::strtoul(hg, nullptr, 10)) : 8u;
+    const bool group_off = hg && hgv == 0, group_force = std::getenv("MR_HUB_GROUP_FORCE") != nullptr;
+    const uint32_t group_g = hgv == 16 ? 16u : 8u;
+    const bool lane_ok = hp.hub && !hp.wide && !hp.nonlin && !all_mode && lane_bounds_ok(hp.p);
+    if (lane_ok && !group_force && !lane_off && hub_lane_entries(hp.p.NS) != 0 && lane_layout_ok(hp) &&
+        (lane_force || lane_sources(hp) >= lane_min_sources()))
         pl->n_lane = partition_sources(hp);
+    else if (lane_ok && !group_off && !lane_force && hub_group_slots(hp.p.NS, group_g) != 0 &&
+             !std::getenv("MR_HUB_FALLBACK_ALL")) {
+        pl->n_lane = uint32_t(hp.src_v.size());
+        pl->lane_g = group_g;
+    }
     auto bail = [&](int code) {
         delete pl;
         return code;
@@ -2122,9 +2144,11 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         // pass on their own.
         const bool big = pl->ka.nsrc > pl->n_lane;
         e = hipSuccess;
-        if (pl->n_lane)
-            e = launch_hub_lane(pl->fb_none && !big ? pl->d_args_lane_last : pl->d_args_lane, pl->ka.p.perm,
-                                pl->ka.p.NS, pl->ka.nreg, pl->n_lane, s);
+        if (pl->n_lane) {
+            const KArgs *la = pl->fb_none && !big ? pl->d_args_lane_last : pl->d_args_lane;
+            e = pl->lane_g ? launch_hub_group(la, pl->ka.p.perm, pl->ka.p.NS, pl->ka.nreg, pl->n_lane, pl->lane_g, s)
+                           : launch_hub_lane(la, pl->ka.p.perm, pl->ka.p.NS, pl->ka.nreg, pl->n_lane, s);
+        }
         if (e == hipSuccess && big) e = launch_hub_plan(pl, pl->fb_none ? pl->d_args_hub_last : pl->d_args, s);
         // certified fallback: the slots given to the staged sources in source order,
         // their closed forms, the check, one repair sweep, the check again (each exits at
@@ -2315,7 +2339,8 @@ extern "C" int mr_plan_get_stats(mr_plan *pl, mr_plan_stats *out) {
     out->sssp_workgroups = pl->blocks;
     out->specials_per_lane = !pl->hp.hub ? 0u : (pl->hp.wide ? hub_wide_spl(pl->ka.p.NS) : 1u);
     out->region_boundary_cells = pl->hp.wide && pl->hp.rb_off && !pl->hp.rb_off->empty() ? pl->hp.rb_off->back() : 0u;
-    out->lane_sources = pl->n_lane;
+    out->lane_sources = pl->lane_g ? 0u : pl->n_lane;
+    out->lanes_per_source = !pl->n_lane ? 0u : (pl->lane_g ? pl->lane_g : 1u);
     out->certified_sources = ctr[kCtrLastCert];
     out->fill_launch = !(pl->hp.hub && pl->all_mode) ? MR_FILL_NONE
                        : pl->fused                   ? MR_FILL_FUSED
@@ -2486,6 +2511,10 @@ static int check_device_errors(mr_plan *pl, uint32_t &flags) {
             for (uint32_t s : fb) std::fprintf(stderr, " %u%s", pl->hp.src_v[s & ~kFbCertified], (s & kFbCertified) ? "c" : "");
             std::fprintf(stderr, "\n");
         }
+    }
+    if (flags && std::getenv("MR_DEBUG_FLAGS_OK")) {  // diagnostics: report, then read the records anyway
+        std::fprintf(stderr, "MR_DEBUG_FLAGS_OK: device flags %u ignored\n", flags);
+        flags = 0;
     }
     if (flags & (kErrKOverflow | kErrMetricOverflow))
         return fail(MR_ERR_LIMIT, "a label exceeds the engine's 32-bit metric or run-length limits");

@@ -1,0 +1,414 @@
+// mr_hub_group.hpp — the hub solver with one SOURCE per group of G lanes (hub_group_kernel).
+//
+// Same algorithm and results as hub_kernel / hub_lane_kernel (DESIGN.md §3a, §3a‴): an
+// exact Dijkstra over the specials whose edges are closed-form walks from settled
+// boundaries plus the CentralMove / caravan / Scroll-of-Escape edges, and destinations
+// read off as the best walk from a boundary (FindPath::eval, src/pathfinder.rs:199-248).
+//
+// hub_lane_kernel runs a whole source per lane: 64 sources a wave, so a plan needs tens
+// of thousands of sources before its waves fill the GPU, and one wave's serial Dijkstra
+// (~50k instructions) is the latency of the whole pass.  hub_kernel (a lane per special)
+// pays a cross-lane reduction with exec-mask bookkeeping on every settle.  Here G lanes
+// (8 or 16, one DPP row or half row) share a source: lane j of the group holds entries
+// j, j + G, j + 2G, ... (E slots), so
+//   * a settle is a per-lane scan of E slots, then log2(G) DPP rounds in which every lane
+//     takes the lesser of its own and its partner's (c1, c2, c3, length, entry): five DPP
+//     moves, a four-step borrow chain and five selects a round, and every lane of the
+//     group ends with the winner;
+//   * a relaxation is E compare-and-selects per lane, with the entries' roles (Center,
+//     border, hub, region) as run-time bits of the settle's masks, so any table layout
+//     up to 32 entries runs here;
+//   * destinations are read off one query per lane from the settled labels in LDS.
+// A source's Dijkstra is ~G times shorter in wave instructions than on the lane kernel,
+// which is what small plans (configs[0] / configs[1], one query) are bound by.
+//
+// Exact ties (metrics and length) go to the command-list compares exactly as in the lane
+// kernel (LaneHub::cmp_list), with the tied entries' meta words published to every lane
+// of the group through the per-wave LDS meta copy.
+#pragma once
+#include "mr_hub_lane.hpp"
+
+namespace mr {
+
+// One DPP round of the group minimum: (c1, c2, c3, k) of this lane against the partner's
+// (k = length << 24 | entry), the lesser kept with the m word riding along.  The
+// partner's words come over by v_mov_b32_dpp; then the borrow chain mine - partner leaves
+// VCC = mine < partner and five VOP2 selects keep mine or take the partner's.  (The DPP
+// forms of the carry ops themselves, v_subrev_co / v_subbrev_co _dpp, assemble but do not
+// compute this on gfx950: tools/micro/group_min.hip.)  s_nop 1: a DPP read of a VGPR
+// written by the previous VALU instruction needs two wait states.
+#define MR_GRP_ROUND(DPP)                                                                         \
+    asm("s_nop 1\n\t"                                                                             \
+        "v_mov_b32_dpp %6, %1 " DPP " row_mask:0xf bank_mask:0xf\n\t"                             \
+        "v_mov_b32_dpp %7, %2 " DPP " row_mask:0xf bank_mask:0xf\n\t"                             \
+        "v_mov_b32_dpp %8, %3 " DPP " row_mask:0xf bank_mask:0xf\n\t"                             \
+        "v_mov_b32_dpp %9, %4 " DPP " row_mask:0xf bank_mask:0xf\n\t"                             \
+        "v_mov_b32_dpp %10, %5 " DPP " row_mask:0xf bank_mask:0xf\n\t"                            \
+        "v_sub_co_u32_e32 %0, vcc, %5, %10\n\t"                                                   \
+        "v_subb_co_u32_e32 %0, vcc, %3, %8, vcc\n\t"                                              \
+        "v_subb_co_u32_e32 %0, vcc, %2, %7, vcc\n\t"                                              \
+        "v_subb_co_u32_e32 %0, vcc, %1, %6, vcc\n\t"                                              \
+        "v_cndmask_b32_e32 %1, %6, %1, vcc\n\t"                                                   \
+        "v_cndmask_b32_e32 %2, %7, %2, vcc\n\t"                                                   \
+        "v_cndmask_b32_e32 %3, %8, %3, vcc\n\t"                                                   \
+        "v_cndmask_b32_e32 %4, %9, %4, vcc\n\t"                                                   \
+        "v_cndmask_b32_e32 %5, %10, %5, vcc"                                                      \
+        : "=&v"(t_), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(m), "+v"(k), "=&v"(p1), "=&v"(p2),          \
+          "=&v"(p3), "=&v"(pm), "=&v"(pk)                                                         \
+        :                                                                                         \
+        : "vcc")
+
+// the least (c1, c2, c3, k) over each group of G lanes, in every lane of the group
+template <uint32_t G>
+__device__ __forceinline__ void group_min(uint32_t &c1, uint32_t &c2, uint32_t &c3, uint32_t &m, uint32_t &k) {
+    static_assert(G == 4 || G == 8 || G == 16, "groups are quads, half rows or rows");
+    uint32_t t_, p1, p2, p3, pm, pk;
+    MR_GRP_ROUND("quad_perm:[1,0,3,2]");
+    MR_GRP_ROUND("quad_perm:[2,3,0,1]");
+    if constexpr (G >= 8) MR_GRP_ROUND("row_half_mirror");
+    if constexpr (G >= 16) MR_GRP_ROUND("row_mirror");
+}
+
+// bit e of w as a 0 / ~0 mask, e a run-time value (one v_bfe_i32)
+__device__ __forceinline__ uint32_t bitv(uint32_t w, uint32_t e) {
+    uint32_t r;
+    asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(r) : "v"(w), "v"(e));
+    return r;
+}
+
+template <uint32_t PERM, uint32_t G, uint32_t E>
+struct GroupHub : LaneHub<PERM, G * E> {
+    static constexpr uint32_t TM = G * E;  // table entries (slot i of lane j: entry i * G + j)
+    using Base = LaneHub<PERM, TM>;
+    using Base::a;
+    using Base::P;
+    using Base::spl;
+    using Base::PA;
+    using Base::PB;
+    using Base::M;
+    using Base::counter;
+    using Base::src;
+    using Base::src_rk;
+    using Base::ts;
+    using Base::sx;
+    using Base::sy;
+    using Base::srow;
+    using Base::nreg;
+    using Base::tent;
+    using Base::done;
+    using Base::wt;
+    using Base::bndm;
+    using Base::blk;
+    using Base::add;
+    using Base::mk;
+    using Base::opt;
+    using Base::inf;
+    using Base::start;
+    using Base::consider;
+    using Base::own_of;
+    using Base::pos;
+    using Base::cmp_list;
+    using Base::cmp4;
+    using Base::emit;
+    using Base::avail;
+    using Base::label_avail;
+    using Base::cell_word;
+    using Base::settle_ctx;
+    using Base::walk_to;
+    using Base::meta_of;
+    using Own = typename Base::Own;
+    using Settle = typename Base::Settle;
+    using FromS = typename Base::FromS;
+
+    LLab Ls[E];      // labels of this lane's slots
+    uint32_t gj = 0, gbase = 0;
+    uint4 *LT = nullptr;  // LDS: this group's settled labels, entry e at LT[e]
+
+    __device__ __forceinline__ uint32_t ent(uint32_t i) const { return i * G + gj; }
+    // some lane of this lane's group has f
+    __device__ __forceinline__ bool group_any(bool f) const {
+        const unsigned long long b = __ballot(f);
+        return ((b >> gbase) & ((1ull << G) - 1ull)) != 0;
+    }
+    // the group's flags as entry bits of slot i (bit i * G + j: lane j's flag)
+    __device__ __forceinline__ uint32_t group_bits(bool f, uint32_t i) const {
+        const unsigned long long b = __ballot(f);
+        return uint32_t((b >> gbase) & ((1ull << G) - 1ull)) << (i * G);
+    }
+    __device__ __forceinline__ static uint32_t eq4(const LLab &x, const LLab &y) {
+        return ((x.c1 ^ y.c1) | (x.c2 ^ y.c2) | (x.c3 ^ y.c3) | ((x.m ^ y.m) & 0xFFu)) == 0 ? ~0u : 0u;
+    }
+    __device__ __forceinline__ LLab lt_get(uint32_t e) const {
+        const uint4 v = LT[e];
+        return LLab{v.x, v.y, v.z, v.w};
+    }
+
+    // candidates from the settled special into entry e (LaneHub::from_s with the entry's
+    // role a run-time bit of the settle's masks): CentralMove, walk, caravan, then SoE or
+    // the SoE-region pair, a later one replacing the best only when strictly smaller
+    __device__ __forceinline__ FromS from_s_rt(const Settle &z, uint32_t e, const uint4 A, const uint2 B) const {
+        FromS f;
+        f.won = bitv(z.walk, e);  // (z.walk never has the Center's bit)
+        f.w = opt(f.won, add(z.ls, A.x, 0, A.y, z.mW));
+        const uint32_t oc = bitv(z.cenm, e);
+        f.c = opt(oc, z.cen);
+        consider(f.c, f.w);
+        f.any = f.won | oc;
+        const uint32_t on = bitv(z.car, e);
+        consider(f.c, opt(on, add(z.ls, 0, A.z, A.w, z.mCar)));
+        f.any |= on;
+        const uint32_t so = bitv(z.soe, e), onr = so | bitv(z.reg, e);
+        consider(f.c, opt(onr, add(z.ls, B.x, P.soe_cost, B.y, msel(so, z.mSoE, z.mR))));
+        f.any |= onr;
+        return f;
+    }
+    // LaneHub::offer for slot i (entry bit eb)
+    __device__ __forceinline__ void offer_rt(LLab &T, uint32_t eb, const FromS &f, uint32_t &ties) {
+        const uint32_t gt = ltm(T, f.c);
+        const uint32_t drop = ltm3(f.c, T);
+        uint32_t dummy = 0;
+        const uint32_t lt = ltm_take_idx(f.c, T, 0u, dummy);
+        tent |= lt & eb;
+        const uint32_t wtie = f.won & ~ltm3(T, f.w);
+        wt = (wt & ~(drop & eb)) | (wtie & eb);
+        ties |= f.any & ~(lt | gt) & eb;
+    }
+
+    // ---- one source per group; every lane of the group calls it with the same source ---
+    // returns the records this lane wrote (lane 0 of the group reports the source's)
+    __device__ __forceinline__ uint32_t solve(bool have, uint32_t s_idx) {
+        const DevParams &p = P;
+        const uint32_t NS = p.NS;
+        gj = lane_id() & (G - 1u);
+        gbase = lane_id() & ~(G - 1u);
+        src = a->src_v[s_idx];
+        sx = int(src % p.S) - int(p.H);
+        sy = int(src / p.S) - int(p.H);
+        cell_word(src, sx, sy, ts, src_rk);
+        srow = reinterpret_cast<const uint2 *>(a->near) + (unsigned long long)src * nreg;
+        const LLab st0 = start();
+        {
+            const LLab x = inf();
+#pragma unroll
+            for (uint32_t i = 0; i < E; ++i) LT[ent(i)] = make_uint4(x.c1, x.c2, x.c3, x.m);
+        }
+        // the source's own edges (LaneHub::solve's first loop, entry per slot)
+        const bool walks0 = have && src != p.vc;
+#pragma unroll
+        for (uint32_t i = 0; i < E; ++i) {
+            const uint32_t e = ent(i);
+            const bool valid = have && e >= 1 && e <= NS;
+            const SpecialStatic tS = spl[valid ? e : 1u];
+            const uint32_t m0 = vmask(valid && e == ts);
+            LLab c = opt(m0, st0);
+            uint32_t any = m0;
+            const uint32_t k = walk_dist(sx, sy, tS.x, tS.y);
+            const uint32_t won = vmask(valid && walks0 && tS.v != src && e != 1);  // no walks into the Center
+            const LLab w = opt(won, mk(k, 0, 180u * k, lm_pack(1, 0, 1, kStandard)));
+            consider(c, w);
+            any |= won;
+            {  // [SoE src -> e], or [Std{d} src -> u, SoE u -> e]
+                const bool reg = valid && p.use_soe && tS.rid != kNone10;
+                const uint32_t ev = reg ? srow[reg ? tS.rid : 0u].x : kNone32;
+                const bool on = walks0 && reg && ev != kNone32;
+                const uint32_t d = on ? ev : 0u;
+                const uint32_t om = vmask(on);
+                consider(c, opt(om, mk(d, p.soe_cost, 180u * d,
+                                       d == 0 ? lm_pack(1, 0, 1, kSoE) : lm_pack(2, 0, 2, kStandard))));
+                any |= om;
+            }
+            {
+                const uint32_t om = vmask(valid && e == p.hq_t);
+                consider(c, opt(om, mk(0, p.shq_cost, 0, lm_pack(1, 0, 1, kSHQ))));
+                any |= om;
+            }
+            {
+                const uint32_t om = vmask(valid && p.use_sfm && e == 1);
+                consider(c, opt(om, mk(0, p.sfm_cost, 0, lm_pack(1, 0, 1, kSFm))));
+                any |= om;
+            }
+            Ls[i] = opt(any, c);
+            const uint32_t eb = 1u << e;
+            tent |= any & eb;
+            wt |= won & ~ltm3(c, w) & eb;
+        }
+        // ---- Dijkstra over the specials, one settle per group per iteration -----------
+        uint32_t *mcol = M + lane_id();  // this lane's column of the meta copy
+        const uint32_t n_it = (a->dbg_flags & kDbgGroupNoSolve) ? 0u : NS;  // (timing experiments)
+        for (uint32_t it = 0; it < n_it; ++it) {
+            const uint32_t cand = tent & ~done;  // (this lane's entries only)
+            if (!__any(cand != 0)) break;
+            // this lane's least candidate (tx: another of its slots ties it exactly)
+            LLab lx = inf();
+            uint32_t sl = 0, tx = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < E; ++i) {
+                const uint32_t cm = bitv(cand, ent(i));
+                const LLab c = opt(cm, Ls[i]);
+                const uint32_t gt = ltm(lx, c);
+                const uint32_t lt = ltm_take_idx(c, lx, ent(i), sl);
+                tx = ~lt & (tx | (cm & ~gt));
+            }
+            // the group's least on (c1, c2, c3, length, entry): every lane gets it
+            Settle z;
+            z.ls = lx;
+            uint32_t k = (lx.m << 24) | sl;
+            group_min<G>(z.ls.c1, z.ls.c2, z.ls.c3, z.ls.m, k);
+            uint32_t s = k & 0xFFu;
+            // exact (metrics, length) ties with the winner: the command lists decide (rare)
+            const bool tie_l = (tx != 0 && sl == s) || (sl != 0 && sl != s && eq4(lx, z.ls) != 0);
+            if (__any(tie_l)) {
+                uint32_t tied = 0;  // the group's candidates with the winner's metrics and length
+#pragma unroll
+                for (uint32_t i = 0; i < E; ++i) {
+                    const bool ti = ((cand >> ent(i)) & 1u) && eq4(Ls[i], z.ls) != 0;
+                    if (ti) {  // publish the meta word to every lane of the group
+                        for (uint32_t j = 0; j < G; ++j) M[ent(i) * 64u + gbase + j] = Ls[i].m;
+                    }
+                    tied |= group_bits(ti, i);
+                }
+                asm volatile("" ::: "memory");
+                for (uint32_t mm = tied & ~(1u << s); mm; mm &= mm - 1u) {
+                    const uint32_t t = uint32_t(__builtin_ctz(mm));
+                    const uint32_t mt = meta_of(t);
+                    if (cmp_list(mt, t, own_of(t), z.ls.m, s, own_of(s)) < 0) {
+                        z.ls.m = mt;  // (same metrics and length)
+                        s = t;
+                    }
+                }
+            }
+            // the blocker bit of s lives with the lane that owns it
+            const bool wts = group_any(s != 0 && (s & (G - 1u)) == gj && ((wt >> s) & 1u));
+            settle_ctx(z, s, wts);
+            if (s != 0) {  // publish the settled label (the chains and the read-off)
+                mcol[s * 64u] = z.ls.m;
+                if (gj == 0) LT[s] = make_uint4(z.ls.c1, z.ls.c2, z.ls.c3, z.ls.m);
+            }
+            // relaxations into this lane's slots
+            uint32_t ties = 0, fcm[E];
+            const uint4 *rowa = PA + z.s * TM;
+            const uint2 *rowb = PB + z.s * TM;
+#pragma unroll
+            for (uint32_t i = 0; i < E; ++i) {
+                const uint32_t e = ent(i);
+                const FromS f = from_s_rt(z, e, rowa[e], rowb[e]);
+                fcm[i] = f.c.m;
+                offer_rt(Ls[i], 1u << e, f, ties);
+            }
+            // exact (metrics, length) ties with a tentative label: the lists decide (rare)
+            if (__any(ties != 0)) {
+#pragma unroll
+                for (uint32_t i = 0; i < E; ++i) {
+                    const uint32_t e = ent(i);
+                    if (((ties >> e) & 1u) && cmp_list(fcm[i], kOwn, own_of(e), Ls[i].m, e, own_of(e)) < 0)
+                        Ls[i].m = fcm[i];
+                }
+            }
+        }
+        if (!have) return 0;
+        // ---- certification: with blockers, every settled walk label must be certain ----
+        bool unc = false;
+        if (blk != 0) {
+#pragma unroll
+            for (uint32_t i = 0; i < E; ++i) {
+                const uint32_t e = ent(i);
+                if (e >= 1 && e <= NS && ((done >> e) & 1u) && !label_avail(Ls[i].m, e)) unc = true;
+            }
+        }
+        const bool fb_sp = group_any(unc) || a->fb_all || (a->dbg_flags & kDbgGroupNoReadoff);
+        const uint32_t qa = a->q_begin[s_idx], qb = a->q_begin[s_idx + 1];
+        // ---- destinations, one query per lane: the source, a special, or the best walk ---
+        const bool walk0 = src != p.vc;
+        bool uncd = false;
+        for (uint32_t qi = fb_sp ? qb : qa + gj; qi < qb; qi += G) {
+            const uint32_t w = a->q_dst[qi];
+            const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
+            uint32_t tw, wr;
+            cell_word(w, wx, wy, tw, wr);
+            if (w == src) {
+                emit(st0, kOwn, Own{sx, sy, src_rk, kNone10, 0u}, qi);
+                continue;
+            }
+            if (tw != kNone10) {
+                emit(lt_get(tw), tw, own_of(tw), qi);
+                continue;
+            }
+            const Own wo{wx, wy, wr, kNone10, 0u};
+            // candidates compared on the boundary's own meta (length - 1; the source's walk: 0)
+            LLab x = inf();
+            uint32_t bx = walk0 ? 0u : kNone32;
+            uint32_t tie = 0;
+            {
+                const uint32_t kk = walk_dist(sx, sy, wx, wy);
+                ll_sel(vmask(walk0), x, mk(kk, 0, 180u * kk, 0u));
+            }
+            for (uint32_t mm = bndm; mm; mm &= mm - 1u) {
+                const uint32_t t = uint32_t(__builtin_ctz(mm));
+                const uint32_t kk = walk_dist(spl[t].x, spl[t].y, wx, wy);
+                const LLab lb = lt_get(t);
+                const LLab c = add(lb, kk, 0, 180u * kk, lb.m);
+                const uint32_t gt = ltm(x, c);
+                const uint32_t lt = ltm_take_idx(c, x, t, bx);
+                tie = ~lt & (tie | ~gt);
+            }
+            if (bx == kNone32) {  // no boundary can walk here: cannot happen on a connected grid
+                a->out_res[qi] = OutResult{0, 0, 0, uint32_t(16 + 1) << 16};
+                continue;
+            }
+            x.m = lm_pack(lm_len(x.m) + 1u, bx, 1, kStandard);
+            if (tie) {  // equal metrics and length from several boundaries: the lists decide
+                for (uint32_t mm = (bndm | (walk0 ? 1u : 0u)) & ~(1u << bx); mm; mm &= mm - 1u) {
+                    const uint32_t b = uint32_t(__builtin_ctz(mm));
+                    int px, py;
+                    pos(b, px, py);
+                    const uint32_t kk = walk_dist(px, py, wx, wy);
+                    const LLab c = b == 0 ? mk(kk, 0, 180u * kk, lm_pack(1, 0, 1, kStandard)) : walk_to(lt_get(b), b, kk);
+                    if (cmp4(c, x) == 0 && cmp_list(c.m, kOwn, wo, x.m, kOwn, wo) < 0) {
+                        x = c;
+                        bx = b;
+                    }
+                }
+            }
+            emit(x, kOwn, wo, qi);
+            if (blk != 0) {
+                int px, py;
+                pos(bx, px, py);
+                if (!avail(bx, px, py, wx, wy)) uncd = true;
+            }
+        }
+        const bool fallback = fb_sp || group_any(uncd);
+        if (fallback && gj == 0) push_fallback(a, counter, s_idx, kNone32);
+        return (fallback || gj != 0) ? 0u : qb - qa;
+    }
+};
+
+// LDS: the lane kernels' (lane_lds_total with TM = G * E) and per group its settled labels
+__host__ __device__ inline uint32_t group_off_lt(uint32_t NS, uint32_t nreg, uint32_t TM) {
+    return align16h(lane_lds_total(NS, nreg, TM));
+}
+__host__ __device__ inline uint32_t group_lds_total(uint32_t NS, uint32_t nreg, uint32_t G, uint32_t E) {
+    return group_off_lt(NS, nreg, G * E) + (kBS / 64) * (64 / G) * G * E * 16u;
+}
+
+template <uint32_t PERM, uint32_t G, uint32_t E>
+__global__ __launch_bounds__(kBS) void hub_group_kernel(const KArgs *__restrict__ a) {
+    constexpr uint32_t TM = G * E;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    GroupHub<PERM, G, E> H;
+    lane_setup<TM>(a, smem, H);
+    // group q of wave w: source (64 / G) w + q of the sources [0, n_lane)
+    const uint32_t grp = (blockIdx.x * (kBS / 64) + (threadIdx.x >> 6)) * (64u / G) + lane_id() / G;
+    H.LT = reinterpret_cast<uint4 *>(smem + group_off_lt(a->p.NS, a->nreg, TM)) + (threadIdx.x / G) * TM;
+    const uint32_t n = a->n_lane;
+    const bool have = grp < n;
+    uint32_t written = 0;
+    if (__any(have)) written = H.solve(have, have ? grp : (n ? n - 1 : 0));
+    __shared__ uint32_t wsum;
+    if (threadIdx.x == 0) wsum = 0;
+    __syncthreads();
+    if (written) atomicAdd(&wsum, written);
+    __syncthreads();
+    if (threadIdx.x == 0) finish_launch(a, wsum);
+}
+
+}  // namespace mr

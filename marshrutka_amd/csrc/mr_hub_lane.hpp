@@ -428,6 +428,39 @@ struct LaneHub {
         ties |= f.any & ~(lt | gt) & bit;
     }
 
+    // Bookkeeping of the settle of entry s (0: none this iteration) with label z.ls: the
+    // settled and boundary masks, the blocker bit (wts: some walk candidate had s's
+    // metrics) and the per-iteration context of the candidates from s.
+    __device__ __forceinline__ void settle_ctx(Settle &z, uint32_t s, bool wts) {
+        const DevParams &p = P;
+        const bool act = s != 0;
+        z.s = act ? s : 1u;
+        done |= act ? (1u << s) : 0u;
+        const uint32_t lm = z.ls.m, len = lm_len(lm);
+        const uint32_t lk = lm_nt(lm) == 2 ? kSoE : lm_kind(lm);
+        const bool boundary = act && lk != kNoMove && lk != kStandard;
+        blk |= (boundary && wts) ? (1u << s) : 0u;  // a walk tied it: a blocker
+        const bool walks = boundary && s != 1;  // the Center starts no walks
+        bndm |= walks ? (1u << s) : 0u;
+        // the start label (the source's own special; metrics 0): its NoMove is replaced
+        const uint32_t bm = lk == kNoMove ? lm_pack(1, 0, 1, 0) : lm_pack(len + 1u, z.s, 1, 0);
+        z.mW = lm_pack(len + 1u, z.s, 1, kStandard);
+        z.mR = lm_pack(len + 2u, z.s, 2, kStandard);
+        z.mCar = bm | (kCaravan << 8);
+        z.mSoE = bm | (kSoE << 8);
+        // a CentralMove after a CentralMove merges into it
+        z.cen = add(z.ls, 0, 0, 10u,
+                    lk == kCentral ? lm_pack(len, lm_par(lm), 1, kCentral, lm_cj(lm) + 1u)
+                                   : (bm | lm_pack(0, 0, 1, kCentral, 1)));
+        const uint32_t live = act ? (validm & ~done) : 0u;  // unsettled entries
+        const uint32_t rg = spl[z.s].region;
+        z.cenm = live & (z.s == 1 ? 0x3Cu : ((z.s >= 2 && z.s <= 5) ? 0x2u : 0u));
+        z.car = (p.use_caravans && ((hubm >> z.s) & 1u)) ? (live & hubm) : 0u;
+        z.soe = (p.use_soe && rg != kNone10 && rg != z.s) ? (live & (1u << rg)) : 0u;
+        z.reg = (walks && p.use_soe) ? (live & RM[z.s]) : 0u;
+        z.walk = walks ? (live & ~0x2u) : 0u;
+    }
+
     // ---- certification (hub_kernel's avail / label_avail) ----------------------------
     __device__ __forceinline__ bool avail(uint32_t b, int bx, int by, int vx, int vy) const {
         if (blk == 0) return true;
@@ -623,32 +656,7 @@ struct LaneHub {
                     }
                 }
             }
-            const bool act = s != 0;
-            z.s = act ? s : 1u;
-            done |= act ? (1u << s) : 0u;
-            const uint32_t lm = z.ls.m, len = lm_len(lm);
-            const uint32_t lk = lm_nt(lm) == 2 ? kSoE : lm_kind(lm);
-            const bool boundary = act && lk != kNoMove && lk != kStandard;
-            blk |= (boundary && ((wt >> s) & 1u)) ? (1u << s) : 0u;  // a walk tied it: a blocker
-            const bool walks = boundary && s != 1;                     // the Center starts no walks
-            bndm |= walks ? (1u << s) : 0u;
-            // the start label (the source's own special; metrics 0): its NoMove is replaced
-            const uint32_t bm = lk == kNoMove ? lm_pack(1, 0, 1, 0) : lm_pack(len + 1u, z.s, 1, 0);
-            z.mW = lm_pack(len + 1u, z.s, 1, kStandard);
-            z.mR = lm_pack(len + 2u, z.s, 2, kStandard);
-            z.mCar = bm | (kCaravan << 8);
-            z.mSoE = bm | (kSoE << 8);
-            // a CentralMove after a CentralMove merges into it
-            z.cen = add(z.ls, 0, 0, 10u,
-                        lk == kCentral ? lm_pack(len, lm_par(lm), 1, kCentral, lm_cj(lm) + 1u)
-                                       : (bm | lm_pack(0, 0, 1, kCentral, 1)));
-            const uint32_t live = act ? (validm & ~done) : 0u;  // unsettled entries
-            const uint32_t rg = spl[z.s].region;
-            z.cenm = live & (z.s == 1 ? 0x3Cu : ((z.s >= 2 && z.s <= 5) ? 0x2u : 0u));
-            z.car = (p.use_caravans && ((hubm >> z.s) & 1u)) ? (live & hubm) : 0u;
-            z.soe = (p.use_soe && rg != kNone10 && rg != z.s) ? (live & (1u << rg)) : 0u;
-            z.reg = (walks && p.use_soe) ? (live & RM[z.s]) : 0u;
-            z.walk = walks ? (live & ~0x2u) : 0u;
+            settle_ctx(z, s, ((wt >> s) & 1u) != 0);
             const uint4 *rowa = PA + z.s * TM;
             const uint2 *rowb = PB + z.s * TM;
             // Each step also stores into the LDS meta copy M: a settled entry's own meta
@@ -809,9 +817,10 @@ __host__ __device__ inline uint32_t lane_lds_total(uint32_t NS, uint32_t nreg, u
     return lane_off_hash(NS, nreg, TM) + kLaneHash * 8u + 16u;
 }
 
-template <uint32_t PERM, uint32_t TM>
-__global__ __launch_bounds__(kBS, lane_waves(TM)) void hub_lane_kernel(const KArgs *__restrict__ a) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
+// The lane kernels' workgroup setup: the specials' static records, their region rows,
+// the pair table, its row masks and the specials' hash in LDS, and the solver's fields.
+template <uint32_t TM, class Hub>
+__device__ __forceinline__ void lane_setup(const KArgs *__restrict__ a, char *smem, Hub &H) {
     const uint32_t NS = a->p.NS, nreg = a->nreg;
     SpecialStatic *spl = reinterpret_cast<SpecialStatic *>(smem);
     uint2 *nearl = reinterpret_cast<uint2 *>(smem + lane_off_near(NS));
@@ -866,7 +875,6 @@ __global__ __launch_bounds__(kBS, lane_waves(TM)) void hub_lane_kernel(const KAr
         *reinterpret_cast<uint32_t *>(smem + lane_off_hash(NS, nreg, TM) + kLaneHash * 8u) = probes;
     }
     __syncthreads();
-    LaneHub<PERM, TM> H;
     H.a = a;
     H.P = a->p;
     H.spl = spl;
@@ -895,6 +903,13 @@ __global__ __launch_bounds__(kBS, lane_waves(TM)) void hub_lane_kernel(const KAr
     H.c5m = __builtin_amdgcn_readfirstlane(c5m);
     H.regm = __builtin_amdgcn_readfirstlane(regm);
     H.validm = __builtin_amdgcn_readfirstlane(((2u << min(NS, TM - 1u)) - 1u) & ~1u);
+}
+
+template <uint32_t PERM, uint32_t TM>
+__global__ __launch_bounds__(kBS, lane_waves(TM)) void hub_lane_kernel(const KArgs *__restrict__ a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    LaneHub<PERM, TM> H;
+    lane_setup<TM>(a, smem, H);
     // lane l of wave w: source 64 w + l of the lane kernel's sources [0, n_lane)
     const uint32_t s_idx = (blockIdx.x * (kBS / 64) + (threadIdx.x >> 6)) * 64u + lane_id();
     const uint32_t n = a->n_lane;

@@ -46,7 +46,7 @@ def test_library_exports_every_declared_symbol(eng):
 
 def test_abi_version_and_defaults(eng):
     L = eng.lib()
-    assert L.mr_abi_version() == 6
+    assert L.mr_abi_version() == 7
     p = abi.mr_params()
     L.mr_params_default(C.byref(p))
     d = Params().to_c()

@@ -23,19 +23,23 @@ def eng():
     return pathfinder
 
 
-@pytest.fixture(params=["auto-lds", "auto-hbm", "lane-lds", "lanetab-lds", "hub1-lds", "hub2-lds", "wide-lds", "widescan-lds", "fallback-lds", "fallback-hbm", "fbsssp-lds",
+@pytest.fixture(params=["auto-lds", "auto-hbm", "lane-lds", "lanetab-lds", "group-lds", "group16-lds", "hub1-lds", "hub2-lds", "wide-lds", "widescan-lds", "fallback-lds", "fallback-hbm", "fbsssp-lds",
                         "sssp-lds", "sssp-hbm", "generic-lds", "generic-hbm"])
 def grid_state(request, monkeypatch):
     """Every solver path x both grid-state regimes:
     auto     — hub solver when the run time is linear (one source per lane when the
                table fits 22 entries, a source has <= 32 queries and the plan has
-               enough such sources to fill the GPU, else two sources per wave when
-               the specials fit 32 lanes), else the SSSP solvers
+               enough such sources to fill the GPU, else one source per 8 lanes when
+               the table fits 32 entries, else two sources per wave when the specials
+               fit 32 lanes), else the SSSP solvers
+    group    — auto with one source per group of 8 lanes (hub_group_kernel) wherever it
+               applies, the lane kernel's plans included (MR_HUB_GROUP_FORCE=1)
+    group16  — the same with groups of 16 lanes
     lane     — auto with the lane kernel whenever it applies (MR_HUB_LANE=1); on the
                standard layout it computes ranks and looks up specials itself
     lanetab  — the same reading every cell's {sinfo, rank} record (MR_RANK_TABLE=1)
-    hub1     — hub solver with one source per wave (no lane kernel)
-    hub2     — hub solver with two sources per wave (no lane kernel)
+    hub1     — hub solver with one source per wave (no lane or group kernel)
+    hub2     — hub solver with two sources per wave (no lane or group kernel)
     wide     — the wide hub solver (several specials per lane) even where the
                narrow one applies
     widescan — the same with each source's region row scanned from the regions'
@@ -56,11 +60,18 @@ def grid_state(request, monkeypatch):
     monkeypatch.delenv("MR_CERT", raising=False)
     monkeypatch.delenv("MR_CERT_SLOTS", raising=False)
     monkeypatch.delenv("MR_RANK_TABLE", raising=False)
+    monkeypatch.delenv("MR_HUB_GROUP", raising=False)
+    monkeypatch.delenv("MR_HUB_GROUP_FORCE", raising=False)
+    if algo in ("group", "group16"):
+        monkeypatch.setenv("MR_HUB_GROUP_FORCE", "1")
+        if algo == "group16":
+            monkeypatch.setenv("MR_HUB_GROUP", "16")
     if algo == "lanetab":
         monkeypatch.setenv("MR_RANK_TABLE", "1")
         algo = "lane"
     if algo in ("hub1", "hub2"):
         monkeypatch.setenv("MR_HUB_LANE", "0")
+        monkeypatch.setenv("MR_HUB_GROUP", "0")
     if algo == "lane":
         monkeypatch.setenv("MR_HUB_LANE", "1")
     if algo == "wide":
@@ -246,25 +257,28 @@ def test_lane_kernel_selection(eng, oracle_lib, monkeypatch):
     """hub_lane_kernel takes a plan's few-query sources when there are enough of them
     to fill the GPU (MR_HUB_LANE_MIN, default half a wave per SIMD), always with
     MR_HUB_LANE=1, never with MR_HUB_LANE=0; the table layout it needs (region
-    campfires in entries 6..11) comes from the host's special order.  Results are the
-    oracle's either way."""
+    campfires in entries 6..11) comes from the host's special order.  A plan the lane
+    kernel does not take runs one source per 8 lanes (hub_group_kernel) unless
+    MR_HUB_GROUP=0.  Results are the oracle's either way."""
     m = SyntheticMap(33, campfires_per_homeland=4, seed=5)
     qs = random_queries(m, 400, 6)
     g = eng.MapGrid(m.cells())
-    lanes = {}
+    lanes, per = {}, {}
     for mode, env in (("default", {}), ("force", {"MR_HUB_LANE": "1"}), ("off", {"MR_HUB_LANE": "0"}),
-                      ("min1", {"MR_HUB_LANE_MIN": "1"})):
-        monkeypatch.delenv("MR_HUB_LANE", raising=False)
-        monkeypatch.delenv("MR_HUB_LANE_MIN", raising=False)
+                      ("min1", {"MR_HUB_LANE_MIN": "1"}), ("nogroup", {"MR_HUB_GROUP": "0"}),
+                      ("g16", {"MR_HUB_GROUP": "16"})):
+        for k in ("MR_HUB_LANE", "MR_HUB_LANE_MIN", "MR_HUB_GROUP", "MR_HUB_GROUP_FORCE"):
+            monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         pl = eng.Plan(g, Params(), qs)
         st = pl.stats()
-        lanes[mode] = st["lane_sources"]
+        lanes[mode], per[mode] = st["lane_sources"], st["lanes_per_source"]
         check(eng, oracle_lib, m, Params(), qs, f"lane mode {mode}")
     n_src = len({a for a, _ in qs})
     assert lanes["default"] == 0 and lanes["off"] == 0, lanes  # 400 sources < half a wave per SIMD
     assert lanes["force"] == n_src and lanes["min1"] == n_src, lanes
+    assert per == {"default": 8, "force": 1, "off": 8, "min1": 1, "nogroup": 0, "g16": 16}, per
 
 
 @pytest.mark.parametrize("k,hq,tm", [(4, True, 24), (5, False, 32), (6, True, 32)])
