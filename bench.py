@@ -439,6 +439,11 @@ def main():
     if pipe is not None:
         pipe.drain()
     torch.cuda.synchronize()
+    # the counters of a finished pass: a plan whose pass handed no source to the fallback
+    # ends its later passes with the hub launch (the certificate and SSSP launches would
+    # only exit at once), as a serving caller's plan does after its first fetch
+    for p_ in plans:
+        p_.stats()
     for p_ in plans:
         p_.kernel_ms()  # reset the per-launch event window to the timed region
     if dist_on:

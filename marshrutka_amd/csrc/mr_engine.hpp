@@ -266,7 +266,7 @@ constexpr uint32_t kErrKOverflow = 1u, kErrMetricOverflow = 2u, kErrBucket = 4u,
 // KArgs::dbg_flags bit (tests only): the fill launch raises kErrChain
 constexpr uint32_t kDbgInjectFlag = 16u;
 // KArgs::dbg_flags bits (timing experiments only, results are not valid): hub_group_kernel
-// skips its Dijkstra / its destinations
-constexpr uint32_t kDbgGroupNoSolve = 32u, kDbgGroupNoReadoff = 64u;
+// skips its Dijkstra / its destinations / the list compares of exact ties
+constexpr uint32_t kDbgGroupNoSolve = 32u, kDbgGroupNoReadoff = 64u, kDbgGroupNoTies = 128u;
 
 }  // namespace mr

@@ -1669,7 +1669,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     const char *hg = std::getenv("MR_HUB_GROUP");
     const uint32_t hgv = hg ? uint32_t(std::strtoul(hg, nullptr, 10)) : 8u;
     const bool group_off = hg && hgv == 0, group_force = std::getenv("MR_HUB_GROUP_FORCE") != nullptr;
-    const uint32_t group_g = hgv == 16 ? 16u : 8u;
+    const uint32_t group_g = hgv == 16 ? 16u : (hgv == 32 ? 32u : 8u);
     const bool lane_ok = hp.hub && !hp.wide && !hp.nonlin && !all_mode && lane_bounds_ok(hp.p);
     if (lane_ok && !group_force && !lane_off && hub_lane_entries(hp.p.NS) != 0 && lane_layout_ok(hp) &&
         (lane_force || lane_sources(hp) >= lane_min_sources()))

@@ -22,9 +22,9 @@
 // A source's Dijkstra is ~G times shorter in wave instructions than on the lane kernel,
 // which is what small plans (configs[0] / configs[1], one query) are bound by.
 //
-// Exact ties (metrics and length) go to the command-list compares exactly as in the lane
-// kernel (LaneHub::cmp_list), with the tied entries' meta words published to every lane
-// of the group through the per-wave LDS meta copy.
+// Exact (metrics, length) ties between candidates into one entry go to the command-list
+// compares exactly as in the lane kernel (LaneHub::cmp_list); ties between two entries at
+// a settle need none (either may settle first, LaneHub::solve).
 #pragma once
 #include "mr_hub_lane.hpp"
 
@@ -58,15 +58,41 @@ namespace mr {
         :                                                                                         \
         : "vcc")
 
-// the least (c1, c2, c3, k) over each group of G lanes, in every lane of the group
+// the same round with the partner's words already in p1..pk (the cross-row round)
+__device__ __forceinline__ void grp_take(uint32_t &c1, uint32_t &c2, uint32_t &c3, uint32_t &m, uint32_t &k, uint32_t p1,
+                                         uint32_t p2, uint32_t p3, uint32_t pm, uint32_t pk) {
+    uint32_t t_;
+    asm("v_sub_co_u32_e32 %0, vcc, %5, %10\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %3, %8, vcc\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %2, %7, vcc\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %1, %6, vcc\n\t"
+        "v_cndmask_b32_e32 %1, %6, %1, vcc\n\t"
+        "v_cndmask_b32_e32 %2, %7, %2, vcc\n\t"
+        "v_cndmask_b32_e32 %3, %8, %3, vcc\n\t"
+        "v_cndmask_b32_e32 %4, %9, %4, vcc\n\t"
+        "v_cndmask_b32_e32 %5, %10, %5, vcc"
+        : "=&v"(t_), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(m), "+v"(k)
+        : "v"(p1), "v"(p2), "v"(p3), "v"(pm), "v"(pk)
+        : "vcc");
+}
+
+// the least (c1, c2, c3, k) over each group of G lanes, in every lane of the group: DPP
+// rounds inside a row of 16 lanes, and for 32-lane groups one more through the LDS
+// crossbar (ds_swizzle, lane ^ 16: no memory access)
 template <uint32_t G>
 __device__ __forceinline__ void group_min(uint32_t &c1, uint32_t &c2, uint32_t &c3, uint32_t &m, uint32_t &k) {
-    static_assert(G == 4 || G == 8 || G == 16, "groups are quads, half rows or rows");
+    static_assert(G == 4 || G == 8 || G == 16 || G == 32, "groups are quads, half rows, rows or half waves");
     uint32_t t_, p1, p2, p3, pm, pk;
     MR_GRP_ROUND("quad_perm:[1,0,3,2]");
     MR_GRP_ROUND("quad_perm:[2,3,0,1]");
     if constexpr (G >= 8) MR_GRP_ROUND("row_half_mirror");
     if constexpr (G >= 16) MR_GRP_ROUND("row_mirror");
+    if constexpr (G >= 32) {
+        constexpr int kXor16 = 0x1F | (0x10 << 10);  // bitmask mode: and 0x1f, or 0, xor 0x10
+        grp_take(c1, c2, c3, m, k, __builtin_amdgcn_ds_swizzle(int(c1), kXor16), __builtin_amdgcn_ds_swizzle(int(c2), kXor16),
+                 __builtin_amdgcn_ds_swizzle(int(c3), kXor16), __builtin_amdgcn_ds_swizzle(int(m), kXor16),
+                 __builtin_amdgcn_ds_swizzle(int(k), kXor16));
+    }
 }
 
 // bit e of w as a 0 / ~0 mask, e a run-time value (one v_bfe_i32)
@@ -123,20 +149,13 @@ struct GroupHub : LaneHub<PERM, G * E> {
     LLab Ls[E];      // labels of this lane's slots
     uint32_t gj = 0, gbase = 0;
     uint4 *LT = nullptr;  // LDS: this group's settled labels, entry e at LT[e]
+    uint2 *SR = nullptr;  // LDS: this group's copy of the source's region row (nreg entries)
 
     __device__ __forceinline__ uint32_t ent(uint32_t i) const { return i * G + gj; }
     // some lane of this lane's group has f
     __device__ __forceinline__ bool group_any(bool f) const {
         const unsigned long long b = __ballot(f);
         return ((b >> gbase) & ((1ull << G) - 1ull)) != 0;
-    }
-    // the group's flags as entry bits of slot i (bit i * G + j: lane j's flag)
-    __device__ __forceinline__ uint32_t group_bits(bool f, uint32_t i) const {
-        const unsigned long long b = __ballot(f);
-        return uint32_t((b >> gbase) & ((1ull << G) - 1ull)) << (i * G);
-    }
-    __device__ __forceinline__ static uint32_t eq4(const LLab &x, const LLab &y) {
-        return ((x.c1 ^ y.c1) | (x.c2 ^ y.c2) | (x.c3 ^ y.c3) | ((x.m ^ y.m) & 0xFFu)) == 0 ? ~0u : 0u;
     }
     __device__ __forceinline__ LLab lt_get(uint32_t e) const {
         const uint4 v = LT[e];
@@ -185,7 +204,15 @@ struct GroupHub : LaneHub<PERM, G * E> {
         sx = int(src % p.S) - int(p.H);
         sy = int(src / p.S) - int(p.H);
         cell_word(src, sx, sy, ts, src_rk);
-        srow = reinterpret_cast<const uint2 *>(a->near) + (unsigned long long)src * nreg;
+        {  // the source's region row, copied into LDS (the list compares read it)
+            const uint2 *rg = reinterpret_cast<const uint2 *>(a->near) + (unsigned long long)src * nreg;
+            for (uint32_t r = gj; r < nreg; r += G) SR[r] = rg[r];
+            srow = SR;
+        }
+        // this source's query range and this lane's first destination, loaded now so that
+        // their latency hides behind the Dijkstra
+        const uint32_t qa = a->q_begin[s_idx], qb = a->q_begin[s_idx + 1];
+        const uint32_t w_first = qa + gj < qb ? a->q_dst[qa + gj] : 0u;
         const LLab st0 = start();
         {
             const LLab x = inf();
@@ -238,43 +265,32 @@ struct GroupHub : LaneHub<PERM, G * E> {
         for (uint32_t it = 0; it < n_it; ++it) {
             const uint32_t cand = tent & ~done;  // (this lane's entries only)
             if (!__any(cand != 0)) break;
-            // this lane's least candidate (tx: another of its slots ties it exactly)
+            // this lane's least candidate
             LLab lx = inf();
-            uint32_t sl = 0, tx = 0;
+            uint32_t sl = 0;
 #pragma unroll
             for (uint32_t i = 0; i < E; ++i) {
                 const uint32_t cm = bitv(cand, ent(i));
-                const LLab c = opt(cm, Ls[i]);
-                const uint32_t gt = ltm(lx, c);
-                const uint32_t lt = ltm_take_idx(c, lx, ent(i), sl);
-                tx = ~lt & (tx | (cm & ~gt));
+                ltm_take_i(opt(cm, Ls[i]), lx, ent(i), sl);
             }
-            // the group's least on (c1, c2, c3, length, entry): every lane gets it
+            // the group's least on (c1, c2, c3, length, entry): every lane gets it.  Exact
+            // (metrics, length) ties between entries settle in entry order: which one
+            // settles first changes no label (LaneHub::solve, MR_LANE_SETTLE_TIES).
             Settle z;
             z.ls = lx;
             uint32_t k = (lx.m << 24) | sl;
             group_min<G>(z.ls.c1, z.ls.c2, z.ls.c3, z.ls.m, k);
-            uint32_t s = k & 0xFFu;
-            // exact (metrics, length) ties with the winner: the command lists decide (rare)
-            const bool tie_l = (tx != 0 && sl == s) || (sl != 0 && sl != s && eq4(lx, z.ls) != 0);
-            if (__any(tie_l)) {
-                uint32_t tied = 0;  // the group's candidates with the winner's metrics and length
+            const uint32_t s = k & 0xFFu;
+            // the pair-table words of s into this lane's slots, read before the settle's
+            // bookkeeping so that their latency overlaps it
+            uint4 pa_[E];
+            uint2 pb_[E];
+            {
+                const uint32_t zs = s != 0 ? s : 1u;
 #pragma unroll
                 for (uint32_t i = 0; i < E; ++i) {
-                    const bool ti = ((cand >> ent(i)) & 1u) && eq4(Ls[i], z.ls) != 0;
-                    if (ti) {  // publish the meta word to every lane of the group
-                        for (uint32_t j = 0; j < G; ++j) M[ent(i) * 64u + gbase + j] = Ls[i].m;
-                    }
-                    tied |= group_bits(ti, i);
-                }
-                asm volatile("" ::: "memory");
-                for (uint32_t mm = tied & ~(1u << s); mm; mm &= mm - 1u) {
-                    const uint32_t t = uint32_t(__builtin_ctz(mm));
-                    const uint32_t mt = meta_of(t);
-                    if (cmp_list(mt, t, own_of(t), z.ls.m, s, own_of(s)) < 0) {
-                        z.ls.m = mt;  // (same metrics and length)
-                        s = t;
-                    }
+                    pa_[i] = PA[zs * TM + ent(i)];
+                    pb_[i] = PB[zs * TM + ent(i)];
                 }
             }
             // the blocker bit of s lives with the lane that owns it
@@ -286,17 +302,15 @@ struct GroupHub : LaneHub<PERM, G * E> {
             }
             // relaxations into this lane's slots
             uint32_t ties = 0, fcm[E];
-            const uint4 *rowa = PA + z.s * TM;
-            const uint2 *rowb = PB + z.s * TM;
 #pragma unroll
             for (uint32_t i = 0; i < E; ++i) {
                 const uint32_t e = ent(i);
-                const FromS f = from_s_rt(z, e, rowa[e], rowb[e]);
+                const FromS f = from_s_rt(z, e, pa_[i], pb_[i]);
                 fcm[i] = f.c.m;
                 offer_rt(Ls[i], 1u << e, f, ties);
             }
             // exact (metrics, length) ties with a tentative label: the lists decide (rare)
-            if (__any(ties != 0)) {
+            if (__any(ties != 0) && !(a->dbg_flags & kDbgGroupNoTies)) {
 #pragma unroll
                 for (uint32_t i = 0; i < E; ++i) {
                     const uint32_t e = ent(i);
@@ -316,12 +330,11 @@ struct GroupHub : LaneHub<PERM, G * E> {
             }
         }
         const bool fb_sp = group_any(unc) || a->fb_all || (a->dbg_flags & kDbgGroupNoReadoff);
-        const uint32_t qa = a->q_begin[s_idx], qb = a->q_begin[s_idx + 1];
         // ---- destinations, one query per lane: the source, a special, or the best walk ---
         const bool walk0 = src != p.vc;
         bool uncd = false;
         for (uint32_t qi = fb_sp ? qb : qa + gj; qi < qb; qi += G) {
-            const uint32_t w = a->q_dst[qi];
+            const uint32_t w = qi == qa + gj ? w_first : a->q_dst[qi];
             const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
             uint32_t tw, wr;
             cell_word(w, wx, wy, tw, wr);
@@ -386,8 +399,11 @@ struct GroupHub : LaneHub<PERM, G * E> {
 __host__ __device__ inline uint32_t group_off_lt(uint32_t NS, uint32_t nreg, uint32_t TM) {
     return align16h(lane_lds_total(NS, nreg, TM));
 }
+__host__ __device__ inline uint32_t group_off_sr(uint32_t NS, uint32_t nreg, uint32_t G, uint32_t E) {
+    return group_off_lt(NS, nreg, G * E) + (kBS / G) * G * E * 16u;
+}
 __host__ __device__ inline uint32_t group_lds_total(uint32_t NS, uint32_t nreg, uint32_t G, uint32_t E) {
-    return group_off_lt(NS, nreg, G * E) + (kBS / 64) * (64 / G) * G * E * 16u;
+    return group_off_sr(NS, nreg, G, E) + (kBS / G) * nreg * 8u;
 }
 
 template <uint32_t PERM, uint32_t G, uint32_t E>
@@ -399,6 +415,7 @@ __global__ __launch_bounds__(kBS) void hub_group_kernel(const KArgs *__restrict_
     // group q of wave w: source (64 / G) w + q of the sources [0, n_lane)
     const uint32_t grp = (blockIdx.x * (kBS / 64) + (threadIdx.x >> 6)) * (64u / G) + lane_id() / G;
     H.LT = reinterpret_cast<uint4 *>(smem + group_off_lt(a->p.NS, a->nreg, TM)) + (threadIdx.x / G) * TM;
+    H.SR = reinterpret_cast<uint2 *>(smem + group_off_sr(a->p.NS, a->nreg, G, E)) + (threadIdx.x / G) * a->nreg;
     const uint32_t n = a->n_lane;
     const bool have = grp < n;
     uint32_t written = 0;

@@ -173,6 +173,22 @@ __device__ __forceinline__ uint32_t ltm_take_idx(const LLab &c, LLab &d, uint32_
         : "vcc");
     return k;
 }
+// the same without the mask (the scans: only the index is wanted)
+__device__ __forceinline__ void ltm_take_i(const LLab &c, LLab &d, uint32_t ci, uint32_t &i) {
+    uint32_t t;
+    asm("v_sub_co_u32_sdwa %0, vcc, %7, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %8, %3, vcc\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %9, %4, vcc\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %10, %5, vcc\n\t"
+        "v_cndmask_b32_e32 %5, %5, %10, vcc\n\t"
+        "v_cndmask_b32_e32 %4, %4, %9, vcc\n\t"
+        "v_cndmask_b32_e32 %3, %3, %8, vcc\n\t"
+        "v_cndmask_b32_e32 %2, %2, %7, vcc\n\t"
+        "v_cndmask_b32_e32 %1, %1, %6, vcc"
+        : "=&v"(t), "+&v"(i), "+&v"(d.m), "+&v"(d.c3), "+&v"(d.c2), "+&v"(d.c1)
+        : "v"(ci), "v"(c.m), "v"(c.c3), "v"(c.c2), "v"(c.c1)
+        : "vcc");
+}
 // x < y on the metrics (c1, c2, c3) alone
 __device__ __forceinline__ uint32_t ltm3(const LLab &x, const LLab &y) {
     uint32_t t, r;
@@ -453,11 +469,11 @@ struct LaneHub {
                     lk == kCentral ? lm_pack(len, lm_par(lm), 1, kCentral, lm_cj(lm) + 1u)
                                    : (bm | lm_pack(0, 0, 1, kCentral, 1)));
         const uint32_t live = act ? (validm & ~done) : 0u;  // unsettled entries
-        const uint32_t rg = spl[z.s].region;
+        const uint32_t rg = spl[z.s].region, rmr = RM[z.s];  // (both read up front: one LDS round trip)
         z.cenm = live & (z.s == 1 ? 0x3Cu : ((z.s >= 2 && z.s <= 5) ? 0x2u : 0u));
         z.car = (p.use_caravans && ((hubm >> z.s) & 1u)) ? (live & hubm) : 0u;
         z.soe = (p.use_soe && rg != kNone10 && rg != z.s) ? (live & (1u << rg)) : 0u;
-        z.reg = (walks && p.use_soe) ? (live & RM[z.s]) : 0u;
+        z.reg = (walks && p.use_soe) ? (live & rmr) : 0u;
         z.walk = walks ? (live & ~0x2u) : 0u;
     }
 
@@ -608,7 +624,7 @@ struct LaneHub {
             if (!__any(cand != 0)) break;
             // the settle candidate: least (c1, c2, c3, length), two interleaved chains
             // (odd and even entries) for the latency, then merged; ta / tb: the chain's
-            // best has an exact tie
+            // best has an exact tie (MR_LANE_SETTLE_TIES only)
             LLab la = inf(), lb = inf();
             uint32_t sa = 0, sb = 0, ta = 0, tb = 0;
 #pragma unroll
@@ -618,27 +634,33 @@ struct LaneHub {
                 uint32_t &tx = (t & 1u) ? ta : tb;
                 const uint32_t cm = bitm(cand, t);
                 const LLab c = opt(cm, L[t]);
-#ifdef MR_LANE_CLASSIC
-                const uint32_t lt = ltm(c, lx), gt = ltm(lx, c);
-                tx = ~lt & (tx | (cm & ~gt));
-                ll_sel(lt, lx, c);
-                sx_ = msel(lt, t, sx_);
-#else
+#ifdef MR_LANE_SETTLE_TIES
                 const uint32_t gt = ltm(lx, c);
                 const uint32_t lt = ltm_take_idx(c, lx, t, sx_);
                 tx = ~lt & (tx | (cm & ~gt));
+#else
+                (void)tx;
+                ltm_take_i(c, lx, t, sx_);
 #endif
                 MR_LANE_FENCE();
             }
             Settle z;
             z.ls = la;
-            uint32_t s, tie;
+            uint32_t s, tie = 0;
             {
-                const uint32_t lt = ltm(lb, la), gt = ltm(la, lb);
+                const uint32_t lt = ltm(lb, la);
                 ll_sel(lt, z.ls, lb);
                 s = msel(lt, sb, sa);
+#ifdef MR_LANE_SETTLE_TIES
+                const uint32_t gt = ltm(la, lb);
                 tie = msel(lt, tb, ta | (vmask(sb != 0) & ~gt));
+#endif
             }
+            // Exact (metrics, length) ties between two entries need no list compare here:
+            // whichever settles first, both labels and every relaxation come out the same
+            // (a candidate from one tied entry into the other is one command longer, and
+            // candidates into a third entry that tie are ordered by their lists in offer).
+            // MR_LANE_SETTLE_TIES keeps the reference's pop order (tests: equal results).
             if (__any(tie != 0)) {  // exact (metrics, length) ties: the command lists decide (rare)
                 uint32_t tied = 0;  // the entries with the winner's metrics and length
 #pragma unroll
@@ -836,18 +858,18 @@ __device__ __forceinline__ void lane_setup(const KArgs *__restrict__ a, char *sm
         nearl[t * nreg + r] = nearg[(unsigned long long)a->sp[t].v * nreg + r];
     }
     __syncthreads();
-    // the pair table (LaneHub::from_s)
+    // the pair table (LaneHub::from_s), from the LDS copies of the specials and their rows
     for (uint32_t i = threadIdx.x; i < TM * TM; i += kBS) {
         const uint32_t s = i / TM, t = i % TM;
         uint4 A = make_uint4(0, 0, 0, 0);
         uint2 B = make_uint2(0, 0);
         if (s >= 1 && s <= NS && t >= 1 && t <= NS) {
-            const SpecialStatic ss = a->sp[s], st = a->sp[t];
+            const SpecialStatic ss = spl[s], st = spl[t];
             const uint32_t wd = walk_dist(ss.x, ss.y, st.x, st.y);
             const uint32_t md = uint32_t(abs(ss.x - st.x) + abs(ss.y - st.y));
             A = make_uint4(wd, 180u * wd, (st.coef5 ? 5u : 2u) * md, rgt * md);
             if (st.rid != kNone10) {
-                const uint32_t d = nearg[(unsigned long long)ss.v * nreg + st.rid].x;
+                const uint32_t d = nearl[s * nreg + st.rid].x;
                 if (d != kNone32) {
                     B = make_uint2(d, 180u * d);
                     if (d != 0) atomicOr(rm + s, 1u << t);

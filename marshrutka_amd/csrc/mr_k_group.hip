@@ -21,6 +21,7 @@ static const void *group_fn_ge(uint32_t perm) {
 uint32_t hub_group_slots(uint32_t NS, uint32_t G) {
     if (G == 8) return NS + 1 <= 24 ? 3u : (NS + 1 <= 32 ? 4u : 0u);
     if (G == 16) return NS + 1 <= 32 ? 2u : 0u;
+    if (G == 32) return NS + 1 <= 32 ? 1u : 0u;
     return 0u;
 }
 
@@ -37,6 +38,7 @@ hipError_t launch_hub_group(const KArgs *d_args, const uint32_t perm[3], uint32_
     if (G == 8 && E == 3) fn = group_fn_ge<8, 3>(k);
     else if (G == 8 && E == 4) fn = group_fn_ge<8, 4>(k);
     else if (G == 16 && E == 2) fn = group_fn_ge<16, 2>(k);
+    else if (G == 32 && E == 1) fn = group_fn_ge<32, 1>(k);
     if (!fn) return hipErrorInvalidValue;
     const uint32_t bytes = group_lds_total(NS, nreg, G, E);
     if (bytes > 64u * 1024u) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));

@@ -23,7 +23,7 @@ def eng():
     return pathfinder
 
 
-@pytest.fixture(params=["auto-lds", "auto-hbm", "lane-lds", "lanetab-lds", "group-lds", "group16-lds", "hub1-lds", "hub2-lds", "wide-lds", "widescan-lds", "fallback-lds", "fallback-hbm", "fbsssp-lds",
+@pytest.fixture(params=["auto-lds", "auto-hbm", "lane-lds", "lanetab-lds", "group-lds", "group16-lds", "group32-lds", "hub1-lds", "hub2-lds", "wide-lds", "widescan-lds", "fallback-lds", "fallback-hbm", "fbsssp-lds",
                         "sssp-lds", "sssp-hbm", "generic-lds", "generic-hbm"])
 def grid_state(request, monkeypatch):
     """Every solver path x both grid-state regimes:
@@ -35,6 +35,7 @@ def grid_state(request, monkeypatch):
     group    — auto with one source per group of 8 lanes (hub_group_kernel) wherever it
                applies, the lane kernel's plans included (MR_HUB_GROUP_FORCE=1)
     group16  — the same with groups of 16 lanes
+    group32  — the same with groups of 32 lanes (the last round through ds_swizzle)
     lane     — auto with the lane kernel whenever it applies (MR_HUB_LANE=1); on the
                standard layout it computes ranks and looks up specials itself
     lanetab  — the same reading every cell's {sinfo, rank} record (MR_RANK_TABLE=1)
@@ -62,10 +63,10 @@ def grid_state(request, monkeypatch):
     monkeypatch.delenv("MR_RANK_TABLE", raising=False)
     monkeypatch.delenv("MR_HUB_GROUP", raising=False)
     monkeypatch.delenv("MR_HUB_GROUP_FORCE", raising=False)
-    if algo in ("group", "group16"):
+    if algo in ("group", "group16", "group32"):
         monkeypatch.setenv("MR_HUB_GROUP_FORCE", "1")
-        if algo == "group16":
-            monkeypatch.setenv("MR_HUB_GROUP", "16")
+        if algo != "group":
+            monkeypatch.setenv("MR_HUB_GROUP", algo[5:])
     if algo == "lanetab":
         monkeypatch.setenv("MR_RANK_TABLE", "1")
         algo = "lane"

@@ -1,0 +1,18 @@
+#!/bin/bash
+# round 4: settle ties without list compares (lane + group kernels): parity, c4 A/B, c2 timings
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "not group16" > gpurun_out/t_parity_r04t.log 2>&1 || exit 1
+L=gpurun_out/group_time4.log; : > $L
+for env in "MR_HUB_GROUP=8" "MR_HUB_GROUP=16" "MR_HUB_GROUP=32" "MR_HUB_GROUP=0" "MR_HUB_GROUP=16 MR_DBG_FLAGS=128" "MR_HUB_GROUP=16 MR_DBG_FLAGS=32" "MR_HUB_GROUP=32 MR_DBG_FLAGS=32"; do
+  env $env timeout -k 10 120 python -u tools/probes/group_time.py >> $L 2>&1 || exit 1
+done
+for env in "MR_HUB_GROUP=16" "MR_HUB_GROUP=32" "MR_HUB_GROUP=0"; do
+  env $env timeout -k 10 120 python -u tools/probes/group_time.py 15 1 4 15 >> $L 2>&1 || exit 1
+done
+MR_HUB_GROUP=16 timeout -k 10 120 python bench.py --workload c2 --steps 50 --warmup 5 --no-cpu-baseline --e2e-reps 3 > gpurun_out/b_c2_g16b.json 2> gpurun_out/b_c2_g16b.err || exit 1
+for i in 1 2; do
+timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --e2e-reps 0 > gpurun_out/b_c4_new$i.json 2> gpurun_out/b_c4_new$i.err || exit 1
+MR_LIB_PATH=marshrutka_amd/lib/variants/ties/libmarshrutka_pf.so timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --e2e-reps 0 > gpurun_out/b_c4_ties$i.json 2> gpurun_out/b_c4_ties$i.err || exit 1
+done

@@ -16,6 +16,7 @@ qs = random_queries(m, nq, seed + 17)
 pl = eng.Plan(g, Params(), qs, max_cmds=6)
 for _ in range(3):
     pl.run()
+pl.stats()  # (a pass without fallback sources is known: later passes are the hub launch alone)
 pl.kernel_ms()
 for _ in range(20):
     pl.run()
