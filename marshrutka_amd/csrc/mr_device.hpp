@@ -1492,7 +1492,7 @@ __device__ __forceinline__ uint32_t push_fallback(const KArgs *__restrict__ a, u
 // a boundary special whose label ties a walk candidate on all three metrics
 // (the tie is then decided by length/commands, which a StandardMove can flip) —
 // is detected and such sources are re-solved by the SSSP kernel.  DESIGN.md §3b.
-__device__ __forceinline__ uint32_t walk_dist(int ax, int ay, int bx, int by) {
+__host__ __device__ __forceinline__ uint32_t walk_dist(int ax, int ay, int bx, int by) {
     uint32_t d = uint32_t(abs(ax - bx) + abs(ay - by));
     if ((ay == 0 && by == 0 && ax != 0 && bx != 0 && ((ax < 0) != (bx < 0))) ||
         (ax == 0 && bx == 0 && ay != 0 && by != 0 && ((ay < 0) != (by < 0))))

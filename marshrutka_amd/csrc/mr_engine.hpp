@@ -208,6 +208,9 @@ struct KArgs {
     // 1: every cell's rank is std_rank of its position (mr_hub_lane.hpp; checked at grid
     // creation), so the lane kernel reads no per-cell record
     uint32_t rank_std;
+    // lane and group kernels: the plan's LDS block (lane_blob_bytes, mr_hub_lane.hpp), built
+    // once on the host (lane_blob_build) and copied by every workgroup
+    const uint4 *lane_blob;
 };
 // fb_cert[i] of a staged entry before cert_select_kernel gives it a slot (or none)
 constexpr uint32_t kFbStaged = 0xFFFFFFFEu;

@@ -49,6 +49,8 @@ uint32_t hub_lane_entries(uint32_t NS);
 hipError_t launch_hub_lane(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t n_lane,
                            hipStream_t stream);
 uint32_t hub_group_slots(uint32_t NS, uint32_t G);
+uint32_t lane_blob_build(const SpecialStatic *sp, uint32_t NS, uint32_t nreg, uint32_t TM, uint32_t rgt,
+                         const uint32_t *near_tab, std::vector<uint32_t> &blob);
 uint32_t hub_group_lds_bytes(uint32_t NS, uint32_t nreg, uint32_t G);
 hipError_t launch_hub_group(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t n,
                             uint32_t G, hipStream_t stream);
@@ -1386,6 +1388,7 @@ struct mr_plan {
     double fill_ms = 0.0;                 // all-destinations: average fill launch of the last window
     uint32_t *d_near = nullptr, *d_fb = nullptr;
     uint32_t *d_near_sp = nullptr, *d_rb_off = nullptr, *d_rb_cell = nullptr;  // wide hub tables
+    uint32_t *d_lane_blob = nullptr;  // lane / group kernels: the plan's LDS block (lane_blob_build)
     OutCmd *d_ovf = nullptr;              // command-overflow pool (labels longer than max_cmds)
     uint32_t hub_blocks = 0, fb_blocks = 0, spw = 1, cus = 256, fill_per_cu = 8;
     unsigned long long *d_dbg = nullptr;  // diagnostic builds: per-workgroup phase cycles
@@ -1489,7 +1492,8 @@ struct mr_plan {
                         (void *)d_fb, (void *)d_args_hub_last, (void *)d_args_fill, (void *)d_rec,
                         (void *)d_args_lane, (void *)d_args_lane_last,
                         (void *)d_tab,
-                        (void *)d_lex, (void *)d_sstate, (void *)d_near_sp, (void *)d_rb_off, (void *)d_rb_cell, (void *)d_ovf})
+                        (void *)d_lex, (void *)d_sstate, (void *)d_near_sp, (void *)d_rb_off, (void *)d_rb_cell, (void *)d_ovf,
+                        (void *)d_lane_blob})
             if (p) (void)pfree(p);
         if (ev_last && ev_last_orphan) (void)hipEventDestroy(ev_last);
         for (auto &e : timed) {
@@ -1670,7 +1674,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     const uint32_t hgv = hg ? uint32_t(std::strtoul(hg, nullptr, 10)) : 8u;
     const bool group_off = hg && hgv == 0, group_force = std::getenv("MR_HUB_GROUP_FORCE") != nullptr;
     const uint32_t group_g = hgv == 16 ? 16u : (hgv == 32 ? 32u : 8u);
-    const bool lane_ok = hp.hub && !hp.wide && !hp.nonlin && !all_mode && lane_bounds_ok(hp.p);
+    const bool lane_ok = hp.hub && !hp.wide && !hp.nonlin && !all_mode && hp.near && lane_bounds_ok(hp.p);
     if (lane_ok && !group_force && !lane_off && hub_lane_entries(hp.p.NS) != 0 && lane_layout_ok(hp) &&
         (lane_force || lane_sources(hp) >= lane_min_sources()))
         pl->n_lane = partition_sources(hp);
@@ -1927,6 +1931,13 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         if (pl->n_lane && (pmalloc(reinterpret_cast<void **>(&pl->d_args_lane), sizeof(KArgs)) != hipSuccess ||
                            pmalloc(reinterpret_cast<void **>(&pl->d_args_lane_last), sizeof(KArgs)) != hipSuccess))
             return bail(fail(MR_ERR_DEVICE, "kernel args"));
+        if (pl->n_lane) {  // the lane / group kernels' LDS block, built once per plan
+            const uint32_t TM = pl->lane_g ? pl->lane_g * hub_group_slots(NS, pl->lane_g) : hub_lane_entries(NS);
+            std::vector<uint32_t> blob;
+            lane_blob_build(hp.sp.data(), NS, hp.nreg, TM, hp.p.rgt, hp.near->data(), blob);
+            if (upload(pl->d_lane_blob, blob) != MR_OK) return bail(fail(MR_ERR_DEVICE, "lane tables"));
+            ka.lane_blob = reinterpret_cast<const uint4 *>(pl->d_lane_blob);
+        }
     }
 #ifdef MR_HUBDUMP
     if (const char *e = std::getenv("MR_DEBUG_SRC"))

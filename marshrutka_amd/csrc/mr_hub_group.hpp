@@ -193,26 +193,35 @@ struct GroupHub : LaneHub<PERM, G * E> {
         ties |= f.any & ~(lt | gt) & eb;
     }
 
+    // The source, its query range, this lane's first destination and its entry of the
+    // source's region row: global loads issued before the workgroup's setup, so that their
+    // latency hides behind the table copy (the kernel calls this first).
+    uint32_t qa = 0, qb = 0, w_first = 0;
+    uint2 sr0 = make_uint2(0, 0);
+    __device__ __forceinline__ void prefetch(uint32_t s_idx) {
+        gj = lane_id() & (G - 1u);
+        gbase = lane_id() & ~(G - 1u);
+        src = a->src_v[s_idx];
+        qa = a->q_begin[s_idx];
+        qb = a->q_begin[s_idx + 1];
+        w_first = qa + gj < qb ? a->q_dst[qa + gj] : 0u;
+        if (gj < a->nreg) sr0 = reinterpret_cast<const uint2 *>(a->near)[(unsigned long long)src * a->nreg + gj];
+    }
+
     // ---- one source per group; every lane of the group calls it with the same source ---
     // returns the records this lane wrote (lane 0 of the group reports the source's)
     __device__ __forceinline__ uint32_t solve(bool have, uint32_t s_idx) {
         const DevParams &p = P;
         const uint32_t NS = p.NS;
-        gj = lane_id() & (G - 1u);
-        gbase = lane_id() & ~(G - 1u);
-        src = a->src_v[s_idx];
         sx = int(src % p.S) - int(p.H);
         sy = int(src / p.S) - int(p.H);
         cell_word(src, sx, sy, ts, src_rk);
         {  // the source's region row, copied into LDS (the list compares read it)
             const uint2 *rg = reinterpret_cast<const uint2 *>(a->near) + (unsigned long long)src * nreg;
-            for (uint32_t r = gj; r < nreg; r += G) SR[r] = rg[r];
+            if (gj < nreg) SR[gj] = sr0;
+            for (uint32_t r = gj + G; r < nreg; r += G) SR[r] = rg[r];
             srow = SR;
         }
-        // this source's query range and this lane's first destination, loaded now so that
-        // their latency hides behind the Dijkstra
-        const uint32_t qa = a->q_begin[s_idx], qb = a->q_begin[s_idx + 1];
-        const uint32_t w_first = qa + gj < qb ? a->q_dst[qa + gj] : 0u;
         const LLab st0 = start();
         {
             const LLab x = inf();
@@ -411,15 +420,18 @@ __global__ __launch_bounds__(kBS) void hub_group_kernel(const KArgs *__restrict_
     constexpr uint32_t TM = G * E;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     GroupHub<PERM, G, E> H;
-    lane_setup<TM>(a, smem, H);
     // group q of wave w: source (64 / G) w + q of the sources [0, n_lane)
     const uint32_t grp = (blockIdx.x * (kBS / 64) + (threadIdx.x >> 6)) * (64u / G) + lane_id() / G;
-    H.LT = reinterpret_cast<uint4 *>(smem + group_off_lt(a->p.NS, a->nreg, TM)) + (threadIdx.x / G) * TM;
-    H.SR = reinterpret_cast<uint2 *>(smem + group_off_sr(a->p.NS, a->nreg, G, E)) + (threadIdx.x / G) * a->nreg;
     const uint32_t n = a->n_lane;
     const bool have = grp < n;
+    const uint32_t s_idx = have ? grp : (n ? n - 1 : 0);
+    H.a = a;
+    H.prefetch(s_idx);
+    lane_setup<TM>(a, smem, H);
+    H.LT = reinterpret_cast<uint4 *>(smem + group_off_lt(a->p.NS, a->nreg, TM)) + (threadIdx.x / G) * TM;
+    H.SR = reinterpret_cast<uint2 *>(smem + group_off_sr(a->p.NS, a->nreg, G, E)) + (threadIdx.x / G) * a->nreg;
     uint32_t written = 0;
-    if (__any(have)) written = H.solve(have, have ? grp : (n ? n - 1 : 0));
+    if (__any(have)) written = H.solve(have, s_idx);
     __shared__ uint32_t wsum;
     if (threadIdx.x == 0) wsum = 0;
     __syncthreads();

@@ -83,7 +83,7 @@ __device__ __host__ __forceinline__ constexpr uint32_t lm_pack(uint32_t len, uin
 constexpr uint32_t kInf1 = ~0u;  // c1 of a label that is not there
 // the specials' cells by hash (kLaneHash slots of {vertex, entry}, linear probing)
 constexpr uint32_t kLaneHash = 64;
-__device__ __forceinline__ uint32_t lane_hash(uint32_t v) { return (v * 0x9E3779B1u) >> 26; }
+__host__ __device__ __forceinline__ uint32_t lane_hash(uint32_t v) { return (v * 0x9E3779B1u) >> 26; }
 
 struct LLab {
     uint32_t c1, c2, c3, m;
@@ -816,9 +816,12 @@ struct LaneHub {
     }
 };
 
-// the lane kernel's LDS: the specials' static records, their region rows, the pair table
-// (TM x TM uint4 + uint2), its row masks (TM words) and per wave the meta copy of the
-// rare paths (TM x 64 words)
+// The lane kernels' LDS.  Its first part is a per-plan block the host builds once
+// (lane_blob, mr_host.cpp) and every workgroup copies in one pass: the specials' static
+// records, their region rows, the pair table (TM x TM uint4 + uint2), its row masks (TM
+// words), the specials' cells by hash (kLaneHash slots) and a header {longest probe
+// sequence, hub mask, cost-5 mask, region mask}.  Then per wave the meta copy of the
+// rare paths (TM x 64 words).
 __host__ __device__ inline uint32_t lane_off_near(uint32_t NS) { return align16h((NS + 1) * uint32_t(sizeof(SpecialStatic))); }
 __host__ __device__ inline uint32_t lane_off_pt(uint32_t NS, uint32_t nreg) {
     return align16h(lane_off_near(NS) + (NS + 1) * nreg * 8u);
@@ -829,102 +832,57 @@ __host__ __device__ inline uint32_t lane_off_pb(uint32_t NS, uint32_t nreg, uint
 __host__ __device__ inline uint32_t lane_off_rm(uint32_t NS, uint32_t nreg, uint32_t TM) {
     return lane_off_pb(NS, nreg, TM) + TM * TM * 8u;
 }
-__host__ __device__ inline uint32_t lane_off_meta(uint32_t NS, uint32_t nreg, uint32_t TM) {
+__host__ __device__ inline uint32_t lane_off_hash(uint32_t NS, uint32_t nreg, uint32_t TM) {
     return align16h(lane_off_rm(NS, nreg, TM) + TM * 4u);
 }
-__host__ __device__ inline uint32_t lane_off_hash(uint32_t NS, uint32_t nreg, uint32_t TM) {
-    return lane_off_meta(NS, nreg, TM) + (kBS / 64) * TM * 64u * 4u;
+__host__ __device__ inline uint32_t lane_off_hdr(uint32_t NS, uint32_t nreg, uint32_t TM) {
+    return lane_off_hash(NS, nreg, TM) + kLaneHash * 8u;
+}
+// the host-built block (a multiple of 16 bytes)
+__host__ __device__ inline uint32_t lane_blob_bytes(uint32_t NS, uint32_t nreg, uint32_t TM) {
+    return lane_off_hdr(NS, nreg, TM) + 16u;
+}
+__host__ __device__ inline uint32_t lane_off_meta(uint32_t NS, uint32_t nreg, uint32_t TM) {
+    return lane_blob_bytes(NS, nreg, TM);
 }
 __host__ __device__ inline uint32_t lane_lds_total(uint32_t NS, uint32_t nreg, uint32_t TM) {
-    return lane_off_hash(NS, nreg, TM) + kLaneHash * 8u + 16u;
+    return lane_off_meta(NS, nreg, TM) + (kBS / 64) * TM * 64u * 4u;
 }
 
-// The lane kernels' workgroup setup: the specials' static records, their region rows,
-// the pair table, its row masks and the specials' hash in LDS, and the solver's fields.
+// The lane kernels' workgroup setup: the plan's block copied into LDS (16 B a thread per
+// step; the same block for every workgroup, so after the first ones it comes from L2),
+// and the solver's fields.
 template <uint32_t TM, class Hub>
 __device__ __forceinline__ void lane_setup(const KArgs *__restrict__ a, char *smem, Hub &H) {
     const uint32_t NS = a->p.NS, nreg = a->nreg;
-    SpecialStatic *spl = reinterpret_cast<SpecialStatic *>(smem);
-    uint2 *nearl = reinterpret_cast<uint2 *>(smem + lane_off_near(NS));
-    uint4 *pa = reinterpret_cast<uint4 *>(smem + lane_off_pt(NS, nreg));
-    uint2 *pb = reinterpret_cast<uint2 *>(smem + lane_off_pb(NS, nreg, TM));
-    uint32_t *rm = reinterpret_cast<uint32_t *>(smem + lane_off_rm(NS, nreg, TM));
-    const uint2 *nearg = reinterpret_cast<const uint2 *>(a->near);
-    const uint32_t rgt = a->p.rgt;
-    for (uint32_t t = threadIdx.x; t <= NS; t += kBS) spl[t] = a->sp[t];
-    for (uint32_t t = threadIdx.x; t < TM; t += kBS) rm[t] = 0;
-    for (uint32_t i = threadIdx.x; i < NS * nreg; i += kBS) {
-        const uint32_t t = 1 + i / nreg, r = i % nreg;
-        nearl[t * nreg + r] = nearg[(unsigned long long)a->sp[t].v * nreg + r];
-    }
-    __syncthreads();
-    // the pair table (LaneHub::from_s), from the LDS copies of the specials and their rows
-    for (uint32_t i = threadIdx.x; i < TM * TM; i += kBS) {
-        const uint32_t s = i / TM, t = i % TM;
-        uint4 A = make_uint4(0, 0, 0, 0);
-        uint2 B = make_uint2(0, 0);
-        if (s >= 1 && s <= NS && t >= 1 && t <= NS) {
-            const SpecialStatic ss = spl[s], st = spl[t];
-            const uint32_t wd = walk_dist(ss.x, ss.y, st.x, st.y);
-            const uint32_t md = uint32_t(abs(ss.x - st.x) + abs(ss.y - st.y));
-            A = make_uint4(wd, 180u * wd, (st.coef5 ? 5u : 2u) * md, rgt * md);
-            if (st.rid != kNone10) {
-                const uint32_t d = nearl[s * nreg + st.rid].x;
-                if (d != kNone32) {
-                    B = make_uint2(d, 180u * d);
-                    if (d != 0) atomicOr(rm + s, 1u << t);
-                }
-            }
-        }
-        pa[i] = A;
-        pb[i] = B;
-    }
-    // the specials' cells by hash: thread 0 inserts them (linear probing) and records the
-    // longest probe sequence, which bounds every lookup
-    if (threadIdx.x == 0) {
-        uint2 *ht = reinterpret_cast<uint2 *>(smem + lane_off_hash(NS, nreg, TM));
-        for (uint32_t h = 0; h < kLaneHash; ++h) ht[h] = make_uint2(kNone32, kNone10);
-        uint32_t probes = 1;
-        for (uint32_t t = 1; t <= NS && t < TM; ++t) {
-            uint32_t h = lane_hash(spl[t].v), k = 1;
-            while (ht[h].x != kNone32) {
-                h = (h + 1u) & (kLaneHash - 1u);
-                ++k;
-            }
-            ht[h] = make_uint2(spl[t].v, t);
-            probes = max(probes, k);
-        }
-        *reinterpret_cast<uint32_t *>(smem + lane_off_hash(NS, nreg, TM) + kLaneHash * 8u) = probes;
+    {
+        const uint4 *blob = a->lane_blob;
+        uint4 *dst = reinterpret_cast<uint4 *>(smem);
+        const uint32_t n16 = lane_blob_bytes(NS, nreg, TM) / 16u;
+        for (uint32_t i = threadIdx.x; i < n16; i += kBS) dst[i] = blob[i];
     }
     __syncthreads();
     H.a = a;
     H.P = a->p;
-    H.spl = spl;
-    H.nearS = nearl;
-    H.PA = pa;
-    H.PB = pb;
-    H.RM = rm;
+    H.spl = reinterpret_cast<const SpecialStatic *>(smem);
+    H.nearS = reinterpret_cast<const uint2 *>(smem + lane_off_near(NS));
+    H.PA = reinterpret_cast<const uint4 *>(smem + lane_off_pt(NS, nreg));
+    H.PB = reinterpret_cast<const uint2 *>(smem + lane_off_pb(NS, nreg, TM));
+    H.RM = reinterpret_cast<const uint32_t *>(smem + lane_off_rm(NS, nreg, TM));
     H.M = reinterpret_cast<uint32_t *>(smem + lane_off_meta(NS, nreg, TM)) + (threadIdx.x >> 6) * (TM * 64u);
     H.HT = reinterpret_cast<const uint2 *>(smem + lane_off_hash(NS, nreg, TM));
-    H.ht_probes = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t *>(smem + lane_off_hash(NS, nreg, TM) +
-                                                                                    kLaneHash * 8u));
+    const uint4 hdr = *reinterpret_cast<const uint4 *>(smem + lane_off_hdr(NS, nreg, TM));
+    H.ht_probes = __builtin_amdgcn_readfirstlane(hdr.x);
+    H.hubm = __builtin_amdgcn_readfirstlane(hdr.y);
+    H.c5m = __builtin_amdgcn_readfirstlane(hdr.z);
+    H.regm = __builtin_amdgcn_readfirstlane(hdr.w);
+    H.validm = __builtin_amdgcn_readfirstlane(((2u << min(NS, TM - 1u)) - 1u) & ~1u);
     H.rank = a->rank;
     H.sinfo = a->sinfo;
     H.rank_inv = a->rank_inv;
     H.cell = a->cell;
     H.counter = a->counter;
     H.nreg = nreg;
-    uint32_t hubm = 0, c5m = 0, regm = 0;
-    for (uint32_t t = 1; t <= NS && t < TM; ++t) {
-        const SpecialStatic st = spl[t];
-        hubm |= (st.flags & kSpHub) ? (1u << t) : 0u;
-        c5m |= st.coef5 ? (1u << t) : 0u;
-        regm |= st.rid != kNone10 ? (1u << t) : 0u;
-    }
-    H.hubm = __builtin_amdgcn_readfirstlane(hubm);
-    H.c5m = __builtin_amdgcn_readfirstlane(c5m);
-    H.regm = __builtin_amdgcn_readfirstlane(regm);
-    H.validm = __builtin_amdgcn_readfirstlane(((2u << min(NS, TM - 1u)) - 1u) & ~1u);
 }
 
 template <uint32_t PERM, uint32_t TM>

@@ -2,6 +2,11 @@
 // for the six comparator permutations; host-side launch helpers called from mr_host.cpp.
 #include "mr_hub_lane.hpp"
 
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
 namespace mr {
 
 // the kernel of each comparator permutation, per table size: 22 here, 24 and 32 in
@@ -40,6 +45,59 @@ static const void *lane_fn(const uint32_t perm[3], uint32_t NS) {
         case 32: return lane_fn_tm<32>(k);
         default: return nullptr;
     }
+}
+
+// The lane and group kernels' per-plan LDS block for a table of TM entries (layout:
+// lane_off_* in mr_hub_lane.hpp): the specials' records, their rows of the grid's region
+// table, the pair table of walks / caravans / SoE-region candidates and its row masks
+// (LaneHub::from_s), the specials' cells by hash, and the header words.  near_tab is the
+// grid's region table ({distance, rank} per vertex and region).  Returns the byte size.
+uint32_t lane_blob_build(const SpecialStatic *sp, uint32_t NS, uint32_t nreg, uint32_t TM, uint32_t rgt,
+                         const uint32_t *near_tab, std::vector<uint32_t> &blob) {
+    const uint32_t bytes = lane_blob_bytes(NS, nreg, TM);
+    blob.assign(bytes / 4, 0u);
+    char *base = reinterpret_cast<char *>(blob.data());
+    std::memcpy(base, sp, (NS + 1) * sizeof(SpecialStatic));
+    uint2 *nearl = reinterpret_cast<uint2 *>(base + lane_off_near(NS));
+    for (uint32_t t = 1; t <= NS; ++t)
+        for (uint32_t r = 0; r < nreg; ++r) {
+            const uint32_t *e = near_tab + 2ull * ((unsigned long long)sp[t].v * nreg + r);
+            nearl[t * nreg + r] = make_uint2(e[0], e[1]);
+        }
+    uint4 *pa = reinterpret_cast<uint4 *>(base + lane_off_pt(NS, nreg));
+    uint2 *pb = reinterpret_cast<uint2 *>(base + lane_off_pb(NS, nreg, TM));
+    uint32_t *rm = reinterpret_cast<uint32_t *>(base + lane_off_rm(NS, nreg, TM));
+    for (uint32_t s = 1; s <= NS && s < TM; ++s)
+        for (uint32_t t = 1; t <= NS && t < TM; ++t) {
+            const SpecialStatic &ss = sp[s], &st = sp[t];
+            const uint32_t wd = walk_dist(ss.x, ss.y, st.x, st.y);
+            const uint32_t md = uint32_t(std::abs(ss.x - st.x) + std::abs(ss.y - st.y));
+            pa[s * TM + t] = make_uint4(wd, 180u * wd, (st.coef5 ? 5u : 2u) * md, rgt * md);
+            if (st.rid != kNone10) {
+                const uint32_t d = nearl[s * nreg + st.rid].x;
+                if (d != kNone32) {
+                    pb[s * TM + t] = make_uint2(d, 180u * d);
+                    if (d != 0) rm[s] |= 1u << t;
+                }
+            }
+        }
+    uint2 *ht = reinterpret_cast<uint2 *>(base + lane_off_hash(NS, nreg, TM));
+    for (uint32_t h = 0; h < kLaneHash; ++h) ht[h] = make_uint2(kNone32, kNone10);
+    uint32_t probes = 1, hubm = 0, c5m = 0, regm = 0;
+    for (uint32_t t = 1; t <= NS && t < TM; ++t) {
+        uint32_t h = lane_hash(sp[t].v), k = 1;
+        while (ht[h].x != kNone32) {
+            h = (h + 1u) & (kLaneHash - 1u);
+            ++k;
+        }
+        ht[h] = make_uint2(sp[t].v, t);
+        probes = std::max(probes, k);
+        hubm |= (sp[t].flags & kSpHub) ? (1u << t) : 0u;
+        c5m |= sp[t].coef5 ? (1u << t) : 0u;
+        regm |= sp[t].rid != kNone10 ? (1u << t) : 0u;
+    }
+    *reinterpret_cast<uint4 *>(base + lane_off_hdr(NS, nreg, TM)) = make_uint4(probes, hubm, c5m, regm);
+    return bytes;
 }
 
 uint32_t hub_lane_lds_bytes(uint32_t NS, uint32_t nreg) {
