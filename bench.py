@@ -206,6 +206,8 @@ def algorithmic_bytes(plan, stats, V):
     b += stats["fallback_sources"] * V * BYTES_PER_VERTEX_SOLVE
     if stats["solver"] == "hub_wide":
         kern = "hub_wide_kernel"
+    elif stats.get("lanes_per_source", 0) > 1:  # one source per group of 8 / 16 / 32 lanes
+        kern = "hub_group_kernel"
     elif stats.get("lane_sources", 0) == 0:
         kern = "hub_kernel"
     else:  # one source per lane; sources with many queries stay on hub_kernel
@@ -571,7 +573,8 @@ def main():
                               "kernel_ms spans the fill's two launches; pass_ms is the caller-stream span of a pass (the specials' "
                               "solve runs beside the previous pass's fill, DESIGN.md 3b)" if all_dst else
                               "hub solver: instruction-issue bound Dijkstra over the specials (one source per lane: "
-                              "hub_lane_kernel; per wave: hub_kernel; see roofline.issue); bytes = "
+                              "hub_lane_kernel; per group of lanes: hub_group_kernel; per wave: hub_kernel; see "
+                              "roofline.issue); bytes = "
                               "queries in, results and command slots out, per-source region rows, plus V*20 B "
                               "per SSSP fallback source (DESIGN.md section 4)")
                      if stats["solver"] in ("hub", "hub_wide") else

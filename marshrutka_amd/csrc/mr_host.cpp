@@ -1667,13 +1667,17 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     // layout it does not hold) run one source per group of G lanes when the table fits 32
     // entries: a source's Dijkstra is then ~G times shorter in wave instructions, which
     // is what a small plan's pass time is (hub_group_kernel).  MR_HUB_GROUP=0: never,
-    // =8 / =16: the group size (default 8); MR_HUB_GROUP_FORCE=1: even where the lane
+    // =8 / =16 / =32: the group size; MR_HUB_GROUP_FORCE=1: even where the lane
     // kernel applies.  The certificate's table export is hub_kernel's, so
     // MR_HUB_FALLBACK_ALL keeps hub_kernel.
     const char *hg = std::getenv("MR_HUB_GROUP");
     const uint32_t hgv = hg ? uint32_t(std::strtoul(hg, nullptr, 10)) : 8u;
     const bool group_off = hg && hgv == 0, group_force = std::getenv("MR_HUB_GROUP_FORCE") != nullptr;
-    const uint32_t group_g = hgv == 16 ? 16u : (hgv == 32 ? 32u : 8u);
+    // default size: 16 lanes (c2: 46 us a pass against 60 with 8 and 51 with 32), 32 for
+    // plans of at most 1024 sources (a lone source: 29 us against 31), whose waves leave
+    // most SIMDs empty
+    const uint32_t group_g = hg ? (hgv == 16 ? 16u : (hgv == 32 ? 32u : 8u))
+                                : (hp.src_v.size() <= 1024 ? 32u : 16u);
     const bool lane_ok = hp.hub && !hp.wide && !hp.nonlin && !all_mode && hp.near && lane_bounds_ok(hp.p);
     if (lane_ok && !group_force && !lane_off && hub_lane_entries(hp.p.NS) != 0 && lane_layout_ok(hp) &&
         (lane_force || lane_sources(hp) >= lane_min_sources()))
@@ -2787,6 +2791,12 @@ extern "C" void mr_plan_destroy(mr_plan *pl) {
                              "MR_STAMPS hub (sum over waves): sources=%llu iterations=%llu boundaries=%llu cycles: "
                              "init=%llu select=%llu edges=%llu boundary=%llu emit=%llu dequeue=%llu\n",
                              h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]);
+            if (pl->lane_g && h[9])
+                std::fprintf(stderr,
+                             "MR_STAMPS group (per wave, %llu waves, last pass): setup=%.0f own_edges=%.0f scan_min=%.0f "
+                             "settle=%.0f relax=%.0f readoff=%.0f\n",
+                             h[9], double(h[10]) / h[9], double(h[11]) / h[9], double(h[12]) / h[9], double(h[13]) / h[9],
+                             double(h[14]) / h[9], double(h[15]) / h[9]);
         }
     }
 #endif

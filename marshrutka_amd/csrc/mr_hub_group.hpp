@@ -102,8 +102,26 @@ __device__ __forceinline__ uint32_t bitv(uint32_t w, uint32_t e) {
     return r;
 }
 
+// diagnostic builds (-DMR_STAMPS): phase cycles per wave (s_memtime), summed into
+// a->dbg[dbg_blocks * 10 + 9 ..] by each wave's lane 0 (mr_plan_destroy prints them)
+#ifdef MR_STAMPS
+#define MR_GSTAMP(i)                                                        \
+    do {                                                                    \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();       \
+        gst[i] += now_ - gst_last;                                          \
+        gst_last = now_;                                                    \
+    } while (0)
+#else
+#define MR_GSTAMP(i) \
+    do {             \
+    } while (0)
+#endif
+
 template <uint32_t PERM, uint32_t G, uint32_t E>
 struct GroupHub : LaneHub<PERM, G * E> {
+#ifdef MR_STAMPS
+    unsigned long long gst[6] = {0, 0, 0, 0, 0, 0}, gst_last = 0;
+#endif
     static constexpr uint32_t TM = G * E;  // table entries (slot i of lane j: entry i * G + j)
     using Base = LaneHub<PERM, TM>;
     using Base::a;
@@ -213,6 +231,7 @@ struct GroupHub : LaneHub<PERM, G * E> {
     __device__ __forceinline__ uint32_t solve(bool have, uint32_t s_idx) {
         const DevParams &p = P;
         const uint32_t NS = p.NS;
+        MR_GSTAMP(0);  // (0: kernel start to here: the prefetch and the table copy)
         sx = int(src % p.S) - int(p.H);
         sy = int(src / p.S) - int(p.H);
         cell_word(src, sx, sy, ts, src_rk);
@@ -270,6 +289,7 @@ struct GroupHub : LaneHub<PERM, G * E> {
         }
         // ---- Dijkstra over the specials, one settle per group per iteration -----------
         uint32_t *mcol = M + lane_id();  // this lane's column of the meta copy
+        MR_GSTAMP(1);  // (1: the source's own edges)
         const uint32_t n_it = (a->dbg_flags & kDbgGroupNoSolve) ? 0u : NS;  // (timing experiments)
         for (uint32_t it = 0; it < n_it; ++it) {
             const uint32_t cand = tent & ~done;  // (this lane's entries only)
@@ -290,6 +310,7 @@ struct GroupHub : LaneHub<PERM, G * E> {
             uint32_t k = (lx.m << 24) | sl;
             group_min<G>(z.ls.c1, z.ls.c2, z.ls.c3, z.ls.m, k);
             const uint32_t s = k & 0xFFu;
+            MR_GSTAMP(2);  // (2: scan and group minimum)
             // the pair-table words of s into this lane's slots, read before the settle's
             // bookkeeping so that their latency overlaps it
             uint4 pa_[E];
@@ -309,6 +330,7 @@ struct GroupHub : LaneHub<PERM, G * E> {
                 mcol[s * 64u] = z.ls.m;
                 if (gj == 0) LT[s] = make_uint4(z.ls.c1, z.ls.c2, z.ls.c3, z.ls.m);
             }
+            MR_GSTAMP(3);  // (3: the settle's bookkeeping and its LDS reads)
             // relaxations into this lane's slots
             uint32_t ties = 0, fcm[E];
 #pragma unroll
@@ -327,7 +349,9 @@ struct GroupHub : LaneHub<PERM, G * E> {
                         Ls[i].m = fcm[i];
                 }
             }
+            MR_GSTAMP(4);
         }
+        MR_GSTAMP(4);  // (4: relaxations and their ties, from the last stamp of each iteration)
         if (!have) return 0;
         // ---- certification: with blockers, every settled walk label must be certain ----
         bool unc = false;
@@ -400,6 +424,7 @@ struct GroupHub : LaneHub<PERM, G * E> {
         }
         const bool fallback = fb_sp || group_any(uncd);
         if (fallback && gj == 0) push_fallback(a, counter, s_idx, kNone32);
+        MR_GSTAMP(5);  // (5: certification and the destinations)
         return (fallback || gj != 0) ? 0u : qb - qa;
     }
 };
@@ -426,12 +451,22 @@ __global__ __launch_bounds__(kBS) void hub_group_kernel(const KArgs *__restrict_
     const bool have = grp < n;
     const uint32_t s_idx = have ? grp : (n ? n - 1 : 0);
     H.a = a;
+#ifdef MR_STAMPS
+    H.gst_last = __builtin_amdgcn_s_memtime();
+#endif
     H.prefetch(s_idx);
     lane_setup<TM>(a, smem, H);
     H.LT = reinterpret_cast<uint4 *>(smem + group_off_lt(a->p.NS, a->nreg, TM)) + (threadIdx.x / G) * TM;
     H.SR = reinterpret_cast<uint2 *>(smem + group_off_sr(a->p.NS, a->nreg, G, E)) + (threadIdx.x / G) * a->nreg;
     uint32_t written = 0;
     if (__any(have)) written = H.solve(have, s_idx);
+#ifdef MR_STAMPS
+    if (a->dbg && lane_id() == 0) {
+        unsigned long long *h = a->dbg + (unsigned long long)a->dbg_blocks * 10 + 9;
+        atomicAdd(h, 1ull);
+        for (int i = 0; i < 6; ++i) atomicAdd(h + 1 + i, H.gst[i]);
+    }
+#endif
     __shared__ uint32_t wsum;
     if (threadIdx.x == 0) wsum = 0;
     __syncthreads();

@@ -29,7 +29,7 @@ def grid_state(request, monkeypatch):
     """Every solver path x both grid-state regimes:
     auto     — hub solver when the run time is linear (one source per lane when the
                table fits 22 entries, a source has <= 32 queries and the plan has
-               enough such sources to fill the GPU, else one source per 8 lanes when
+               enough such sources to fill the GPU, else one source per 16 or 32 lanes when
                the table fits 32 entries, else two sources per wave when the specials
                fit 32 lanes), else the SSSP solvers
     group    — auto with one source per group of 8 lanes (hub_group_kernel) wherever it
@@ -65,8 +65,7 @@ def grid_state(request, monkeypatch):
     monkeypatch.delenv("MR_HUB_GROUP_FORCE", raising=False)
     if algo in ("group", "group16", "group32"):
         monkeypatch.setenv("MR_HUB_GROUP_FORCE", "1")
-        if algo != "group":
-            monkeypatch.setenv("MR_HUB_GROUP", algo[5:])
+        monkeypatch.setenv("MR_HUB_GROUP", algo[5:] or "8")
     if algo == "lanetab":
         monkeypatch.setenv("MR_RANK_TABLE", "1")
         algo = "lane"
@@ -259,8 +258,8 @@ def test_lane_kernel_selection(eng, oracle_lib, monkeypatch):
     to fill the GPU (MR_HUB_LANE_MIN, default half a wave per SIMD), always with
     MR_HUB_LANE=1, never with MR_HUB_LANE=0; the table layout it needs (region
     campfires in entries 6..11) comes from the host's special order.  A plan the lane
-    kernel does not take runs one source per 8 lanes (hub_group_kernel) unless
-    MR_HUB_GROUP=0.  Results are the oracle's either way."""
+    kernel does not take runs one source per group of lanes (hub_group_kernel: 32 for
+    plans of at most 1024 sources, else 16) unless MR_HUB_GROUP=0.  Results are the oracle's either way."""
     m = SyntheticMap(33, campfires_per_homeland=4, seed=5)
     qs = random_queries(m, 400, 6)
     g = eng.MapGrid(m.cells())
@@ -279,7 +278,7 @@ def test_lane_kernel_selection(eng, oracle_lib, monkeypatch):
     n_src = len({a for a, _ in qs})
     assert lanes["default"] == 0 and lanes["off"] == 0, lanes  # 400 sources < half a wave per SIMD
     assert lanes["force"] == n_src and lanes["min1"] == n_src, lanes
-    assert per == {"default": 8, "force": 1, "off": 8, "min1": 1, "nogroup": 0, "g16": 16}, per
+    assert per == {"default": 32, "force": 1, "off": 32, "min1": 1, "nogroup": 0, "g16": 16}, per
 
 
 @pytest.mark.parametrize("k,hq,tm", [(4, True, 24), (5, False, 32), (6, True, 32)])

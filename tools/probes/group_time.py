@@ -24,3 +24,4 @@ ms, n = pl.kernel_ms()
 st = pl.stats()
 print(f"S={size} q={nq} flags={os.environ.get('MR_DBG_FLAGS', '0')} group={os.environ.get('MR_HUB_GROUP', '8')} "
       f"lanes/src={st['lanes_per_source']} sources={st['num_sources']} kernel {ms * 1000:.1f} us ({n} passes)", flush=True)
+del pl  # (MR_STAMPS builds print their phase cycles when the plan is destroyed)

@@ -23,7 +23,7 @@ for W in $WLS; do
   K=""; [ $W = c3 ] && K="--kernels hub_fill_kernel"  # c3 prices the fill (bench.py roofline.kernel)
   python3 "$R/tools/pmc_summary.py" $K --workload $W --queries $(qpg $W) --fetch $O/pmc_FETCH_SIZE_$W --write $O/pmc_WRITE_SIZE_$W --out $O/pmc_$W.json > /dev/null || exit 1
   echo "$W pmc ok"
-  K2=hub_kernel; [ $W = c4 ] && K2=hub_lane_kernel; [ $W = c3 ] && K2=hub_fill_kernel; [ $W = c5 ] && K2=hub_wide_kernel
+  K2=hub_kernel; [ $W = c4 ] && K2=hub_lane_kernel; [ $W = c2 ] && K2=hub_group_kernel; [ $W = c3 ] && K2=hub_fill_kernel; [ $W = c5 ] && K2=hub_wide_kernel
   bash "$R/tools/gpu_sq.sh" $W $O/sq_$W && python3 "$R/tools/sq_summary.py" --workload $W --kernel $K2 --sq $O/sq_$W --queries $(qpg $W) --out $O/sq_$W.json > /dev/null || exit 1
   echo "$W sq ok"
 done
