@@ -2794,9 +2794,9 @@ extern "C" void mr_plan_destroy(mr_plan *pl) {
             if (pl->lane_g && h[9])
                 std::fprintf(stderr,
                              "MR_STAMPS group (per wave, %llu waves, last pass): setup=%.0f own_edges=%.0f scan_min=%.0f "
-                             "settle=%.0f relax=%.0f readoff=%.0f\n",
+                             "settle=%.0f relax=%.0f cmds_cert=%.0f destinations=%.0f\n",
                              h[9], double(h[10]) / h[9], double(h[11]) / h[9], double(h[12]) / h[9], double(h[13]) / h[9],
-                             double(h[14]) / h[9], double(h[15]) / h[9]);
+                             double(h[14]) / h[9], double(h[7]) / h[9], double(h[15]) / h[9]);
         }
     }
 #endif

@@ -120,7 +120,7 @@ __device__ __forceinline__ uint32_t bitv(uint32_t w, uint32_t e) {
 template <uint32_t PERM, uint32_t G, uint32_t E>
 struct GroupHub : LaneHub<PERM, G * E> {
 #ifdef MR_STAMPS
-    unsigned long long gst[6] = {0, 0, 0, 0, 0, 0}, gst_last = 0;
+    unsigned long long gst[8] = {0, 0, 0, 0, 0, 0, 0, 0}, gst_last = 0;
 #endif
     static constexpr uint32_t TM = G * E;  // table entries (slot i of lane j: entry i * G + j)
     using Base = LaneHub<PERM, TM>;
@@ -165,15 +165,65 @@ struct GroupHub : LaneHub<PERM, G * E> {
     using FromS = typename Base::FromS;
 
     LLab Ls[E];      // labels of this lane's slots
+    int ex[E], ey[E];  // their cells (the read-off's walks)
+    uint32_t *W = nullptr;  // LDS: this group's destinations of the current batch (G words)
     uint32_t gj = 0, gbase = 0;
     uint4 *LT = nullptr;  // LDS: this group's settled labels, entry e at LT[e]
     uint2 *SR = nullptr;  // LDS: this group's copy of the source's region row (nreg entries)
+    // LDS: per settled entry e of this group its meta word and tail commands,
+    // CT[2e] = {meta, cmd0}, CT[2e + 1] = {cmd1 (a SoE after a walk), -}: written once after
+    // the Dijkstra (every lane its own entries), read by the emission's chain walk
+    uint4 *CT = nullptr;
+
+    // a label's record and commands: the last command wc when `last` (a destination's
+    // walk, or the start label's NoMove), then the tail commands of entry e and of its
+    // parents up to the source (LaneHub::emit with the commands precomputed in CT)
+    __device__ __forceinline__ void emit_ct(const LLab &x, uint32_t e, bool last, const Cmd &wc, uint32_t qi) const {
+        const DevParams &p = P;
+        OutResult &o = a->out_res[qi];
+        OutCmd *oc = a->out_cmd + (unsigned long long)qi * p.max_cmds;
+        const uint32_t len = lm_len(x.m);
+        const uint32_t legs = Base::metric(x, 0), money = Base::metric(x, 1), time = Base::metric(x, 2);
+        uint32_t status = 16;
+        if (len > p.max_cmds) {  // the overflow pool, else MR_ERR_CAPACITY
+            const uint32_t off = atomicAdd(counter + kCtrOvf, len);
+            if (p.max_cmds == 0 || off + len > a->ovf_cap || off + len < off) {
+                o = OutResult{legs, money, time, (uint32_t(16 - 4) << 16) | (len & 0xFFFFu)};
+                return;
+            }
+            oc[0] = OutCmd{kOvfTag, off, len, 0};
+            oc = a->ovf + off;
+            status = 16 + kStatusOverflow;
+        }
+        int at = int(len) - 1;
+        if (last && at >= 0) oc[at--] = OutCmd{wc.kp, wc.from, wc.to, 0};
+        for (uint32_t guard = 0; e != 0 && at >= 0 && guard <= TM; ++guard) {
+            const uint4 h = CT[2 * e];
+            if (lm_nt(h.x) == 2) {
+                const uint4 t2 = CT[2 * e + 1];
+                oc[at--] = OutCmd{t2.x, t2.y, t2.z, 0};
+            }
+            if (at >= 0) oc[at--] = OutCmd{h.y, h.z, h.w, 0};
+            e = lm_par(h.x);
+        }
+        if (at != -1 || e != 0) atomicOr(counter + kCtrFlags, kErrChain);
+        o = OutResult{legs, money, time, (status << 16) | (len & 0xFFFFu)};
+    }
 
     __device__ __forceinline__ uint32_t ent(uint32_t i) const { return i * G + gj; }
     // some lane of this lane's group has f
     __device__ __forceinline__ bool group_any(bool f) const {
         const unsigned long long b = __ballot(f);
         return ((b >> gbase) & ((1ull << G) - 1ull)) != 0;
+    }
+    // the group's flags as entry bits of slot i (bit i * G + j: lane j's flag)
+    __device__ __forceinline__ uint32_t group_bits(bool f, uint32_t i) const {
+        const unsigned long long b = __ballot(f);
+        return uint32_t((b >> gbase) & ((1ull << G) - 1ull)) << (i * G);
+    }
+    // x and y agree on (c1, c2, c3, length)
+    __device__ __forceinline__ static bool eq4(const LLab &x, const LLab &y) {
+        return ((x.c1 ^ y.c1) | (x.c2 ^ y.c2) | (x.c3 ^ y.c3) | ((x.m ^ y.m) & 0xFFu)) == 0;
     }
     __device__ __forceinline__ LLab lt_get(uint32_t e) const {
         const uint4 v = LT[e];
@@ -254,6 +304,8 @@ struct GroupHub : LaneHub<PERM, G * E> {
             const uint32_t e = ent(i);
             const bool valid = have && e >= 1 && e <= NS;
             const SpecialStatic tS = spl[valid ? e : 1u];
+            ex[i] = e == 0 ? sx : tS.x;
+            ey[i] = e == 0 ? sy : tS.y;
             const uint32_t m0 = vmask(valid && e == ts);
             LLab c = opt(m0, st0);
             uint32_t any = m0;
@@ -353,6 +405,19 @@ struct GroupHub : LaneHub<PERM, G * E> {
         }
         MR_GSTAMP(4);  // (4: relaxations and their ties, from the last stamp of each iteration)
         if (!have) return 0;
+        // ---- the settled entries' tail commands, every lane its own (emit_ct) ------------
+#pragma unroll
+        for (uint32_t i = 0; i < E; ++i) {
+            const uint32_t e = ent(i);
+            if (e >= 1 && e <= NS && ((done >> e) & 1u)) {
+                const uint32_t m = Ls[i].m;
+                const Own o = own_of(e);
+                const Cmd c0 = Base::tail(m, o, 0);
+                const Cmd c1 = lm_nt(m) == 2 ? Base::tail(m, o, 1) : Cmd{0, 0, 0};
+                CT[2 * e] = make_uint4(m, c0.kp, c0.from, c0.to);
+                CT[2 * e + 1] = make_uint4(c1.kp, c1.from, c1.to, 0u);
+            }
+        }
         // ---- certification: with blockers, every settled walk label must be certain ----
         bool unc = false;
         if (blk != 0) {
@@ -363,63 +428,99 @@ struct GroupHub : LaneHub<PERM, G * E> {
             }
         }
         const bool fb_sp = group_any(unc) || a->fb_all || (a->dbg_flags & kDbgGroupNoReadoff);
-        // ---- destinations, one query per lane: the source, a special, or the best walk ---
+        MR_GSTAMP(6);  // (6: the tail commands and the certification of settled labels)
+        // ---- destinations: each query by the whole group, its record by one lane --------
+        // A plain destination's label is the best walk from a boundary (the source's walk
+        // included): every lane prices the walks from its own slots, the group minimum
+        // picks the boundary (exact ties: the lists decide, below); queries go G at a time,
+        // query j's label kept by lane j, then every lane emits its own.
         const bool walk0 = src != p.vc;
         bool uncd = false;
-        for (uint32_t qi = fb_sp ? qb : qa + gj; qi < qb; qi += G) {
-            const uint32_t w = qi == qa + gj ? w_first : a->q_dst[qi];
-            const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
-            uint32_t tw, wr;
-            cell_word(w, wx, wy, tw, wr);
-            if (w == src) {
-                emit(st0, kOwn, Own{sx, sy, src_rk, kNone10, 0u}, qi);
-                continue;
-            }
-            if (tw != kNone10) {
-                emit(lt_get(tw), tw, own_of(tw), qi);
-                continue;
-            }
-            const Own wo{wx, wy, wr, kNone10, 0u};
-            // candidates compared on the boundary's own meta (length - 1; the source's walk: 0)
-            LLab x = inf();
-            uint32_t bx = walk0 ? 0u : kNone32;
-            uint32_t tie = 0;
-            {
-                const uint32_t kk = walk_dist(sx, sy, wx, wy);
-                ll_sel(vmask(walk0), x, mk(kk, 0, 180u * kk, 0u));
-            }
-            for (uint32_t mm = bndm; mm; mm &= mm - 1u) {
-                const uint32_t t = uint32_t(__builtin_ctz(mm));
-                const uint32_t kk = walk_dist(spl[t].x, spl[t].y, wx, wy);
-                const LLab lb = lt_get(t);
-                const LLab c = add(lb, kk, 0, 180u * kk, lb.m);
-                const uint32_t gt = ltm(x, c);
-                const uint32_t lt = ltm_take_idx(c, x, t, bx);
-                tie = ~lt & (tie | ~gt);
-            }
-            if (bx == kNone32) {  // no boundary can walk here: cannot happen on a connected grid
-                a->out_res[qi] = OutResult{0, 0, 0, uint32_t(16 + 1) << 16};
-                continue;
-            }
-            x.m = lm_pack(lm_len(x.m) + 1u, bx, 1, kStandard);
-            if (tie) {  // equal metrics and length from several boundaries: the lists decide
-                for (uint32_t mm = (bndm | (walk0 ? 1u : 0u)) & ~(1u << bx); mm; mm &= mm - 1u) {
-                    const uint32_t b = uint32_t(__builtin_ctz(mm));
-                    int px, py;
-                    pos(b, px, py);
-                    const uint32_t kk = walk_dist(px, py, wx, wy);
-                    const LLab c = b == 0 ? mk(kk, 0, 180u * kk, lm_pack(1, 0, 1, kStandard)) : walk_to(lt_get(b), b, kk);
-                    if (cmp4(c, x) == 0 && cmp_list(c.m, kOwn, wo, x.m, kOwn, wo) < 0) {
-                        x = c;
-                        bx = b;
+        const uint32_t nq = fb_sp ? 0u : qb - qa;
+        for (uint32_t j0 = 0; j0 < nq; j0 += G) {
+            W[gj] = j0 == 0 ? w_first : (j0 + gj < nq ? a->q_dst[qa + j0 + gj] : 0u);
+            const uint32_t nb = min(G, nq - j0);
+            uint32_t rk_ = 0, rw = 0, rbx = 0, rtie = 0;  // this lane's record: kind, destination, boundary, tie
+            LLab rx = inf();
+            for (uint32_t j = 0; j < nb; ++j) {
+                const uint32_t w = W[j];
+                const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
+                uint32_t tw, wr;
+                cell_word(w, wx, wy, tw, wr);
+                uint32_t kind = 3, bx = 0, tie = 0;
+                LLab x = inf();
+                if (w == src) {
+                    kind = 1;
+                } else if (tw != kNone10) {
+                    kind = 2;
+                    bx = tw;
+                } else {
+                    // candidates compared on the boundary's own meta (length - 1; the source's walk: 0)
+                    LLab lx = inf(), cs[E];
+                    uint32_t sl = 0;
+#pragma unroll
+                    for (uint32_t i = 0; i < E; ++i) {
+                        const uint32_t e = ent(i);
+                        const bool on = e == 0 ? walk0 : ((bndm >> e) & 1u) != 0;
+                        const uint32_t kk = walk_dist(ex[i], ey[i], wx, wy);
+                        const LLab b0 = e == 0 ? LLab{0u, 0u, 0u, 0u} : Ls[i];
+                        cs[i] = opt(vmask(on), add(b0, kk, 0, 180u * kk, b0.m));
+                        ltm_take_i(cs[i], lx, e, sl);
                     }
+                    x = lx;
+                    uint32_t k = (lx.m << 24) | sl;
+                    group_min<G>(x.c1, x.c2, x.c3, x.m, k);
+                    bx = k & 0xFFu;
+                    // the other boundaries with the winner's metrics and length (entry bits)
+#pragma unroll
+                    for (uint32_t i = 0; i < E; ++i)
+                        tie |= group_bits(ent(i) != bx && cs[i].c1 != kInf1 && eq4(cs[i], x), i);
+                    if (x.c1 == kInf1) kind = 0;  // no boundary can walk here: cannot happen on a connected grid
+                }
+                if (j == gj) {
+                    rk_ = kind;
+                    rw = w;
+                    rbx = bx;
+                    rtie = tie;
+                    rx = x;
                 }
             }
-            emit(x, kOwn, wo, qi);
-            if (blk != 0) {
-                int px, py;
-                pos(bx, px, py);
-                if (!avail(bx, px, py, wx, wy)) uncd = true;
+            // every lane its own query's record and commands
+            const uint32_t qi = qa + j0 + gj;
+            if (gj < nb) {
+                const uint32_t w = rw;
+                const int wx = int(w % p.S) - int(p.H), wy = int(w / p.S) - int(p.H);
+                if (rk_ == 1) {  // the start label: [NoMove src]
+                    emit_ct(st0, 0u, true, Cmd{kNoMove << 29, src_rk, src_rk}, qi);
+                } else if (rk_ == 2) {
+                    emit_ct(lt_get(rbx), rbx, false, Cmd{0, 0, 0}, qi);
+                } else if (rk_ == 0) {
+                    a->out_res[qi] = OutResult{0, 0, 0, uint32_t(16 + 1) << 16};
+                } else {
+                    uint32_t tw, wr;
+                    cell_word(w, wx, wy, tw, wr);
+                    const Own wo{wx, wy, wr, kNone10, 0u};
+                    LLab x = rx;
+                    uint32_t bx = rbx;
+                    x.m = lm_pack(lm_len(x.m) + 1u, bx, 1, kStandard);
+                    if (rtie && !(a->dbg_flags & kDbgGroupNoTies)) {  // equal metrics and length: the lists decide
+                        for (uint32_t mm = rtie; mm; mm &= mm - 1u) {
+                            const uint32_t b = uint32_t(__builtin_ctz(mm));
+                            int px, py;
+                            pos(b, px, py);
+                            const uint32_t kk = walk_dist(px, py, wx, wy);
+                            const LLab c = b == 0 ? mk(kk, 0, 180u * kk, lm_pack(1, 0, 1, kStandard)) : walk_to(lt_get(b), b, kk);
+                            if (cmp4(c, x) == 0 && cmp_list(c.m, kOwn, wo, x.m, kOwn, wo) < 0) {
+                                x = c;
+                                bx = b;
+                            }
+                        }
+                    }
+                    int px, py;
+                    pos(bx, px, py);
+                    emit_ct(x, bx, true, Cmd{(kStandard << 29) | walk_dist(px, py, wx, wy), Base::rk(bx), wr}, qi);
+                    if (blk != 0 && !avail(bx, px, py, wx, wy)) uncd = true;
+                }
             }
         }
         const bool fallback = fb_sp || group_any(uncd);
@@ -436,8 +537,14 @@ __host__ __device__ inline uint32_t group_off_lt(uint32_t NS, uint32_t nreg, uin
 __host__ __device__ inline uint32_t group_off_sr(uint32_t NS, uint32_t nreg, uint32_t G, uint32_t E) {
     return group_off_lt(NS, nreg, G * E) + (kBS / G) * G * E * 16u;
 }
+__host__ __device__ inline uint32_t group_off_ct(uint32_t NS, uint32_t nreg, uint32_t G, uint32_t E) {
+    return align16h(group_off_sr(NS, nreg, G, E) + (kBS / G) * nreg * 8u);
+}
+__host__ __device__ inline uint32_t group_off_w(uint32_t NS, uint32_t nreg, uint32_t G, uint32_t E) {
+    return group_off_ct(NS, nreg, G, E) + (kBS / G) * G * E * 32u;
+}
 __host__ __device__ inline uint32_t group_lds_total(uint32_t NS, uint32_t nreg, uint32_t G, uint32_t E) {
-    return group_off_sr(NS, nreg, G, E) + (kBS / G) * nreg * 8u;
+    return group_off_w(NS, nreg, G, E) + kBS * 4u;
 }
 
 template <uint32_t PERM, uint32_t G, uint32_t E>
@@ -458,6 +565,8 @@ __global__ __launch_bounds__(kBS) void hub_group_kernel(const KArgs *__restrict_
     lane_setup<TM>(a, smem, H);
     H.LT = reinterpret_cast<uint4 *>(smem + group_off_lt(a->p.NS, a->nreg, TM)) + (threadIdx.x / G) * TM;
     H.SR = reinterpret_cast<uint2 *>(smem + group_off_sr(a->p.NS, a->nreg, G, E)) + (threadIdx.x / G) * a->nreg;
+    H.CT = reinterpret_cast<uint4 *>(smem + group_off_ct(a->p.NS, a->nreg, G, E)) + (threadIdx.x / G) * (2 * TM);
+    H.W = reinterpret_cast<uint32_t *>(smem + group_off_w(a->p.NS, a->nreg, G, E)) + (threadIdx.x / G) * G;
     uint32_t written = 0;
     if (__any(have)) written = H.solve(have, s_idx);
 #ifdef MR_STAMPS
@@ -465,6 +574,8 @@ __global__ __launch_bounds__(kBS) void hub_group_kernel(const KArgs *__restrict_
         unsigned long long *h = a->dbg + (unsigned long long)a->dbg_blocks * 10 + 9;
         atomicAdd(h, 1ull);
         for (int i = 0; i < 6; ++i) atomicAdd(h + 1 + i, H.gst[i]);
+        atomicAdd(h - 2, H.gst[6]);  // (the hub words h[7], h[8]: unused by this kernel)
+        atomicAdd(h - 1, H.gst[7]);
     }
 #endif
     __shared__ uint32_t wsum;
