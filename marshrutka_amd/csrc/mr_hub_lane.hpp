@@ -763,7 +763,7 @@ struct LaneHub {
             const uint32_t bq = vvolatile(bndm);
             LLab x = inf();
             uint32_t bx = walk0 ? 0u : kNone32;
-            uint32_t tie = 0;
+            uint32_t tie = 0;  // the boundaries whose walk ties the best so far exactly (entry bits)
             {
                 const uint32_t k = walk_dist(sx, sy, wx, wy);
                 ll_sel(vmask(walk0), x, mk(k, 0, 180u * k, 0u));
@@ -775,19 +775,22 @@ struct LaneHub {
                 const LLab c = opt(cm, add(L[t], k, 0, 180u * k, L[t].m));
 #ifdef MR_LANE_CLASSIC
                 const uint32_t lt = ltm(c, x), gt = ltm(x, c);
-                tie = ~lt & (tie | (cm & ~gt));
+                tie = ~lt & (tie | (cm & ~gt & (1u << t)));
                 ll_sel(lt, x, c);
                 bx = msel(lt, t, bx);
 #else
                 const uint32_t gt = ltm(x, c);
                 const uint32_t lt = ltm_take_idx(c, x, t, bx);
-                tie = ~lt & (tie | (cm & ~gt));
+                tie = ~lt & (tie | (cm & ~gt & (1u << t)));
 #endif
                 MR_LANE_FENCE();
             }
             x.m = lm_pack(lm_len(x.m) + 1u, bx == kNone32 ? 0u : bx, 1, kStandard);
-            if (tie) {  // equal metrics and length from several boundaries: the lists decide
-                for (uint32_t m = (bndm | (walk0 ? 1u : 0u)) & ~(1u << bx); m; m &= m - 1u) {
+            // Equal metrics and length from several boundaries: the lists decide, among the
+            // boundaries that tied the final best only (a strictly better walk cleared the
+            // set; the source's walk, visited first, is never taken on a tie)
+            if (tie) {
+                for (uint32_t m = tie; m; m &= m - 1u) {
                     const uint32_t b = uint32_t(__builtin_ctz(m));
                     int px, py;
                     pos(b, px, py);
