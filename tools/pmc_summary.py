@@ -23,7 +23,7 @@ import json
 import os
 from collections import defaultdict
 
-SOLVE_KERNELS = ("hub_lane_kernel", "hub_wide_kernel", "hub_fill_kernel", "hub_kernel", "solve_kernel", "fill_kernel")
+SOLVE_KERNELS = ("hub_group_kernel", "hub_lane_kernel", "hub_wide_kernel", "hub_fill_kernel", "hub_kernel", "solve_kernel", "fill_kernel")
 
 
 def per_dispatch(path: str, counter: str):
