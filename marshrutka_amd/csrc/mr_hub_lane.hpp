@@ -264,10 +264,16 @@ struct LaneHub {
         return 0;
     }
 
-    __device__ __forceinline__ uint32_t rk(uint32_t e) const { return e == 0 ? src_rk : spl[e].rk; }
+    // (branchless: row 0 of the LDS copy exists and is read anyway, then the source's
+    // values are selected; divergent branches around each LDS read cost more)
+    __device__ __forceinline__ uint32_t rk(uint32_t e) const {
+        const uint32_t r = spl[e].rk;
+        return e == 0 ? src_rk : r;
+    }
     __device__ __forceinline__ void pos(uint32_t e, int &x, int &y) const {
-        x = e == 0 ? sx : spl[e].x;
-        y = e == 0 ? sy : spl[e].y;
+        const int rx = spl[e].x, ry = spl[e].y;
+        x = e == 0 ? sx : rx;
+        y = e == 0 ? sy : ry;
     }
     // region row entry r of entry p's cell (p = 0: the source)
     __device__ __forceinline__ uint2 near_of(uint32_t p, uint32_t r) const { return p == 0 ? srow[r] : nearS[p * nreg + r]; }
@@ -290,7 +296,8 @@ struct LaneHub {
     __device__ __forceinline__ Own own_of(uint32_t e) const {
         int x, y;
         pos(e, x, y);
-        return Own{x, y, rk(e), e == 0 ? kNone10 : spl[e].rid, (c5m >> e) & 1u};
+        const uint32_t rid = spl[e].rid;
+        return Own{x, y, rk(e), e == 0 ? kNone10 : rid, (c5m >> e) & 1u};
     }
     __device__ __forceinline__ Cmd tail(uint32_t meta, const Own &o, int i) const {
         const uint32_t p = lm_par(meta), kind = lm_kind(meta), nt = lm_nt(meta);
@@ -507,7 +514,7 @@ struct LaneHub {
     }
 
     // ---- output (Core::emit) --------------------------------------------------------
-    __device__ __forceinline__ void emit(const LLab &x, uint32_t xid, const Own &xo, uint32_t qi) const {
+    __device__ __forceinline__ void emit(const LLab x, uint32_t xid, const Own xo, uint32_t qi) const {
         const DevParams &p = P;
         OutResult &o = a->out_res[qi];
         OutCmd *oc = a->out_cmd + (unsigned long long)qi * p.max_cmds;
@@ -526,17 +533,30 @@ struct LaneHub {
         }
         int at = int(len) - 1;
         uint32_t e = x.m;
-        Own eo = xo;
+        // the current label's own cell, as scalars (an Own copied along the loop went to
+        // scratch memory)
+        int ox = xo.x, oy = xo.y;
+        uint32_t ork = xo.rk, orid = xo.rid, oc5 = xo.c5;
         uint32_t eid = xid;
         for (uint32_t guard = 0; at >= 0 && guard <= TM + 1; ++guard) {
-            for (int j = int(lm_nt(e)) - 1; j >= 0 && at >= 0; --j, --at) {
-                const Cmd c = tail(e, eo, j);
-                oc[at] = OutCmd{c.kp, c.from, c.to, 0};
+            const Own eo{ox, oy, ork, orid, oc5};
+            if (lm_nt(e) == 2 && at >= 0) {
+                const Cmd c = tail(e, eo, 1);
+                oc[at--] = OutCmd{c.kp, c.from, c.to, 0};
+            }
+            if (at >= 0) {
+                const Cmd c = tail(e, eo, 0);
+                oc[at--] = OutCmd{c.kp, c.from, c.to, 0};
             }
             eid = lm_par(e);
             if (eid == 0) break;
             e = meta_of(eid);
-            eo = own_of(eid);
+            const Own n = own_of(eid);
+            ox = n.x;
+            oy = n.y;
+            ork = n.rk;
+            orid = n.rid;
+            oc5 = n.c5;
         }
         if (at != -1 || eid != 0) atomicOr(counter + kCtrFlags, kErrChain);
         o = OutResult{legs, money, time, (status << 16) | (len & 0xFFFFu)};
