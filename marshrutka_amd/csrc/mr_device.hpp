@@ -2522,7 +2522,16 @@ struct HubWide : HubSolver<1> {
 #pragma unroll
         for (uint32_t i = 0; i < SPL; ++i) {
             const uint32_t own = SS(i).rk;
+#ifdef MR_WIDE_SETTLE_TIES
             const bool take = c[i] && (!any || cmp_rlab(my[i], own, bv, bown) < 0);
+#else
+            // Exact (metrics, length) ties at a settle need no list compare: either entry
+            // may settle first (every candidate out of a settled entry is strictly greater
+            // than its label in (metrics, length); LaneHub::solve)
+            int r = cmp_metrics(my[i].m0, my[i].m1, my[i].m2, bv.m0, bv.m1, bv.m2);
+            if (r == 0 && rl_len(my[i]) != rl_len(bv)) r = rl_len(my[i]) < rl_len(bv) ? -1 : 1;
+            const bool take = c[i] && (!any || r < 0);
+#endif
             sel_rlab(take, bv, my[i]);
             bt = take ? j + 64u * i : bt;
             bown = take ? own : bown;
@@ -2533,7 +2542,11 @@ struct HubWide : HubSolver<1> {
         const unsigned long long m =
             p.perm[0] == 2u ? seg_narrow<64, 20u>(cand, metric(bv, p.perm[0]), metric(bv, p.perm[1]), metric(bv, p.perm[2]), rl_len(bv))
                             : seg_narrow<64, 16u>(cand, metric(bv, p.perm[0]), metric(bv, p.perm[1]), metric(bv, p.perm[2]), rl_len(bv));
+#ifdef MR_WIDE_SETTLE_TIES
         if (__popcll(m) == 1) return bcast(bt, uint32_t(__ffsll((long long)m) - 1));
+#else
+        return bcast(bt, uint32_t(__ffsll((long long)m) - 1));  // (several lanes tied: the lowest)
+#endif
         // equal metrics and length in several lanes: compare the command lists
         if (cand) write_rec(bt, expand(bv, bown), 1);
         wave_sync();
