@@ -1627,6 +1627,13 @@ struct HubSolver : Core<false> {
         else
             bal = seg_narrow<LPS, 16u>(c, mm3[p.perm[0]], mm3[p.perm[1]], mm3[p.perm[2]], rl_len(my));
         const unsigned long long m = seg_bits<LPS>(bal);
+#ifndef MR_HUB_SETTLE_TIES
+        // Exact ties of metrics and length between specials need no list compare: either
+        // may settle first (every candidate out of a settled special is strictly greater
+        // than its label in (metrics, length)), so the lowest lane
+        (void)own;
+        return m ? uint32_t(__ffsll((long long)m) - 1) : kNone32;
+#endif
         uint32_t win = __popcll(m) == 1 ? uint32_t(__ffsll((long long)m) - 1) : kNone32;
         if (!seg_single<LPS>(bal)) {
             const bool tied = __popcll(m) > 1;
