@@ -337,6 +337,9 @@ struct LaneHub {
         for (uint32_t t = 1; t < TM; ++t) M[t * 64u + l] = L[t].m;
     }
     __device__ __forceinline__ uint32_t meta_of(uint32_t e) const { return M[e * 64u + lane_id()]; }
+    // per wave: each relaxation's best candidate meta into entry t (t * 64 + lane), read
+    // by the relaxation ties; M holds the settled entries' metas (written at their settle)
+    uint32_t *MC = nullptr;
     // lexicographic compare of two equal-length command lists (metas x and y), walking
     // from the last command towards the first (hub_kernel's cmp_list); xid/yid name the
     // table entries the labels are (kOwn for built ones), so a shared prefix stops the walk
@@ -699,17 +702,19 @@ struct LaneHub {
                 }
             }
             settle_ctx(z, s, ((wt >> s) & 1u) != 0);
+            if (s != 0) M[s * 64u + lane_id()] = z.ls.m;  // (the settled meta, for the chains)
+            // no candidate out of any lane's settle (the last settles): nothing to relax
+            if (!__any((z.walk | z.cenm | z.car | z.soe | z.reg) != 0)) continue;
             const uint4 *rowa = PA + z.s * TM;
             const uint2 *rowb = PB + z.s * TM;
-            // Each step also stores into the LDS meta copy M: a settled entry's own meta
-            // (the command chains of the list compares walk settled entries only) and
-            // for the others the meta of this iteration's best candidate, which the tie
-            // path below reads instead of rebuilding the candidate.
+            // Each step also stores into the per-wave LDS copy MC the meta of this
+            // iteration's best candidate, which the tie path below reads instead of
+            // rebuilding the candidate.
             // The pair-table words of entry t are read MR_LANE_PF entries ahead: the fences
             // keep each entry's code in place, so a read issued in its own entry left the
             // wave parked on it (SQ: ~31 % of the kernel's wave cycles waiting).
             uint32_t ties = 0;
-            uint32_t *ml = M + lane_id();
+            uint32_t *ml = MC + lane_id();
             uint4 pa[MR_LANE_PF + 1];
             uint2 pb[MR_LANE_PF + 1];
 #pragma unroll
@@ -728,7 +733,7 @@ struct LaneHub {
                 const uint2 B = (t >= 6 && t < 6 + kLaneRegs) ? pb[(t - 1) % R] : make_uint2(0, 0);
                 const FromS f = from_s(z, t, pa[(t - 1) % R], B);
                 offer(t, f, ties);
-                ml[t * 64u] = msel(bitm(done, t), L[t].m, f.c.m);
+                ml[t * 64u] = f.c.m;
                 MR_LANE_FENCE();
             }
             // exact (metrics, length) ties with a tentative label: the command lists decide
@@ -913,6 +918,7 @@ __global__ __launch_bounds__(kBS, lane_waves(TM)) void hub_lane_kernel(const KAr
     extern __shared__ __attribute__((aligned(16))) char smem[];
     LaneHub<PERM, TM> H;
     lane_setup<TM>(a, smem, H);
+    H.MC = reinterpret_cast<uint32_t *>(smem + lane_lds_total(a->p.NS, a->nreg, TM)) + (threadIdx.x >> 6) * (TM * 64u);
     // lane l of wave w: source 64 w + l of the lane kernel's sources [0, n_lane)
     const uint32_t s_idx = (blockIdx.x * (kBS / 64) + (threadIdx.x >> 6)) * 64u + lane_id();
     const uint32_t n = a->n_lane;

@@ -100,8 +100,11 @@ uint32_t lane_blob_build(const SpecialStatic *sp, uint32_t NS, uint32_t nreg, ui
     return bytes;
 }
 
+// (the lane kernel's LDS: the lane kernels' block and meta copy, then its per-wave
+// candidate metas, LaneHub::MC)
 uint32_t hub_lane_lds_bytes(uint32_t NS, uint32_t nreg) {
-    return lane_lds_total(NS, nreg, hub_lane_entries(NS));
+    const uint32_t TM = hub_lane_entries(NS);
+    return lane_lds_total(NS, nreg, TM) + (kBS / 64) * TM * 64u * 4u;
 }
 
 hipError_t launch_hub_lane(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t n_lane,
@@ -109,6 +112,7 @@ hipError_t launch_hub_lane(const KArgs *d_args, const uint32_t perm[3], uint32_t
     const void *fn = lane_fn(perm, NS);
     if (!fn) return hipErrorInvalidValue;
     const uint32_t bytes = hub_lane_lds_bytes(NS, nreg);
+    if (bytes > 64u * 1024u) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
     const uint32_t waves = (n_lane + 63u) / 64u, blocks = (waves + 3u) / 4u;
     void *args[] = {const_cast<KArgs **>(&d_args)};
     return hipLaunchKernel(fn, dim3(blocks ? blocks : 1u), dim3(kBS), args, bytes, stream);
