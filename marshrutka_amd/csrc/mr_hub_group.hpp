@@ -383,6 +383,8 @@ struct GroupHub : LaneHub<PERM, G * E> {
                 if (gj == 0) LT[s] = make_uint4(z.ls.c1, z.ls.c2, z.ls.c3, z.ls.m);
             }
             MR_GSTAMP(3);  // (3: the settle's bookkeeping and its LDS reads)
+            // no candidate out of any group's settle (the last settles): nothing to relax
+            if (!__any((z.walk | z.cenm | z.car | z.soe | z.reg) != 0)) continue;
             // relaxations into this lane's slots
             uint32_t ties = 0, fcm[E];
 #pragma unroll
