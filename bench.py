@@ -49,9 +49,11 @@ WORKLOADS = {
                     "the reference, SURVEY 8c), default FindPath params; a step is one whole query through the "
                     "device path (the reference runs it on the CPU)"),
     # max_cmds: command slots per query record (what the N > 1 gather moves); the app's
-    # default orders give labels of at most 4 commands on these maps, the Time-first c5
-    # up to 14+; a longer label goes to the rank's overflow pool (its slot is tagged)
-    "c2": dict(size=65, queries_per_gpu=10_000, campfires=4, seed=2024, max_cmds=6,
+    # default orders give labels of at most 4 commands on these maps (c4's 1M batch:
+    # 52k / 47k / 302k / 599k labels of 1 / 2 / 3 / 4, tools/probes/cmd_hist.py), the
+    # Time-first c5 up to 14+; a longer label goes to the rank's overflow pool (its slot
+    # is tagged)
+    "c2": dict(size=65, queries_per_gpu=10_000, campfires=4, seed=2024, max_cmds=4,
                desc="configs[1]: 10k uniform (src,dst) per GPU on a 65x65 synthetic map (64x64 -> odd 65), "
                     "default FindPath params"),
     # c3: 1024 sources a pass (4.5 GB of cell words), far past the 256 MiB Infinity Cache,
@@ -61,7 +63,7 @@ WORKLOADS = {
                     "sources per GPU per pass; a step answers V queries per source (SURVEY 8d c3)"),
     # c4: one 1M-query batch for the whole job (strong scaling), split by source over
     # the ranks: N = 1 answers all of configs[3] on one GPU
-    "c4": dict(size=1025, queries_total=1_000_000, campfires=4, seed=4096, max_cmds=6,
+    "c4": dict(size=1025, queries_total=1_000_000, campfires=4, seed=4096, max_cmds=4,
                desc="configs[3]: one batch of 1M uniform (src,dst) queries on a 1025x1025 synthetic map "
                     "(1024 -> odd 1025), default FindPath params, its sources sharded over the GPUs"),
     "c5": dict(size=4097, queries_per_gpu=10_000, campfires=64, clustered=True, seed=4097, sort=(1, 2), max_cmds=16,
