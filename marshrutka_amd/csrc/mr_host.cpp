@@ -1596,13 +1596,16 @@ static uint32_t lane_sources(const HostPlan &hp) {
     for (size_t i = 0; i + 1 < hp.q_begin.size(); ++i) c += hp.q_begin[i + 1] - hp.q_begin[i] <= kLaneMaxQ;
     return c;
 }
-// half a wave per SIMD of the current device (MR_HUB_LANE_MIN overrides)
+// the lane kernel from 160 sources a CU (40 960 on MI355X): below, a plan's lane-kernel
+// waves run one round at a wave per SIMD or less, latency-bound, and the group kernel is
+// faster (1025^2 map: 20k sources 66 us against 97, 40k even, 60k 149 against 105);
+// MR_HUB_LANE_MIN overrides
 static uint32_t lane_min_sources() {
     if (const char *e = std::getenv("MR_HUB_LANE_MIN")) return uint32_t(std::strtoul(e, nullptr, 10));
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         cus = 256;
-    return uint32_t(cus) * 4u * 32u;
+    return uint32_t(cus) * 160u;
 }
 
 // Hub plans on the lane kernel: the sources with at most kLaneMaxQ queries first (one
@@ -1673,11 +1676,13 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     const char *hg = std::getenv("MR_HUB_GROUP");
     const uint32_t hgv = hg ? uint32_t(std::strtoul(hg, nullptr, 10)) : 8u;
     const bool group_off = hg && hgv == 0, group_force = std::getenv("MR_HUB_GROUP_FORCE") != nullptr;
-    // default size: 16 lanes (c2: 46 us a pass against 60 with 8 and 51 with 32), 32 for
-    // plans of at most 1024 sources (a lone source: 29 us against 31), whose waves leave
-    // most SIMDs empty
+    // default size by sources (tools/gpu_r04zi.sh): 32 lanes up to 1 024 (a lone
+    // source: 23 us against 31 with 16), 16 up to 4 096 (c2, 3 821 sources: 37 us against
+    // 44 with 8), else 8 (1025^2 map, 5k / 20k sources: 34 / 66 us against 53 / 129 with
+    // 16: more groups per wave, fewer waves)
+    const size_t nsrc_g = hp.src_v.size();
     const uint32_t group_g = hg ? (hgv == 16 ? 16u : (hgv == 32 ? 32u : 8u))
-                                : (hp.src_v.size() <= 1024 ? 32u : 16u);
+                                : (nsrc_g <= 1024 ? 32u : (nsrc_g <= 4096 ? 16u : 8u));
     const bool lane_ok = hp.hub && !hp.wide && !hp.nonlin && !all_mode && hp.near && lane_bounds_ok(hp.p);
     if (lane_ok && !group_force && !lane_off && hub_lane_entries(hp.p.NS) != 0 && lane_layout_ok(hp) &&
         (lane_force || lane_sources(hp) >= lane_min_sources()))

@@ -160,6 +160,8 @@ struct GroupHub : LaneHub<PERM, G * E> {
     using Base::settle_ctx;
     using Base::walk_to;
     using Base::meta_of;
+    using Base::mstride;
+    using Base::mcolumn;
     using Own = typename Base::Own;
     using Settle = typename Base::Settle;
     using FromS = typename Base::FromS;
@@ -340,7 +342,7 @@ struct GroupHub : LaneHub<PERM, G * E> {
             wt |= won & ~ltm3(c, w) & eb;
         }
         // ---- Dijkstra over the specials, one settle per group per iteration -----------
-        uint32_t *mcol = M + lane_id();  // this lane's column of the meta copy
+        uint32_t *mcol = M + mcolumn;  // this group's column of the meta copy
         MR_GSTAMP(1);  // (1: the source's own edges)
         const uint32_t n_it = (a->dbg_flags & kDbgGroupNoSolve) ? 0u : NS;  // (timing experiments)
         for (uint32_t it = 0; it < n_it; ++it) {
@@ -379,7 +381,7 @@ struct GroupHub : LaneHub<PERM, G * E> {
             const bool wts = group_any(s != 0 && (s & (G - 1u)) == gj && ((wt >> s) & 1u));
             settle_ctx(z, s, wts);
             if (s != 0) {  // publish the settled label (the chains and the read-off)
-                mcol[s * 64u] = z.ls.m;
+                mcol[s * mstride] = z.ls.m;
                 if (gj == 0) LT[s] = make_uint4(z.ls.c1, z.ls.c2, z.ls.c3, z.ls.m);
             }
             MR_GSTAMP(3);  // (3: the settle's bookkeeping and its LDS reads)
@@ -532,12 +534,17 @@ struct GroupHub : LaneHub<PERM, G * E> {
     }
 };
 
-// LDS: the lane kernels' (lane_lds_total with TM = G * E) and per group its settled labels
-__host__ __device__ inline uint32_t group_off_lt(uint32_t NS, uint32_t nreg, uint32_t TM) {
-    return align16h(lane_lds_total(NS, nreg, TM));
+// LDS: the lane kernels' block (TM = G * E), then per group its meta column (TM words:
+// the group shares one, LaneHub::mstride / mcolumn), its settled labels, the source's
+// region row, the tail commands and the batch's destinations
+__host__ __device__ inline uint32_t group_off_m(uint32_t NS, uint32_t nreg, uint32_t G, uint32_t E) {
+    return lane_off_meta(NS, nreg, G * E);
+}
+__host__ __device__ inline uint32_t group_off_lt(uint32_t NS, uint32_t nreg, uint32_t G, uint32_t E) {
+    return align16h(group_off_m(NS, nreg, G, E) + (kBS / G) * G * E * 4u);
 }
 __host__ __device__ inline uint32_t group_off_sr(uint32_t NS, uint32_t nreg, uint32_t G, uint32_t E) {
-    return group_off_lt(NS, nreg, G * E) + (kBS / G) * G * E * 16u;
+    return group_off_lt(NS, nreg, G, E) + (kBS / G) * G * E * 16u;
 }
 __host__ __device__ inline uint32_t group_off_ct(uint32_t NS, uint32_t nreg, uint32_t G, uint32_t E) {
     return align16h(group_off_sr(NS, nreg, G, E) + (kBS / G) * nreg * 8u);
@@ -565,7 +572,10 @@ __global__ __launch_bounds__(kBS) void hub_group_kernel(const KArgs *__restrict_
 #endif
     H.prefetch(s_idx);
     lane_setup<TM>(a, smem, H);
-    H.LT = reinterpret_cast<uint4 *>(smem + group_off_lt(a->p.NS, a->nreg, TM)) + (threadIdx.x / G) * TM;
+    H.M = reinterpret_cast<uint32_t *>(smem + group_off_m(a->p.NS, a->nreg, G, E)) + (threadIdx.x / G) * TM;
+    H.mstride = 1u;  // (one meta column per group)
+    H.mcolumn = 0u;
+    H.LT = reinterpret_cast<uint4 *>(smem + group_off_lt(a->p.NS, a->nreg, G, E)) + (threadIdx.x / G) * TM;
     H.SR = reinterpret_cast<uint2 *>(smem + group_off_sr(a->p.NS, a->nreg, G, E)) + (threadIdx.x / G) * a->nreg;
     H.CT = reinterpret_cast<uint4 *>(smem + group_off_ct(a->p.NS, a->nreg, G, E)) + (threadIdx.x / G) * (2 * TM);
     H.W = reinterpret_cast<uint32_t *>(smem + group_off_w(a->p.NS, a->nreg, G, E)) + (threadIdx.x / G) * G;

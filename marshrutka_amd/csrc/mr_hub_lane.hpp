@@ -332,11 +332,15 @@ struct LaneHub {
     uint32_t ht_probes;  // the longest probe sequence in HT
     __device__ __forceinline__ void dump_meta() const {
         const uint32_t l = lane_id();
-        M[l] = start().m;
+        M[mcolumn] = start().m;
+        (void)l;
 #pragma unroll
-        for (uint32_t t = 1; t < TM; ++t) M[t * 64u + l] = L[t].m;
+        for (uint32_t t = 1; t < TM; ++t) M[t * mstride + mcolumn] = L[t].m;
     }
-    __device__ __forceinline__ uint32_t meta_of(uint32_t e) const { return M[e * 64u + lane_id()]; }
+    __device__ __forceinline__ uint32_t meta_of(uint32_t e) const { return M[e * mstride + mcolumn]; }
+    // the meta copy's layout: entry t of this lane's column at t * mstride + mcolumn (the
+    // lane kernel: a column per lane; the group kernel: one per group)
+    uint32_t mstride = 64u, mcolumn = 0u;
     // per wave: each relaxation's best candidate meta into entry t (t * 64 + lane), read
     // by the relaxation ties; M holds the settled entries' metas (written at their settle)
     uint32_t *MC = nullptr;
@@ -702,7 +706,7 @@ struct LaneHub {
                 }
             }
             settle_ctx(z, s, ((wt >> s) & 1u) != 0);
-            if (s != 0) M[s * 64u + lane_id()] = z.ls.m;  // (the settled meta, for the chains)
+            if (s != 0) M[s * mstride + mcolumn] = z.ls.m;  // (the settled meta, for the chains)
             // no candidate out of any lane's settle (the last settles): nothing to relax
             if (!__any((z.walk | z.cenm | z.car | z.soe | z.reg) != 0)) continue;
             const uint4 *rowa = PA + z.s * TM;
@@ -898,6 +902,8 @@ __device__ __forceinline__ void lane_setup(const KArgs *__restrict__ a, char *sm
     H.PB = reinterpret_cast<const uint2 *>(smem + lane_off_pb(NS, nreg, TM));
     H.RM = reinterpret_cast<const uint32_t *>(smem + lane_off_rm(NS, nreg, TM));
     H.M = reinterpret_cast<uint32_t *>(smem + lane_off_meta(NS, nreg, TM)) + (threadIdx.x >> 6) * (TM * 64u);
+    H.mstride = 64u;
+    H.mcolumn = lane_id();
     H.HT = reinterpret_cast<const uint2 *>(smem + lane_off_hash(NS, nreg, TM));
     const uint4 hdr = *reinterpret_cast<const uint4 *>(smem + lane_off_hdr(NS, nreg, TM));
     H.ht_probes = __builtin_amdgcn_readfirstlane(hdr.x);
