@@ -258,11 +258,13 @@ def as_expected(label):
     return (label.legs, label.money, label.time_s, tuple(c.as_tuple() for c in label.commands))
 
 
-def end_to_end(m, grid, params, qpg, seed, max_cmds, reps):
+def end_to_end(m, grid, params, qpg, seed, max_cmds, reps, pinned=False):
     """Whole-call throughput of fresh batches: plan creation (host grouping by source,
     the per-plan tables, the uploads), one pass, the device->host copy and decode of
     every label (mr_plan_fetch), synchronised.  The queries are built as a numpy
-    mr_query array beforehand (the caller's input).  Median over `reps` batches."""
+    mr_query array beforehand (the caller's input).  Median over `reps` batches.
+    pinned: the output arrays page-locked once (mr_host_register), as a serving caller
+    reusing them would: the fetch DMAs straight into them."""
     import numpy as np
     import torch
     from marshrutka_amd import pathfinder
@@ -272,6 +274,9 @@ def end_to_end(m, grid, params, qpg, seed, max_cmds, reps):
     bufs = pathfinder.fetch_buffers(qpg, max_cmds)
     for b in bufs:
         np.frombuffer(b, dtype=np.uint8).fill(0)
+    if pinned:
+        for b in bufs:
+            pathfinder.pin_host(b)
     for r in range(reps):
         rng = np.random.default_rng(seed + 1000 + r)
         src = rng.integers(0, V, qpg, dtype=np.int64)
@@ -288,9 +293,12 @@ def end_to_end(m, grid, params, qpg, seed, max_cmds, reps):
         t3 = time.perf_counter()
         del plan
         rows.append((t3 - t0, t1 - t0, t2 - t1, t3 - t2))
+    if pinned:
+        for b in bufs:
+            pathfinder.unpin_host(b)
     rows.sort()
     tot, cr, run, fe = rows[len(rows) // 2]
-    return {"e2e_queries_per_s": qpg / tot, "queries": qpg, "ms": tot * 1e3, "plan_create_ms": cr * 1e3,
+    return {"e2e_queries_per_s": qpg / tot, "output_arrays": "page-locked" if pinned else "pageable", "queries": qpg, "ms": tot * 1e3, "plan_create_ms": cr * 1e3,
             "run_ms": run * 1e3, "fetch_ms": fe * 1e3, "reps": reps,
             "what": "fresh batch: Plan create (host grouping, tables, H2D) + one pass + mr_plan_fetch (D2H and "
                     "decode of every label) into the caller's output arrays (allocated once, reused across batches), "
@@ -586,6 +594,9 @@ def main():
         out["gather_check"] = gather_check
     if rank == 0 and not all_dst and args.e2e_reps > 0:
         out["end_to_end"] = end_to_end(m, grid, params, qpg, wl["seed"], wl.get("max_cmds", 16), args.e2e_reps)
+        # the same with the output arrays page-locked once (mr_host_register)
+        out["end_to_end_pinned"] = end_to_end(m, grid, params, qpg, wl["seed"], wl.get("max_cmds", 16), args.e2e_reps,
+                                              pinned=True)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and all_dst:
         cb, parity = cpu_baseline_all(m, params, plan, mine, args.cpu_seconds)
         out["cpu_baseline"] = cb

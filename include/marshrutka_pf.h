@@ -292,6 +292,13 @@ double mr_plan_kernel_ms(mr_plan *plan, uint32_t *n_launches);
  * next plan needs no hipMalloc).  Blocks of live plans are untouched; safe at any time.
  * mr_grid_destroy trims too, and a failing device allocation trims and retries once. */
 void mr_cache_trim(void);
+/* Page-locks [p, p + bytes) of caller memory (hipHostRegister) that mr_plan_fetch then
+ * fills by direct DMA instead of through the engine's pinned stage and a host copy: for
+ * a caller that reuses its fetch buffers batch after batch.  mr_host_unregister(p)
+ * before the memory is freed.  MR_ERR_INVALID_ARG on a null or empty range,
+ * MR_ERR_DEVICE when the runtime refuses. */
+int mr_host_register(void *p, uint64_t bytes);
+int mr_host_unregister(void *p);
 /* Waits for the plan's passes and frees it.  Device pointers the plan handed out
  * (mr_plan_device_outputs, mr_sssp_device_records / _tables) are invalid afterwards:
  * their memory may back the next plan's buffers, so a reader on another stream must

@@ -189,6 +189,8 @@ extern "C" {
     pub fn mr_plan_kernel_ms(plan: *mut mr_plan, n_launches: *mut u32) -> f64;
     pub fn mr_plan_destroy(plan: *mut mr_plan);
     pub fn mr_cache_trim();
+    pub fn mr_host_register(p: *mut c_void, bytes: u64) -> c_int;
+    pub fn mr_host_unregister(p: *mut c_void) -> c_int;
 
     // all destinations of each source
     pub fn mr_sssp_plan_create(grid: *const mr_grid, params: *const mr_params, sources: *const mr_cell_index,

@@ -666,7 +666,60 @@ static void region_bounds(const mr_grid *g, int h, std::vector<uint32_t> &regs, 
 
 namespace {
 
+// Per-batch host arrays recycled across plans.  A fresh array of a million entries is
+// mapped page by page on first touch (~1 k faults per 4 MB, the pool's threads all taking
+// the address-space lock); a recycled one is mapped already, and keeps its size, so a
+// resize to a batch no larger writes nothing.  Up to kSpareMax arrays per type are kept.
+template <class T> struct SpareVecs {
+    static constexpr size_t kSpareMax = 16, kMinBytes = size_t(1) << 16;
+    std::mutex mu;
+    std::vector<std::vector<T>> v;
+    static SpareVecs &get() {
+        static SpareVecs *s = new SpareVecs();
+        return *s;
+    }
+};
+// `out` = a spare of at least n entries (the smallest such, else the largest), resized to n
+template <class T> static void spare_take(std::vector<T> &out, size_t n) {
+    if (n * sizeof(T) >= SpareVecs<T>::kMinBytes && out.capacity() < n) {
+        SpareVecs<T> &sv = SpareVecs<T>::get();
+        std::lock_guard<std::mutex> lk(sv.mu);
+        size_t best = sv.v.size();
+        for (size_t i = 0; i < sv.v.size(); ++i) {
+            const size_t c = sv.v[i].capacity();
+            if (best == sv.v.size()) best = i;
+            else {
+                const size_t b = sv.v[best].capacity();
+                if ((b < n && c > b) || (c >= n && c < b)) best = i;
+            }
+        }
+        if (best < sv.v.size()) {
+            out.swap(sv.v[best]);
+            sv.v.erase(sv.v.begin() + std::ptrdiff_t(best));
+        }
+    }
+    out.resize(n);
+}
+template <class T> static void spare_put(std::vector<T> &v) {
+    if (v.capacity() * sizeof(T) < SpareVecs<T>::kMinBytes) return;
+    SpareVecs<T> &sv = SpareVecs<T>::get();
+    std::lock_guard<std::mutex> lk(sv.mu);
+    if (sv.v.size() >= SpareVecs<T>::kSpareMax) {  // drop the smallest
+        size_t k = 0;
+        for (size_t i = 1; i < sv.v.size(); ++i)
+            if (sv.v[i].capacity() < sv.v[k].capacity()) k = i;
+        if (sv.v[k].capacity() >= v.capacity()) return;
+        sv.v.erase(sv.v.begin() + std::ptrdiff_t(k));
+    }
+    sv.v.emplace_back();
+    sv.v.back().swap(v);
+}
+
 struct HostPlan {
+    ~HostPlan() {
+        for (std::vector<uint32_t> *a : {&src_v, &q_begin, &q_dst, &q_id, &q_pos}) spare_put(*a);
+        spare_put(q_status);
+    }
     DevParams p{};
     uint32_t homeland = 0, hq_v = 0xFFFFFFFFu;  // the key of the grid's shared sinfo (build_sinfo)
     std::vector<SpecialStatic> sp;
@@ -896,8 +949,9 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     hp.nq = n;
     const double tb0 = timing_on() ? now_ms() : 0.0;
     HostPool &pool = HostPool::get();
-    // at least 32k queries a part (a part's work must outweigh waking a thread)
-    const uint32_t parts = std::max(1u, std::min(pool.size(), n / 32768u));
+    // at least 8k queries a part (a part's work must outweigh waking a thread; 125k
+    // queries on 3 parts took 1.2 ms)
+    const uint32_t parts = std::max(1u, std::min(pool.size(), n / 8192u));
     constexpr uint32_t kBits = 13, kB = 1u << kBits;
     // An invalid query gets the source key 2^32 - 1: its low bits are all ones, so with
     // enough passes to cover every vertex id (two while V < 2^26) it sorts after every
@@ -914,8 +968,8 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     tmp.resize(n);
     qs_dst.resize(n);
     hist.resize(size_t(parts) * kB);
-    hp.q_status.resize(n);
-    hp.q_pos.resize(n);
+    spare_take(hp.q_status, n);
+    spare_take(hp.q_pos, n);
     std::vector<uint32_t> bad(parts + 1, 0);
     // lookups, fused with the first pass's histogram
     pool.run(parts, [&](uint32_t pt) {
@@ -1001,10 +1055,10 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
         starts[pt + 1] = c;
     });
     for (uint32_t pt = 0; pt < parts; ++pt) starts[pt + 1] += starts[pt];
-    hp.src_v.resize(starts[parts]);
-    hp.q_begin.resize(starts[parts] + 1);
-    hp.q_dst.resize(m);
-    hp.q_id.resize(m);
+    spare_take(hp.src_v, starts[parts]);
+    spare_take(hp.q_begin, starts[parts] + 1);
+    spare_take(hp.q_dst, m);
+    spare_take(hp.q_id, m);
     pool.run(parts, [&](uint32_t pt) {
         uint32_t si = starts[pt];
         for (uint32_t k = chunk_lo(m, parts, pt), e = chunk_lo(m, parts, pt + 1); k < e; ++k) {
@@ -1304,7 +1358,7 @@ static hipError_t copy_d2h(const D2HSeg *seg, int n, hipStream_t s) {
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         return e;
     }
-    constexpr size_t kChunk = size_t(16) << 20;
+    constexpr size_t kChunk = size_t(4) << 20;  // (16 MB: 1M fetch 5.3 ms, one chunk's DMA and copy-out not overlapped)
     PinnedStage &st = stage_down();
     std::lock_guard<std::mutex> lk(st.mu);
     char *buf = static_cast<char *>(st.get(2 * kChunk));
@@ -1361,6 +1415,21 @@ static hipError_t dev_malloc(void **p, size_t bytes) {
 }
 
 extern "C" void mr_cache_trim(void) { trim_cache_all(); }
+
+extern "C" int mr_host_register(void *p, uint64_t bytes) {
+    if (!p || !bytes) return fail(MR_ERR_INVALID_ARG, "mr_host_register: null or empty range");
+    if (!mr_device_available()) return fail(MR_ERR_NO_DEVICE, "no gfx950 device visible");
+    const hipError_t e = hipHostRegister(p, size_t(bytes), hipHostRegisterDefault);
+    if (e != hipSuccess) return fail(MR_ERR_DEVICE, std::string("hipHostRegister: ") + hipGetErrorString(e));
+    return MR_OK;
+}
+
+extern "C" int mr_host_unregister(void *p) {
+    if (!p) return fail(MR_ERR_INVALID_ARG, "mr_host_unregister: null pointer");
+    const hipError_t e = hipHostUnregister(p);
+    if (e != hipSuccess) return fail(MR_ERR_DEVICE, std::string("hipHostUnregister: ") + hipGetErrorString(e));
+    return MR_OK;
+}
 
 struct mr_plan {
     const mr_grid *grid = nullptr;
@@ -1621,7 +1690,11 @@ static uint32_t partition_sources(HostPlan &hp) {
     if (n_lane == ns) return n_lane;
     for (uint32_t i = 0; i < ns; ++i)
         if (hp.q_begin[i + 1] - hp.q_begin[i] > kLaneMaxQ) order.push_back(i);
-    std::vector<uint32_t> src(ns), qb(ns + 1), qd(hp.q_dst.size()), qi(hp.q_id.size());
+    std::vector<uint32_t> src, qb, qd, qi;
+    spare_take(src, ns);
+    spare_take(qb, ns + 1);
+    spare_take(qd, hp.q_dst.size());
+    spare_take(qi, hp.q_id.size());
     uint32_t off = 0;
     for (uint32_t j = 0; j < ns; ++j) {
         const uint32_t i = order[j];
@@ -1638,6 +1711,7 @@ static uint32_t partition_sources(HostPlan &hp) {
     hp.q_begin.swap(qb);
     hp.q_dst.swap(qd);
     hp.q_id.swap(qi);
+    for (std::vector<uint32_t> *a : {&src, &qb, &qd, &qi}) spare_put(*a);
     return n_lane;
 }
 
@@ -2640,32 +2714,53 @@ static bool plan_fetch_device(mr_plan *pl, mr_result *results, mr_command *pool,
     if (e == hipSuccess) e = hipMemcpyAsync(&tailw[1], off + (nq - 1), 4, hipMemcpyDeviceToHost, pl->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(&tailw[2], cnt + (nq - 1), 4, hipMemcpyDeviceToHost, pl->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(pl->stream);
+    // every command fits the caller's pool (offsets are the prefix of the counts): results
+    // and commands in one pipelined copy, else the results first, to find the cut
+    const uint64_t total = uint64_t(tailw[1]) + tailw[2];
+    const bool fits = !(tailw[0] & 1u) && total <= pool_cap && total <= pcap;
     if (e == hipSuccess) {
-        const D2HSeg sg{results, d_out, size_t(nq) * sizeof(mr_result)};
-        e = copy_d2h(&sg, 1, pl->stream);
+        const D2HSeg sg[2] = {{results, d_out, size_t(nq) * sizeof(mr_result)},
+                              {pool, d_pool, fits ? size_t(total) * sizeof(mr_command) : 0}};
+        e = copy_d2h(sg, 2, pl->stream);
     }
     // queries without a record (an invalid index), and the status to return: the first
     // error in query order, or MR_ERR_CAPACITY once a label's commands do not fit the
-    // caller's pool (written up to the first such label), as the host decoder does
-    const uint64_t total = uint64_t(tailw[1]) + tailw[2];
+    // caller's pool (written up to the first such label), as the host decoder does; per
+    // part of the queries on the host pool, combined in order
     uint64_t end = total;
     ret = MR_OK;
-    if (e == hipSuccess && !(tailw[0] & 1u))
-        for (uint32_t i = 0; i < nq; ++i) {
-            mr_result &r = results[i];
-            if (hp.q_status[i] != MR_OK) {
-                std::memset(&r, 0, sizeof(r));
-                r.status = hp.q_status[i];
+    if (e == hipSuccess && !(tailw[0] & 1u)) {
+        HostPool &hpool = HostPool::get();
+        const uint32_t parts = nq >= 65536u ? hpool.size() : 1u;
+        std::vector<uint64_t> p_end(parts, total);
+        std::vector<int32_t> p_ret(parts, MR_OK);
+        hpool.run(parts, [&](uint32_t pt) {
+            uint64_t en = total;
+            int32_t rt = MR_OK;
+            for (uint32_t i = chunk_lo(nq, parts, pt), ie = chunk_lo(nq, parts, pt + 1); i < ie; ++i) {
+                mr_result &r = results[i];
+                if (hp.q_status[i] != MR_OK) {
+                    std::memset(&r, 0, sizeof(r));
+                    r.status = hp.q_status[i];
+                }
+                if (r.status == MR_OK && uint64_t(r.command_offset) + r.n_commands > pool_cap) {
+                    en = std::min<uint64_t>(en, r.command_offset);
+                    rt = MR_ERR_CAPACITY;  // (the host decoder's rule: a short pool wins over other errors)
+                } else if (rt == MR_OK && r.status != MR_OK) {
+                    rt = r.status;
+                }
             }
-            if (r.status == MR_OK && uint64_t(r.command_offset) + r.n_commands > pool_cap) {
-                end = std::min<uint64_t>(end, r.command_offset);
-                ret = MR_ERR_CAPACITY;  // (the host decoder's rule: a short pool wins over other errors)
-            } else if (ret == MR_OK && r.status != MR_OK) {
-                ret = r.status;
-            }
+            p_end[pt] = en;
+            p_ret[pt] = rt;
+        });
+        for (uint32_t pt = 0; pt < parts; ++pt) {
+            end = std::min(end, p_end[pt]);
+            if (p_ret[pt] == MR_ERR_CAPACITY) ret = MR_ERR_CAPACITY;
+            else if (ret == MR_OK) ret = p_ret[pt];
         }
+    }
     const uint64_t ncopy = std::min<uint64_t>(end, pcap);
-    if (e == hipSuccess && ncopy && !(tailw[0] & 1u)) {
+    if (e == hipSuccess && !fits && ncopy && !(tailw[0] & 1u)) {
         const D2HSeg sg{pool, d_pool, size_t(ncopy) * sizeof(mr_command)};
         e = copy_d2h(&sg, 1, pl->stream);
     }

@@ -26,7 +26,7 @@ LIB_PATH = os.environ.get("MR_LIB_PATH") or os.path.join(os.path.dirname(os.path
 EXPORTED_SYMBOLS = [
     "mr_grid_create", "mr_grid_destroy", "mr_grid_square_size", "mr_params_default", "mr_find_path",
     "mr_find_path_batch", "mr_plan_create", "mr_plan_create_ex", "mr_plan_run", "mr_plan_fetch", "mr_plan_device_outputs",
-    "mr_plan_num_sources", "mr_plan_record_queries", "mr_plan_fallback_sources", "mr_plan_wait", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_cache_trim", "mr_plan_bind_outputs", "mr_plan_bind_outputs_ex", "mr_decode_records", "mr_abi_version", "mr_last_error",
+    "mr_plan_num_sources", "mr_plan_record_queries", "mr_plan_fallback_sources", "mr_plan_wait", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_cache_trim", "mr_host_register", "mr_host_unregister", "mr_plan_bind_outputs", "mr_plan_bind_outputs_ex", "mr_decode_records", "mr_abi_version", "mr_last_error",
     "mr_device_available", "mr_parse_map_html", "mr_parse_error", "mr_grid_from_html",
     "mr_command_time", "mr_duration_display", "mr_render_schedule",
     "mr_sssp_plan_create", "mr_sssp_records", "mr_sssp_device_records", "mr_sssp_record_pitch", "mr_sssp_device_tables", "mr_sssp_label", "mr_sssp_labels", "mr_plan_fill_ms",
@@ -96,6 +96,10 @@ def lib():
         L.mr_plan_destroy.argtypes = [vp]
         L.mr_cache_trim.argtypes = []
         L.mr_cache_trim.restype = None
+        L.mr_host_register.argtypes = [vp, C.c_uint64]
+        L.mr_host_register.restype = C.c_int
+        L.mr_host_unregister.argtypes = [vp]
+        L.mr_host_unregister.restype = C.c_int
         L.mr_abi_version.restype = C.c_uint32
         L.mr_last_error.restype = C.c_char_p
         L.mr_device_available.restype = C.c_int
@@ -357,6 +361,20 @@ def labels_digest(results, pool, n: int, order=None) -> str:
         h.update(np.ascontiguousarray(r[f]).tobytes())
     h.update(cmds[starts + within].tobytes())
     return h.hexdigest()
+
+
+def pin_host(arr) -> None:
+    """mr_host_register: page-lock a host buffer (a ctypes array, e.g. of fetch_buffers)
+    so mr_plan_fetch fills it by direct DMA; unpin_host(arr) before it is freed."""
+    st = lib().mr_host_register(C.addressof(arr), C.sizeof(arr))
+    if st != MR_OK:
+        raise EngineError(st, last_error())
+
+
+def unpin_host(arr) -> None:
+    st = lib().mr_host_unregister(C.addressof(arr))
+    if st != MR_OK:
+        raise EngineError(st, last_error())
 
 
 def fetch_buffers(n: int, max_cmds: int = 16):

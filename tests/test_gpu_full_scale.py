@@ -18,6 +18,7 @@ count and a digest of the command list, tests/label_digest.py) with numpy.
   path, and a 2000-query batch.  The oracle needs minutes and ~13 GB per solve at
   that size, so its answers are committed fixtures (tests/golden/make_full_scale.py).
 """
+import ctypes as C
 import json
 import os
 import random
@@ -27,7 +28,7 @@ import pytest
 
 import label_digest as ld
 from golden_util import as_expected
-from marshrutka_amd.abi import SORT_MONEY, SORT_TIME, CellIndex, Params
+from marshrutka_amd.abi import SORT_MONEY, SORT_TIME, CellIndex, Params, mr_command
 from marshrutka_amd.mapgen import SyntheticMap, random_queries, random_query_cells
 
 pytestmark = pytest.mark.gpu
@@ -104,6 +105,16 @@ def test_c4_full_scale(eng, oracle_lib, c4_map):
     plan.run()
     plan.run()  # the bench's steady state: a rerun of the same plan
     res, pool = plan.fetch_raw()
+    # the same fetch into page-locked arrays (mr_host_register: direct DMA) writes the same bytes
+    pres, ppool = plan.fetch_buffers()
+    for b in (pres, ppool):
+        eng.pin_host(b)
+    plan.fetch_raw((pres, ppool))
+    for b in (pres, ppool):
+        eng.unpin_host(b)
+    assert np.array_equal(np.frombuffer(pres, dtype=np.uint8), np.frombuffer(res, dtype=np.uint8))
+    nb_cmd = int(np.frombuffer(res, dtype=np.uint32).reshape(n, 8)[:, 4].astype(np.int64).sum()) * C.sizeof(mr_command)
+    assert np.array_equal(np.frombuffer(ppool, dtype=np.uint8, count=nb_cmd), np.frombuffer(pool, dtype=np.uint8, count=nb_cmd))
     st = plan.stats()
     assert st["solver"] == "hub" and st["num_sources"] >= 645_000, st
     props = ld.label_properties(res, pool, n, keys[q_src], keys[q_dst])

@@ -533,7 +533,9 @@ def test_device_fetch_matches_host_decode(eng, monkeypatch, max_cmds):
     """mr_plan_fetch expands the records on the device (mr_k_decode.hip) and copies the
     ABI arrays once; MR_HOST_DECODE=1 keeps the host decoder.  Both must write the same
     bytes: invalid queries, labels in the overflow pool (few command slots), Time-first
-    Fleetfoot labels, and a caller pool too short for every label (MR_ERR_CAPACITY)."""
+    Fleetfoot labels, and a caller pool too short for every label (MR_ERR_CAPACITY).
+    "pinned": the device path into page-locked caller arrays (mr_host_register: direct
+    DMA, no stage)."""
     import ctypes as C
     from marshrutka_amd.abi import MR_ERR_CAPACITY, mr_command, mr_query, mr_result
     from marshrutka_amd import pathfinder as pf
@@ -544,7 +546,7 @@ def test_device_fetch_matches_host_decode(eng, monkeypatch, max_cmds):
     qs[77] = (qs[77][0], CellIndex(2, 1, 999, 0))
     for params in (Params(), Params(fleetfoot=2, sort_by=(SORT_TIME, SORT_MONEY), use_sfm=True)):
         out = {}
-        for mode in ("device", "host"):
+        for mode in ("device", "pinned", "host"):
             if mode == "host":
                 monkeypatch.setenv("MR_HOST_DECODE", "1")
             else:
@@ -554,11 +556,18 @@ def test_device_fetch_matches_host_decode(eng, monkeypatch, max_cmds):
             for cap in (len(qs) * 24, 500):
                 res = (mr_result * len(qs))()
                 pool = (mr_command * cap)()
+                if mode == "pinned":
+                    pf.pin_host(res)
+                    pf.pin_host(pool)
                 st = pf.lib().mr_plan_fetch(plan.handle, res, pool, cap)
+                if mode == "pinned":
+                    pf.unpin_host(res)
+                    pf.unpin_host(pool)
                 out[(mode, cap)] = (st, bytes(res), bytes(pool))
         for cap in (len(qs) * 24, 500):
-            d, h = out[("device", cap)], out[("host", cap)]
-            assert d[0] == h[0], (cap, d[0], h[0])
-            assert d[1] == h[1], cap
-            assert d[2] == h[2], cap
+            for mode in ("device", "pinned"):
+                d, h = out[(mode, cap)], out[("host", cap)]
+                assert d[0] == h[0], (mode, cap, d[0], h[0])
+                assert d[1] == h[1], (mode, cap)
+                assert d[2] == h[2], (mode, cap)
         assert out[("device", 500)][0] == MR_ERR_CAPACITY or out[("device", 500)][0] < 0
