@@ -290,7 +290,9 @@ double mr_plan_kernel_ms(mr_plan *plan, uint32_t *n_launches);
 /* Frees the device blocks the engine keeps for reuse by later plans (plan buffers go
  * back to a per-device cache of up to 16 GiB when a plan is destroyed, so creating the
  * next plan needs no hipMalloc).  Blocks of live plans are untouched; safe at any time.
- * mr_grid_destroy trims too, and a failing device allocation trims and retries once. */
+ * mr_grid_destroy trims too, and a failing device allocation trims and retries once.
+ * It also releases the host arrays kept for the next plans' grouping (at most 256 MiB
+ * per element type). */
 void mr_cache_trim(void);
 /* Page-locks [p, p + bytes) of caller memory (hipHostRegister) that mr_plan_fetch then
  * fills by direct DMA instead of through the engine's pinned stage and a host copy: for

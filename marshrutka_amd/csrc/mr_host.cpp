@@ -669,11 +669,22 @@ namespace {
 // Per-batch host arrays recycled across plans.  A fresh array of a million entries is
 // mapped page by page on first touch (~1 k faults per 4 MB, the pool's threads all taking
 // the address-space lock); a recycled one is mapped already, and keeps its size, so a
-// resize to a batch no larger writes nothing.  Up to kSpareMax arrays per type are kept.
+// resize to a batch no larger writes nothing.  Up to kSpareMax arrays and kMaxBytes per
+// type are kept (mr_cache_trim releases them).
 template <class T> struct SpareVecs {
-    static constexpr size_t kSpareMax = 16, kMinBytes = size_t(1) << 16;
+    static constexpr size_t kSpareMax = 16, kMinBytes = size_t(1) << 16, kMaxBytes = size_t(256) << 20;
     std::mutex mu;
     std::vector<std::vector<T>> v;
+    size_t bytes() const {
+        size_t b = 0;
+        for (const std::vector<T> &a : v) b += a.capacity() * sizeof(T);
+        return b;
+    }
+    void clear() {
+        std::lock_guard<std::mutex> lk(mu);
+        v.clear();
+        v.shrink_to_fit();
+    }
     static SpareVecs &get() {
         static SpareVecs *s = new SpareVecs();
         return *s;
@@ -701,10 +712,12 @@ template <class T> static void spare_take(std::vector<T> &out, size_t n) {
     out.resize(n);
 }
 template <class T> static void spare_put(std::vector<T> &v) {
-    if (v.capacity() * sizeof(T) < SpareVecs<T>::kMinBytes) return;
+    const size_t vb = v.capacity() * sizeof(T);
+    if (vb < SpareVecs<T>::kMinBytes || vb > SpareVecs<T>::kMaxBytes) return;
     SpareVecs<T> &sv = SpareVecs<T>::get();
     std::lock_guard<std::mutex> lk(sv.mu);
-    if (sv.v.size() >= SpareVecs<T>::kSpareMax) {  // drop the smallest
+    // drop the smallest while full (by count or bytes), unless v is no larger
+    while (!sv.v.empty() && (sv.v.size() >= SpareVecs<T>::kSpareMax || sv.bytes() + vb > SpareVecs<T>::kMaxBytes)) {
         size_t k = 0;
         for (size_t i = 1; i < sv.v.size(); ++i)
             if (sv.v[i].capacity() < sv.v[k].capacity()) k = i;
@@ -1414,7 +1427,11 @@ static hipError_t dev_malloc(void **p, size_t bytes) {
     return e;
 }
 
-extern "C" void mr_cache_trim(void) { trim_cache_all(); }
+extern "C" void mr_cache_trim(void) {
+    trim_cache_all();
+    SpareVecs<uint32_t>::get().clear();
+    SpareVecs<int32_t>::get().clear();
+}
 
 extern "C" int mr_host_register(void *p, uint64_t bytes) {
     if (!p || !bytes) return fail(MR_ERR_INVALID_ARG, "mr_host_register: null or empty range");
