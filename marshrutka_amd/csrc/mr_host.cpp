@@ -1615,7 +1615,22 @@ static void use_slot(mr_plan *pl, uint32_t i) {
 // launch and the hub launch that ends a pass on its own (last_launch marks the
 // kernel whose last workgroup resets the per-pass counters).
 static int upload_args(mr_plan *pl) {
-    auto put = [](KArgs *d, const KArgs &k) { return hipMemcpy(d, &k, sizeof(KArgs), hipMemcpyHostToDevice) == hipSuccess; };
+    // every block queued on the plan's stream, then one synchronisation (a blocking copy
+    // each cost ~10 us: up to six per plan); the host copies live in `held` until then.
+    // Callers hold a drained plan, so nothing of the stream's is in flight.
+    KArgs held[6];
+    uint32_t nh = 0;
+    bool ok = true;
+    auto put = [&](KArgs *d, const KArgs &k) {
+        held[nh] = k;
+        ok = ok && hipMemcpyAsync(d, &held[nh], sizeof(KArgs), hipMemcpyHostToDevice, pl->stream) == hipSuccess;
+        ++nh;
+        return ok;
+    };
+    struct Drain {
+        mr_plan *pl;
+        ~Drain() { (void)hipStreamSynchronize(pl->stream); }
+    } drain{pl};
     KArgs k = pl->ka;
     const bool hub = pl->hp.hub;
     // tests: MR_DBG_INJECT_SLOT=<slot> makes the fill of that slot's passes raise a
@@ -1647,7 +1662,7 @@ static int upload_args(mr_plan *pl) {
         }
         if (pl->d_args_lane && (!put(pl->d_args_lane, k) || !put(pl->d_args_lane_last, l))) return MR_ERR_DEVICE;
     }
-    return MR_OK;
+    return ok && hipStreamSynchronize(pl->stream) == hipSuccess ? MR_OK : MR_ERR_DEVICE;
 }
 
 // The lane kernel adds metrics without overflow checks and keeps distances in 16
@@ -2574,9 +2589,10 @@ static int decode_record(const mr_grid *g, const CmdScale &cs, const OutResult &
     return MR_OK;
 }
 
-static int check_device_errors(mr_plan *pl, uint32_t &flags) {
+static int check_device_errors(mr_plan *pl, uint32_t &flags, uint32_t *ctr_out = nullptr) {
     uint32_t ctr[kCtrWords];
     if (int st = read_counters(pl, ctr)) return st;
+    if (ctr_out) std::memcpy(ctr_out, ctr, sizeof(ctr));  // (read before the flags are collected)
     flags = ctr[kCtrFlags];
     if (flags) (void)hipMemset(pl->d_counter + kCtrFlags, 0, 4);  // collected
     // overlap plans: the other slots' counter blocks belong to earlier passes; their
@@ -2640,12 +2656,9 @@ static int check_device_errors(mr_plan *pl, uint32_t &flags) {
 // than max_cmds commands come back with status MR_ERR_CAPACITY in *over.
 static int plan_collect(mr_plan *pl, std::vector<OutResult> &res, std::vector<OutCmd> &cmd,
                         std::vector<OutCmd> &ovf) {
-    if (!plan_sync(pl)) return fail(MR_ERR_DEVICE, "sync");
-    uint32_t flags = 0;
-    int st = check_device_errors(pl, flags);
+    uint32_t flags = 0, ctr[kCtrWords];
+    const int st = check_device_errors(pl, flags, ctr);  // (syncs the plan)
     if (st != MR_OK) return st;
-    uint32_t ctr[kCtrWords];
-    if ((st = read_counters(pl, ctr))) return st;
     const uint32_t nov = std::min(ctr[kCtrLastOvf], pl->ka.ovf_cap);
     ovf.resize(nov);
     if (nov && hipMemcpy(ovf.data(), pl->ka.ovf, size_t(nov) * sizeof(OutCmd), hipMemcpyDeviceToHost) != hipSuccess)
@@ -2699,11 +2712,8 @@ static bool plan_fetch_device(mr_plan *pl, mr_result *results, mr_command *pool,
     const mr_cell_index *idx_rank = grid_idx_rank(pl->grid, pl->device);
     if (!idx_rank) return false;
     const double tm0 = timing_on() ? now_ms() : 0.0;
-    if (!plan_sync(pl)) return (ret = fail(MR_ERR_DEVICE, "sync")), true;
-    uint32_t flags = 0;
-    if ((ret = check_device_errors(pl, flags)) != MR_OK) return true;
-    uint32_t ctr[kCtrWords];
-    if ((ret = read_counters(pl, ctr)) != MR_OK) return true;
+    uint32_t flags = 0, ctr[kCtrWords];
+    if ((ret = check_device_errors(pl, flags, ctr)) != MR_OK) return true;  // (syncs the plan)
     const uint32_t nov = std::min(ctr[kCtrLastOvf], pl->ka.ovf_cap);
     const uint64_t bound = uint64_t(nrec) * mc + nov, pcap = std::min<uint64_t>(pool_cap, std::max<uint64_t>(bound, 1));
     const CmdScale cs = cmd_scale(hp);
