@@ -1831,16 +1831,35 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
             }
             const std::vector<uint32_t> *arr[4] = {&hp.src_v, &hp.q_begin, &hp.q_dst, &hp.q_id};
             const size_t at[4] = {a0, a1, a2, a3};
+            // words [a, b) of the block: the pieces of the four arrays that fall in them
+            auto pack_range = [&](size_t a, size_t b) {
+                for (int j = 0; j < 4; ++j) {
+                    const size_t s = std::max(a, at[j]), e = std::min(b, at[j] + arr[j]->size());
+                    if (s < e) std::memcpy(pack + s, arr[j]->data() + (s - at[j]), (e - s) * 4);
+                }
+            };
             HostPool &hpool = HostPool::get();
-            const uint32_t parts = words >= (size_t(1) << 18) ? hpool.size() : 1u;
-            hpool.run(4 * parts, [&](uint32_t j) {
-                const std::vector<uint32_t> &v = *arr[j / parts];
-                const uint32_t pt = j % parts, lo = chunk_lo(uint32_t(v.size()), parts, pt),
-                               hi = chunk_lo(uint32_t(v.size()), parts, pt + 1);
-                if (hi > lo) std::memcpy(pack + at[j / parts] + lo, v.data() + lo, size_t(hi - lo) * 4);
-            });
-            if (hipMemcpy(pl->d_qblock, pack, words * 4, hipMemcpyHostToDevice) != hipSuccess)
-                return bail(fail(MR_ERR_DEVICE, "upload query block"));
+            if (words < (size_t(1) << 18)) {
+                pack_range(0, words);
+                if (hipMemcpy(pl->d_qblock, pack, words * 4, hipMemcpyHostToDevice) != hipSuccess)
+                    return bail(fail(MR_ERR_DEVICE, "upload query block"));
+            } else {
+                // 4 MB chunks: the DMA of chunk c runs while host threads pack chunk c + 1
+                // (packed and copied in one go: 0.85 ms at 1M queries)
+                constexpr size_t kUp = size_t(1) << 20;
+                const uint32_t parts = hpool.size();
+                hipError_t e = hipSuccess;
+                for (size_t lo = 0; lo < words && e == hipSuccess; lo += kUp) {
+                    const size_t hi = std::min(words, lo + kUp);
+                    hpool.run(parts, [&](uint32_t pt) {
+                        pack_range(lo + (hi - lo) * pt / parts, lo + (hi - lo) * (pt + 1) / parts);
+                    });
+                    e = hipMemcpyAsync(pl->d_qblock + lo, pack + lo, (hi - lo) * 4, hipMemcpyHostToDevice, nullptr);
+                }
+                // (the stage is not unlocked, nor the block used, before the copies are done)
+                const hipError_t es = hipStreamSynchronize(nullptr);
+                if (e != hipSuccess || es != hipSuccess) return bail(fail(MR_ERR_DEVICE, "upload query block"));
+            }
         }
         pl->d_src = pl->d_qblock + a0;
         pl->d_qb = pl->d_qblock + a1;
