@@ -272,7 +272,8 @@ typedef struct mr_plan_stats {
     uint32_t certified_sources; /* of fallback_sources, those answered by the fixed-point certificate
                                    in the last pass (the rest ran the SSSP kernel; ABI 6) */
     uint32_t lanes_per_source;  /* hub solver: lanes that share one source's Dijkstra over the
-                                   specials: 1 hub_lane_kernel, 8 or 16 hub_group_kernel, 0 hub_kernel
+                                   specials: 1 hub_lane_kernel, 8, 16 or 32 hub_group_kernel (by
+                                   plan size, or MR_HUB_GROUP), 0 hub_kernel
                                    and the others (ABI 7) */
 } mr_plan_stats;
 enum {
@@ -292,7 +293,8 @@ double mr_plan_kernel_ms(mr_plan *plan, uint32_t *n_launches);
  * next plan needs no hipMalloc).  Blocks of live plans are untouched; safe at any time.
  * mr_grid_destroy trims too, and a failing device allocation trims and retries once.
  * It also releases the host arrays kept for the next plans' grouping (at most 256 MiB
- * per element type). */
+ * per element type) and every calling thread's grouping scratch (about 20 B per query of
+ * that thread's largest batch; a plan being created keeps its own until it returns). */
 void mr_cache_trim(void);
 /* Page-locks [p, p + bytes) of caller memory (hipHostRegister) that mr_plan_fetch then
  * fills by direct DMA instead of through the engine's pinned stage and a host copy: for

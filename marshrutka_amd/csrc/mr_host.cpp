@@ -12,6 +12,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <mutex>
 #include <chrono>
 #include <thread>
@@ -21,6 +22,7 @@
 
 #include "../../include/marshrutka_pf.h"
 #include "mr_engine.hpp"
+#include "mr_pool.hpp"
 
 // hipMalloc for the grid's long-lived device tables: on out-of-memory the plan block
 // cache (below) is trimmed and the allocation retried once
@@ -83,86 +85,6 @@ static int fail(int code, const std::string &msg) {
     return code;
 }
 
-// ------------------------------------------------------------------ host threads
-// A persistent pool for the per-batch host work (grouping a batch by source, the fetch's
-// copies): run(n, fn) calls fn(i) for every i in [0, n) on the pool's workers and the
-// calling thread, and returns when every call has finished.  One job at a time (callers
-// are serialised); min(16, hardware threads) threads (MR_HOST_THREADS overrides: a GPU
-// box's share of its host is 16 CPUs, more threads would only time-slice).
-class HostPool {
-  public:
-    static HostPool &get() {
-        static HostPool *p = new HostPool();  // never destroyed: workers wait on it at exit
-        return *p;
-    }
-    uint32_t size() const { return nthreads_; }
-    void run(uint32_t n, const std::function<void(uint32_t)> &fn) {
-        if (n == 0) return;
-        if (nthreads_ <= 1 || n == 1) {
-            for (uint32_t i = 0; i < n; ++i) fn(i);
-            return;
-        }
-        std::lock_guard<std::mutex> job(job_mu_);
-        fn_ = &fn;
-        n_ = n;
-        done_.store(0, std::memory_order_relaxed);
-        const uint64_t g = (ticket_.load(std::memory_order_relaxed) >> 32) + 1;
-        ticket_.store(g << 32, std::memory_order_release);  // publishes fn_ and n_ with the new job
-        if (sleepers_.load(std::memory_order_acquire) > 0) {
-            std::lock_guard<std::mutex> lk(mu_);
-            cv_.notify_all();
-        }
-        work(g);
-        while (done_.load(std::memory_order_acquire) < n) __builtin_ia32_pause();
-    }
-
-  private:
-    HostPool() {
-        nthreads_ = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-        if (const char *e = std::getenv("MR_HOST_THREADS")) nthreads_ = uint32_t(std::max(1, std::min(64, std::atoi(e))));
-        for (uint32_t t = 1; t < nthreads_; ++t) std::thread([this] { loop(); }).detach();
-    }
-    // Items are claimed by compare-and-swap on {job, next item}: a worker still in an
-    // old job can never take (and lose) an item of the next one.
-    void work(uint64_t g) {
-        for (;;) {
-            uint64_t v = ticket_.load(std::memory_order_acquire);
-            if ((v >> 32) != g || uint32_t(v) >= n_) return;
-            if (!ticket_.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel)) continue;
-            (*fn_)(uint32_t(v));
-            done_.fetch_add(1, std::memory_order_release);
-        }
-    }
-    void loop() {
-        uint64_t seen = 0;
-        for (;;) {
-            uint64_t g = ticket_.load(std::memory_order_acquire) >> 32;
-            // spin briefly for the next job (a batch's phases come back to back), then sleep: a
-            // longer spin burns the CPU quota a GPU box gives the process (cgroup cpu.max)
-            for (int k = 0; g == seen && k < 2000; ++k) {
-                __builtin_ia32_pause();
-                g = ticket_.load(std::memory_order_acquire) >> 32;
-            }
-            if (g == seen) {
-                std::unique_lock<std::mutex> lk(mu_);
-                sleepers_.fetch_add(1, std::memory_order_acq_rel);
-                cv_.wait(lk, [&] { return (ticket_.load(std::memory_order_acquire) >> 32) != seen; });
-                sleepers_.fetch_sub(1, std::memory_order_acq_rel);
-                g = ticket_.load(std::memory_order_acquire) >> 32;
-            }
-            seen = g;
-            work(g);
-        }
-    }
-    uint32_t nthreads_ = 1;
-    std::mutex job_mu_, mu_;
-    std::condition_variable cv_;
-    const std::function<void(uint32_t)> *fn_ = nullptr;
-    uint32_t n_ = 0;
-    std::atomic<uint64_t> ticket_{0};  // job << 32 | next item
-    std::atomic<uint32_t> done_{0};
-    std::atomic<int> sleepers_{0};
-};
 // [0, n) in `parts` near-equal ranges: range p is [chunk_lo(n, parts, p), chunk_lo(n, parts, p + 1))
 static inline uint32_t chunk_lo(uint32_t n, uint32_t parts, uint32_t p) { return uint32_t(uint64_t(n) * p / parts); }
 
@@ -769,6 +691,36 @@ static uint32_t caravan_unit_time(uint32_t route_guru) {
     return uint32_t((240ull * rgn[rg] + rgd[rg] - 1) / rgd[rg]);
 }
 
+// Per calling thread: the grouping scratch of build_plan (about 20 B per query of the
+// thread's largest batch), registered so that mr_cache_trim can release every thread's.
+struct GroupScratch;
+static std::mutex g_scratch_mu;
+static std::vector<GroupScratch *> g_scratch;
+struct GroupScratch {
+    std::mutex mu;  // held by build_plan while it uses the vectors, and by the trim
+    std::vector<uint64_t> kv, tmp;  // source << 32 | query index
+    std::vector<uint32_t> hist, dst;
+    GroupScratch() {
+        std::lock_guard<std::mutex> lk(g_scratch_mu);
+        g_scratch.push_back(this);
+    }
+    ~GroupScratch() {
+        std::lock_guard<std::mutex> lk(g_scratch_mu);
+        g_scratch.erase(std::find(g_scratch.begin(), g_scratch.end(), this));
+    }
+    void release() {
+        std::lock_guard<std::mutex> lk(mu);
+        std::vector<uint64_t>().swap(kv);
+        std::vector<uint64_t>().swap(tmp);
+        std::vector<uint32_t>().swap(hist);
+        std::vector<uint32_t>().swap(dst);
+    }
+};
+static void trim_group_scratch() {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    for (GroupScratch *g : g_scratch) g->release();
+}
+
 static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs, uint32_t n, uint32_t max_cmds,
                       HostPlan &hp) {
     const double tbs = timing_on() ? now_ms() : 0.0;
@@ -972,11 +924,11 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     const uint32_t passes = V < (1u << (2 * kBits)) ? 2u : 3u;
     // scratch reused across plans of this thread (no fresh pages per batch); the pool's
     // workers reach it through these references (a thread_local named inside a lambda
-    // would be the worker's own)
-    static thread_local std::vector<uint64_t> kv_s, tmp_s;  // source << 32 | query index
-    static thread_local std::vector<uint32_t> hist_s, dst_s;
-    std::vector<uint64_t> &kv = kv_s, &tmp = tmp_s;
-    std::vector<uint32_t> &hist = hist_s, &qs_dst = dst_s;
+    // would be the worker's own); mr_cache_trim releases it
+    static thread_local GroupScratch scr;
+    std::lock_guard<std::mutex> scr_lk(scr.mu);
+    std::vector<uint64_t> &kv = scr.kv, &tmp = scr.tmp;
+    std::vector<uint32_t> &hist = scr.hist, &qs_dst = scr.dst;
     kv.resize(n);
     tmp.resize(n);
     qs_dst.resize(n);
@@ -1344,13 +1296,18 @@ static PinnedStage &stage_down() {
     return *s;
 }
 // true when [p, p + bytes) is page-locked host memory HIP can DMA into directly
-static bool host_pinned(const void *p) {
-    hipPointerAttribute_t at{};
-    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    return at.type == hipMemoryTypeHost && at.hostPointer != nullptr;
+// Caller ranges page-locked through mr_host_register: start -> bytes.  A fetch takes the
+// direct DMA only into a destination range one of them covers whole (a range registered
+// shorter than the fetch writes goes through the pinned stage).
+static std::mutex g_reg_mu;
+static std::map<uintptr_t, size_t> g_reg;
+static bool host_pinned(const void *p, size_t bytes) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_reg.upper_bound(a);
+    if (it == g_reg.begin()) return false;
+    --it;
+    return a >= it->first && a + bytes <= it->first + it->second;
 }
 // Device -> host copies of `n` segments into caller memory on `s`: straight DMA when the
 // destination is pinned, else through the pinned stage in 16 MB chunks, two in flight:
@@ -1364,7 +1321,7 @@ static hipError_t copy_d2h(const D2HSeg *seg, int n, hipStream_t s) {
     hipError_t e = hipSuccess;
     bool direct = true;
     for (int i = 0; i < n; ++i)
-        if (seg[i].bytes && !host_pinned(seg[i].dst)) direct = false;
+        if (seg[i].bytes && !host_pinned(seg[i].dst, seg[i].bytes)) direct = false;
     if (direct) {
         for (int i = 0; i < n && e == hipSuccess; ++i)
             if (seg[i].bytes) e = hipMemcpyAsync(seg[i].dst, seg[i].src, seg[i].bytes, hipMemcpyDeviceToHost, s);
@@ -1431,6 +1388,7 @@ extern "C" void mr_cache_trim(void) {
     trim_cache_all();
     SpareVecs<uint32_t>::get().clear();
     SpareVecs<int32_t>::get().clear();
+    trim_group_scratch();
 }
 
 extern "C" int mr_host_register(void *p, uint64_t bytes) {
@@ -1438,11 +1396,17 @@ extern "C" int mr_host_register(void *p, uint64_t bytes) {
     if (!mr_device_available()) return fail(MR_ERR_NO_DEVICE, "no gfx950 device visible");
     const hipError_t e = hipHostRegister(p, size_t(bytes), hipHostRegisterDefault);
     if (e != hipSuccess) return fail(MR_ERR_DEVICE, std::string("hipHostRegister: ") + hipGetErrorString(e));
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_reg[reinterpret_cast<uintptr_t>(p)] = size_t(bytes);
     return MR_OK;
 }
 
 extern "C" int mr_host_unregister(void *p) {
     if (!p) return fail(MR_ERR_INVALID_ARG, "mr_host_unregister: null pointer");
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        g_reg.erase(reinterpret_cast<uintptr_t>(p));
+    }
     const hipError_t e = hipHostUnregister(p);
     if (e != hipSuccess) return fail(MR_ERR_DEVICE, std::string("hipHostUnregister: ") + hipGetErrorString(e));
     return MR_OK;

@@ -28,7 +28,7 @@ import pytest
 
 import label_digest as ld
 from golden_util import as_expected
-from marshrutka_amd.abi import SORT_MONEY, SORT_TIME, CellIndex, Params, mr_command
+from marshrutka_amd.abi import SORT_MONEY, SORT_TIME, CellIndex, Params, mr_command, mr_result
 from marshrutka_amd.mapgen import SyntheticMap, random_queries, random_query_cells
 
 pytestmark = pytest.mark.gpu
@@ -70,19 +70,27 @@ def _sources_of_every_kind(m, rng):
     return srcs
 
 
-def test_c4_full_scale(eng, oracle_lib, c4_map):
-    """configs[3] at its stated size: the bench's whole 1M-query batch on one GPU (645k
-    unique sources), every label property-checked, plus 1 000 destinations for each of
-    32 sources against the oracle's Dijkstra from each source: 16 of every kind (Center,
-    border-1 cells, campfires, on-axis, random) and the 16 batch sources with the most
-    queries (whose batch queries are checked too), and 64 batch queries against the
-    oracle's single-query eval."""
+@pytest.fixture(scope="module")
+def c4_batch(c4_map):
+    """bench.py's configs[3] batch: 1M uniform queries on the 1025^2 map (645k sources),
+    as row-major cells and as mr_query records."""
     m, arr = c4_map
+    uni_src, uni_dst = random_query_cells(m, 1_000_000, 4096 + 17)
+    return uni_src, uni_dst, m.query_array(uni_src, uni_dst, arr)
+
+
+@pytest.fixture(scope="module")
+def c4_sources(c4_map, c4_batch):
+    """32 sources with 1 000 destinations each and the oracle's Dijkstra from each of
+    them (mro_sssp_digest_batch: every cell's label, src/pathfinder.rs:219-246 run to
+    completion): 16 of every kind (Center, border-1 cells, campfires, on-axis, random)
+    and the 16 batch sources with the most queries."""
+    import oracle_lib
+    oracle_lib.build()
+    m, arr = c4_map
+    uni_src, _, _ = c4_batch
     V = m.size * m.size
-    keys = ld.cell_keys(arr)
     rng = random.Random(4096)
-    uni_src, uni_dst = random_query_cells(m, 1_000_000, 4096 + 17)  # bench.py's c4 batch
-    nb = len(uni_src)
     srcs = _sources_of_every_kind(m, rng)
     cnt = np.bincount(uni_src, minlength=V)
     for c in np.argsort(-cnt, kind="stable"):
@@ -91,17 +99,37 @@ def test_c4_full_scale(eng, oracle_lib, c4_map):
         ci = m.index_at(int(c))
         if ci not in srcs:
             srcs.append(ci)
-    extra_src, extra_dst = [], []
     cf_cells = [m.cell_of(c) for c in m.campfires()]
+    dsts = []
     for s in srcs:
-        d = rng.sample(range(V), 1000 - len(cf_cells) - 2) + cf_cells + [m.cell_of(CellIndex.center()), m.cell_of(s)]
-        extra_src += [m.cell_of(s)] * len(d)
-        extra_dst += d
-    q_src = np.concatenate([uni_src, np.array(extra_src)])
-    q_dst = np.concatenate([uni_dst, np.array(extra_dst)])
-    n = len(q_src)
+        dsts.append(np.array(rng.sample(range(V), 1000 - len(cf_cells) - 2) + cf_cells +
+                             [m.cell_of(CellIndex.center()), m.cell_of(s)], dtype=np.int64))
+    og = oracle_lib.OracleGrid.from_array(arr)
+    want = og.sssp_digests(Params(), srcs, threads=ORACLE_THREADS)
+    return srcs, dsts, want, og
+
+
+def _tail_digests(res, pool, n_total: int, first: int):
+    """label_digest fields of records first..n_total-1 of a fetch (no work on the rest)."""
+    raw = np.frombuffer(res, dtype=np.uint8, count=n_total * C.sizeof(mr_result))
+    return ld.digests(raw[first * C.sizeof(mr_result):], pool, n_total - first)
+
+
+def test_c4_full_scale(eng, c4_map, c4_batch, c4_sources):
+    """configs[3] at its stated size: the bench's whole 1M-query batch on one GPU (645k
+    unique sources) as the bench runs it.  Every source runs on hub_lane_kernel (plan
+    stats), every label is property-checked, and the batch's own queries are compared
+    with the oracle: >= 2 000 of them through the oracle's Dijkstra from the busiest
+    batch sources (whole label: metrics, command count, command-list digest), and 64
+    random ones through the oracle's single-query FindPath::eval."""
+    m, arr = c4_map
+    uni_src, uni_dst, qarr = c4_batch
+    _, _, _, og = c4_sources
+    V = m.size * m.size
+    keys = ld.cell_keys(arr)
+    n = len(uni_src)
     g = eng.MapGrid.from_array(arr)
-    plan = eng.Plan(g, Params(), None, max_cmds=6, query_array=m.query_array(q_src, q_dst, arr))
+    plan = eng.Plan(g, Params(), None, max_cmds=6, query_array=qarr)
     plan.run()
     plan.run()  # the bench's steady state: a rerun of the same plan
     res, pool = plan.fetch_raw()
@@ -117,26 +145,107 @@ def test_c4_full_scale(eng, oracle_lib, c4_map):
     assert np.array_equal(np.frombuffer(ppool, dtype=np.uint8, count=nb_cmd), np.frombuffer(pool, dtype=np.uint8, count=nb_cmd))
     st = plan.stats()
     assert st["solver"] == "hub" and st["num_sources"] >= 645_000, st
-    props = ld.label_properties(res, pool, n, keys[q_src], keys[q_dst])
+    # the headline kernel answered every source of the batch
+    assert st["lanes_per_source"] == 1 and st["lane_sources"] == st["num_sources"], st
+    assert st["fallback_sources"] == 0, st
+    props = ld.label_properties(res, pool, n, keys[uni_src], keys[uni_dst])
     assert all(v == 0 for v in props.values()), props
     got = ld.digests(res, pool, n)
-    og = oracle_lib.OracleGrid.from_array(arr)
-    want = og.sssp_digests(Params(), srcs, threads=ORACLE_THREADS)
-    for i, s in enumerate(srcs):
-        sel = np.arange(nb + i * 1000, nb + (i + 1) * 1000)
-        bad = ld.mismatches(got, {f: want[f][i] for f in want}, idx_got=sel, idx_exp=q_dst[sel])
-        assert bad.size == 0, (str(s), len(bad), [str(m.index_at(int(q_dst[sel][j]))) for j in bad[:4]])
-        mine = np.nonzero(uni_src[:nb] == m.cell_of(s))[0]  # the source's own queries of the batch
-        if mine.size:
-            bad = ld.mismatches(got, {f: want[f][i] for f in want}, idx_got=mine, idx_exp=q_dst[mine])
-            assert bad.size == 0, (str(s), "batch queries", len(bad))
+    # >= 2 000 batch queries: every query of the busiest batch sources, one oracle
+    # Dijkstra per source, 32 sources at a time (33 MB of digests per source)
+    cnt = np.bincount(uni_src, minlength=V)
+    busiest = np.argsort(-cnt, kind="stable")
+    take = int(np.searchsorted(np.cumsum(cnt[busiest]), 2000)) + 1
+    checked = 0
+    for lo in range(0, take, 32):
+        chunk = busiest[lo:lo + 32]
+        want = og.sssp_digests(Params(), [m.index_at(int(c)) for c in chunk], threads=ORACLE_THREADS)
+        for i, c in enumerate(chunk):
+            mine = np.nonzero(uni_src == c)[0]
+            bad = ld.mismatches(got, {f: want[f][i] for f in want}, idx_got=mine, idx_exp=uni_dst[mine])
+            assert bad.size == 0, (str(m.index_at(int(c))), len(bad), [str(m.index_at(int(uni_dst[mine][j]))) for j in bad[:4]])
+            checked += mine.size
+        del want
+    assert checked >= 2000, checked
     # uniform batch queries from random sources: the oracle's own single-query eval
-    sample = rng.sample(range(nb), 64)
+    rng = random.Random(4097)
+    sample = rng.sample(range(n), 64)
     pairs = [(m.index_at(int(uni_src[i])), m.index_at(int(uni_dst[i]))) for i in sample]
     eres, epool = og.find_path_batch_raw(Params(), pairs, threads=ORACLE_THREADS)
     ed = ld.digests(eres, epool, len(sample))
     bad = ld.mismatches(got, ed, idx_got=np.array(sample))
     assert bad.size == 0, [pairs[j] for j in bad[:4]]
+
+
+def test_c4_lane_kernel_vs_oracle(eng, c4_map, c4_batch, c4_sources):
+    """hub_lane_kernel itself against the oracle at configs[3]: 32 sources x 1 000
+    destinations (32 000 labels), each plan the bench's whole 1M batch plus every one
+    of the 32 sources with at most 32 queries in all (kLaneMaxQ: a source with more
+    runs on hub_kernel), so each compared label is the lane kernel's read-off; the plan
+    stats prove that every source of every plan ran on it."""
+    m, arr = c4_map
+    uni_src, uni_dst, qarr = c4_batch
+    srcs, dsts, want, _ = c4_sources
+    V = m.size * m.size
+    nb = len(uni_src)
+    cnt = np.bincount(uni_src, minlength=V)
+    caps = [32 - int(cnt[m.cell_of(s)]) for s in srcs]
+    assert min(caps) >= 16, caps
+    n_plans = max(-(-len(d) // c) for d, c in zip(dsts, caps))
+    g = eng.MapGrid.from_array(arr)
+    bufs = None
+    compared = 0
+    for p in range(n_plans):
+        ex_src, ex_dst, owner = [], [], []
+        for i, (s, d, c) in enumerate(zip(srcs, dsts, caps)):
+            piece = d[p * c:(p + 1) * c]
+            ex_src.append(np.full(len(piece), m.cell_of(s), dtype=np.int64))
+            ex_dst.append(piece)
+            owner.append(np.full(len(piece), i, dtype=np.int64))
+        ex_src, ex_dst, owner = np.concatenate(ex_src), np.concatenate(ex_dst), np.concatenate(owner)
+        q = np.concatenate([qarr, m.query_array(ex_src, ex_dst, arr)])
+        plan = eng.Plan(g, Params(), None, max_cmds=6, query_array=q)
+        plan.run()
+        st = plan.stats()
+        assert st["solver"] == "hub" and st["lanes_per_source"] == 1, st
+        assert st["lane_sources"] == st["num_sources"] and st["fallback_sources"] == 0, st
+        if bufs is None:
+            bufs = eng.fetch_buffers(len(q) + 1024, 6)
+        res, pool = plan.fetch_raw(bufs)
+        got = _tail_digests(res, pool, len(q), nb)
+        for i in range(len(srcs)):
+            sel = np.nonzero(owner == i)[0]
+            if sel.size == 0:
+                continue
+            bad = ld.mismatches(got, {f: want[f][i] for f in want}, idx_got=sel, idx_exp=ex_dst[sel])
+            assert bad.size == 0, (p, str(srcs[i]), len(bad), [str(m.index_at(int(ex_dst[sel][j]))) for j in bad[:4]])
+            compared += sel.size
+        del plan
+    assert compared == sum(len(d) for d in dsts) >= 32_000, compared
+
+
+def test_c4_busy_sources_hub_kernel(eng, c4_map, c4_batch, c4_sources):
+    """The same 32 sources with all 1 000 destinations each in one plan beside the 1M
+    batch: sources with more than 32 queries leave the lane kernel for hub_kernel (a
+    lane per query), so this compares hub_kernel's read-off at configs[3]'s size."""
+    m, arr = c4_map
+    uni_src, uni_dst, qarr = c4_batch
+    srcs, dsts, want, _ = c4_sources
+    nb = len(uni_src)
+    ex_src = np.concatenate([np.full(len(d), m.cell_of(s), dtype=np.int64) for s, d in zip(srcs, dsts)])
+    ex_dst = np.concatenate(dsts)
+    q = np.concatenate([qarr, m.query_array(ex_src, ex_dst, arr)])
+    g = eng.MapGrid.from_array(arr)
+    plan = eng.Plan(g, Params(), None, max_cmds=6, query_array=q)
+    plan.run()
+    st = plan.stats()
+    assert st["solver"] == "hub" and st["lane_sources"] == st["num_sources"] - len(srcs), st
+    res, pool = plan.fetch_raw()
+    got = _tail_digests(res, pool, len(q), nb)
+    for i, s in enumerate(srcs):
+        sel = np.arange(i * 1000, (i + 1) * 1000)
+        bad = ld.mismatches(got, {f: want[f][i] for f in want}, idx_got=sel, idx_exp=ex_dst[sel])
+        assert bad.size == 0, (str(s), len(bad), [str(m.index_at(int(ex_dst[sel][j]))) for j in bad[:4]])
 
 
 @pytest.mark.parametrize("ff", [1, 3])

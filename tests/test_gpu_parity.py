@@ -168,6 +168,29 @@ def test_c2_full_batch(eng, oracle_lib):
     check(eng, oracle_lib, m, Params(), qs, "c2 full batch")
 
 
+@pytest.mark.parametrize("group", [8, 16, 32])
+def test_c2_full_batch_group_kernel(eng, oracle_lib, monkeypatch, group):
+    """configs[1]'s whole batch on hub_group_kernel at each group size (MR_HUB_GROUP),
+    the plan stats proving which kernel answered, every label against the oracle's
+    FindPath::eval (src/pathfinder.rs:199-248)."""
+    for v in ("MR_HUB_LANE", "MR_HUB_FALLBACK_ALL", "MR_ALGO", "MR_HUB_WIDE", "MR_HUB_SPW"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setenv("MR_HUB_GROUP", str(group))
+    monkeypatch.setenv("MR_HUB_GROUP_FORCE", "1")
+    m = SyntheticMap(65, campfires_per_homeland=4, seed=2024)  # bench.py c2
+    qs = random_queries(m, 10_000, 2024 + 17)
+    g = eng.MapGrid(m.cells())
+    plan = eng.Plan(g, Params(), qs)
+    plan.run()
+    st = plan.stats()
+    # lanes_per_source = G: every source of the plan ran on hub_group_kernel
+    assert st["solver"] == "hub" and st["lanes_per_source"] == group and st["fallback_sources"] == 0, st
+    got = plan.fetch()
+    exp = oracle_lib.OracleGrid(m.cells()).find_path_batch(Params(), qs, threads=0)
+    bad = [(q, e, r) for q, e, r in zip(qs, exp, got) if as_expected(e) != as_expected(r)]
+    assert not bad, f"G={group}: {len(bad)}/{len(qs)} mismatches; first: {bad[0]}"
+
+
 @pytest.mark.parametrize("max_cmds", [1, 3, 16])
 def test_certificate_sfm_fleetfoot_vs_oracle(eng, oracle_lib, monkeypatch, max_cmds):
     """The scenario whose two plans once disagreed (tools/plan_diff.py; DESIGN.md
