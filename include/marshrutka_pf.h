@@ -102,6 +102,19 @@ const char *mr_parse_error(void);
 int mr_grid_from_html(const char *html, uint64_t len, mr_grid **out);
 /* MapGrid::square_size / homeland_size (src/grid.rs:280-282) */
 uint32_t mr_grid_square_size(const mr_grid *grid);
+/* The grid's Scroll-of-Escape region table of `homeland` (grid preprocessing, the
+ * analogue of MapGrid::parse's nearest-campfire pass, src/grid.rs:134-230,297-325):
+ * the regions are the homeland's campfires in CellIndex order, a cell belongs to the
+ * region of its nearest campfire (the Center to none), and for every row-major cell v
+ * and region r the table holds {distance, rank} of the nearest cell of r: walk distance
+ * on the 4-grid without the Center, ties by the cell's CellIndex rank; {0xFFFFFFFF,
+ * 0xFFFFFFFF} for the Center.  Built on the current device on first use (by this call or
+ * by a hub plan's creation) and shared by the grid's plans.  *nreg = regions; *build_ms =
+ * the build's wall time in ms (upload of the cells' regions and the device passes).
+ * With out != NULL copies the V x nreg x 2 words (cap_words must hold them, else
+ * MR_ERR_CAPACITY).  MR_ERR_NO_DEVICE without a gfx950 device; no reference counterpart. */
+int mr_grid_region_table(mr_grid *grid, uint32_t homeland, uint32_t *out, uint64_t cap_words, uint32_t *nreg,
+                         double *build_ms);
 
 /* ---- query parameters: every FindPath field (src/pathfinder.rs:183-196) -- */
 enum { MR_SORT_LEGS = 0, MR_SORT_TIME = 1, MR_SORT_MONEY = 2 }; /* CostComparator, src/cost.rs:76-81 */

@@ -52,7 +52,9 @@ hipError_t launch_hub_lane(const KArgs *d_args, const uint32_t perm[3], uint32_t
                            hipStream_t stream);
 uint32_t hub_group_slots(uint32_t NS, uint32_t G);
 uint32_t lane_blob_build(const SpecialStatic *sp, uint32_t NS, uint32_t nreg, uint32_t TM, uint32_t rgt,
-                         const uint32_t *near_tab, std::vector<uint32_t> &blob);
+                         const uint32_t *near_sp, std::vector<uint32_t> &blob);
+hipError_t region_table_build(const uint16_t *reg, const uint32_t *rank, uint32_t S, uint32_t nreg, void *tab,
+                              void *axis, hipStream_t stream);
 uint32_t hub_group_lds_bytes(uint32_t NS, uint32_t nreg, uint32_t G);
 hipError_t launch_hub_group(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t n,
                             uint32_t G, hipStream_t stream);
@@ -165,12 +167,13 @@ struct mr_grid {
     std::vector<uint32_t> campfires;       // vertex ids, CellIndex order
     std::vector<uint32_t> nearest[4];      // nearest campfire vertex per homeland (kNone32)
     // hub solver: per homeland, the regions (campfires of the homeland, CellIndex order) and
-    // for every vertex and region the nearest cell of that region by walk distance avoiding
-    // the Center, ties by CellIndex order: near[2*(v*nreg+r)] = {distance, rank of the cell}
+    // (on the device, d_near) for every vertex and region the nearest cell of that region by
+    // walk distance avoiding the Center, ties by CellIndex order:
+    // near[2*(v*nreg+r)] = {distance, rank of the cell}
     mutable std::mutex near_mu;
     mutable std::vector<uint32_t> regions[4];
-    mutable std::vector<uint32_t> near[4];
-    mutable bool near_built[4] = {false, false, false, false};
+    mutable bool regions_built[4] = {false, false, false, false};
+    mutable double region_ms[4] = {0, 0, 0, 0};  // device build time of each table (ms, wall)
     // wide hub solver: per homeland, each region's boundary cells (cells of the region
     // with a neighbour outside it, the Center excluded), {x | y << 16, rank}, by region
     mutable std::vector<uint32_t> rb_off[4], rb_cell[4];
@@ -444,89 +447,100 @@ extern "C" int mr_device_available(void) {
     return std::strncmp(prop->gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
 }
 
-// Region tables for the hub solver (built lazily, once per grid and homeland).
-// A multi-source BFS per region over the grid minus the Center (walks cannot
-// cross it, src/pathfinder.rs:30-53) propagates (distance, rank of origin)
-// lexicographic minima along shortest paths.
-static const std::vector<uint32_t> &region_table(const mr_grid *g, int h, const std::vector<uint32_t> *&regions) {
+// The SoE regions of homeland h: its Homeland-indexed campfires in CellIndex order
+// (src/grid.rs:143-146), one region per campfire.
+static const std::vector<uint32_t> &region_list(const mr_grid *g, int h) {
     std::lock_guard<std::mutex> lk(g->near_mu);
-    regions = &g->regions[h];
-    if (g->near_built[h]) return g->near[h];
-    const uint32_t V = g->V, S = g->S;
-    std::vector<uint32_t> regs;
-    for (uint32_t v : g->campfires) {
-        const mr_cell_index &c = g->idx[v];
-        if (c.kind == MR_CELL_HOMELAND && c.sub == h) regs.push_back(v);  // campfires: CellIndex order
+    if (!g->regions_built[h]) {
+        std::vector<uint32_t> regs;
+        for (uint32_t v : g->campfires) {
+            const mr_cell_index &c = g->idx[v];
+            if (c.kind == MR_CELL_HOMELAND && c.sub == h) regs.push_back(v);
+        }
+        g->regions[h] = std::move(regs);
+        g->regions_built[h] = true;
     }
-    const uint32_t nreg = uint32_t(regs.size());
-    std::vector<uint32_t> rid(V, kNone32);
-    for (uint32_t r = 0; r < nreg; ++r) rid[regs[r]] = r;
-    std::vector<uint32_t> tab(size_t(V) * nreg * 2, kNone32);
-    // one BFS per region, spread over host threads (c5: 64 regions x 16.8 M cells)
-    std::atomic<uint32_t> next{0};
-    auto worker = [&]() {
-    std::vector<uint32_t> dist(V), org(V), cur, nxt;
-    for (uint32_t r = next++; r < nreg; r = next++) {
-        std::fill(dist.begin(), dist.end(), kNone32);
-        cur.clear();
-        for (uint32_t v = 0; v < V; ++v) {
-            if (v == g->vc || g->nearest[h][v] != regs[r]) continue;
-            dist[v] = 0;
-            org[v] = v;
-            cur.push_back(v);
-        }
-        for (uint32_t d = 0; !cur.empty(); ++d) {
-            nxt.clear();
-            for (uint32_t u : cur) {
-                const uint32_t x = u % S, y = u / S;
-                const uint32_t nb[4] = {x > 0 ? u - 1 : kNone32, x + 1 < S ? u + 1 : kNone32,
-                                        y > 0 ? u - S : kNone32, y + 1 < S ? u + S : kNone32};
-                for (uint32_t w : nb) {
-                    if (w == kNone32 || w == g->vc) continue;
-                    if (dist[w] == kNone32) {
-                        dist[w] = d + 1;
-                        org[w] = org[u];
-                        nxt.push_back(w);
-                    } else if (dist[w] == d + 1 && g->rank[org[u]] < g->rank[org[w]]) {
-                        org[w] = org[u];
-                    }
-                }
-            }
-            cur.swap(nxt);
-        }
-        for (uint32_t v = 0; v < V; ++v) {
-            tab[(size_t(v) * nreg + r) * 2] = dist[v];
-            tab[(size_t(v) * nreg + r) * 2 + 1] = dist[v] == kNone32 ? kNone32 : g->rank[org[v]];
-        }
-    }
-    };
-    const uint32_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    const uint32_t nt = std::min<uint32_t>(hw, std::max<uint32_t>(1, nreg));
-    std::vector<std::thread> pool;
-    for (uint32_t i = 1; i < nt; ++i) pool.emplace_back(worker);
-    worker();
-    for (auto &t : pool) t.join();
-    g->regions[h] = std::move(regs);
-    g->near[h] = std::move(tab);
-    g->near_built[h] = true;
-    (void)rid;
-    return g->near[h];
+    return g->regions[h];
 }
 
-// The region table of homeland h on the current device (uploaded once per grid).
-static const uint32_t *region_table_device(const mr_grid *g, int h, const std::vector<uint32_t> &tab) {
+// The region table of homeland h on the current device, built there once per grid
+// (mr_k_region.hip: a separable L1 transform of (distance, rank) in three passes) from
+// the region of every cell (the nearest campfire, computed at grid creation) and the
+// device rank table.  The grid's plans share it; nullptr on a device error.
+static const uint32_t *region_table_device(const mr_grid *g, int h, const uint32_t *d_rank) {
+    const std::vector<uint32_t> &regs = region_list(g, h);
     std::lock_guard<std::mutex> lk(g->near_mu);
-    if (!g->d_near[h]) {
-        uint32_t *d = nullptr;
-        const size_t bytes = std::max<size_t>(tab.size(), 1) * 4;
-        if (dev_malloc(reinterpret_cast<void **>(&d), bytes) != hipSuccess) return nullptr;
-        if (!tab.empty() && hipMemcpy(d, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
-            (void)hipFree(d);
-            return nullptr;
-        }
-        g->d_near[h] = d;
+    if (g->d_near[h]) return g->d_near[h];
+    const double t0 = now_ms();
+    const uint32_t V = g->V, S = g->S, nreg = uint32_t(regs.size());
+    std::unordered_map<uint32_t, uint16_t> rid;
+    for (uint32_t r = 0; r < nreg; ++r) rid[regs[r]] = uint16_t(r);
+    std::vector<uint16_t> reg(V, 0xFFFFu);
+    {
+        const std::vector<uint32_t> &nearest = g->nearest[h];
+        HostPool &pool = HostPool::get();
+        const uint32_t parts = std::max(1u, std::min(pool.size(), V / 65536u));
+        pool.run(parts, [&](uint32_t pt) {
+            uint32_t last = kNone32;
+            uint16_t lr = 0xFFFFu;
+            for (uint32_t v = chunk_lo(V, parts, pt); v < chunk_lo(V, parts, pt + 1); ++v) {
+                const uint32_t c = nearest[v];
+                if (v == g->vc || c == kNone32) continue;
+                if (c != last) {
+                    auto it = rid.find(c);
+                    lr = it == rid.end() ? 0xFFFFu : it->second;
+                    last = c;
+                }
+                reg[v] = lr;
+            }
+        });
     }
-    return g->d_near[h];
+    uint32_t *d = nullptr;
+    uint16_t *d_reg = nullptr;
+    void *d_axis = nullptr;
+    hipStream_t st = nullptr;
+    bool ok = nreg > 0 && dev_malloc(reinterpret_cast<void **>(&d), size_t(V) * nreg * 8) == hipSuccess &&
+              dev_malloc(reinterpret_cast<void **>(&d_reg), size_t(V) * 2) == hipSuccess &&
+              dev_malloc(&d_axis, size_t(2) * S * nreg * 8) == hipSuccess &&
+              hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
+              hipMemcpyAsync(d_reg, reg.data(), size_t(V) * 2, hipMemcpyHostToDevice, st) == hipSuccess &&
+              region_table_build(d_reg, d_rank, S, nreg, d, d_axis, st) == hipSuccess &&
+              hipStreamSynchronize(st) == hipSuccess;
+    if (st) (void)hipStreamDestroy(st);
+    if (d_reg) (void)hipFree(d_reg);
+    if (d_axis) (void)hipFree(d_axis);
+    if (!ok) {
+        (void)hipGetLastError();
+        if (d) (void)hipFree(d);
+        return nullptr;
+    }
+    g->d_near[h] = d;
+    g->region_ms[h] = now_ms() - t0;
+    return d;
+}
+
+// Rows of the region table for the plan's specials (t = 1 .. NS) into near_sp
+// ((NS + 1) x nreg x {distance, rank}), copied from the device table once per grid,
+// homeland and cell (cached).
+static int special_rows_from_table(const mr_grid *g, int h, const uint32_t *d_near, uint32_t nreg,
+                                   const std::vector<SpecialStatic> &sp, std::vector<uint32_t> &near_sp) {
+    const uint32_t NS = uint32_t(sp.size()) - 1;
+    near_sp.assign(size_t(NS + 1) * nreg * 2, kNone32);
+    std::lock_guard<std::mutex> lk(g->near_mu);
+    auto &cache = g->near_sp_cache[h];
+    for (uint32_t t = 1; t <= NS; ++t) {
+        const uint32_t v = sp[t].v;
+        uint32_t *row = &near_sp[size_t(t) * nreg * 2];
+        auto it = cache.find(v);
+        if (it == cache.end()) {
+            std::vector<uint32_t> r(size_t(nreg) * 2);
+            if (hipMemcpy(r.data(), d_near + size_t(v) * nreg * 2, size_t(nreg) * 8, hipMemcpyDeviceToHost) != hipSuccess)
+                return MR_ERR_DEVICE;
+            it = cache.emplace(v, std::move(r)).first;
+        }
+        std::copy(it->second.begin(), it->second.end(), row);
+    }
+    return MR_OK;
 }
 
 // Boundary cells of the regions (wide hub solver).  Seen from outside a region, its
@@ -666,7 +680,7 @@ struct HostPlan {
     uint32_t fleetfoot_raw = 0;
     bool hub = false;                       // hub solver applicable (small tables)
     bool nonlin = false;                    // hub with a non-linear run time (near-tie certification)
-    const std::vector<uint32_t> *near = nullptr;
+    bool near = false;                      // the grid's device region table (V x regions)
     uint32_t nreg = 0;
     bool wide = false;                      // hub_wide_kernel (NS > 63 or no V x regions table)
     std::vector<uint32_t> near_sp;          // wide: (NS+1) x nreg x {distance, rank} rows of the specials
@@ -840,23 +854,20 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     hp.hub = hp.wide = hp.nonlin = false;
     if ((linear || nonlin_ok) && narrow_ok && !force_wide) {
         hp.nonlin = !linear;
-        const std::vector<uint32_t> *regs = nullptr;
-        const std::vector<uint32_t> &tab = region_table(g, prm->homeland, regs);
+        const std::vector<uint32_t> &regs = region_list(g, prm->homeland);
         hp.hub = true;
-        hp.nreg = uint32_t(regs->size());
-        hp.near = &tab;
-        for (uint32_t r = 0; r < hp.nreg; ++r) hp.sp[tix((*regs)[r])].rid = r;
+        hp.nreg = uint32_t(regs.size());
+        hp.near = true;  // the device table (built at plan creation) and the specials' rows
+        for (uint32_t r = 0; r < hp.nreg; ++r) hp.sp[tix(regs[r])].rid = r;
     } else if (linear && hub_wide_spl(NS) != 0 && nregs <= 256) {
         std::vector<uint32_t> regs;
         region_bounds(g, prm->homeland, regs, hp.rb_off, hp.rb_cell);
-        if (table_ok) {  // the source's row read from the table instead of scanned
-            const std::vector<uint32_t> *tregs = nullptr;
-            hp.near = &region_table(g, prm->homeland, tregs);
-        }
+        hp.near = table_ok;  // the source's row read from the device table instead of scanned
         hp.hub = hp.wide = true;
         hp.nreg = uint32_t(regs.size());
         for (uint32_t r = 0; r < hp.nreg; ++r) hp.sp[tix(regs[r])].rid = r;
-        // the specials' rows (row 0, the source, is computed per source on the device)
+        // the specials' rows (row 0, the source, is computed per source on the device);
+        // with the table they are its rows, copied at plan creation
         const uint32_t nr = hp.nreg;
         hp.near_sp.assign(size_t(NS + 1) * nr * 2, kNone32);
         const std::vector<uint32_t> &nearh = g->nearest[prm->homeland];
@@ -867,12 +878,8 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
         // scan is O(boundary cells) per special, 28 ms a plan at c5 when done per plan).
         for (uint32_t t = 1; t <= NS; ++t) {
             const uint32_t v = order[t];
-            if (v == g->vc) continue;
+            if (v == g->vc || hp.near) continue;
             uint32_t *row = &hp.near_sp[size_t(t) * nr * 2];
-            if (hp.near) {
-                std::copy(hp.near->begin() + long(size_t(v) * nr * 2), hp.near->begin() + long(size_t(v + 1) * nr * 2), row);
-                continue;
-            }
             {
                 std::lock_guard<std::mutex> lk(g->near_mu);
                 auto it = g->near_sp_cache[prm->homeland].find(v);
@@ -1069,6 +1076,35 @@ static std::vector<uint2> build_cell(const mr_grid *g, const std::vector<uint32_
     return out;
 }
 
+// The grid's device rank tables (rank, rank_inv), uploaded on the first device that asks
+// (the caller holds near_mu); false on an upload error.
+static bool grid_rank_upload(const mr_grid *g, int dev) {
+    auto up = [](uint32_t *&d, const std::vector<uint32_t> &h) {
+        if (dev_malloc(reinterpret_cast<void **>(&d), std::max<size_t>(h.size(), 1) * 4) != hipSuccess) return false;
+        if (!h.empty() && hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(d);
+            d = nullptr;
+            return false;
+        }
+        return true;
+    };
+    if (!up(g->d_rank, g->rank)) return false;
+    if (!up(g->d_rank_inv, g->rank_inv)) {
+        (void)hipFree(g->d_rank);
+        g->d_rank = nullptr;
+        return false;
+    }
+    g->d_dev = dev;
+    return true;
+}
+// The device rank table on `dev`: the grid's shared copy, nullptr when it lives on another
+// device (or cannot be uploaded)
+static const uint32_t *grid_rank_device(const mr_grid *g, int dev) {
+    std::lock_guard<std::mutex> lk(g->near_mu);
+    if (g->d_dev == -1 && !grid_rank_upload(g, dev)) return nullptr;
+    return g->d_dev == dev ? g->d_rank : nullptr;
+}
+
 static bool grid_tables(const mr_grid *g, int dev, const HostPlan &hp, uint32_t *&rank, uint32_t *&rank_inv,
                         uint32_t *&sinfo, uint2 *&cell) {
     std::lock_guard<std::mutex> lk(g->near_mu);
@@ -1082,15 +1118,7 @@ static bool grid_tables(const mr_grid *g, int dev, const HostPlan &hp, uint32_t 
         }
         return true;
     };
-    if (g->d_dev == -1) {
-        if (!up(g->d_rank, g->rank)) return false;
-        if (!up(g->d_rank_inv, g->rank_inv)) {
-            (void)hipFree(g->d_rank);
-            g->d_rank = nullptr;
-            return false;
-        }
-        g->d_dev = dev;
-    }
+    if (g->d_dev == -1 && !grid_rank_upload(g, dev)) return false;
     uint32_t *ds = nullptr;
     uint2 *dc = nullptr;
     for (const mr_grid::SinfoDev &e : g->d_sinfo)
@@ -1382,6 +1410,35 @@ static hipError_t dev_malloc(void **p, size_t bytes) {
         e = hipMalloc(p, bytes);
     }
     return e;
+}
+
+extern "C" int mr_grid_region_table(mr_grid *g, uint32_t homeland, uint32_t *out, uint64_t cap_words, uint32_t *nreg,
+                                    double *build_ms) {
+    if (!g || homeland > 3) return fail(MR_ERR_INVALID_ARG, "mr_grid_region_table: null grid or homeland > 3");
+    if (!mr_device_available()) return fail(MR_ERR_NO_DEVICE, "no gfx950 device visible (no CPU fallback)");
+    const std::vector<uint32_t> &regs = region_list(g, int(homeland));
+    const uint64_t words = uint64_t(g->V) * regs.size() * 2;
+    if (nreg) *nreg = uint32_t(regs.size());
+    if (out && cap_words < words) return fail(MR_ERR_CAPACITY, "mr_grid_region_table: output shorter than V x nreg x 2");
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return fail(MR_ERR_DEVICE, "hipGetDevice");
+    const uint32_t *rank = grid_rank_device(g, dev);
+    uint32_t *own = nullptr;
+    if (!rank) {  // the grid's tables live on another device: this one gets its own rank copy
+        if (dev_malloc(reinterpret_cast<void **>(&own), size_t(g->V) * 4) != hipSuccess ||
+            hipMemcpy(own, g->rank.data(), size_t(g->V) * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            if (own) (void)hipFree(own);
+            return fail(MR_ERR_DEVICE, "rank table upload");
+        }
+        rank = own;
+    }
+    const uint32_t *d = region_table_device(g, int(homeland), rank);
+    if (own) (void)hipFree(own);
+    if (!d) return fail(MR_ERR_DEVICE, "region table build");
+    if (build_ms) *build_ms = g->region_ms[homeland];
+    if (out && words && hipMemcpy(out, d, words * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(MR_ERR_DEVICE, "region table copy");
+    return MR_OK;
 }
 
 extern "C" void mr_cache_trim(void) {
@@ -1939,8 +1996,10 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         if (pmalloc(reinterpret_cast<void **>(&pl->d_fb), std::max<size_t>(nsrc, 1) * 4) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "hub tables"));
         if (hp.near) {
-            ka.near = region_table_device(g, prm->homeland, *hp.near);
-            if (!ka.near) return bail(fail(MR_ERR_DEVICE, "region table upload"));
+            ka.near = region_table_device(g, prm->homeland, pl->d_rank);
+            if (!ka.near) return bail(fail(MR_ERR_DEVICE, "region table build"));
+            if ((st = special_rows_from_table(g, prm->homeland, ka.near, hp.nreg, hp.sp, hp.near_sp)) != MR_OK)
+                return bail(fail(st, "region table rows"));
         }
         if (hp.wide) {
             std::vector<uint32_t> off(hp.rb_off->begin(), hp.rb_off->end());
@@ -2032,7 +2091,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         if (pl->n_lane) {  // the lane / group kernels' LDS block, built once per plan
             const uint32_t TM = pl->lane_g ? pl->lane_g * hub_group_slots(NS, pl->lane_g) : hub_lane_entries(NS);
             std::vector<uint32_t> blob;
-            lane_blob_build(hp.sp.data(), NS, hp.nreg, TM, hp.p.rgt, hp.near->data(), blob);
+            lane_blob_build(hp.sp.data(), NS, hp.nreg, TM, hp.p.rgt, hp.near_sp.data(), blob);
             if (upload(pl->d_lane_blob, blob) != MR_OK) return bail(fail(MR_ERR_DEVICE, "lane tables"));
             ka.lane_blob = reinterpret_cast<const uint4 *>(pl->d_lane_blob);
         }

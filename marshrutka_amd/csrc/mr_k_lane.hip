@@ -50,10 +50,11 @@ static const void *lane_fn(const uint32_t perm[3], uint32_t NS) {
 // The lane and group kernels' per-plan LDS block for a table of TM entries (layout:
 // lane_off_* in mr_hub_lane.hpp): the specials' records, their rows of the grid's region
 // table, the pair table of walks / caravans / SoE-region candidates and its row masks
-// (LaneHub::from_s), the specials' cells by hash, and the header words.  near_tab is the
-// grid's region table ({distance, rank} per vertex and region).  Returns the byte size.
+// (LaneHub::from_s), the specials' cells by hash, and the header words.  near_sp holds the
+// specials' rows of the grid's region table ({distance, rank} per special t and region, at
+// 2 * (t * nreg + r)).  Returns the byte size.
 uint32_t lane_blob_build(const SpecialStatic *sp, uint32_t NS, uint32_t nreg, uint32_t TM, uint32_t rgt,
-                         const uint32_t *near_tab, std::vector<uint32_t> &blob) {
+                         const uint32_t *near_sp, std::vector<uint32_t> &blob) {
     const uint32_t bytes = lane_blob_bytes(NS, nreg, TM);
     blob.assign(bytes / 4, 0u);
     char *base = reinterpret_cast<char *>(blob.data());
@@ -61,7 +62,7 @@ uint32_t lane_blob_build(const SpecialStatic *sp, uint32_t NS, uint32_t nreg, ui
     uint2 *nearl = reinterpret_cast<uint2 *>(base + lane_off_near(NS));
     for (uint32_t t = 1; t <= NS; ++t)
         for (uint32_t r = 0; r < nreg; ++r) {
-            const uint32_t *e = near_tab + 2ull * ((unsigned long long)sp[t].v * nreg + r);
+            const uint32_t *e = near_sp + 2ull * ((unsigned long long)t * nreg + r);
             nearl[t * nreg + r] = make_uint2(e[0], e[1]);
         }
     uint4 *pa = reinterpret_cast<uint4 *>(base + lane_off_pt(NS, nreg));

@@ -28,7 +28,7 @@ EXPORTED_SYMBOLS = [
     "mr_find_path_batch", "mr_plan_create", "mr_plan_create_ex", "mr_plan_run", "mr_plan_fetch", "mr_plan_device_outputs",
     "mr_plan_num_sources", "mr_plan_record_queries", "mr_plan_fallback_sources", "mr_plan_wait", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_cache_trim", "mr_host_register", "mr_host_unregister", "mr_plan_bind_outputs", "mr_plan_bind_outputs_ex", "mr_decode_records", "mr_abi_version", "mr_last_error",
     "mr_device_available", "mr_parse_map_html", "mr_parse_error", "mr_grid_from_html",
-    "mr_command_time", "mr_duration_display", "mr_render_schedule",
+    "mr_command_time", "mr_duration_display", "mr_render_schedule", "mr_grid_region_table",
     "mr_sssp_plan_create", "mr_sssp_records", "mr_sssp_device_records", "mr_sssp_record_pitch", "mr_sssp_device_tables", "mr_sssp_label", "mr_sssp_labels", "mr_plan_fill_ms",
 ]
 
@@ -131,6 +131,9 @@ def lib():
         L.mr_sssp_label.restype = C.c_int
         L.mr_sssp_labels.argtypes = [vp, C.c_uint32, C.POINTER(mr_result), C.POINTER(mr_command), C.c_uint64]
         L.mr_sssp_labels.restype = C.c_int
+        L.mr_grid_region_table.argtypes = [vp, C.c_uint32, vp, C.c_uint64, C.POINTER(C.c_uint32),
+                                           C.POINTER(C.c_double)]
+        L.mr_grid_region_table.restype = C.c_int
         L.mr_plan_fill_ms.argtypes = [vp]
         L.mr_plan_fill_ms.restype = C.c_double
         _lib = L
@@ -216,6 +219,24 @@ class MapGrid:
 
     def homeland_size(self) -> int:  # src/grid.rs:280-282
         return self.square_size // 2
+
+    def region_table(self, homeland: int, fetch: bool = True):
+        """mr_grid_region_table: (regions, build_ms, table) — the device-built SoE region
+        table of `homeland` as a (V, regions, 2) uint32 array ({distance, rank}), or None
+        with fetch=False (build / timing only)."""
+        import numpy as np
+        nreg, ms = C.c_uint32(), C.c_double()
+        st = lib().mr_grid_region_table(self.handle, homeland, None, 0, C.byref(nreg), C.byref(ms))
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+        if not fetch:
+            return nreg.value, ms.value, None
+        V = self.square_size ** 2
+        out = np.empty((V, nreg.value, 2), dtype=np.uint32)
+        st = lib().mr_grid_region_table(self.handle, homeland, out.ctypes.data, out.size, C.byref(nreg), C.byref(ms))
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+        return nreg.value, ms.value, out
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -974,3 +974,60 @@ extern "C" int mro_duration_display(int64_t seconds, char *buf, uint32_t cap) {
     }
     return int(s.size());
 }
+
+// The hub solver's SoE region table (TEST INFRASTRUCTURE: the checker of the engine's
+// device-built mr_grid_region_table).  A region is the set of cells whose nearest
+// campfire of the query homeland (src/grid.rs:297-325) is one campfire; walks cannot
+// cross the Center (its only edges are CentralMoves, src/pathfinder.rs:30-53).  One
+// breadth-first search per region over the grid minus the Center from all of its
+// cells, keeping per cell the least (distance, rank of the origin cell).
+// region[v]: region index of row-major cell v (0xFFFFFFFF: none), rank[v]: its
+// CellIndex rank; out: S*S x nreg x {distance, rank}.
+extern "C" int mro_region_table_bfs(uint32_t S, const uint32_t *rank, const uint32_t *region, uint32_t nreg,
+                                    uint32_t *out, uint32_t threads) {
+    if (S < 3 || !(S & 1u) || !rank || !region || !out) return MR_ERR_INVALID_ARG;
+    const uint32_t V = S * S, vc = (S / 2) * S + S / 2, NONE = 0xFFFFFFFFu;
+    std::atomic<uint32_t> next{0};
+    auto worker = [&]() {
+        std::vector<uint32_t> dist(V), org(V), cur, nxt;
+        for (uint32_t r = next++; r < nreg; r = next++) {
+            std::fill(dist.begin(), dist.end(), NONE);
+            cur.clear();
+            for (uint32_t v = 0; v < V; ++v)
+                if (v != vc && region[v] == r) {
+                    dist[v] = 0;
+                    org[v] = v;
+                    cur.push_back(v);
+                }
+            for (uint32_t d = 0; !cur.empty(); ++d) {
+                nxt.clear();
+                for (uint32_t u : cur) {
+                    const uint32_t x = u % S, y = u / S;
+                    const uint32_t nb[4] = {x > 0 ? u - 1 : NONE, x + 1 < S ? u + 1 : NONE, y > 0 ? u - S : NONE,
+                                            y + 1 < S ? u + S : NONE};
+                    for (uint32_t w : nb) {
+                        if (w == NONE || w == vc) continue;
+                        if (dist[w] == NONE) {
+                            dist[w] = d + 1;
+                            org[w] = org[u];
+                            nxt.push_back(w);
+                        } else if (dist[w] == d + 1 && rank[org[u]] < rank[org[w]]) {
+                            org[w] = org[u];
+                        }
+                    }
+                }
+                cur.swap(nxt);
+            }
+            for (uint32_t v = 0; v < V; ++v) {
+                out[(size_t(v) * nreg + r) * 2] = dist[v];
+                out[(size_t(v) * nreg + r) * 2 + 1] = dist[v] == NONE ? NONE : rank[org[v]];
+            }
+        }
+    };
+    if (threads == 0) threads = std::max(1u, std::thread::hardware_concurrency());
+    std::vector<std::thread> pool;
+    for (uint32_t i = 1; i < std::min(threads, std::max(nreg, 1u)); ++i) pool.emplace_back(worker);
+    worker();
+    for (auto &t : pool) t.join();
+    return MR_OK;
+}

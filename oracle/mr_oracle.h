@@ -55,6 +55,13 @@ int mro_find_path_batch(const mro_grid *grid, const mr_params *params, const mr_
  * src/pathfinder.rs:279-285).  Returns the length written (< cap). */
 int mro_duration_display(int64_t seconds, char *buf, uint32_t cap);
 
+/* The hub solver's SoE region table by one BFS per region over the grid minus the
+ * Center (the checker of mr_grid_region_table): region[v] = region index of row-major
+ * cell v (0xFFFFFFFF: none), rank[v] = its CellIndex rank; out = S*S x nreg x
+ * {distance, rank of the nearest region cell}. */
+int mro_region_table_bfs(uint32_t S, const uint32_t *rank, const uint32_t *region, uint32_t nreg, uint32_t *out,
+                         uint32_t threads);
+
 #ifdef __cplusplus
 }
 #endif

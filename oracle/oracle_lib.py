@@ -55,6 +55,8 @@ def lib():
         L.mro_sssp_digest_batch.argtypes = [C.c_void_p, C.POINTER(mr_params), C.POINTER(mr_cell_index), C.c_uint32,
                                             C.c_uint32, vp, vp, vp, vp, vp, vp]
         L.mro_sssp_digest_batch.restype = C.c_int
+        L.mro_region_table_bfs.argtypes = [C.c_uint32, vp, vp, C.c_uint32, vp, C.c_uint32]
+        L.mro_region_table_bfs.restype = C.c_int
         L.mro_duration_display.argtypes = [C.c_int64, C.c_char_p, C.c_uint32]
         L.mro_duration_display.restype = C.c_int
         _lib = L
@@ -158,6 +160,19 @@ class OracleGrid:
         if st != MR_OK:
             raise ValueError(f"oracle sssp_digests failed: {st}")
         return out
+
+
+def region_table_bfs(S: int, rank, region, nreg: int, threads: int = 0):
+    """mro_region_table_bfs: the SoE region table of a map (one BFS per region over the
+    grid minus the Center) as a (S*S, nreg, 2) uint32 array {distance, rank}."""
+    import numpy as np
+    rank = np.ascontiguousarray(rank, dtype=np.uint32)
+    region = np.ascontiguousarray(region, dtype=np.uint32)
+    out = np.empty((S * S, nreg, 2), dtype=np.uint32)
+    st = lib().mro_region_table_bfs(S, rank.ctypes.data, region.ctypes.data, nreg, out.ctypes.data, threads)
+    if st != MR_OK:
+        raise ValueError(f"oracle region_table_bfs failed: {st}")
+    return out
 
 
 def duration_display(seconds: int) -> str:
