@@ -367,7 +367,16 @@ def main():
     # the app's defaults (src/app.rs:782-811), with the workload's sort order
     params = Params(sort_by=wl["sort"]) if "sort" in wl else Params()
     all_dst = bool(wl.get("all_destinations"))
-    grid = pathfinder.MapGrid.from_array(m.cells_array())
+    cells_in = m.cells_array()
+    tg = time.perf_counter()
+    grid = pathfinder.MapGrid.from_array(cells_in)
+    grid_ms = (time.perf_counter() - tg) * 1e3
+    # grid preprocessing the hub plans need: the query homeland's region table, built on
+    # the device (mr_grid_region_table); timed here, before the first plan would build it
+    nreg, region_ms, _ = grid.region_table(params.homeland, fetch=False)
+    grid_load = {"grid_create_ms": grid_ms, "region_table_ms": region_ms, "regions": nreg,
+                 "note": "mr_grid_create on the host (layout check, ranks, nearest campfires) and the "
+                         "device build of the V x regions table (DESIGN.md section 4), once per map"}
     fb_total_probe = None  # N > 1 query batches: sources the probe pass saw re-solved
     if all_dst:
         # distinct sources, a contiguous block per rank; no cross-rank data path
@@ -384,8 +393,10 @@ def main():
         # need no Python object each); a source's key is its cell
         q_src, q_dst = random_query_cells(m, total_q, wl["seed"] + 17)
         cells_arr = m.cells_array()
-        keys = q_src.tolist()
+        keys = q_src
+        ts = time.perf_counter()
         shards = shard_by_source(keys, world)
+        shard_ms = (time.perf_counter() - ts) * 1e3
 
         def my_queries(sh):
             idx = np.asarray(sh, dtype=np.int64)
@@ -590,6 +601,9 @@ def main():
                      if stats["solver"] in ("hub", "hub_wide") else
                      "SSSP kernel: SURVEY 8d bytes, V*20 B per unique source"},
     }
+    out["grid_load"] = grid_load
+    if not all_dst and world > 1:
+        out["config"]["shard_ms"] = shard_ms  # shard_by_source over the whole batch (host, untimed)
     if gather_check is not None:
         out["gather_check"] = gather_check
     if rank == 0 and not all_dst and args.e2e_reps > 0:

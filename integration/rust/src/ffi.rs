@@ -158,6 +158,8 @@ extern "C" {
     pub fn mr_parse_error() -> *const c_char;
     pub fn mr_grid_from_html(html: *const c_char, len: u64, out: *mut *mut mr_grid) -> c_int;
     pub fn mr_grid_square_size(grid: *const mr_grid) -> u32;
+    pub fn mr_grid_region_table(grid: *mut mr_grid, homeland: u32, out: *mut u32, cap_words: u64, nreg: *mut u32,
+                                build_ms: *mut f64) -> c_int;
     pub fn mr_params_default(p: *mut mr_params);
 
     // FindPath::eval (src/pathfinder.rs:199-248), one query and batches

@@ -245,6 +245,121 @@ struct mr_grid {
 
 static constexpr uint32_t kNone32 = 0xFFFFFFFFu;
 
+// CellIndex rank (position in the derived Ord, src/index.rs:41-46) of a canonical index
+// on a complete map of homeland size H: Center, then Homeland{h, (x, y)} by (h, x, y),
+// then Border{b, shift} by (b, shift)
+static inline uint32_t closed_rank(const mr_cell_index &c, uint32_t H) {
+    if (c.kind == MR_CELL_CENTER) return 0;
+    if (c.kind == MR_CELL_HOMELAND) return 1u + c.sub * H * H + (c.x - 1u) * H + (c.y - 1u);
+    return 1u + 4u * H * H + c.sub * H + (c.x - 1u);
+}
+
+// Grid creation's fast path (host threads, no hash map): the cells' labels are every
+// canonical index of homeland size H, laid out by one unit step per homeland axis and
+// border (any orientation).  It checks every cell against that layout (a bijection onto
+// the V canonical indices), the index adjacency (src/pathfinder.rs:24-138) against the
+// geometric 4-neighbourhood on the cells near the axes, the Center and the edges (every
+// other cell repeats the neighbourhood of a homeland cell (2, 2)), and computes the
+// ranks in closed form.  False (nothing decided) sends the map to the generic path,
+// which also reports what is wrong with it.
+static bool grid_fast_layout(mr_grid *g, const mr_cell *cells) {
+    const uint32_t n = g->V, S = g->S, H = g->H;
+    if (H < 3) return false;
+    HostPool &pool = HostPool::get();
+    const uint32_t parts = std::max(1u, std::min(pool.size(), n / 65536u));
+    std::atomic<bool> bad{false};
+    pool.run(parts, [&](uint32_t pt) {
+        for (uint32_t i = chunk_lo(n, parts, pt); i < chunk_lo(n, parts, pt + 1); ++i) {
+            const mr_cell_index c = build_index(cells[i].index);  // src/index.rs:419-431
+            if (!canonical(c) || cells[i].poi > MR_POI_FORUM || cells[i].index.reserved ||
+                (c.kind != MR_CELL_CENTER && (c.x > H || c.y > H)))
+                bad.store(true, std::memory_order_relaxed);
+            g->idx[i] = c;
+            g->poi[i] = cells[i].poi;
+        }
+    });
+    const uint32_t vc = H * S + H;
+    if (bad.load() || g->idx[vc].kind != MR_CELL_CENTER) return false;
+    // the unit steps, from the 5 x 5 cells round the Center
+    uint32_t hv[4][3], bv[4];
+    for (auto &r : hv) r[0] = r[1] = r[2] = kNone32;
+    for (uint32_t &x : bv) x = kNone32;
+    for (int dy = -2; dy <= 2; ++dy)
+        for (int dx = -2; dx <= 2; ++dx) {
+            const uint32_t v = uint32_t(int(vc) + dy * int(S) + dx);
+            const mr_cell_index &c = g->idx[v];
+            if (c.kind == MR_CELL_HOMELAND) {
+                const int k = c.x == 1 && c.y == 1 ? 0 : (c.x == 2 && c.y == 1 ? 1 : (c.x == 1 && c.y == 2 ? 2 : -1));
+                if (k >= 0) hv[c.sub][k] = v;
+            } else if (c.kind == MR_CELL_BORDER && c.x == 1) {
+                bv[c.sub] = v;
+            }
+        }
+    for (int h = 0; h < 4; ++h) {
+        if (hv[h][0] == kNone32 || hv[h][1] == kNone32 || hv[h][2] == kNone32 || bv[h] == kNone32) return false;
+        g->ux[h] = int64_t(hv[h][1]) - int64_t(hv[h][0]);
+        g->uy[h] = int64_t(hv[h][2]) - int64_t(hv[h][0]);
+        g->ub[h] = int64_t(bv[h]) - int64_t(vc);
+        if (int64_t(hv[h][0]) != int64_t(vc) + g->ux[h] + g->uy[h]) return false;
+    }
+    // every cell where its index puts it
+    pool.run(parts, [&](uint32_t pt) {
+        for (uint32_t v = chunk_lo(n, parts, pt); v < chunk_lo(n, parts, pt + 1); ++v) {
+            const mr_cell_index &c = g->idx[v];
+            int64_t w = -1;
+            if (c.kind == MR_CELL_CENTER) w = vc;
+            else if (c.kind == MR_CELL_HOMELAND) w = int64_t(vc) + c.x * g->ux[c.sub] + c.y * g->uy[c.sub];
+            else w = int64_t(vc) + c.x * g->ub[c.sub];
+            if (w != int64_t(v)) bad.store(true, std::memory_order_relaxed);
+        }
+    });
+    if (bad.load()) return false;
+    // the index adjacency on the band of cells within 2 of an axis or of the map's edge
+    pool.run(parts, [&](uint32_t pt) {
+        std::vector<uint64_t> a, b;
+        for (uint32_t y = chunk_lo(S, parts, pt); y < chunk_lo(S, parts, pt + 1); ++y) {
+            const uint32_t ay = uint32_t(std::abs(int(y) - int(H)));
+            for (uint32_t x = 0; x < S; ++x) {
+                const uint32_t ax = uint32_t(std::abs(int(x) - int(H)));
+                if (std::min(ax, ay) > 2 && std::max(ax, ay) + 1 < H) {
+                    // interior run of the row: jump to the band cell before the axis / edge
+                    x = ax < H ? (x < H ? H - 3 : S - 3) : x;
+                    continue;
+                }
+                const uint32_t v = y * S + x;
+                index_neighbours(g->idx[v], int(H), a);
+                b.clear();
+                if (x > 0) b.push_back(ci_key(g->idx[v - 1]));
+                if (x + 1 < S) b.push_back(ci_key(g->idx[v + 1]));
+                if (y > 0) b.push_back(ci_key(g->idx[v - S]));
+                if (y + 1 < S) b.push_back(ci_key(g->idx[v + S]));
+                std::sort(b.begin(), b.end());
+                if (a != b) bad.store(true, std::memory_order_relaxed);
+            }
+        }
+    });
+    if (bad.load()) return false;
+    g->vc = vc;
+    g->fast = g->exact = true;
+    g->rank.resize(n);
+    g->rank_inv.resize(n);
+    std::atomic<bool> std_ok{true};
+    pool.run(parts, [&](uint32_t pt) {
+        bool ok = true;
+        for (uint32_t v = chunk_lo(n, parts, pt); v < chunk_lo(n, parts, pt + 1); ++v) {
+            const uint32_t r = closed_rank(g->idx[v], H);
+            g->rank[v] = r;
+            g->rank_inv[r] = v;
+            ok = ok && r == std_rank(g->gx(v), g->gy(v), H);
+        }
+        if (!ok) std_ok.store(false, std::memory_order_relaxed);
+    });
+    g->rank_std = std_ok.load() && !std::getenv("MR_RANK_TABLE");  // (tests: force the table)
+    for (uint32_t r = 0; r < n; ++r)
+        if (g->poi[g->rank_inv[r]] == MR_POI_CAMPFIRE) g->campfires.push_back(g->rank_inv[r]);
+    return true;
+}
+
 extern "C" int mr_grid_create(const mr_cell *cells, uint32_t n, mr_grid **out) {
     if (!cells || !out) return fail(MR_ERR_INVALID_ARG, "null argument");
     *out = nullptr;
@@ -259,139 +374,199 @@ extern "C" int mr_grid_create(const mr_cell *cells, uint32_t n, mr_grid **out) {
     g->V = n;
     g->idx.resize(n);
     g->poi.resize(n);
-    g->index.reserve(n * 2);
-    for (uint32_t i = 0; i < n; ++i) {
-        mr_cell_index c = cells[i].index;
-        // MapGrid::parse builds every index canonically (src/index.rs:419-431)
-        c = build_index(c);
-        if (!canonical(c) || cells[i].poi > MR_POI_FORUM || cells[i].index.reserved) {
+    // the standard layout in any orientation: the fast path; anything else, the checks
+    // cell by cell with a hash map of the indices (and their error messages)
+    const double tg0 = timing_on() ? now_ms() : 0.0;
+    if (!grid_fast_layout(g, cells)) {
+        g->fast = g->exact = false;
+        g->campfires.clear();
+        g->index.reserve(n * 2);
+        for (uint32_t i = 0; i < n; ++i) {
+            mr_cell_index c = cells[i].index;
+            // MapGrid::parse builds every index canonically (src/index.rs:419-431)
+            c = build_index(c);
+            if (!canonical(c) || cells[i].poi > MR_POI_FORUM || cells[i].index.reserved) {
+                delete g;
+                return fail(MR_ERR_INVALID_GRID, "invalid cell index or poi at cell " + std::to_string(i));
+            }
+            if (!g->index.emplace(ci_key(c), i).second) {
+                delete g;
+                return fail(MR_ERR_INVALID_GRID, "duplicate cell index at cell " + std::to_string(i));
+            }
+            g->idx[i] = c;
+            g->poi[i] = cells[i].poi;
+        }
+        uint32_t vc;
+        if (!g->find(ci_make(MR_CELL_CENTER, 0, 0, 0), vc) || g->gx(vc) != 0 || g->gy(vc) != 0) {
             delete g;
-            return fail(MR_ERR_INVALID_GRID, "invalid cell index or poi at cell " + std::to_string(i));
+            return fail(MR_ERR_INVALID_GRID, "Center missing or not at (0,0) (src/grid.rs:122-133)");
         }
-        if (!g->index.emplace(ci_key(c), i).second) {
-            delete g;
-            return fail(MR_ERR_INVALID_GRID, "duplicate cell index at cell " + std::to_string(i));
-        }
-        g->idx[i] = c;
-        g->poi[i] = cells[i].poi;
-    }
-    uint32_t vc;
-    if (!g->find(ci_make(MR_CELL_CENTER, 0, 0, 0), vc) || g->gx(vc) != 0 || g->gy(vc) != 0) {
-        delete g;
-        return fail(MR_ERR_INVALID_GRID, "Center missing or not at (0,0) (src/grid.rs:122-133)");
-    }
-    g->vc = vc;
-    // the index adjacency must be the geometric 4-neighbourhood
-    std::vector<uint64_t> a, b;
-    const int S_ = int(g->S);
-    for (uint32_t v = 0; v < n; ++v) {
-        const mr_cell_index &c = g->idx[v];
-        if ((c.kind == MR_CELL_HOMELAND && (c.x > g->H || c.y > g->H)) || (c.kind == MR_CELL_BORDER && c.x > g->H)) {
-            delete g;
-            return fail(MR_ERR_INVALID_GRID, "cell index outside the homeland size");
-        }
-        index_neighbours(c, int(g->H), a);
-        b.clear();
-        int x = int(v % g->S), y = int(v / g->S);
-        if (x > 0) b.push_back(ci_key(g->idx[v - 1]));
-        if (x + 1 < S_) b.push_back(ci_key(g->idx[v + 1]));
-        if (y > 0) b.push_back(ci_key(g->idx[v - g->S]));
-        if (y + 1 < S_) b.push_back(ci_key(g->idx[v + g->S]));
-        std::sort(b.begin(), b.end());
-        if (a != b) {
-            delete g;
-            return fail(MR_ERR_INVALID_GRID, "cell labels are not a consistent 4-grid at cell " + std::to_string(v));
-        }
-    }
-    // the layout's unit steps per homeland and border (find()'s arithmetic path)
-    if (g->H >= 2) {
-        bool ok = true;
-        for (int h = 0; h < 4 && ok; ++h) {
-            uint32_t v11, v21, v12, vb;
-            ok = g->find(ci_make(MR_CELL_HOMELAND, uint8_t(h), 1, 1), v11) &&
-                 g->find(ci_make(MR_CELL_HOMELAND, uint8_t(h), 2, 1), v21) &&
-                 g->find(ci_make(MR_CELL_HOMELAND, uint8_t(h), 1, 2), v12) && g->find(build_border(h, 1), vb);
-            if (!ok) break;
-            g->ux[h] = int64_t(v21) - int64_t(v11);
-            g->uy[h] = int64_t(v12) - int64_t(v11);
-            g->ub[h] = int64_t(vb) - int64_t(vc);
-            ok = int64_t(v11) == int64_t(vc) + g->ux[h] + g->uy[h];
-        }
-        g->fast = ok;
-        // every cell where the formula puts it: find() may then trust the formula
-        bool all = ok;
-        for (uint32_t v = 0; v < n && all; ++v) {
+        g->vc = vc;
+        // the index adjacency must be the geometric 4-neighbourhood
+        std::vector<uint64_t> a, b;
+        const int S_ = int(g->S);
+        for (uint32_t v = 0; v < n; ++v) {
             const mr_cell_index &c = g->idx[v];
-            int64_t w = -1;
-            if (c.kind == MR_CELL_CENTER) w = vc;
-            else if (c.kind == MR_CELL_HOMELAND) w = int64_t(vc) + c.x * g->ux[c.sub] + c.y * g->uy[c.sub];
-            else if (c.kind == MR_CELL_BORDER) w = int64_t(vc) + c.x * g->ub[c.sub];
-            all = w == int64_t(v);
+            if ((c.kind == MR_CELL_HOMELAND && (c.x > g->H || c.y > g->H)) || (c.kind == MR_CELL_BORDER && c.x > g->H)) {
+                delete g;
+                return fail(MR_ERR_INVALID_GRID, "cell index outside the homeland size");
+            }
+            index_neighbours(c, int(g->H), a);
+            b.clear();
+            int x = int(v % g->S), y = int(v / g->S);
+            if (x > 0) b.push_back(ci_key(g->idx[v - 1]));
+            if (x + 1 < S_) b.push_back(ci_key(g->idx[v + 1]));
+            if (y > 0) b.push_back(ci_key(g->idx[v - g->S]));
+            if (y + 1 < S_) b.push_back(ci_key(g->idx[v + g->S]));
+            std::sort(b.begin(), b.end());
+            if (a != b) {
+                delete g;
+                return fail(MR_ERR_INVALID_GRID, "cell labels are not a consistent 4-grid at cell " + std::to_string(v));
+            }
         }
-        g->exact = all;
-    }
-    // rank = position in the derived Ord of CellIndex (src/index.rs:41-46)
-    {
-        std::vector<std::pair<uint64_t, uint32_t>> keys(n);
-        for (uint32_t v = 0; v < n; ++v) keys[v] = {ci_key(g->idx[v]), v};
-        std::sort(keys.begin(), keys.end());
-        g->rank.resize(n);
-        g->rank_inv.resize(n);
-        for (uint32_t r = 0; r < n; ++r) {
-            g->rank[keys[r].second] = r;
-            g->rank_inv[r] = keys[r].second;
+        // the layout's unit steps per homeland and border (find()'s arithmetic path)
+        if (g->H >= 2) {
+            bool ok = true;
+            for (int h = 0; h < 4 && ok; ++h) {
+                uint32_t v11, v21, v12, vb;
+                ok = g->find(ci_make(MR_CELL_HOMELAND, uint8_t(h), 1, 1), v11) &&
+                     g->find(ci_make(MR_CELL_HOMELAND, uint8_t(h), 2, 1), v21) &&
+                     g->find(ci_make(MR_CELL_HOMELAND, uint8_t(h), 1, 2), v12) && g->find(build_border(h, 1), vb);
+                if (!ok) break;
+                g->ux[h] = int64_t(v21) - int64_t(v11);
+                g->uy[h] = int64_t(v12) - int64_t(v11);
+                g->ub[h] = int64_t(vb) - int64_t(vc);
+                ok = int64_t(v11) == int64_t(vc) + g->ux[h] + g->uy[h];
+            }
+            g->fast = ok;
+            // every cell where the formula puts it: find() may then trust the formula
+            bool all = ok;
+            for (uint32_t v = 0; v < n && all; ++v) {
+                const mr_cell_index &c = g->idx[v];
+                int64_t w = -1;
+                if (c.kind == MR_CELL_CENTER) w = vc;
+                else if (c.kind == MR_CELL_HOMELAND) w = int64_t(vc) + c.x * g->ux[c.sub] + c.y * g->uy[c.sub];
+                else if (c.kind == MR_CELL_BORDER) w = int64_t(vc) + c.x * g->ub[c.sub];
+                all = w == int64_t(v);
+            }
+            g->exact = all;
         }
-        for (uint32_t r = 0; r < n; ++r)
-            if (g->poi[keys[r].second] == MR_POI_CAMPFIRE) g->campfires.push_back(keys[r].second);
-        bool std_ok = true;
-        for (uint32_t v = 0; v < n && std_ok; ++v) std_ok = g->rank[v] == std_rank(g->gx(v), g->gy(v), g->H);
-        g->rank_std = std_ok && !std::getenv("MR_RANK_TABLE");  // (tests: force the table)
+        // rank = position in the derived Ord of CellIndex (src/index.rs:41-46)
+        {
+            std::vector<std::pair<uint64_t, uint32_t>> keys(n);
+            for (uint32_t v = 0; v < n; ++v) keys[v] = {ci_key(g->idx[v]), v};
+            std::sort(keys.begin(), keys.end());
+            g->rank.resize(n);
+            g->rank_inv.resize(n);
+            for (uint32_t r = 0; r < n; ++r) {
+                g->rank[keys[r].second] = r;
+                g->rank_inv[r] = keys[r].second;
+            }
+            for (uint32_t r = 0; r < n; ++r)
+                if (g->poi[keys[r].second] == MR_POI_CAMPFIRE) g->campfires.push_back(keys[r].second);
+            bool std_ok = true;
+            for (uint32_t v = 0; v < n && std_ok; ++v) std_ok = g->rank[v] == std_rank(g->gx(v), g->gy(v), g->H);
+            g->rank_std = std_ok && !std::getenv("MR_RANK_TABLE");  // (tests: force the table)
+        }
     }
-    // nearest campfire per homeland (src/grid.rs:134-230, 297-325): the argmin
-    // of (manhattan distance, |x|!=|y|, |x|+|y|, |x|, |y|) over the homeland's
-    // Homeland-indexed campfires, computed by one multi-source BFS per homeland
-    // (lexicographic (dist, key) minima propagate along shortest paths).
+    // nearest campfire per homeland (src/grid.rs:134-230, 297-325): the argmin of
+    // (Manhattan distance, |x|!=|y|, |x|+|y|, |x|, |y|) over the homeland's Homeland-indexed
+    // campfires (the reference's projections give the same, tests/test_oracle_kat.py).
+    // Along one row y the distance to campfire f is x - fx + |y - fy| for fx <= x and
+    // fx - x + |y - fy| for fx >= x, so the best campfire at x is the better of a prefix
+    // minimum of (|y - fy| - fx, key) over the campfires left of x and a suffix minimum of
+    // (fx + |y - fy|, key) over those right of it: O(S + campfires) a row, rows on the
+    // host threads.
     for (int h = 0; h < 4; ++h) {
-        std::vector<uint32_t> dist(n, kNone32), nc(n, kNone32);
-        std::vector<uint64_t> key(n, ~0ull);
-        std::vector<uint32_t> cur, nxt;
-        for (uint32_t v : g->campfires) {
-            const mr_cell_index &c = g->idx[v];
-            if (c.kind != MR_CELL_HOMELAND || c.sub != h) continue;
-            uint64_t ax = uint64_t(std::abs(g->gx(v))), ay = uint64_t(std::abs(g->gy(v)));
-            dist[v] = 0;
-            nc[v] = v;
-            key[v] = (uint64_t(ax != ay) << 62) | ((ax + ay) << 40) | (ax << 20) | ay;
-            cur.push_back(v);
-        }
-        if (cur.empty()) {
+        bool any = false;
+        for (uint32_t v : g->campfires) any = any || (g->idx[v].kind == MR_CELL_HOMELAND && g->idx[v].sub == h);
+        if (!any) {
             delete g;
             // MapGrid::parse reaches unreachable!() in this case (src/grid.rs:209)
             return fail(MR_ERR_INVALID_GRID, "a homeland has no campfire (the reference panics, src/grid.rs:209)");
         }
-        for (uint32_t d = 0; !cur.empty(); ++d) {
-            nxt.clear();
-            for (uint32_t u : cur) {
-                int x = int(u % g->S), y = int(u / g->S);
-                uint32_t nb[4] = {x > 0 ? u - 1 : kNone32, x + 1 < S_ ? u + 1 : kNone32,
-                                  y > 0 ? u - g->S : kNone32, y + 1 < S_ ? u + g->S : kNone32};
-                for (uint32_t w : nb) {
-                    if (w == kNone32) continue;
-                    if (dist[w] == kNone32) {
-                        dist[w] = d + 1;
-                        key[w] = key[u];
-                        nc[w] = nc[u];
-                        nxt.push_back(w);
-                    } else if (dist[w] == d + 1 && key[u] < key[w]) {
-                        key[w] = key[u];
-                        nc[w] = nc[u];
+    }
+    const double tg1 = timing_on() ? now_ms() : 0.0;
+    {
+        struct Cf {
+            int64_t fx, fy;
+            uint64_t key;
+            uint32_t v;
+        };
+        std::vector<Cf> cfs[4];
+        for (uint32_t v : g->campfires) {
+            const mr_cell_index &c = g->idx[v];
+            if (c.kind != MR_CELL_HOMELAND) continue;
+            const int64_t fx = int64_t(v % g->S), fy = int64_t(v / g->S);
+            const uint64_t ax = uint64_t(std::abs(g->gx(v))), ay = uint64_t(std::abs(g->gy(v)));
+            cfs[c.sub].push_back(Cf{fx, fy, (uint64_t(ax != ay) << 62) | ((ax + ay) << 40) | (ax << 20) | ay, v});
+        }
+        for (int h = 0; h < 4; ++h) {
+            std::sort(cfs[h].begin(), cfs[h].end(), [](const Cf &p, const Cf &q) { return p.fx < q.fx; });
+            g->nearest[h].assign(n, kNone32);
+        }
+        const uint32_t S = g->S;
+        HostPool &pool = HostPool::get();
+        const uint32_t parts = std::max(1u, std::min(pool.size() * 4, S / 16u));
+        pool.run(parts, [&](uint32_t pt) {
+            std::vector<std::pair<int64_t, uint64_t>> suf;
+            std::vector<uint32_t> sufi;
+            for (uint32_t y = chunk_lo(S, parts, pt); y < chunk_lo(S, parts, pt + 1); ++y)
+                for (int h = 0; h < 4; ++h) {
+                    const std::vector<Cf> &cf = cfs[h];
+                    const size_t k = cf.size();
+                    // suffix minima of (fx + |y - fy|, key) over the campfires sorted by fx
+                    suf.resize(k + 1);
+                    sufi.resize(k + 1);
+                    suf[k] = {INT64_MAX, ~0ull};
+                    sufi[k] = kNone32;
+                    for (size_t i = k; i-- > 0;) {
+                        const std::pair<int64_t, uint64_t> c{cf[i].fx + std::abs(int64_t(y) - cf[i].fy), cf[i].key};
+                        if (c < suf[i + 1]) {
+                            suf[i] = c;
+                            sufi[i] = cf[i].v;
+                        } else {
+                            suf[i] = suf[i + 1];
+                            sufi[i] = sufi[i + 1];
+                        }
+                    }
+                    std::pair<int64_t, uint64_t> pre{INT64_MAX, ~0ull};  // (|y - fy| - fx, key), fx <= x
+                    uint32_t prei = kNone32;
+                    size_t j = 0;  // first campfire with fx > x
+                    uint32_t *out = &g->nearest[h][size_t(y) * S];
+                    for (uint32_t x = 0; x < S; ++x) {
+                        while (j < k && cf[j].fx <= int64_t(x)) {
+                            const std::pair<int64_t, uint64_t> c{std::abs(int64_t(y) - cf[j].fy) - cf[j].fx, cf[j].key};
+                            if (c < pre) {
+                                pre = c;
+                                prei = cf[j].v;
+                            }
+                            ++j;
+                        }
+                        // right of x: the campfires from the first with fx >= x (fx == x is in both)
+                        size_t jj = j;
+                        while (jj > 0 && cf[jj - 1].fx == int64_t(x)) --jj;
+                        std::pair<int64_t, uint64_t> best{INT64_MAX, ~0ull};
+                        uint32_t bi = kNone32;
+                        if (prei != kNone32) {
+                            best = {pre.first + int64_t(x), pre.second};
+                            bi = prei;
+                        }
+                        if (sufi[jj] != kNone32) {
+                            const std::pair<int64_t, uint64_t> c{suf[jj].first - int64_t(x), suf[jj].second};
+                            if (c < best) {
+                                best = c;
+                                bi = sufi[jj];
+                            }
+                        }
+                        out[x] = bi;
                     }
                 }
-            }
-            cur.swap(nxt);
-        }
-        g->nearest[h] = std::move(nc);
+        });
     }
+    if (timing_on())
+        std::fprintf(stderr, "[mr] grid_create V=%u: layout+ranks %.2f ms, nearest campfires %.2f ms (%s path)\n", n,
+                     tg1 - tg0, now_ms() - tg1, g->exact ? "fast" : "generic");
     *out = g;
     return MR_OK;
 }

@@ -11,30 +11,48 @@ records to rank 0 (RCCL over xGMI on MI355X; gloo in the CPU tests).
 """
 from __future__ import annotations
 
-import heapq
 from typing import Dict, Iterable, List, Mapping, Optional, Sequence
 
 
 def shard_by_source(src_keys: Sequence[int], world: int,
                     extra_cost: Optional[Mapping[int, float]] = None) -> List[List[int]]:
     """Returns, per rank, the (ascending) query indices it owns.  A source's cost is
-    its query count plus extra_cost.get(source key, 0) (in query units)."""
-    groups: Dict[int, List[int]] = {}
-    for i, s in enumerate(src_keys):
-        groups.setdefault(s, []).append(i)
-    extra = extra_cost or {}
-    cost = {k: len(v) + float(extra.get(k, 0.0)) for k, v in groups.items()}
-    # LPT: costliest sources first, ties by source key, each to the least-loaded rank
-    order = sorted(groups.items(), key=lambda kv: (-cost[kv[0]], kv[0]))
-    heap = [(0.0, r) for r in range(world)]
-    out: List[List[int]] = [[] for _ in range(world)]
-    for key, idxs in order:
-        load, r = heapq.heappop(heap)
-        out[r].extend(idxs)
-        heapq.heappush(heap, (load + cost[key], r))
-    for r in range(world):
-        out[r].sort()
-    return out
+    its query count plus extra_cost.get(source key, 0) (in query units).
+
+    Longest processing time first: the costliest sources first, ties by source key, each
+    to the least-loaded rank (ties by rank).  Vectorised by cost class: within a run of
+    sources of one cost c, rank r is picked at loads L_r, L_r + c, L_r + 2c, ... so the
+    picks are the run's length smallest (load, rank) pairs of those sequences, in order
+    (the same assignment as a heap popping the least-loaded rank source by source; costs
+    are integers, so the loads are exact)."""
+    import numpy as np
+    keys = np.asarray(src_keys, dtype=np.int64)
+    if keys.size == 0:
+        return [[] for _ in range(world)]
+    uniq, inv, counts = np.unique(keys, return_inverse=True, return_counts=True)
+    cost = counts.astype(np.float64)
+    for k, e in (extra_cost or {}).items():
+        i = int(np.searchsorted(uniq, k))
+        if i < uniq.size and uniq[i] == k:
+            cost[i] += float(e)
+    order = np.lexsort((uniq, -cost))
+    cs = cost[order]
+    runs = np.concatenate([[0], np.flatnonzero(np.diff(cs)) + 1, [cs.size]])
+    load = np.zeros(world, dtype=np.float64)
+    rank_of = np.empty(uniq.size, dtype=np.int64)
+    ranks = np.arange(world, dtype=np.int64)
+    for a, b in zip(runs[:-1], runs[1:]):
+        m, c = int(b - a), float(cs[a])
+        # at most m picks per rank
+        t = np.arange(m, dtype=np.float64)
+        cand_load = (load[:, None] + t[None, :] * c).ravel()
+        cand_rank = np.repeat(ranks, m)
+        pick = np.lexsort((cand_rank, cand_load))[:m]
+        got = cand_rank[pick]
+        rank_of[order[a:b]] = got
+        load += c * np.bincount(got, minlength=world)
+    rq = rank_of[inv]
+    return [np.flatnonzero(rq == r).tolist() for r in range(world)]
 
 
 class SourceCosts:

@@ -213,3 +213,42 @@ def test_engine_records_gather_gloo_world2():
     assert len(summary) == 2
     for covered, bad in summary:
         assert covered == 400 and bad == 0, summary
+
+
+def _lpt_heap(src_keys, world, extra_cost=None):
+    """The plain LPT (a heap of rank loads, source by source) that shard_by_source vectorises."""
+    import heapq
+    groups = {}
+    for i, s in enumerate(src_keys):
+        groups.setdefault(s, []).append(i)
+    extra = extra_cost or {}
+    cost = {k: len(v) + float(extra.get(k, 0.0)) for k, v in groups.items()}
+    heap = [(0.0, r) for r in range(world)]
+    out = [[] for _ in range(world)]
+    for key, idxs in sorted(groups.items(), key=lambda kv: (-cost[kv[0]], kv[0])):
+        load, r = heapq.heappop(heap)
+        out[r].extend(idxs)
+        heapq.heappush(heap, (load + cost[key], r))
+    return [sorted(o) for o in out]
+
+
+def test_shard_by_source_equals_heap_lpt():
+    import random
+    rng = random.Random(5)
+    for trial in range(40):
+        world = rng.choice([1, 2, 3, 4, 7, 8])
+        n = rng.choice([0, 1, 5, 100, 3000])
+        keys = [rng.randrange(max(1, n // rng.choice([1, 2, 5]))) for _ in range(n)]
+        extra = {k: rng.choice([1e7, 3.0, 250.0]) for k in rng.sample(sorted(set(keys)), min(len(set(keys)), 3))}
+        for ex in (None, extra):
+            assert shard_by_source(keys, world, ex) == _lpt_heap(keys, world, ex), (trial, world, n)
+
+
+def test_shard_by_source_1m_is_fast():
+    import time
+    import numpy as np
+    keys = np.random.default_rng(1).integers(0, 1_050_625, 1_000_000)
+    t0 = time.perf_counter()
+    shards = shard_by_source(keys, 8)
+    assert time.perf_counter() - t0 < 5.0
+    assert sum(len(s) for s in shards) == 1_000_000
