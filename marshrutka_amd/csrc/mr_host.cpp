@@ -55,6 +55,18 @@ uint32_t lane_blob_build(const SpecialStatic *sp, uint32_t NS, uint32_t nreg, ui
                          const uint32_t *near_sp, std::vector<uint32_t> &blob);
 hipError_t region_table_build(const uint16_t *reg, const uint32_t *rank, uint32_t S, uint32_t nreg, void *tab,
                               void *axis, hipStream_t stream);
+struct GroupGeom {
+    long long vc, ux[4], uy[4], ub[4];
+    uint32_t H, V;
+};
+size_t group_scratch_bytes(uint32_t n, uint32_t V);
+hipError_t group_queries_device(const void *q, uint32_t n, const GroupGeom &geo, uint32_t lane_max_q, void *scratch,
+                                uint32_t *src_v, uint32_t *q_begin, uint32_t *q_dst, uint32_t *q_id, uint32_t *cnt,
+                                uint32_t *inv, uint32_t inv_cap, hipStream_t s);
+hipError_t partition_sources_device(uint32_t n, uint32_t V, const void *scratch, const uint32_t *src_v,
+                                    const uint32_t *q_begin, const uint32_t *q_dst, const uint32_t *q_id,
+                                    const uint32_t *cnt, uint32_t *src2, uint32_t *qb2, uint32_t *qd2, uint32_t *qi2,
+                                    hipStream_t s);
 uint32_t hub_group_lds_bytes(uint32_t NS, uint32_t nreg, uint32_t G);
 hipError_t launch_hub_group(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t n,
                             uint32_t G, hipStream_t stream);
@@ -860,7 +872,14 @@ struct HostPlan {
     bool wide = false;                      // hub_wide_kernel (NS > 63 or no V x regions table)
     std::vector<uint32_t> near_sp;          // wide: (NS+1) x nreg x {distance, rank} rows of the specials
     const std::vector<uint32_t> *rb_off = nullptr, *rb_cell = nullptr;
+    // Large query batches are grouped on the device (mr_k_groupq.hip): src_v .. q_status
+    // stay empty until a host caller needs them (host_arrays), the counts below hold
+    bool dev_grouped = false, mirrored = false;
+    uint32_t nrec = 0, nsrc = 0, n_small = 0;  // valid queries, sources, sources of <= kLaneMaxQ queries
+    std::vector<uint32_t> invalid;             // device grouping: the invalid queries, ascending
 };
+static uint32_t nrec_of(const HostPlan &hp) { return hp.dev_grouped ? hp.nrec : uint32_t(hp.q_id.size()); }
+static uint32_t nsrc_of(const HostPlan &hp) { return hp.dev_grouped ? hp.nsrc : uint32_t(hp.src_v.size()); }
 
 // (c1, c2) -> (c1, c2', c3): CostComparator::eval_next (src/cost.rs:387-405)
 static void comparator_order(uint8_t s1, uint8_t s2, uint8_t out[3]) {
@@ -910,8 +929,9 @@ static void trim_group_scratch() {
     for (GroupScratch *g : g_scratch) g->release();
 }
 
+static bool dev_group_ok(const mr_grid *g, uint32_t n);
 static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs, uint32_t n, uint32_t max_cmds,
-                      HostPlan &hp) {
+                      HostPlan &hp, bool allow_dev_group = false) {
     const double tbs = timing_on() ? now_ms() : 0.0;
     if (!g || !prm) return fail(MR_ERR_INVALID_ARG, "null grid or params");
     if (prm->sort_by[0] > 2 || prm->sort_by[1] > 2 || prm->homeland > 3)
@@ -1094,6 +1114,10 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     // by (digit, part) keep the sort stable, then each part scatters its own keys.
     const uint32_t V = g->V;
     hp.nq = n;
+    if (allow_dev_group && dev_group_ok(g, n)) {  // grouped by plan_create on the device
+        hp.dev_grouped = true;
+        return MR_OK;
+    }
     const double tb0 = timing_on() ? now_ms() : 0.0;
     HostPool &pool = HostPool::get();
     // at least 8k queries a part (a part's work must outweigh waking a thread; 125k
@@ -1722,6 +1746,8 @@ struct mr_plan {
     bool own_tables = true;  // d_sinfo / d_rank / d_rank_inv / d_cell: false = the grid's shared copies
     uint2 *d_cell = nullptr;
     uint32_t *d_qblock = nullptr;  // the per-batch arrays (d_src, d_qb, d_qd, d_qi point into it)
+    void *d_gscratch = nullptr;    // device grouping: phase 1's scratch, until the partition (plan_create)
+    uint32_t *d_gcnt = nullptr;    // device grouping: its counts
     // certified fallback (query hub plans): per slot a label table,
     // boundary ranks, source, cell words, check state and sweep list; the fill's
     // argument block over the slots
@@ -1758,6 +1784,8 @@ struct mr_plan {
         pstream_release(hub_stream);
         d_src = d_qb = d_qd = d_qi = nullptr;  // inside d_qblock
         pfree(d_qblock);
+        pfree(d_gscratch);
+        pfree(d_gcnt);
         if (!own_tables) {  // the grid's
             d_sinfo = d_rank = d_rank_inv = nullptr;
             d_cell = nullptr;
@@ -1889,6 +1917,7 @@ static bool lane_layout_ok(const HostPlan &hp) {
 
 // sources that would run on the lane kernel (at most kLaneMaxQ queries)
 static uint32_t lane_sources(const HostPlan &hp) {
+    if (hp.dev_grouped) return hp.n_small;
     uint32_t c = 0;
     for (size_t i = 0; i + 1 < hp.q_begin.size(); ++i) c += hp.q_begin[i + 1] - hp.q_begin[i] <= kLaneMaxQ;
     return c;
@@ -1943,6 +1972,176 @@ static uint32_t partition_sources(HostPlan &hp) {
     return n_lane;
 }
 
+// ---- query batches grouped on the device (mr_k_groupq.hip) -------------------------
+// Batches of at least kDevGroupMin queries on a grid whose cells are all where the
+// layout's formula puts them (mr_grid::exact) go up raw: the lookups, the stable sort by
+// source and the lane kernel's partition run on the device, and the host learns counts
+// only.  MR_DEV_GROUP=0: never, =1: any batch on such a grid.
+constexpr uint32_t kDevGroupMin = 32768;
+static bool dev_group_ok(const mr_grid *g, uint32_t n) {
+    if (!g->exact || n == 0 || n >= (1u << 30)) return false;
+    const char *e = std::getenv("MR_DEV_GROUP");
+    if (e && !std::strcmp(e, "0")) return false;
+    if (e && !std::strcmp(e, "1")) return true;
+    return n >= kDevGroupMin;
+}
+
+// The per-batch block's layout for n queries (src_v, q_begin, q_dst, q_id: each bounded
+// by n words, 64-word aligned)
+static void qblock_layout(size_t n, size_t at[5]) {
+    const size_t w = (n + 1 + 63) / 64 * 64;
+    for (int j = 0; j <= 4; ++j) at[j] = size_t(j) * w;
+}
+
+// Phase 1 on the plan's stream: the raw queries up (straight from caller memory that
+// mr_host_register page-locked, else through the pinned stage in 4 MB chunks, host
+// threads copying chunk c + 1 while chunk c's DMA runs), the device grouping into a new
+// query block, then the counts (and any invalid queries' ids) back.
+static int group_on_device(mr_plan *pl, const mr_query *qs, uint32_t n) {
+    HostPlan &hp = pl->hp;
+    const mr_grid *g = pl->grid;
+    GroupGeom geo{};
+    geo.vc = g->vc;
+    for (int h = 0; h < 4; ++h) {
+        geo.ux[h] = g->ux[h];
+        geo.uy[h] = g->uy[h];
+        geo.ub[h] = g->ub[h];
+    }
+    geo.H = g->H;
+    geo.V = g->V;
+    size_t at[5];
+    qblock_layout(n, at);
+    void *d_q = nullptr;
+    const size_t qbytes = size_t(n) * sizeof(mr_query);
+    if (pmalloc(reinterpret_cast<void **>(&pl->d_qblock), at[4] * 4) != hipSuccess ||
+        pmalloc(&d_q, qbytes) != hipSuccess || pmalloc(&pl->d_gscratch, group_scratch_bytes(n, g->V)) != hipSuccess ||
+        pmalloc(reinterpret_cast<void **>(&pl->d_gcnt), 8 * 4 + 4096 * 4) != hipSuccess) {
+        pfree(d_q);
+        return fail(MR_ERR_DEVICE, "hipMalloc device grouping");
+    }
+    pl->d_src = pl->d_qblock + at[0];
+    pl->d_qb = pl->d_qblock + at[1];
+    pl->d_qd = pl->d_qblock + at[2];
+    pl->d_qi = pl->d_qblock + at[3];
+    hipError_t e = hipSuccess;
+    if (host_pinned(qs, qbytes)) {
+        e = hipMemcpyAsync(d_q, qs, qbytes, hipMemcpyHostToDevice, pl->stream);
+    } else {
+        PinnedStage &su = stage_up();
+        std::lock_guard<std::mutex> lk(su.mu);
+        constexpr size_t kUp = size_t(4) << 20;
+        char *stage = static_cast<char *>(su.get(std::min(qbytes, 2 * kUp)));
+        if (!stage) {
+            e = hipMemcpyAsync(d_q, qs, qbytes, hipMemcpyHostToDevice, pl->stream);
+        } else {
+            // two stage halves in turn: a half is refilled only after its previous DMA
+            hipEvent_t done[2] = {nullptr, nullptr};
+            for (hipEvent_t &ev : done)
+                if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+            HostPool &hpool = HostPool::get();
+            const char *src = reinterpret_cast<const char *>(qs);
+            uint32_t c = 0;
+            for (size_t lo = 0; lo < qbytes && e == hipSuccess; lo += kUp, ++c) {
+                const size_t len = std::min(kUp, qbytes - lo);
+                char *half = stage + (c & 1u) * kUp;
+                if (c >= 2 && (e = hipEventSynchronize(done[c & 1u])) != hipSuccess) break;
+                const uint32_t parts = len >= (size_t(1) << 20) ? hpool.size() : 1u;
+                hpool.run(parts, [&](uint32_t pt) {
+                    const size_t a = len * pt / parts, b = len * (pt + 1) / parts;
+                    std::memcpy(half + a, src + lo + a, b - a);
+                });
+                e = hipMemcpyAsync(static_cast<char *>(d_q) + lo, half, len, hipMemcpyHostToDevice, pl->stream);
+                if (e == hipSuccess) e = hipEventRecord(done[c & 1u], pl->stream);
+            }
+            const hipError_t es = hipStreamSynchronize(pl->stream);  // (the stage is in use until here)
+            if (e == hipSuccess) e = es;
+            for (hipEvent_t ev : done)
+                if (ev) (void)hipEventDestroy(ev);
+        }
+    }
+    uint32_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (e == hipSuccess)
+        e = group_queries_device(d_q, n, geo, kLaneMaxQ, pl->d_gscratch, pl->d_src, pl->d_qb, pl->d_qd, pl->d_qi,
+                                 pl->d_gcnt, pl->d_gcnt + 8, 4096, pl->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(cnt, pl->d_gcnt, sizeof(cnt), hipMemcpyDeviceToHost, pl->stream);
+    const hipError_t es = hipStreamSynchronize(pl->stream);
+    if (e == hipSuccess) e = es;
+    pfree(d_q);  // (after the sync: the cache hands blocks out without one)
+    if (e != hipSuccess) return fail(MR_ERR_DEVICE, std::string("device grouping: ") + hipGetErrorString(e));
+    hp.nrec = cnt[0];
+    hp.nsrc = cnt[1];
+    hp.n_small = cnt[2];
+    const uint32_t ninv = cnt[4];
+    if (ninv != n - cnt[0]) return fail(MR_ERR_DEVICE, "device grouping: inconsistent counts");
+    hp.invalid.clear();
+    if (ninv) {
+        if (ninv <= 4096) {
+            hp.invalid.resize(ninv);
+            if (hipMemcpy(hp.invalid.data(), pl->d_gcnt + 8, size_t(ninv) * 4, hipMemcpyDeviceToHost) != hipSuccess)
+                return fail(MR_ERR_DEVICE, "device grouping: invalid list");
+        } else {  // many invalid queries: every query not among the grouped ids
+            std::vector<uint32_t> ids(cnt[0]);
+            if (cnt[0] && hipMemcpy(ids.data(), pl->d_qi, size_t(cnt[0]) * 4, hipMemcpyDeviceToHost) != hipSuccess)
+                return fail(MR_ERR_DEVICE, "device grouping: query ids");
+            std::vector<uint8_t> seen(n, 0);
+            for (uint32_t i : ids) seen[i] = 1;
+            for (uint32_t i = 0; i < n; ++i)
+                if (!seen[i]) hp.invalid.push_back(i);
+        }
+        std::sort(hp.invalid.begin(), hp.invalid.end());
+    }
+    return MR_OK;
+}
+
+// Phase 2 (plans on hub_lane_kernel): the small sources first, into a new block
+static uint32_t partition_on_device(mr_plan *pl) {
+    HostPlan &hp = pl->hp;
+    if (hp.n_small == hp.nsrc) return hp.n_small;
+    size_t at[5];
+    qblock_layout(hp.nq, at);
+    uint32_t *blk = nullptr;
+    if (pmalloc(reinterpret_cast<void **>(&blk), at[4] * 4) != hipSuccess) return kNone32;
+    hipError_t e = partition_sources_device(hp.nq, pl->grid->V, pl->d_gscratch, pl->d_src, pl->d_qb, pl->d_qd, pl->d_qi,
+                                            pl->d_gcnt, blk + at[0], blk + at[1], blk + at[2], blk + at[3], pl->stream);
+    const hipError_t es = hipStreamSynchronize(pl->stream);
+    if (e == hipSuccess) e = es;
+    if (e != hipSuccess) {
+        pfree(blk);
+        return kNone32;
+    }
+    pfree(pl->d_qblock);
+    pl->d_qblock = blk;
+    pl->d_src = blk + at[0];
+    pl->d_qb = blk + at[1];
+    pl->d_qd = blk + at[2];
+    pl->d_qi = blk + at[3];
+    return hp.n_small;
+}
+
+// The host copies of a device-grouped plan's arrays (record order, the fallback
+// sources' cells, the host decoder), fetched on first use
+static int host_arrays(const mr_plan *cpl) {
+    mr_plan *pl = const_cast<mr_plan *>(cpl);
+    HostPlan &hp = pl->hp;
+    if (!hp.dev_grouped || hp.mirrored) return MR_OK;
+    hp.src_v.assign(hp.nsrc, 0u);
+    hp.q_begin.assign(size_t(hp.nsrc) + 1, 0u);
+    hp.q_dst.assign(hp.nrec, 0u);
+    hp.q_id.assign(hp.nrec, 0u);
+    const std::pair<std::vector<uint32_t> *, const uint32_t *> arr[4] = {
+        {&hp.src_v, pl->d_src}, {&hp.q_begin, pl->d_qb}, {&hp.q_dst, pl->d_qd}, {&hp.q_id, pl->d_qi}};
+    for (const auto &a : arr)
+        if (!a.first->empty() &&
+            hipMemcpy(a.first->data(), a.second, a.first->size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+            return fail(MR_ERR_DEVICE, "copy grouped arrays");
+    hp.q_pos.assign(hp.nq, kNone32);
+    hp.q_status.assign(hp.nq, MR_OK);
+    for (uint32_t k = 0; k < hp.nrec; ++k) hp.q_pos[hp.q_id[k]] = k;
+    for (uint32_t i : hp.invalid) hp.q_status[i] = MR_ERR_INVALID_INDEX;
+    hp.mirrored = true;
+    return MR_OK;
+}
+
 static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *qs, uint32_t n, uint32_t max_cmds,
                        mr_plan **out, bool all_mode = false) {
     if (!out || (n && !qs)) return fail(MR_ERR_INVALID_ARG, "null argument");
@@ -1952,7 +2151,12 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     double tm_build = 0, tm_upload = 0, tm_alloc = 0;
     auto pl = new mr_plan();
     pl->grid = g;
-    int st = build_plan(g, prm, qs, n, max_cmds, pl->hp);
+    int st = build_plan(g, prm, qs, n, max_cmds, pl->hp, !all_mode);
+    if (st == MR_OK && pl->hp.dev_grouped) {  // the batch grouped on the device (counts back)
+        if (hipGetDevice(&pl->device) != hipSuccess) st = fail(MR_ERR_DEVICE, "hipGetDevice");
+        else if (pstream_create(&pl->stream) != hipSuccess) st = fail(MR_ERR_DEVICE, "stream");
+        else st = group_on_device(pl, qs, n);
+    }
     if (timing_on()) tm_build = now_ms();
     if (st != MR_OK) {
         delete pl;
@@ -1982,22 +2186,27 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     // source: 23 us against 31 with 16), 16 up to 4 096 (c2, 3 821 sources: 37 us against
     // 44 with 8), else 8 (1025^2 map, 5k / 20k sources: 34 / 66 us against 53 / 129 with
     // 16: more groups per wave, fewer waves)
-    const size_t nsrc_g = hp.src_v.size();
+    const size_t nsrc_g = nsrc_of(hp);
     const uint32_t group_g = hg ? (hgv == 16 ? 16u : (hgv == 32 ? 32u : 8u))
                                 : (nsrc_g <= 1024 ? 32u : (nsrc_g <= 4096 ? 16u : 8u));
     const bool lane_ok = hp.hub && !hp.wide && !hp.nonlin && !all_mode && hp.near && lane_bounds_ok(hp.p);
     if (lane_ok && !group_force && !lane_off && hub_lane_entries(hp.p.NS) != 0 && lane_layout_ok(hp) &&
         (lane_force || lane_sources(hp) >= lane_min_sources()))
-        pl->n_lane = partition_sources(hp);
+        pl->n_lane = hp.dev_grouped ? partition_on_device(pl) : partition_sources(hp);
     else if (lane_ok && !group_off && !lane_force && hub_group_slots(hp.p.NS, group_g) != 0 &&
              !std::getenv("MR_HUB_FALLBACK_ALL")) {
-        pl->n_lane = uint32_t(hp.src_v.size());
+        pl->n_lane = nsrc_of(hp);
         pl->lane_g = group_g;
+    }
+    if (pl->d_gscratch) {  // phase 1's scratch is done with (the partition synchronised)
+        pfree(pl->d_gscratch);
+        pl->d_gscratch = nullptr;
     }
     auto bail = [&](int code) {
         delete pl;
         return code;
     };
+    if (pl->n_lane == kNone32) return bail(fail(MR_ERR_DEVICE, "device partition of the sources"));
     if (hipGetDevice(&pl->device) != hipSuccess) return bail(fail(MR_ERR_DEVICE, "hipGetDevice"));
     if (grid_tables(g, pl->device, hp, pl->d_rank, pl->d_rank_inv, pl->d_sinfo, pl->d_cell)) {
         pl->own_tables = false;
@@ -2009,7 +2218,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     }
     if ((st = upload(pl->d_sp, hp.sp)) || (st = upload(pl->d_hubs, hp.hubs)))
         return bail(st);
-    {  // the per-batch arrays in one device block and one copy (sources, offsets, destinations, query ids)
+    if (!hp.dev_grouped) {  // the per-batch arrays in one device block and one copy (sources, offsets, destinations, query ids)
         const size_t a0 = 0, a1 = a0 + (hp.src_v.size() + 63) / 64 * 64, a2 = a1 + (hp.q_begin.size() + 63) / 64 * 64,
                      a3 = a2 + (hp.q_dst.size() + 63) / 64 * 64, a4 = a3 + (hp.q_id.size() + 63) / 64 * 64;
         // packed in the pinned upload stage (host threads for large batches), one DMA
@@ -2075,7 +2284,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     // bucketed solver, used by the tests to cover both); grid state in LDS when it fits 3
     // workgroups per CU, else per-workgroup HBM slots (MR_GRID_STATE=hbm|lds overrides)
     const uint32_t NS = hp.p.NS, V = hp.p.V;
-    const uint32_t nsrc = uint32_t(hp.src_v.size());
+    const uint32_t nsrc = nsrc_of(hp);
     pl->algo = hp.p.bucket_mode == kBucketLegs ? kAlgoLegs : kAlgoGeneric;
     if (const char *e = std::getenv("MR_ALGO"))
         if (!std::strcmp(e, "generic")) pl->algo = kAlgoGeneric;
@@ -2107,7 +2316,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     }
     pl->blocks = uint32_t(blocks);
     if (timing_on()) tm_alloc = now_ms();
-    if (pstream_create(&pl->stream) != hipSuccess)
+    if (!pl->stream && pstream_create(&pl->stream) != hipSuccess)
         return bail(fail(MR_ERR_DEVICE, "stream"));
     KArgs &ka = pl->ka;
     ka.p = hp.p;
@@ -2618,6 +2827,7 @@ extern "C" uint32_t mr_plan_num_sources(const mr_plan *pl) { return pl ? pl->ka.
 
 extern "C" int mr_plan_record_queries(const mr_plan *pl, uint32_t *query_of_record, uint32_t n) {
     if (!pl || (n && !query_of_record)) return fail(MR_ERR_INVALID_ARG, "null argument");
+    if (int st = host_arrays(pl)) return st;
     const std::vector<uint32_t> &ids = pl->hp.q_id;
     for (uint32_t k = 0; k < n; ++k) query_of_record[k] = k < ids.size() ? ids[k] : kNone32;
     return MR_OK;
@@ -2638,6 +2848,8 @@ extern "C" int mr_plan_fallback_sources(mr_plan *pl, mr_cell_index *out, uint32_
     // entries the certificate answered carry kFbCertified: no search was run for them
     fb.erase(std::remove_if(fb.begin(), fb.end(), [](uint32_t s) { return (s & kFbCertified) != 0; }), fb.end());
     std::sort(fb.begin(), fb.end());
+    if (!fb.empty())
+        if (int st = host_arrays(pl)) return st;
     for (uint32_t k = 0; k < fb.size() && k < cap; ++k) out[k] = pl->grid->idx[pl->hp.src_v[fb[k]]];
     *n = uint32_t(fb.size());
     return MR_OK;
@@ -2822,9 +3034,9 @@ static int check_device_errors(mr_plan *pl, uint32_t &flags, uint32_t *ctr_out =
             return fail(MR_ERR_DEVICE, "copy counter");
         if (oc[kCtrFlags]) (void)hipMemset(k.counter + kCtrFlags, 0, 4);
         flags |= oc[kCtrFlags];  // a fused plan's look-ahead solve may have flagged a slot not yet filled
-        if (flags == 0 && k.used && oc[kCtrLastWritten] != pl->hp.q_id.size())
+        if (flags == 0 && k.used && oc[kCtrLastWritten] != nrec_of(pl->hp))
             return fail(MR_ERR_DEVICE, "internal: " + std::to_string(oc[kCtrLastWritten]) + " of " +
-                                           std::to_string(pl->hp.q_id.size()) + " records written (an earlier pass)");
+                                           std::to_string(nrec_of(pl->hp)) + " records written (an earlier pass)");
     }
 #ifdef MR_HUBDUMP
     if (pl->d_dbg) {
@@ -2848,7 +3060,7 @@ static int check_device_errors(mr_plan *pl, uint32_t &flags, uint32_t *ctr_out =
     if (std::getenv("MR_DEBUG")) {
         std::fprintf(stderr, "MR_DEBUG hub=%d sources=%u fallback=%u flags=%u hub_blocks=%u\n", int(pl->hp.hub),
                      pl->ka.nsrc, ctr[kCtrLastFb], ctr[kCtrFlags], pl->hub_blocks);
-        if (pl->d_fb && ctr[kCtrLastFb] <= pl->ka.nsrc) {
+        if (pl->d_fb && ctr[kCtrLastFb] <= pl->ka.nsrc && host_arrays(pl) == MR_OK) {
             std::vector<uint32_t> fb(ctr[kCtrLastFb]);
             (void)hipMemcpy(fb.data(), pl->d_fb, fb.size() * 4, hipMemcpyDeviceToHost);
             std::fprintf(stderr, "MR_DEBUG fallback sources (vertex):");
@@ -2863,9 +3075,9 @@ static int check_device_errors(mr_plan *pl, uint32_t &flags, uint32_t *ctr_out =
     if (flags & (kErrKOverflow | kErrMetricOverflow))
         return fail(MR_ERR_LIMIT, "a label exceeds the engine's 32-bit metric or run-length limits");
     if (flags) return fail(MR_ERR_DEVICE, "internal invariant violated on device (flags " + std::to_string(flags) + ")");
-    if (pl->runs && ctr[kCtrLastWritten] != pl->hp.q_id.size())
+    if (pl->runs && ctr[kCtrLastWritten] != nrec_of(pl->hp))
         return fail(MR_ERR_DEVICE, "internal: " + std::to_string(ctr[kCtrLastWritten]) + " of " +
-                                       std::to_string(pl->hp.q_id.size()) + " result records written");
+                                       std::to_string(nrec_of(pl->hp)) + " result records written");
     return MR_OK;
 }
 
@@ -2922,7 +3134,7 @@ static const mr_cell_index *grid_idx_rank(const mr_grid *g, int dev) {
 // false (nothing written) when the device path does not apply (the host decoder runs).
 static bool plan_fetch_device(mr_plan *pl, mr_result *results, mr_command *pool, uint64_t pool_cap, int &ret) {
     const HostPlan &hp = pl->hp;
-    const uint32_t nq = hp.nq, nrec = uint32_t(hp.q_id.size()), mc = hp.p.max_cmds;
+    const uint32_t nq = hp.nq, nrec = nrec_of(hp), mc = hp.p.max_cmds;
     if (const char *e = std::getenv("MR_HOST_DECODE"))
         if (!std::strcmp(e, "1")) return false;
     if (!pool || !nq || pl->all_mode) return false;
@@ -2981,11 +3193,23 @@ static bool plan_fetch_device(mr_plan *pl, mr_result *results, mr_command *pool,
         hpool.run(parts, [&](uint32_t pt) {
             uint64_t en = total;
             int32_t rt = MR_OK;
-            for (uint32_t i = chunk_lo(nq, parts, pt), ie = chunk_lo(nq, parts, pt + 1); i < ie; ++i) {
+            const uint32_t i0 = chunk_lo(nq, parts, pt);
+            // (device-grouped plans: the invalid queries from their sorted list)
+            auto inv = std::lower_bound(hp.invalid.begin(), hp.invalid.end(), i0);
+            for (uint32_t i = i0, ie = chunk_lo(nq, parts, pt + 1); i < ie; ++i) {
                 mr_result &r = results[i];
-                if (hp.q_status[i] != MR_OK) {
+                int32_t qs = MR_OK;
+                if (hp.dev_grouped) {
+                    if (inv != hp.invalid.end() && *inv == i) {
+                        qs = MR_ERR_INVALID_INDEX;
+                        ++inv;
+                    }
+                } else {
+                    qs = hp.q_status[i];
+                }
+                if (qs != MR_OK) {
                     std::memset(&r, 0, sizeof(r));
-                    r.status = hp.q_status[i];
+                    r.status = qs;
                 }
                 if (r.status == MR_OK && uint64_t(r.command_offset) + r.n_commands > pool_cap) {
                     en = std::min<uint64_t>(en, r.command_offset);
@@ -3030,6 +3254,7 @@ extern "C" int mr_plan_fetch(mr_plan *pl, mr_result *results, mr_command *pool, 
         if (plan_fetch_device(pl, results, pool, pool_cap, ret)) return ret;
     }
     const double tm0 = timing_on() ? now_ms() : 0.0;
+    if (int sh = host_arrays(pl)) return sh;
     std::vector<OutResult> res;
     std::vector<OutCmd> cmd, ovf;
     int st = plan_collect(pl, res, cmd, ovf);
