@@ -929,7 +929,20 @@ static void trim_group_scratch() {
     for (GroupScratch *g : g_scratch) g->release();
 }
 
-static bool dev_group_ok(const mr_grid *g, uint32_t n);
+// ---- query batches grouped on the device (mr_k_groupq.hip) -------------------------
+// Batches of at least kDevGroupMin queries on a grid whose cells are all where the
+// layout's formula puts them (mr_grid::exact) go up raw: the lookups, the stable sort by
+// source and the lane kernel's partition run on the device, and the host learns counts
+// only.  MR_DEV_GROUP=0: never, =1: any batch on such a grid.
+constexpr uint32_t kDevGroupMin = 32768;
+static bool dev_group_ok(const mr_grid *g, uint32_t n) {
+    if (!g->exact || n == 0 || n >= (1u << 30)) return false;
+    const char *e = std::getenv("MR_DEV_GROUP");
+    if (e && !std::strcmp(e, "0")) return false;
+    if (e && !std::strcmp(e, "1")) return true;
+    return n >= kDevGroupMin;
+}
+
 static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs, uint32_t n, uint32_t max_cmds,
                       HostPlan &hp, bool allow_dev_group = false) {
     const double tbs = timing_on() ? now_ms() : 0.0;
@@ -1972,20 +1985,7 @@ static uint32_t partition_sources(HostPlan &hp) {
     return n_lane;
 }
 
-// ---- query batches grouped on the device (mr_k_groupq.hip) -------------------------
-// Batches of at least kDevGroupMin queries on a grid whose cells are all where the
-// layout's formula puts them (mr_grid::exact) go up raw: the lookups, the stable sort by
-// source and the lane kernel's partition run on the device, and the host learns counts
-// only.  MR_DEV_GROUP=0: never, =1: any batch on such a grid.
-constexpr uint32_t kDevGroupMin = 32768;
-static bool dev_group_ok(const mr_grid *g, uint32_t n) {
-    if (!g->exact || n == 0 || n >= (1u << 30)) return false;
-    const char *e = std::getenv("MR_DEV_GROUP");
-    if (e && !std::strcmp(e, "0")) return false;
-    if (e && !std::strcmp(e, "1")) return true;
-    return n >= kDevGroupMin;
-}
-
+// ---- query batches grouped on the device (mr_k_groupq.hip; dev_group_ok above) -----
 // The per-batch block's layout for n queries (src_v, q_begin, q_dst, q_id: each bounded
 // by n words, 64-word aligned)
 static void qblock_layout(size_t n, size_t at[5]) {
