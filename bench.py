@@ -277,7 +277,9 @@ def end_to_end(m, grid, params, qpg, seed, max_cmds, reps, pinned=False):
     if pinned:
         for b in bufs:
             pathfinder.pin_host(b)
-    for r in range(reps):
+    # one batch before the timed ones: the first also pays one-time setup (the pinned
+    # staging buffers, the sort's first call); it is reported as cold_ms, never in the median
+    for r in range(reps + 1):
         rng = np.random.default_rng(seed + 1000 + r)
         src = rng.integers(0, V, qpg, dtype=np.int64)
         dst = rng.integers(0, V, qpg, dtype=np.int64)
@@ -296,13 +298,14 @@ def end_to_end(m, grid, params, qpg, seed, max_cmds, reps, pinned=False):
     if pinned:
         for b in bufs:
             pathfinder.unpin_host(b)
+    cold = rows.pop(0)
     rows.sort()
     tot, cr, run, fe = rows[len(rows) // 2]
-    return {"e2e_queries_per_s": qpg / tot, "output_arrays": "page-locked" if pinned else "pageable", "queries": qpg, "ms": tot * 1e3, "plan_create_ms": cr * 1e3,
+    return {"e2e_queries_per_s": qpg / tot, "cold_ms": cold[0] * 1e3, "output_arrays": "page-locked" if pinned else "pageable", "queries": qpg, "ms": tot * 1e3, "plan_create_ms": cr * 1e3,
             "run_ms": run * 1e3, "fetch_ms": fe * 1e3, "reps": reps,
             "what": "fresh batch: Plan create (host grouping, tables, H2D) + one pass + mr_plan_fetch (D2H and "
                     "decode of every label) into the caller's output arrays (allocated once, reused across batches), "
-                    "median of reps"}
+                    "median of reps after one untimed batch (cold_ms: its time)"}
 
 
 def cpu_model():
