@@ -99,6 +99,13 @@ __device__ __forceinline__ void cert_load_table(const KArgs *__restrict__ a, uin
 }
 
 // the least extension of cell (x, y)'s grid neighbours (the Center has none); false when
+// The repair sweep's mark on a plain cell word (bit 30: a plain word is b << 20 | k with a
+// 10-bit b): the first check sets it on its failing cells, the sweep on the cells a change
+// reaches; a sweep rewrites every cell it marked, so no mark outlives it.
+constexpr uint32_t kCertDirty = 1u << 30;
+__device__ __forceinline__ uint32_t cert_clean(uint32_t w) {
+    return (w == kViaSource || (w & kViaSpecial)) ? w : (w & ~kCertDirty);
+}
 // a neighbour's label cannot be extended here (counted as a failure)
 template <bool ATOMIC>
 __device__ __forceinline__ bool cert_best4(const DevParams &p, const CertEntry *E, const CellWord *w, uint32_t pitch,
@@ -112,7 +119,7 @@ __device__ __forceinline__ bool cert_best4(const DevParams &p, const CertEntry *
     for (int i = 0; i < 4; ++i) {
         if (nx[i] < 0 || nx[i] >= S || ny[i] < 0 || ny[i] >= S || (nx[i] == H && ny[i] == H)) continue;
         const CellWord *pw = w + (size_t)ny[i] * pitch + nx[i];
-        const uint32_t wu = ATOMIC ? __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : *pw;
+        const uint32_t wu = cert_clean(ATOMIC ? __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : *pw);
         CertLab c;
         if (!cert_ext(p, E, wu, c, FT, nft)) {
             ok = false;
@@ -126,7 +133,7 @@ __device__ __forceinline__ bool cert_best4(const DevParams &p, const CertEntry *
 
 // One launch over every slot's cells (blockIdx.y = slot): failing cells lower the slot's
 // key, count, and widen its box.
-__global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict__ a) {
+__global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict__ a, uint32_t mark) {
     __shared__ CertEntry E[64];
     const uint32_t slot = blockIdx.y;
     const uint32_t nslot = min(a->cert_cap, __hip_atomic_load(a->counter + kCtrCert, __ATOMIC_RELAXED,
@@ -140,7 +147,7 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
     uint32_t key = 0xFFFFFFFFu, nf = 0, x0 = 0xFFFFFFFFu, x1 = 0, y0 = 0xFFFFFFFFu, y1 = 0;
     for (uint32_t v = blockIdx.x * kBS + threadIdx.x; v < p.V; v += gridDim.x * kBS) {
         const uint32_t y = v / S, x = v - y * S;
-        const uint32_t cw = w[(size_t)y * pitch + x];
+        const uint32_t cw = cert_clean(w[(size_t)y * pitch + x]);
         if (cw == kViaSource || v == p.vc) continue;
         CertLab best{};
         bool any;
@@ -204,6 +211,9 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
             }
         }
         if (fail) {
+            // (the check before the sweep: a failing plain cell seeds its queue; only this
+            // thread writes the word, and readers mask the mark)
+            if (mark && !(cw & kViaSpecial)) const_cast<CellWord *>(w)[(size_t)y * pitch + x] = cw | kCertDirty;
             key = min(key, any ? min(own1, best.c1) : own1);
             ++nf;
             x0 = min(x0, x);
@@ -283,19 +293,27 @@ __global__ __launch_bounds__(kSelectBS) void cert_select_kernel(const KArgs *__r
 }
 
 constexpr uint32_t kSweepBS = 1024;      // threads of the sweep's one workgroup per slot
-constexpr uint32_t kSweepBuckets = 16384;  // leading-metric buckets a window may span
+constexpr uint32_t kSweepBuckets = 12288;  // leading-metric buckets a window may span
 constexpr int kSweepMargin = 2;            // cells added round the failing cells' box
 constexpr uint32_t kSweepRunTimes = 8200;  // run-time table (walks of up to 2 S + 3 legs at S = 4097)
 
 // One workgroup per slot: the failing box (+ margin) in order of the leading metric of its
-// current words, bucket by bucket, each cell from its neighbours; then the slot's check
-// state is reset for the next check.  One workgroup (one CU) owns the slot's words during
-// the sweep, so workgroup-scope accesses and the barrier order the buckets (agent scope
-// would take every load past the XCD's L2).
+// cells, bucket by bucket (buckets of the least StandardMove increment: a cell never
+// extends another of its bucket), each cell recomputed from its neighbours' current words.
+// Only the cells that can change are touched: the ones the first check marked (its failing
+// plain cells) and those whose neighbour changed in an earlier bucket — any other cell's
+// word already is its neighbours' least extension, and stays so while they do.  Each
+// bucket holds a queue of those cells (its region of the counting-sorted window, filled
+// through an LDS counter; the mark bit on the word keeps a cell queued once), and a bucket
+// with an empty queue costs no barrier.  The words and queues stay in the slot's buffers;
+// one workgroup (one CU) owns them during the sweep, so workgroup-scope accesses and the
+// barrier order the buckets.  (ff 2 at 1025^2, DESIGN.md section 3d: 100k of the window's
+// 441k cells in 810 of its 1 329 buckets, tools/cert_probe.py.)
 __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__restrict__ a) {
     __shared__ CertEntry E[64];
-    __shared__ uint32_t off[kSweepBuckets];
-    __shared__ uint32_t FT[kSweepRunTimes];  // run times of 0 .. kSweepRunTimes - 1 legs
+    __shared__ uint32_t off[kSweepBuckets];   // bucket j's queue: list[off[j - 1] ..), off[-1] = 0
+    __shared__ uint32_t fill[kSweepBuckets];  // its length so far
+    __shared__ uint32_t FT[kSweepRunTimes];   // run times of 0 .. kSweepRunTimes - 1 legs
     __shared__ uint32_t red[2];
     const uint32_t slot = blockIdx.x, tid = threadIdx.x;
     const uint32_t nslot = min(a->cert_cap, __hip_atomic_load(a->counter + kCtrCert, __ATOMIC_RELAXED,
@@ -315,7 +333,7 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
         atomicMax(st + kCertY1, ps[kCertY1]);
     }
     __syncthreads();
-    if (st[kCertFails] == 0) return;  // certified as it stands
+    if (st[kCertFails] == 0) return;  // certified as it stands (and nothing was marked)
     const DevParams p = a->p;
     cert_load_table(a, slot, E);
     const uint32_t nft = min(kSweepRunTimes, 2u * p.S + 4u);
@@ -340,12 +358,15 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
         return L == 0 ? E[b].m0 + k : E[b].m2 + (k < nft ? FT[k] : run_time_ff(k, p.ff_num, p.ff_den));
     };
     auto plain_word = [&](uint32_t cw) { return cw != kViaSource && !(cw & kViaSpecial); };
+    auto wload = [&](uint32_t x, uint32_t y) {
+        return __hip_atomic_load(w + (size_t)y * pitch + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
     __syncthreads();
     // the window's key range
     uint32_t kmin = 0xFFFFFFFFu, kmax = 0;
     for (uint32_t i = tid; i < area; i += kSweepBS) {
         const uint32_t y = uint32_t(by0) + i / bw, x = uint32_t(bx0) + i % bw;
-        const uint32_t cw = w[(size_t)y * pitch + x];
+        const uint32_t cw = cert_clean(w[(size_t)y * pitch + x]);
         if (!plain_word(cw)) continue;
         const uint32_t kk = lead_of(cw) / W;
         kmin = min(kmin, kk);
@@ -361,22 +382,33 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
     kmin = red[0];
     kmax = red[1];
     const uint32_t nb = kmax >= kmin ? kmax - kmin + 1 : 0;
-    if (nb == 0 || nb > kSweepBuckets) return;  // nothing to sweep / too wide: left to the SSSP kernel
-    for (uint32_t j = tid; j < nb; j += kSweepBS) off[j] = 0;
+    if (nb == 0 || nb > kSweepBuckets) {  // nothing to sweep / too wide: left to the SSSP kernel
+        for (uint32_t i = tid; i < area; i += kSweepBS) {  // (the check's marks come off)
+            const uint32_t y = uint32_t(by0) + i / bw, x = uint32_t(bx0) + i % bw;
+            const uint32_t cw = w[(size_t)y * pitch + x];
+            if (plain_word(cw) && (cw & kCertDirty)) w[(size_t)y * pitch + x] = cw & ~kCertDirty;
+        }
+        return;
+    }
+    const bool full = (a->dbg_flags & kDbgSweepFull) != 0;  // (A/B: every window cell queued)
+    for (uint32_t j = tid; j < nb; j += kSweepBS) {
+        off[j] = 0;
+        fill[j] = 0;
+    }
     __syncthreads();
+    // bucket sizes over the whole window (a queue never outgrows its bucket)
     for (uint32_t i = tid; i < area; i += kSweepBS) {
         const uint32_t y = uint32_t(by0) + i / bw, x = uint32_t(bx0) + i % bw;
-        const uint32_t cw = w[(size_t)y * pitch + x];
+        const uint32_t cw = cert_clean(w[(size_t)y * pitch + x]);
         if (plain_word(cw)) atomicAdd(&off[lead_of(cw) / W - kmin], 1u);
     }
     __syncthreads();
-    // exclusive prefix sum of the counts (each thread a run of buckets, then the runs)
+    // inclusive prefix sum of the sizes (each thread a run of buckets, then the runs):
+    // off[j] ends bucket j's region
     {
         const uint32_t per = (nb + kSweepBS - 1) / kSweepBS, j0 = tid * per, j1 = min(nb, j0 + per);
         uint32_t sum = 0;
         for (uint32_t j = j0; j < j1; ++j) sum += off[j];
-        // block scan of the run sums through LDS (the histogram's tail is free past nb;
-        // a second small array avoids aliasing it)
         __shared__ uint32_t runs[kSweepBS];
         runs[tid] = sum;
         __syncthreads();
@@ -388,35 +420,63 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
         }
         uint32_t acc = runs[tid] - sum;
         for (uint32_t j = j0; j < j1; ++j) {
-            const uint32_t c = off[j];
+            acc += off[j];
             off[j] = acc;
-            acc += c;
         }
     }
     __syncthreads();
+    // the seeds: the cells the first check marked
     for (uint32_t i = tid; i < area; i += kSweepBS) {
         const uint32_t y = uint32_t(by0) + i / bw, x = uint32_t(bx0) + i % bw;
-        const uint32_t cw = w[(size_t)y * pitch + x];
-        if (plain_word(cw)) list[atomicAdd(&off[lead_of(cw) / W - kmin], 1u)] = y << 16 | x;
+        uint32_t cw = w[(size_t)y * pitch + x];
+        if (!plain_word(cw)) continue;
+        if (full && !(cw & kCertDirty)) w[(size_t)y * pitch + x] = (cw |= kCertDirty);
+        if (!(cw & kCertDirty)) continue;
+        const uint32_t j = lead_of(cw & ~kCertDirty) / W - kmin;
+        list[(j ? off[j - 1] : 0u) + atomicAdd(&fill[j], 1u)] = y << 16 | x;
     }
     __syncthreads();
-    // off[j] now ends bucket j.  Bucket by bucket: each cell takes its neighbours' least
-    // extension (a cell of this bucket never extends another of it).
+    // Bucket by bucket: each queued cell takes its neighbours' least extension; a change
+    // queues the neighbours of later buckets that are not queued yet.
     for (uint32_t j = 0; j < nb; ++j) {
-        const uint32_t beg = j ? off[j - 1] : 0u, end = off[j];
-        if (beg == end) continue;
-        for (uint32_t i = beg + tid; i < end; i += kSweepBS) {
+        const uint32_t n = fill[j];  // (uniform: written before the last barrier)
+        if (n == 0) continue;
+        const uint32_t beg = j ? off[j - 1] : 0u;
+        for (uint32_t i = beg + tid; i < beg + n; i += kSweepBS) {
             const uint32_t v = list[i], y = v >> 16, x = v & 0xFFFFu;
             CertLab best{};
             bool any;
             cert_best4<true>(p, E, w, pitch, int(x), int(y), best, any, FT, nft);
-            if (!any) continue;
             CellWord *pw = w + (size_t)y * pitch + x;
-            const uint32_t nw = (best.b << kStBShift) | best.k;
-            if (__hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != nw)
-                __hip_atomic_store(pw, nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t old = __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~kCertDirty;
+            const uint32_t nw = any ? ((best.b << kStBShift) | best.k) : old;
+            // (the mark stays until the end: a processed cell is never queued again)
+            if (nw == old) continue;
+            __hip_atomic_store(pw, nw | kCertDirty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int nx[4] = {int(x) - 1, int(x) + 1, int(x), int(x)}, ny[4] = {int(y), int(y), int(y) - 1, int(y) + 1};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (nx[q] < bx0 || nx[q] > bx1 || ny[q] < by0 || ny[q] > by1) continue;  // (outside the window: fixed)
+                const uint32_t cu = wload(uint32_t(nx[q]), uint32_t(ny[q]));
+                if (!plain_word(cu) || (cu & kCertDirty)) continue;  // (queued or processed already)
+                const uint32_t ju = lead_of(cu) / W - kmin;        // (an untouched cell: its initial bucket)
+                if (ju <= j || ju >= nb) continue;                 // (an earlier or this bucket: not its reader)
+                CellWord *pu = w + (size_t)ny[q] * pitch + nx[q];
+                const uint32_t was = __hip_atomic_fetch_or(pu, kCertDirty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (was & kCertDirty) continue;  // queued already
+                list[off[ju - 1] + atomicAdd(&fill[ju], 1u)] = uint32_t(ny[q]) << 16 | uint32_t(nx[q]);
+            }
         }
         __syncthreads();
+    }
+    // the marks come off every queued cell
+    for (uint32_t j = 0; j < nb; ++j) {
+        const uint32_t beg = j ? off[j - 1] : 0u, n = fill[j];
+        for (uint32_t i = beg + tid; i < beg + n; i += kSweepBS) {
+            const uint32_t v = list[i];
+            CellWord *pw = w + (size_t)(v >> 16) * pitch + (v & 0xFFFFu);
+            *pw = *pw & ~kCertDirty;
+        }
     }
 }
 

@@ -71,7 +71,7 @@ uint32_t hub_group_lds_bytes(uint32_t NS, uint32_t nreg, uint32_t G);
 hipError_t launch_hub_group(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t n,
                             uint32_t G, hipStream_t stream);
 hipError_t launch_cert_select(const KArgs *d_args, hipStream_t stream);
-hipError_t launch_cert_check(const KArgs *d_args, uint32_t gx, uint32_t slots, hipStream_t stream);
+hipError_t launch_cert_check(const KArgs *d_args, uint32_t gx, uint32_t slots, uint32_t mark, hipStream_t stream);
 hipError_t launch_cert_sweep(const KArgs *d_args, uint32_t slots, hipStream_t stream);
 hipError_t decode_records_device(const OutResult *res, const OutCmd *slots, const OutCmd *ovf, uint32_t novf,
                                  const uint32_t *q_id, uint32_t nrec, uint32_t nq, uint32_t mc,
@@ -2709,12 +2709,13 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         if (e == hipSuccess && !pl->fb_none && pl->cert_cap) {
             e = launch_cert_select(pl->d_args, s);
             if (e == hipSuccess) e = launch_fill(pl->d_args_cert, pl->ka.p.perm, pl->cert_fill_gx, 1, s);
-            if (e == hipSuccess) e = launch_cert_check(pl->d_args, pl->cert_check_gx, pl->cert_cap, s);
             // (MR_CERT_NOSWEEP=1: diagnostics, the first check's state stays for MR_CERT_DEBUG)
             static const bool nosweep = std::getenv("MR_CERT_NOSWEEP") != nullptr;
+            // the first check marks its failing cells: the sweep's seeds
+            if (e == hipSuccess) e = launch_cert_check(pl->d_args, pl->cert_check_gx, pl->cert_cap, nosweep ? 0u : 1u, s);
             if (!nosweep) {
                 if (e == hipSuccess) e = launch_cert_sweep(pl->d_args, pl->cert_cap, s);
-                if (e == hipSuccess) e = launch_cert_check(pl->d_args, pl->cert_check_gx, pl->cert_cap, s);
+                if (e == hipSuccess) e = launch_cert_check(pl->d_args, pl->cert_check_gx, pl->cert_cap, 0u, s);
             }
         }
         if (e == hipSuccess && !pl->fb_none)

@@ -11,8 +11,8 @@ hipError_t launch_cert_select(const KArgs *d_args, hipStream_t stream) {
 }
 
 // the check over every slot's cells: gx workgroups per slot, `slots` slots
-hipError_t launch_cert_check(const KArgs *d_args, uint32_t gx, uint32_t slots, hipStream_t stream) {
-    void *args[] = {const_cast<KArgs **>(&d_args)};
+hipError_t launch_cert_check(const KArgs *d_args, uint32_t gx, uint32_t slots, uint32_t mark, hipStream_t stream) {
+    void *args[] = {const_cast<KArgs **>(&d_args), &mark};
     return hipLaunchKernel((const void *)&cert_check_kernel, dim3(gx, slots), dim3(kBS), args, 0, stream);
 }
 
