@@ -293,27 +293,31 @@ __global__ __launch_bounds__(kSelectBS) void cert_select_kernel(const KArgs *__r
 }
 
 constexpr uint32_t kSweepBS = 1024;      // threads of the sweep's one workgroup per slot
-constexpr uint32_t kSweepBuckets = 12288;  // leading-metric buckets a window may span
+constexpr uint32_t kSweepBuckets = 4096;   // leading-metric buckets a window may span
 constexpr int kSweepMargin = 2;            // cells added round the failing cells' box
 constexpr uint32_t kSweepRunTimes = 8200;  // run-time table (walks of up to 2 S + 3 legs at S = 4097)
+constexpr uint32_t kSweepPool = 20480;     // LDS words: the window's words, or its mark bitmap
 
 // One workgroup per slot: the failing box (+ margin) in order of the leading metric of its
 // cells, bucket by bucket (buckets of the least StandardMove increment: a cell never
 // extends another of its bucket), each cell recomputed from its neighbours' current words.
-// Only the cells that can change are touched: the ones the first check marked (its failing
-// plain cells) and those whose neighbour changed in an earlier bucket — any other cell's
-// word already is its neighbours' least extension, and stays so while they do.  Each
-// bucket holds a queue of those cells (its region of the counting-sorted window, filled
-// through an LDS counter; the mark bit on the word keeps a cell queued once), and a bucket
-// with an empty queue costs no barrier.  The words and queues stay in the slot's buffers;
-// one workgroup (one CU) owns them during the sweep, so workgroup-scope accesses and the
-// barrier order the buckets.  (ff 2 at 1025^2, DESIGN.md section 3d: 100k of the window's
-// 441k cells in 810 of its 1 329 buckets, tools/cert_probe.py.)
+// Only the cells that can change are touched: the ones the first check marked (its
+// failing plain cells) and those whose neighbour changed in an earlier bucket — any other
+// cell's word already is its neighbours' least extension, and stays so while they do.
+// Each bucket holds a queue of those cells (its region of the counting-sorted window,
+// filled through an LDS counter; a mark keeps a cell queued once), and a bucket with an
+// empty queue costs no barrier.  A window of at most kSweepPool cells keeps its words in
+// LDS (marks in bit 30) and writes them back at the end; a larger one (up to 32 x
+// kSweepPool cells) keeps its marks in an LDS bitmap and its words in the slot's buffer,
+// owned by this workgroup (one CU) during the sweep, so workgroup-scope accesses and the
+// barrier order the buckets.  Wider windows are left to the SSSP kernel.  (ff 2 at 1025^2,
+// 100k of the window's 441k cells in 810 of its 1 329 buckets.)
 __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__restrict__ a) {
     __shared__ CertEntry E[64];
     __shared__ uint32_t off[kSweepBuckets];   // bucket j's queue: list[off[j - 1] ..), off[-1] = 0
     __shared__ uint32_t fill[kSweepBuckets];  // its length so far
     __shared__ uint32_t FT[kSweepRunTimes];   // run times of 0 .. kSweepRunTimes - 1 legs
+    __shared__ uint32_t pool[kSweepPool];
     __shared__ uint32_t red[2];
     const uint32_t slot = blockIdx.x, tid = threadIdx.x;
     const uint32_t nslot = min(a->cert_cap, __hip_atomic_load(a->counter + kCtrCert, __ATOMIC_RELAXED,
@@ -342,13 +346,15 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
         red[0] = 0xFFFFFFFFu;
         red[1] = 0;
     }
-    const int S = int(p.S);
+    const int S = int(p.S), H = int(p.H);
     const int bx0 = max(0, int(st[kCertX0]) - kSweepMargin), bx1 = min(S - 1, int(st[kCertX1]) + kSweepMargin);
     const int by0 = max(0, int(st[kCertY0]) - kSweepMargin), by1 = min(S - 1, int(st[kCertY1]) + kSweepMargin);
     const uint32_t bw = uint32_t(bx1 - bx0 + 1), area = bw * uint32_t(by1 - by0 + 1);
     const uint32_t pitch = a->rec_pitch;
     CellWord *w = a->cert_rec + (unsigned long long)slot * p.S * pitch;
     uint32_t *list = a->cert_aux + (unsigned long long)slot * p.V;
+    const bool in_lds = area <= kSweepPool;                  // the words in LDS
+    const bool fits = in_lds || area <= 32u * kSweepPool;  // else: left to the SSSP kernel
     // the leading metric: the first in comparator order that grows along a walk; its least
     // StandardMove increment is the bucket width
     const uint32_t L = p.perm[0] != 1u ? p.perm[0] : p.perm[1];
@@ -358,15 +364,21 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
         return L == 0 ? E[b].m0 + k : E[b].m2 + (k < nft ? FT[k] : run_time_ff(k, p.ff_num, p.ff_den));
     };
     auto plain_word = [&](uint32_t cw) { return cw != kViaSource && !(cw & kViaSpecial); };
-    auto wload = [&](uint32_t x, uint32_t y) {
-        return __hip_atomic_load(w + (size_t)y * pitch + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    auto gptr = [&](int x, int y) { return w + (size_t)y * pitch + x; };
+    auto widx = [&](int x, int y) { return uint32_t(y - by0) * bw + uint32_t(x - bx0); };
+    auto inwin = [&](int x, int y) { return x >= bx0 && x <= bx1 && y >= by0 && y <= by1; };
+    // a cell's current word (marks off): LDS inside an LDS window, else the slot's buffer
+    auto word = [&](int x, int y) -> uint32_t {
+        if (in_lds && inwin(x, y)) return cert_clean(pool[widx(x, y)]);
+        return cert_clean(__hip_atomic_load(gptr(x, y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
     };
     __syncthreads();
-    // the window's key range
+    // the window's key range; an LDS window's words come in (with the check's marks)
     uint32_t kmin = 0xFFFFFFFFu, kmax = 0;
     for (uint32_t i = tid; i < area; i += kSweepBS) {
-        const uint32_t y = uint32_t(by0) + i / bw, x = uint32_t(bx0) + i % bw;
-        const uint32_t cw = cert_clean(w[(size_t)y * pitch + x]);
+        const int y = by0 + int(i / bw), x = bx0 + int(i % bw);
+        const uint32_t raw = *gptr(x, y), cw = cert_clean(raw);
+        if (in_lds) pool[i] = raw;
         if (!plain_word(cw)) continue;
         const uint32_t kk = lead_of(cw) / W;
         kmin = min(kmin, kk);
@@ -382,11 +394,11 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
     kmin = red[0];
     kmax = red[1];
     const uint32_t nb = kmax >= kmin ? kmax - kmin + 1 : 0;
-    if (nb == 0 || nb > kSweepBuckets) {  // nothing to sweep / too wide: left to the SSSP kernel
+    if (nb == 0 || nb > kSweepBuckets || !fits) {  // nothing to sweep / too wide: left to the SSSP kernel
         for (uint32_t i = tid; i < area; i += kSweepBS) {  // (the check's marks come off)
-            const uint32_t y = uint32_t(by0) + i / bw, x = uint32_t(bx0) + i % bw;
-            const uint32_t cw = w[(size_t)y * pitch + x];
-            if (plain_word(cw) && (cw & kCertDirty)) w[(size_t)y * pitch + x] = cw & ~kCertDirty;
+            const int y = by0 + int(i / bw), x = bx0 + int(i % bw);
+            const uint32_t cw = *gptr(x, y);
+            if (plain_word(cw) && (cw & kCertDirty)) *gptr(x, y) = cw & ~kCertDirty;
         }
         return;
     }
@@ -395,11 +407,24 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
         off[j] = 0;
         fill[j] = 0;
     }
+    if (!in_lds)
+        for (uint32_t i = tid; i < (area + 31) / 32; i += kSweepBS) pool[i] = 0;  // the mark bitmap
     __syncthreads();
+    // marks: test-and-set (true: this thread set it) and test
+    auto mark = [&](int x, int y) -> bool {
+        const uint32_t i = widx(x, y);
+        if (in_lds) return !(atomicOr(&pool[i], kCertDirty) & kCertDirty);
+        const uint32_t bit = 1u << (i & 31u);
+        return !(atomicOr(&pool[i >> 5], bit) & bit);
+    };
+    auto marked = [&](int x, int y) -> bool {
+        const uint32_t i = widx(x, y);
+        return in_lds ? (pool[i] & kCertDirty) != 0 : ((pool[i >> 5] >> (i & 31u)) & 1u) != 0;
+    };
     // bucket sizes over the whole window (a queue never outgrows its bucket)
     for (uint32_t i = tid; i < area; i += kSweepBS) {
-        const uint32_t y = uint32_t(by0) + i / bw, x = uint32_t(bx0) + i % bw;
-        const uint32_t cw = cert_clean(w[(size_t)y * pitch + x]);
+        const int y = by0 + int(i / bw), x = bx0 + int(i % bw);
+        const uint32_t cw = in_lds ? cert_clean(pool[i]) : cert_clean(*gptr(x, y));
         if (plain_word(cw)) atomicAdd(&off[lead_of(cw) / W - kmin], 1u);
     }
     __syncthreads();
@@ -425,59 +450,75 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
         }
     }
     __syncthreads();
-    // the seeds: the cells the first check marked
+    // the seeds: the cells the first check marked (a bitmap window takes the marks off the
+    // words; an LDS window keeps them in its words)
     for (uint32_t i = tid; i < area; i += kSweepBS) {
-        const uint32_t y = uint32_t(by0) + i / bw, x = uint32_t(bx0) + i % bw;
-        uint32_t cw = w[(size_t)y * pitch + x];
-        if (!plain_word(cw)) continue;
-        if (full && !(cw & kCertDirty)) w[(size_t)y * pitch + x] = (cw |= kCertDirty);
-        if (!(cw & kCertDirty)) continue;
-        const uint32_t j = lead_of(cw & ~kCertDirty) / W - kmin;
-        list[(j ? off[j - 1] : 0u) + atomicAdd(&fill[j], 1u)] = y << 16 | x;
+        const int y = by0 + int(i / bw), x = bx0 + int(i % bw);
+        uint32_t raw = in_lds ? pool[i] : *gptr(x, y);
+        if (!plain_word(raw)) continue;
+        bool seed = (raw & kCertDirty) != 0 || full;
+        if (in_lds) {
+            if (full) pool[i] = raw | kCertDirty;
+        } else {
+            if (raw & kCertDirty) *gptr(x, y) = raw & ~kCertDirty;
+        }
+        if (!seed) continue;
+        if (!in_lds) atomicOr(&pool[i >> 5], 1u << (i & 31u));
+        const uint32_t j = lead_of(raw & ~kCertDirty) / W - kmin;
+        list[(j ? off[j - 1] : 0u) + atomicAdd(&fill[j], 1u)] = uint32_t(y) << 16 | uint32_t(x);
     }
     __syncthreads();
     // Bucket by bucket: each queued cell takes its neighbours' least extension; a change
-    // queues the neighbours of later buckets that are not queued yet.
+    // queues its unmarked neighbours of later buckets.
     for (uint32_t j = 0; j < nb; ++j) {
         const uint32_t n = fill[j];  // (uniform: written before the last barrier)
         if (n == 0) continue;
         const uint32_t beg = j ? off[j - 1] : 0u;
         for (uint32_t i = beg + tid; i < beg + n; i += kSweepBS) {
-            const uint32_t v = list[i], y = v >> 16, x = v & 0xFFFFu;
+            const uint32_t v = list[i];
+            const int y = int(v >> 16), x = int(v & 0xFFFFu);
+            const int nx[4] = {x - 1, x + 1, x, x}, ny[4] = {y, y, y - 1, y + 1};
+            uint32_t nwv[4];
+            bool nok[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {  // (all four reads issued together)
+                nok[q] = !(nx[q] < 0 || nx[q] >= S || ny[q] < 0 || ny[q] >= S || (nx[q] == H && ny[q] == H));
+                nwv[q] = nok[q] ? word(nx[q], ny[q]) : 0u;
+            }
+            const uint32_t old = word(x, y);
             CertLab best{};
-            bool any;
-            cert_best4<true>(p, E, w, pitch, int(x), int(y), best, any, FT, nft);
-            CellWord *pw = w + (size_t)y * pitch + x;
-            const uint32_t old = __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & ~kCertDirty;
-            const uint32_t nw = any ? ((best.b << kStBShift) | best.k) : old;
-            // (the mark stays until the end: a processed cell is never queued again)
-            if (nw == old) continue;
-            __hip_atomic_store(pw, nw | kCertDirty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int nx[4] = {int(x) - 1, int(x) + 1, int(x), int(x)}, ny[4] = {int(y), int(y), int(y) - 1, int(y) + 1};
+            bool any = false;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                if (nx[q] < bx0 || nx[q] > bx1 || ny[q] < by0 || ny[q] > by1) continue;  // (outside the window: fixed)
-                const uint32_t cu = wload(uint32_t(nx[q]), uint32_t(ny[q]));
-                if (!plain_word(cu) || (cu & kCertDirty)) continue;  // (queued or processed already)
-                const uint32_t ju = lead_of(cu) / W - kmin;        // (an untouched cell: its initial bucket)
-                if (ju <= j || ju >= nb) continue;                 // (an earlier or this bucket: not its reader)
-                CellWord *pu = w + (size_t)ny[q] * pitch + nx[q];
-                const uint32_t was = __hip_atomic_fetch_or(pu, kCertDirty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (was & kCertDirty) continue;  // queued already
+                CertLab c;
+                if (!nok[q] || !cert_ext(p, E, nwv[q], c, FT, nft)) continue;
+                if (!any || cert_less(c, best)) best = c;
+                any = true;
+            }
+            const uint32_t nw = any ? ((best.b << kStBShift) | best.k) : old;
+            if (nw == old) continue;
+            if (in_lds) pool[widx(x, y)] = nw | kCertDirty;  // (the mark stays: never queued again)
+            else __hip_atomic_store(gptr(x, y), nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (!nok[q] || !inwin(nx[q], ny[q])) continue;  // (outside the window: fixed)
+                const uint32_t cu = nwv[q];
+                if (!plain_word(cu) || marked(nx[q], ny[q])) continue;  // (queued or processed already)
+                const uint32_t ju = lead_of(cu) / W - kmin;           // (an unmarked cell: its initial bucket)
+                if (ju <= j || ju >= nb) continue;                    // (an earlier or this bucket: not its reader)
+                if (!mark(nx[q], ny[q])) continue;                    // (another thread queued it)
                 list[off[ju - 1] + atomicAdd(&fill[ju], 1u)] = uint32_t(ny[q]) << 16 | uint32_t(nx[q]);
             }
         }
         __syncthreads();
     }
-    // the marks come off every queued cell
-    for (uint32_t j = 0; j < nb; ++j) {
-        const uint32_t beg = j ? off[j - 1] : 0u, n = fill[j];
-        for (uint32_t i = beg + tid; i < beg + n; i += kSweepBS) {
-            const uint32_t v = list[i];
-            CellWord *pw = w + (size_t)(v >> 16) * pitch + (v & 0xFFFFu);
-            *pw = *pw & ~kCertDirty;
+    // an LDS window's words go back, marks off
+    if (in_lds)
+        for (uint32_t i = tid; i < area; i += kSweepBS) {
+            const int y = by0 + int(i / bw), x = bx0 + int(i % bw);
+            const uint32_t raw = pool[i];
+            if (plain_word(raw)) *gptr(x, y) = raw & ~kCertDirty;
         }
-    }
 }
 
 }  // namespace mr

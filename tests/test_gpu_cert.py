@@ -116,3 +116,30 @@ def test_every_source_handed_over(eng, oracle_lib, monkeypatch, cert, size, k, s
                     assert st["certified_sources"] == 0, st
                 else:  # slots for the first 64 a pass; a few may still need the SSSP kernel
                     assert st["certified_sources"] >= min(64, st["num_sources"]) // 2, st
+
+
+def test_more_fallbacks_than_the_staging(eng, oracle_lib, monkeypatch):
+    """A pass that hands over more sources than the certificate's staging holds (4 096
+    entries, kCertStageMax) gives no slots at all: which entries were staged would depend
+    on arrival order, so every handed-over source goes to the SSSP kernel instead
+    (the throughput cliff).  Every source of the 65^2
+    map (4 225 > 4 096) handed over; the labels are still the oracle's."""
+    monkeypatch.setenv("MR_HUB_FALLBACK_ALL", "1")
+    monkeypatch.setenv("MR_CERT_SLOTS", "64")
+    monkeypatch.delenv("MR_CERT", raising=False)
+    m = SyntheticMap(65, campfires_per_homeland=4, seed=2024)
+    V = m.size * m.size
+    rng = random.Random(65)
+    qs = [(m.index_at(v), m.index_at(rng.randrange(V))) for v in range(V)]
+    g = eng.MapGrid(m.cells())
+    params = Params(fleetfoot=2, sort_by=(SORT_TIME, SORT_MONEY))
+    plan = eng.Plan(g, params, qs)
+    plan.run()
+    got = plan.fetch()
+    st = plan.stats()
+    assert st["solver"] == "hub" and st["num_sources"] == V > 4096, st
+    assert st["fallback_sources"] == V and st["certified_sources"] == 0, st
+    sample = rng.sample(range(V), 400)
+    exp = oracle_lib.OracleGrid(m.cells()).find_path_batch(params, [qs[i] for i in sample], threads=0)
+    bad = [(qs[i], e, got[i]) for i, e in zip(sample, exp) if as_expected(e) != as_expected(got[i])]
+    assert not bad, (len(bad), bad[0])
