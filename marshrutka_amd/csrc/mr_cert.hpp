@@ -131,6 +131,26 @@ __device__ __forceinline__ bool cert_best4(const DevParams &p, const CertEntry *
     return ok;
 }
 
+// cert_best4 for the repair sweep's LDS window: a neighbour inside the window
+// [x0, x1] x [y0, y1] is read from its LDS copy (row-major, pool), one outside from w
+__device__ __forceinline__ void cert_best4_lds(const DevParams &p, const CertEntry *E, const CellWord *w, uint32_t pitch,
+                                               const uint32_t *pool, int x0, int y0, int x1, int y1, int x, int y,
+                                               CertLab &best, bool &any, const uint32_t *FT, uint32_t nft) {
+    const int S = int(p.S), H = int(p.H), bw = x1 - x0 + 1;
+    any = false;
+    const int nx[4] = {x - 1, x + 1, x, x}, ny[4] = {y, y, y - 1, y + 1};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (nx[i] < 0 || nx[i] >= S || ny[i] < 0 || ny[i] >= S || (nx[i] == H && ny[i] == H)) continue;
+        const bool in = nx[i] >= x0 && nx[i] <= x1 && ny[i] >= y0 && ny[i] <= y1;
+        const uint32_t raw = in ? pool[(ny[i] - y0) * bw + (nx[i] - x0)] : w[(size_t)ny[i] * pitch + nx[i]];
+        CertLab c;
+        if (!cert_ext(p, E, cert_clean(raw), c, FT, nft)) continue;
+        if (!any || cert_less(c, best)) best = c;
+        any = true;
+    }
+}
+
 // One launch over every slot's cells (blockIdx.y = slot): failing cells lower the slot's
 // key, count, and widen its box.
 __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict__ a, uint32_t mark) {
@@ -292,11 +312,17 @@ __global__ __launch_bounds__(kSelectBS) void cert_select_kernel(const KArgs *__r
     if (tid == 0) a->counter[kCtrCert] = min(nstaged, a->cert_cap);
 }
 
+#ifndef MR_SWEEP_BUCKETS
+#define MR_SWEEP_BUCKETS 4096
+#endif
+#ifndef MR_SWEEP_POOL
+#define MR_SWEEP_POOL 20480
+#endif
 constexpr uint32_t kSweepBS = 1024;      // threads of the sweep's one workgroup per slot
-constexpr uint32_t kSweepBuckets = 4096;   // leading-metric buckets a window may span
+constexpr uint32_t kSweepBuckets = MR_SWEEP_BUCKETS;  // leading-metric buckets a window may span
 constexpr int kSweepMargin = 2;            // cells added round the failing cells' box
 constexpr uint32_t kSweepRunTimes = 8200;  // run-time table (walks of up to 2 S + 3 legs at S = 4097)
-constexpr uint32_t kSweepPool = 20480;     // LDS words: the window's words, or its mark bitmap
+constexpr uint32_t kSweepPool = MR_SWEEP_POOL;  // LDS words: the window's words, or its mark bitmap
 
 // One workgroup per slot: the failing box (+ margin) in order of the leading metric of its
 // cells, bucket by bucket (buckets of the least StandardMove increment: a cell never
@@ -353,7 +379,7 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
     const uint32_t pitch = a->rec_pitch;
     CellWord *w = a->cert_rec + (unsigned long long)slot * p.S * pitch;
     uint32_t *list = a->cert_aux + (unsigned long long)slot * p.V;
-    const bool in_lds = area <= kSweepPool;                  // the words in LDS
+    const bool in_lds = area <= kSweepPool && !(a->dbg_flags & kDbgSweepNoLds);  // the words in LDS
     const bool fits = in_lds || area <= 32u * kSweepPool;  // else: left to the SSSP kernel
     // the leading metric: the first in comparator order that grows along a walk; its least
     // StandardMove increment is the bucket width
@@ -477,32 +503,20 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
         for (uint32_t i = beg + tid; i < beg + n; i += kSweepBS) {
             const uint32_t v = list[i];
             const int y = int(v >> 16), x = int(v & 0xFFFFu);
-            const int nx[4] = {x - 1, x + 1, x, x}, ny[4] = {y, y, y - 1, y + 1};
-            uint32_t nwv[4];
-            bool nok[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {  // (all four reads issued together)
-                nok[q] = !(nx[q] < 0 || nx[q] >= S || ny[q] < 0 || ny[q] >= S || (nx[q] == H && ny[q] == H));
-                nwv[q] = nok[q] ? word(nx[q], ny[q]) : 0u;
-            }
-            const uint32_t old = word(x, y);
             CertLab best{};
-            bool any = false;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                CertLab c;
-                if (!nok[q] || !cert_ext(p, E, nwv[q], c, FT, nft)) continue;
-                if (!any || cert_less(c, best)) best = c;
-                any = true;
-            }
+            bool any;
+            if (in_lds) cert_best4_lds(p, E, w, pitch, pool, bx0, by0, bx1, by1, x, y, best, any, FT, nft);
+            else cert_best4<true>(p, E, w, pitch, x, y, best, any, FT, nft);
+            const uint32_t old = word(x, y);
             const uint32_t nw = any ? ((best.b << kStBShift) | best.k) : old;
             if (nw == old) continue;
             if (in_lds) pool[widx(x, y)] = nw | kCertDirty;  // (the mark stays: never queued again)
             else __hip_atomic_store(gptr(x, y), nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int nx[4] = {x - 1, x + 1, x, x}, ny[4] = {y, y, y - 1, y + 1};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                if (!nok[q] || !inwin(nx[q], ny[q])) continue;  // (outside the window: fixed)
-                const uint32_t cu = nwv[q];
+                if (!inwin(nx[q], ny[q]) || (nx[q] == H && ny[q] == H)) continue;  // (outside the window: fixed)
+                const uint32_t cu = word(nx[q], ny[q]);
                 if (!plain_word(cu) || marked(nx[q], ny[q])) continue;  // (queued or processed already)
                 const uint32_t ju = lead_of(cu) / W - kmin;           // (an unmarked cell: its initial bucket)
                 if (ju <= j || ju >= nb) continue;                    // (an earlier or this bucket: not its reader)

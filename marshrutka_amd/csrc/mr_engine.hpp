@@ -271,6 +271,7 @@ constexpr uint32_t kDbgInjectFlag = 16u;
 // KArgs::dbg_flags bits (timing experiments only, results are not valid): hub_group_kernel
 // skips its Dijkstra / its destinations / the list compares of exact ties
 constexpr uint32_t kDbgGroupNoSolve = 32u, kDbgGroupNoReadoff = 64u, kDbgGroupNoTies = 128u;
-constexpr uint32_t kDbgSweepFull = 256u;  // the repair sweep queues every window cell (A/B)
+constexpr uint32_t kDbgSweepFull = 256u;   // the repair sweep queues every window cell (A/B)
+constexpr uint32_t kDbgSweepNoLds = 512u;  // the repair sweep keeps a small window's words in the slot's buffer
 
 }  // namespace mr
