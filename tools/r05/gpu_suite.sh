@@ -1,0 +1,8 @@
+#!/bin/bash
+# the whole GPU suite (one process), then smoke
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > gpurun_out/gpu_suite.log 2>&1 || { tail -60 gpurun_out/gpu_suite.log; exit 1; }
+tail -3 gpurun_out/gpu_suite.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+tail -3 gpurun_out/smoke.log
