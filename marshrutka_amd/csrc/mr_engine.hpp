@@ -87,6 +87,7 @@ struct DevParams {
     uint32_t W;                   // time bucket width = min StandardMove time increment
     uint32_t ff;                  // Fleetfoot level stored in Standard commands
     uint32_t ff_num, ff_den;      // Fleetfoot ratio (1/1 when level 0 or out of range)
+    uint32_t ff_c, ff_magic, ff_shift;  // 180 num; ceil(x / den) = umulhi(x + den - 1, magic) >> shift (lane kernel)
     uint32_t rgt;                 // caravan seconds per distance unit (RouteGuru applied)
     uint32_t soe_cost, shq_cost, sfm_cost;
     uint32_t use_soe, use_sfm, use_caravans;

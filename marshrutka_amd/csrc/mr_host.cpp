@@ -49,10 +49,10 @@ hipError_t launch_hub_wide(const KArgs *d_args, const uint32_t perm[3], uint32_t
 int hub_wide_blocks_per_cu(const uint32_t perm[3], uint32_t NS, uint32_t bytes);
 uint32_t hub_lane_entries(uint32_t NS);
 hipError_t launch_hub_lane(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t n_lane,
-                           hipStream_t stream);
+                           bool nonlin, hipStream_t stream);
 uint32_t hub_group_slots(uint32_t NS, uint32_t G);
 uint32_t lane_blob_build(const SpecialStatic *sp, uint32_t NS, uint32_t nreg, uint32_t TM, uint32_t rgt,
-                         const uint32_t *near_sp, std::vector<uint32_t> &blob);
+                         uint32_t ff_num, uint32_t ff_den, const uint32_t *near_sp, std::vector<uint32_t> &blob);
 hipError_t region_table_build(const uint16_t *reg, const uint32_t *rank, uint32_t S, uint32_t nreg, void *tab,
                               void *axis, hipStream_t stream);
 struct GroupGeom {
@@ -867,6 +867,7 @@ struct HostPlan {
     uint32_t fleetfoot_raw = 0;
     bool hub = false;                       // hub solver applicable (small tables)
     bool nonlin = false;                    // hub with a non-linear run time (near-tie certification)
+    bool ff_magic_ok = false;               // the lane kernel's run-time magic is exact on this grid (ff_magic)
     bool near = false;                      // the grid's device region table (V x regions)
     uint32_t nreg = 0;
     bool wide = false;                      // hub_wide_kernel (NS > 63 or no V x regions table)
@@ -943,6 +944,33 @@ static bool dev_group_ok(const mr_grid *g, uint32_t n) {
     return n >= kDevGroupMin;
 }
 
+// The lane kernel's Fleetfoot run time ceil(c k / den) as umulhi(c k + den - 1, magic) >>
+// shift (LaneHub::rtime): the least shift whose magic ceil(2^(32 + shift) / den) fits 32
+// bits and gives the exact quotient for every k <= kmax (checked here, k by k: every walk
+// on the grid is shorter than 2 S + 8 legs).  False: no such pair (the plan then stays off
+// the lane kernel).
+static bool ff_magic(uint32_t c, uint32_t den, uint32_t kmax, uint32_t &magic, uint32_t &shift) {
+    magic = 1;
+    shift = 0;
+    if (den <= 1) return true;  // linear: rtime does not use it
+    if (uint64_t(c) * kmax + den - 1 > 0xFFFFFFFFull) return false;
+    for (uint32_t s = 0; s < 32; ++s) {
+        const uint64_t m = ((uint64_t(1) << (32 + s)) + den - 1) / den;
+        if (m > 0xFFFFFFFFull) break;
+        bool ok = true;
+        for (uint64_t k = 0; k <= kmax && ok; ++k) {
+            const uint64_t x = uint64_t(c) * k + den - 1;
+            ok = ((x * m) >> (32 + s)) == x / den;
+        }
+        if (ok) {
+            magic = uint32_t(m);
+            shift = s;
+            return true;
+        }
+    }
+    return false;
+}
+
 static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs, uint32_t n, uint32_t max_cmds,
                       HostPlan &hp, bool allow_dev_group = false) {
     const double tbs = timing_on() ? now_ms() : 0.0;
@@ -968,6 +996,8 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     p.ff_num = ffn[ff];
     p.ff_den = ffd[ff];
     p.W = uint32_t((180ull * p.ff_num) / p.ff_den);  // floor(r*180): min StandardMove increment
+    p.ff_c = 180u * p.ff_num;
+    hp.ff_magic_ok = ff_magic(p.ff_c, p.ff_den, 2u * g->S + 8u, p.ff_magic, p.ff_shift);
     p.rgt = caravan_unit_time(prm->route_guru);
     p.soe_cost = prm->scroll_of_escape_cost;
     p.shq_cost = prm->scroll_of_escape_hq_cost;
@@ -2189,11 +2219,19 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     const size_t nsrc_g = nsrc_of(hp);
     const uint32_t group_g = hg ? (hgv == 16 ? 16u : (hgv == 32 ? 32u : 8u))
                                 : (nsrc_g <= 1024 ? 32u : (nsrc_g <= 4096 ? 16u : 8u));
-    const bool lane_ok = hp.hub && !hp.wide && !hp.nonlin && !all_mode && hp.near && lane_bounds_ok(hp.p);
-    if (lane_ok && !group_force && !lane_off && hub_lane_entries(hp.p.NS) != 0 && lane_layout_ok(hp) &&
-        (lane_force || lane_sources(hp) >= lane_min_sources()))
+    const bool lane_ok = hp.hub && !hp.wide && !all_mode && hp.near && lane_bounds_ok(hp.p);
+    // Fleetfoot 1..3 on the lane kernel (its NL instantiation: the walk certification of
+    // hub_kernel's §3a'') for orders that do not lead with Time.  A Time-first order's
+    // near ties leave a source uncertain now and then (1 in 118k at 1025^2), and hub_kernel
+    // hands such a source to the certificate (§3d: ~4 ms) where a lane-kernel source goes
+    // to the SSSP kernel (16-25 ms).  MR_LANE_NONLIN=0: never, =1: every order.
+    const char *lnl = std::getenv("MR_LANE_NONLIN");
+    const bool lane_nl = hp.nonlin && hp.ff_magic_ok && !(lnl && !std::strcmp(lnl, "0")) &&
+                         ((lnl && !std::strcmp(lnl, "1")) || hp.p.perm[0] != 2u);
+    if (lane_ok && (!hp.nonlin || lane_nl) && !group_force && !lane_off && hub_lane_entries(hp.p.NS) != 0 &&
+        lane_layout_ok(hp) && (lane_force || lane_sources(hp) >= lane_min_sources()))
         pl->n_lane = hp.dev_grouped ? partition_on_device(pl) : partition_sources(hp);
-    else if (lane_ok && !group_off && !lane_force && hub_group_slots(hp.p.NS, group_g) != 0 &&
+    else if (lane_ok && !hp.nonlin && !group_off && !lane_force && hub_group_slots(hp.p.NS, group_g) != 0 &&
              !std::getenv("MR_HUB_FALLBACK_ALL")) {
         pl->n_lane = nsrc_of(hp);
         pl->lane_g = group_g;
@@ -2475,7 +2513,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         if (pl->n_lane) {  // the lane / group kernels' LDS block, built once per plan
             const uint32_t TM = pl->lane_g ? pl->lane_g * hub_group_slots(NS, pl->lane_g) : hub_lane_entries(NS);
             std::vector<uint32_t> blob;
-            lane_blob_build(hp.sp.data(), NS, hp.nreg, TM, hp.p.rgt, hp.near_sp.data(), blob);
+            lane_blob_build(hp.sp.data(), NS, hp.nreg, TM, hp.p.rgt, hp.p.ff_num, hp.p.ff_den, hp.near_sp.data(), blob);
             if (upload(pl->d_lane_blob, blob) != MR_OK) return bail(fail(MR_ERR_DEVICE, "lane tables"));
             ka.lane_blob = reinterpret_cast<const uint4 *>(pl->d_lane_blob);
         }
@@ -2699,7 +2737,7 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         if (pl->n_lane) {
             const KArgs *la = pl->fb_none && !big ? pl->d_args_lane_last : pl->d_args_lane;
             e = pl->lane_g ? launch_hub_group(la, pl->ka.p.perm, pl->ka.p.NS, pl->ka.nreg, pl->n_lane, pl->lane_g, s)
-                           : launch_hub_lane(la, pl->ka.p.perm, pl->ka.p.NS, pl->ka.nreg, pl->n_lane, s);
+                           : launch_hub_lane(la, pl->ka.p.perm, pl->ka.p.NS, pl->ka.nreg, pl->n_lane, pl->hp.nonlin, s);
         }
         if (e == hipSuccess && big) e = launch_hub_plan(pl, pl->fb_none ? pl->d_args_hub_last : pl->d_args, s);
         // certified fallback: the slots given to the staged sources in source order,

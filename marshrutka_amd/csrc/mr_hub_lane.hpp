@@ -206,7 +206,7 @@ __device__ __forceinline__ uint32_t ltm3(const LLab &x, const LLab &y) {
 // money, caravan time (uint4), SoE-region distance from s into t's region and its walk
 // time (uint2; 0 where there is none), and per row s the entries t whose SoE-region
 // candidate applies (distance known and nonzero)
-template <uint32_t PERM, uint32_t TM>
+template <uint32_t PERM, uint32_t TM, bool NL = false>
 struct LaneHub {
     static constexpr uint32_t C1 = PERM / 9, C2 = (PERM / 3) % 3, C3 = PERM % 3;
     const KArgs *__restrict__ a;
@@ -379,9 +379,17 @@ struct LaneHub {
         return res;
     }
 
+    // The time of a run of k StandardMove legs (AggregatedCost, src/cost.rs:122-124): 180 k
+    // s, or with Fleetfoot 1..3 (NL) ceil(180 k num / den) (src/skill.rs:65-71) as a
+    // multiply-high by the plan's magic, exact for k <= 2 S + 8 (checked on the host,
+    // ff_magic in mr_host.cpp: every walk on the grid is shorter)
+    __device__ __forceinline__ uint32_t rtime(uint32_t k) const {
+        if (!NL) return 180u * k;
+        return __umulhi(P.ff_c * k + P.ff_den - 1u, P.ff_magic) >> P.ff_shift;
+    }
     // the walk of k legs from table entry b (label lb) to a plain cell
-    __device__ __forceinline__ static LLab walk_to(const LLab &lb, uint32_t b, uint32_t k) {
-        return add(lb, k, 0, 180u * k, lm_pack(lm_len(lb.m) + 1u, b, 1, kStandard));
+    __device__ __forceinline__ LLab walk_to(const LLab &lb, uint32_t b, uint32_t k) const {
+        return add(lb, k, 0, rtime(k), lm_pack(lm_len(lb.m) + 1u, b, 1, kStandard));
     }
 
     // ---- candidates from one settled special s into entry t ------------------------
@@ -520,6 +528,165 @@ struct LaneHub {
         return avail(b, bx, by, int(u % P.S) - int(P.H), int(u / P.S) - int(P.H));
     }
 
+    // ---- non-linear run times (NL): hub_kernel's walk certification -----------------
+    // near_tie / path_tie / walk_clear of mr_device.hpp (DESIGN.md §3a'') over this lane's
+    // table.  The comparator order is a compile-time constant here.
+    static constexpr bool kLegsBefore = C1 == 0 || (C2 == 0 && C1 != 2);
+    static constexpr bool kMoneyBefore = C1 == 1 || (C2 == 1 && C1 != 2);
+    static constexpr uint32_t kAfter = C1 == 2 ? C2 : (C2 == 2 ? C3 : 3u);  // the metric after Time (3: none)
+    // the gap f(k + m) - f(k) takes one of {lo, hi} for every k: hi = ceil(180 |m| num / den)
+    // (rtime), lo = floor(...); negated and swapped for m < 0
+    __device__ __forceinline__ bool gap_hits(int d0, int m) const {
+        const uint32_t am = uint32_t(m < 0 ? -m : m);
+        const uint32_t h = rtime(am);
+        const int hi0 = int(h), lo0 = int(h) - (h * P.ff_den != P.ff_c * am ? 1 : 0);
+        const int lo = m < 0 ? -hi0 : lo0, hi = m < 0 ? -lo0 : hi0;
+        return d0 + lo == -1 || d0 + lo == 0 || d0 + hi == -1 || d0 + hi == 0;
+    }
+    // Can boundary q (label xq at qx, qy) beat walk(b, .) non-isotonically somewhere on a
+    // shortest b-path to (vx, vy)?  m = d_q(u) - d_b(u) runs within [L1(q, v) - L1(b, v),
+    // L1(q, b) + 2] on those paths; the metrics before Time must be able to tie and the
+    // time gap d0 + (f(k + m) - f(k)) reach -1 or 0.  A time difference beyond 2^22 s is
+    // past any walk's gap (|gap| <= 180 (2 S + 2) + 1 < 2^21), so the rest is 32-bit.
+    __device__ __forceinline__ bool near_tie(const LLab &xq, int qx, int qy, const LLab &xb, int bx, int by, int vx,
+                                             int vy) const {
+        const uint32_t tq = metric(xq, 2), tb = metric(xb, 2);
+        if (kMoneyBefore && metric(xq, 1) != metric(xb, 1)) return false;
+        if ((tq > tb ? tq - tb : tb - tq) > (1u << 22)) return false;
+        const int d0 = int(tq - tb);
+        const int mlo = abs(qx - vx) + abs(qy - vy) - abs(bx - vx) - abs(by - vy);
+        const int mhi = abs(qx - bx) + abs(qy - by) + 2;
+        if (kLegsBefore) {  // the legs tie where m = L_b - L_q
+            const int m = int(metric(xb, 0)) - int(metric(xq, 0));
+            return m != 0 && m >= mlo && m <= mhi && gap_hits(d0, m);
+        }
+        // d0 + 180 m num / den within (-2, 1): m next to -d0 den / (180 num).  The quotient
+        // of two integers below 2^31 and 2^15 in double precision floors exactly.
+        const int m0 = int(floor(double((-2 - d0) * int(P.ff_den)) / double(P.ff_c)));
+        bool hit = false;
+        for (int m = m0 - 1; m <= m0 + 2; ++m) hit = hit || (m != 0 && m >= mlo && m <= mhi && gap_hits(d0, m));
+        return hit;
+    }
+    // Along one L-shaped shortest path from b to v (x first, or y first), is there a cell u
+    // (v excluded) where walk(q, .) beats walk(b, .) and the next leg flips their order?
+    // hub_kernel's path_tie step for step, with the periodic skip (tests/test_path_tie_skip.py).
+    __device__ __forceinline__ bool path_tie(const LLab &xq, uint32_t q, int qx, int qy, const LLab &xb, uint32_t b, int bx, int by,
+                             int vx, int vy, bool x_first, int lists) const {
+        const long long tb = metric(xb, 2), tq = metric(xq, 2), lb = metric(xb, 0), lq = metric(xq, 0);
+        const long long mb = metric(xb, 1), mq = metric(xq, 1);
+        if (kMoneyBefore && mq != mb) return false;
+        const int sxd = vx > bx ? 1 : -1, syd = vy > by ? 1 : -1;
+        const int K = abs(vx - bx) + abs(vy - by), kx = abs(vx - bx), ky = K - kx;
+        // the walks' lengths (the source's walk replaces its NoMove: length 1)
+        const long long nq0 = q == 0 ? 1 : lm_len(xq.m), nq1 = q == 0 ? 1 : lm_len(xq.m) + 1;
+        const long long nb0 = b == 0 ? 1 : lm_len(xb.m), nb1 = b == 0 ? 1 : lm_len(xb.m) + 1;
+        auto cell = [&](int k, int &ux, int &uy) {
+            if (x_first) {
+                ux = k < kx ? bx + sxd * k : vx;
+                uy = k < kx ? by : by + syd * (k - kx);
+            } else {
+                uy = k < ky ? by + syd * k : vy;
+                ux = k < ky ? bx : bx + sxd * (k - ky);
+            }
+        };
+        auto tail = [&](long long dd, long long kk) -> int {  // -1 q ahead, +1 b ahead, 0 the lists
+            if (kAfter == 0) {
+                if (lq + dd != lb + kk) return lq + dd < lb + kk ? -1 : 1;
+            } else if (kAfter == 1) {
+                if (mq != mb) return mq < mb ? -1 : 1;
+            }
+            const long long nq = dd > 0 ? nq1 : nq0, nbb = kk > 0 ? nb1 : nb0;
+            if (nq != nbb) return nq < nbb ? -1 : 1;
+            return (dd > 0 && kk > 0) ? lists : 0;
+        };
+        const int den = int(P.ff_den);
+        int ux, uy, run = 0;
+        cell(0, ux, uy);
+        uint32_t dq = walk_dist(qx, qy, ux, uy);
+        for (int k = 0; k < K;) {
+            if (ux == 0 && uy == 0) return true;
+            int wx, wy;
+            cell(k + 1, wx, wy);
+            const uint32_t dqn = walk_dist(qx, qy, wx, wy);
+            const bool tie_before = !kLegsBefore || lq + dq == lb + k;
+            if (tie_before && dqn > dq) {
+                const long long fq = rtime(dq), fb = rtime(uint32_t(k));
+                const long long delta = ((long long)rtime(dqn) - fq) - ((long long)rtime(uint32_t(k) + 1) - fb);
+                const long long gap = tq + fq - tb - fb;
+                if ((gap == -1 || gap == 0) && delta >= 0) {
+                    const bool q_beats_u = gap == -1 || tail(dq, k) != 1;
+                    const long long gw = gap + delta;
+                    const bool b_beats_w = gw > 0 || (gw == 0 && tail(dqn, k + 1) != -1);
+                    if (q_beats_u && b_beats_w) return true;
+                }
+            }
+            const bool along_x = x_first ? k < kx : k >= ky;
+            const bool plain = k >= 1 && (along_x ? (ux != 0 && wx != 0 && sxd * (ux - qx) >= 0)
+                                                  : (uy != 0 && wy != 0 && syd * (uy - qy) >= 0));
+            run = plain ? run + 1 : 0;
+            if (run >= den) {
+                int j = along_x ? (x_first ? kx : K) : (x_first ? K : ky);
+                const int c0 = along_x ? ux : uy, sd = along_x ? sxd : syd;
+                if (c0 * sd < 0) j = min(j, k + abs(c0) - 1);
+                if (j > k + 1) {
+                    k = j;
+                    run = 0;
+                    cell(k, ux, uy);
+                    dq = walk_dist(qx, qy, ux, uy);
+                    continue;
+                }
+            }
+            ++k;
+            ux = wx;
+            uy = wy;
+            dq = dqn;
+        }
+        return false;
+    }
+    // Is the closed-form walk(b, d_b(v)) (b's label xb) the reference's label of v?  One
+    // L-path must be clean for every boundary (hub_kernel's walk_certain / walk_clear).  The
+    // near_tie filter runs over the register-held table (static entries); the few
+    // boundaries that pass it get the path scans.
+    __device__ __forceinline__ bool walk_certain(uint32_t b, const LLab &xb, int vx, int vy) const {
+        int bx, by;
+        pos(b, bx, by);
+        if ((by == 0 && vy == 0 && bx != 0 && vx != 0 && (bx < 0) != (vx < 0)) ||
+            (bx == 0 && vx == 0 && by != 0 && vy != 0 && (by < 0) != (vy < 0)))
+            return false;  // shortest walks detour round the Center
+        uint32_t need = 0;
+        if (b != 0 && src != P.vc && near_tie(start(), sx, sy, xb, bx, by, vx, vy)) need = 1u;
+#pragma unroll
+        for (uint32_t t = 2; t < TM; ++t)  // (entry 1, the Center, starts no walks)
+            if (((bndm >> t) & 1u) && t != b && near_tie(L[t], spl[t].x, spl[t].y, xb, bx, by, vx, vy)) need |= 1u << t;
+        uint32_t paths = 3u;
+        for (uint32_t m = need; m && paths; m &= m - 1u) {
+            const uint32_t q = uint32_t(__builtin_ctz(m));
+            const LLab xq = get(q);
+            int qx, qy;
+            pos(q, qx, qy);
+            int lists = 0;  // the order of q's and b's command lists when their lengths tie
+            if (q != 0 && b != 0 && lm_len(xq.m) == lm_len(xb.m))
+                lists = cmp_list(meta_of(q), q, own_of(q), meta_of(b), b, own_of(b));
+            uint32_t clean = 0;
+            for (uint32_t xf = 0; xf < 2; ++xf)
+                clean |= path_tie(xq, q, qx, qy, xb, b, bx, by, vx, vy, xf == 0, lists) ? 0u : (1u << xf);
+            paths &= clean;
+        }
+        return paths != 0;
+    }
+    // entry t's settled label (meta): its walk, or the walk to the cell its SoE is read from
+    __device__ __forceinline__ bool label_certain(uint32_t meta, uint32_t t) const {
+        if (lm_kind(meta) != kStandard) return true;
+        const uint32_t b = lm_par(meta);
+        int vx = spl[t].x, vy = spl[t].y;
+        if (lm_nt(meta) != 1) {
+            const uint32_t u = rank_inv[near_of(b, spl[t].rid).y];
+            vx = int(u % P.S) - int(P.H);
+            vy = int(u / P.S) - int(P.H);
+        }
+        return walk_certain(b, get(b), vx, vy);
+    }
+
     // ---- output (Core::emit) --------------------------------------------------------
     __device__ __forceinline__ void emit(const LLab x, uint32_t xid, const Own xo, uint32_t qi) const {
         const DevParams &p = P;
@@ -616,7 +783,7 @@ struct LaneHub {
             if (t != 1) {
                 const uint32_t k = walk_dist(sx, sy, tS.x, tS.y);
                 won = vmask(valid && walks0 && tS.v != src);
-                w = opt(won, mk(k, 0, 180u * k, lm_pack(1, 0, 1, kStandard)));
+                w = opt(won, mk(k, 0, rtime(k), lm_pack(1, 0, 1, kStandard)));
                 consider(c, w);
                 any |= won;
             }
@@ -626,7 +793,7 @@ struct LaneHub {
                 const bool on = walks0 && reg && e != kNone32;
                 const uint32_t d = on ? e : 0u;
                 const uint32_t om = vmask(on);
-                consider(c, opt(om, mk(d, p.soe_cost, 180u * d,
+                consider(c, opt(om, mk(d, p.soe_cost, rtime(d),
                                        d == 0 ? lm_pack(1, 0, 1, kSoE) : lm_pack(2, 0, 2, kStandard))));
                 any |= om;
             }
@@ -765,6 +932,14 @@ struct LaneHub {
                 if (!label_avail(meta_of(t), t)) unc = true;
             }
         }
+        // non-linear run times: every settled walk label must also be certain against
+        // near ties of the time gap (hub_kernel's label_certain)
+        if (NL && !unc && !(a->dbg_flags & 4u)) {
+            for (uint32_t m = done; m && !unc; m &= m - 1u) {
+                const uint32_t t = uint32_t(__builtin_ctz(m));
+                if (!label_certain(meta_of(t), t)) unc = true;
+            }
+        }
         const uint32_t qa = a->q_begin[s_idx], qb = a->q_begin[s_idx + 1];
         const bool fb_sp = unc || a->fb_all;
         // ---- destinations: the source, a special's own label, or the best walk ------------
@@ -795,13 +970,13 @@ struct LaneHub {
             uint32_t tie = 0;  // the boundaries whose walk ties the best so far exactly (entry bits)
             {
                 const uint32_t k = walk_dist(sx, sy, wx, wy);
-                ll_sel(vmask(walk0), x, mk(k, 0, 180u * k, 0u));
+                ll_sel(vmask(walk0), x, mk(k, 0, rtime(k), 0u));
             }
 #pragma unroll
             for (uint32_t t = 2; t < TM; ++t) {
                 const uint32_t k = walk_dist(spl[t].x, spl[t].y, wx, wy);
                 const uint32_t cm = bitm(bq, t);
-                const LLab c = opt(cm, add(L[t], k, 0, 180u * k, L[t].m));
+                const LLab c = opt(cm, add(L[t], k, 0, rtime(k), L[t].m));
 #ifdef MR_LANE_CLASSIC
                 const uint32_t lt = ltm(c, x), gt = ltm(x, c);
                 tie = ~lt & (tie | (cm & ~gt & (1u << t)));
@@ -824,7 +999,7 @@ struct LaneHub {
                     int px, py;
                     pos(b, px, py);
                     const uint32_t k = walk_dist(px, py, wx, wy);
-                    const LLab c = b == 0 ? mk(k, 0, 180u * k, lm_pack(1, 0, 1, kStandard)) : walk_to(get(b), b, k);
+                    const LLab c = b == 0 ? mk(k, 0, rtime(k), lm_pack(1, 0, 1, kStandard)) : walk_to(get(b), b, k);
                     if (cmp4(c, x) == 0 && cmp_list(c.m, kOwn, wo, x.m, kOwn, wo) < 0) {
                         x = c;
                         bx = b;
@@ -841,6 +1016,7 @@ struct LaneHub {
                 pos(bx, px, py);
                 if (!avail(bx, px, py, wx, wy)) unc = true;
             }
+            if (NL && !unc && !(a->dbg_flags & 8u) && !walk_certain(bx, get(bx), wx, wy)) unc = true;
         }
         const bool fallback = fb_sp || unc;
         if (fallback) push_fallback(a, counter, s_idx, kNone32);
@@ -919,10 +1095,11 @@ __device__ __forceinline__ void lane_setup(const KArgs *__restrict__ a, char *sm
     H.nreg = nreg;
 }
 
-template <uint32_t PERM, uint32_t TM>
+// NL: Fleetfoot 1..3 (non-linear run times, the walk certification above)
+template <uint32_t PERM, uint32_t TM, bool NL = false>
 __global__ __launch_bounds__(kBS, lane_waves(TM)) void hub_lane_kernel(const KArgs *__restrict__ a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    LaneHub<PERM, TM> H;
+    LaneHub<PERM, TM, NL> H;
     lane_setup<TM>(a, smem, H);
     H.MC = reinterpret_cast<uint32_t *>(smem + lane_lds_total(a->p.NS, a->nreg, TM)) + (threadIdx.x >> 6) * (TM * 64u);
     // lane l of wave w: source 64 w + l of the lane kernel's sources [0, n_lane)

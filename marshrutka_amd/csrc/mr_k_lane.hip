@@ -17,6 +17,15 @@ template <>
 const void *lane_fn_tm<24>(uint32_t perm);
 template <>
 const void *lane_fn_tm<32>(uint32_t perm);
+// Fleetfoot 1..3 (hub_lane_kernel<PERM, TM, true>): mr_k_lane_nl.hip, mr_k_lane_nl2.hip
+template <uint32_t TM>
+const void *lane_nl_fn_tm(uint32_t perm);
+template <>
+const void *lane_nl_fn_tm<22>(uint32_t perm);
+template <>
+const void *lane_nl_fn_tm<24>(uint32_t perm);
+template <>
+const void *lane_nl_fn_tm<32>(uint32_t perm);
 
 template <>
 const void *lane_fn_tm<22>(uint32_t perm) {
@@ -37,12 +46,12 @@ const void *lane_fn_tm<22>(uint32_t perm) {
 // waves per SIMD, 24 and 32 at one (lane_waves)
 uint32_t hub_lane_entries(uint32_t NS) { return NS + 1 <= 22 ? 22u : (NS + 1 <= 24 ? 24u : (NS + 1 <= 32 ? 32u : 0u)); }
 
-static const void *lane_fn(const uint32_t perm[3], uint32_t NS) {
+static const void *lane_fn(const uint32_t perm[3], uint32_t NS, bool nonlin) {
     const uint32_t k = perm[0] * 9 + perm[1] * 3 + perm[2];
     switch (hub_lane_entries(NS)) {
-        case 22: return lane_fn_tm<22>(k);
-        case 24: return lane_fn_tm<24>(k);
-        case 32: return lane_fn_tm<32>(k);
+        case 22: return nonlin ? lane_nl_fn_tm<22>(k) : lane_fn_tm<22>(k);
+        case 24: return nonlin ? lane_nl_fn_tm<24>(k) : lane_fn_tm<24>(k);
+        case 32: return nonlin ? lane_nl_fn_tm<32>(k) : lane_fn_tm<32>(k);
         default: return nullptr;
     }
 }
@@ -52,9 +61,11 @@ static const void *lane_fn(const uint32_t perm[3], uint32_t NS) {
 // table, the pair table of walks / caravans / SoE-region candidates and its row masks
 // (LaneHub::from_s), the specials' cells by hash, and the header words.  near_sp holds the
 // specials' rows of the grid's region table ({distance, rank} per special t and region, at
-// 2 * (t * nreg + r)).  Returns the byte size.
+// 2 * (t * nreg + r)).  Walk times are the Fleetfoot ceil of 180 s a leg (ff_num / ff_den;
+// 1 / 1 without).  Returns the byte size.
 uint32_t lane_blob_build(const SpecialStatic *sp, uint32_t NS, uint32_t nreg, uint32_t TM, uint32_t rgt,
-                         const uint32_t *near_sp, std::vector<uint32_t> &blob) {
+                         uint32_t ff_num, uint32_t ff_den, const uint32_t *near_sp, std::vector<uint32_t> &blob) {
+    auto run_time = [&](uint32_t k) { return uint32_t((180ull * k * ff_num + ff_den - 1) / ff_den); };
     const uint32_t bytes = lane_blob_bytes(NS, nreg, TM);
     blob.assign(bytes / 4, 0u);
     char *base = reinterpret_cast<char *>(blob.data());
@@ -73,11 +84,11 @@ uint32_t lane_blob_build(const SpecialStatic *sp, uint32_t NS, uint32_t nreg, ui
             const SpecialStatic &ss = sp[s], &st = sp[t];
             const uint32_t wd = walk_dist(ss.x, ss.y, st.x, st.y);
             const uint32_t md = uint32_t(std::abs(ss.x - st.x) + std::abs(ss.y - st.y));
-            pa[s * TM + t] = make_uint4(wd, 180u * wd, (st.coef5 ? 5u : 2u) * md, rgt * md);
+            pa[s * TM + t] = make_uint4(wd, run_time(wd), (st.coef5 ? 5u : 2u) * md, rgt * md);
             if (st.rid != kNone10) {
                 const uint32_t d = nearl[s * nreg + st.rid].x;
                 if (d != kNone32) {
-                    pb[s * TM + t] = make_uint2(d, 180u * d);
+                    pb[s * TM + t] = make_uint2(d, run_time(d));
                     if (d != 0) rm[s] |= 1u << t;
                 }
             }
@@ -109,8 +120,8 @@ uint32_t hub_lane_lds_bytes(uint32_t NS, uint32_t nreg) {
 }
 
 hipError_t launch_hub_lane(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t n_lane,
-                           hipStream_t stream) {
-    const void *fn = lane_fn(perm, NS);
+                           bool nonlin, hipStream_t stream) {
+    const void *fn = lane_fn(perm, NS, nonlin);
     if (!fn) return hipErrorInvalidValue;
     const uint32_t bytes = hub_lane_lds_bytes(NS, nreg);
     if (bytes > 64u * 1024u) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));

@@ -23,7 +23,7 @@ def eng():
     return pathfinder
 
 
-@pytest.fixture(params=["auto-lds", "auto-hbm", "lane-lds", "lanetab-lds", "group-lds", "group16-lds", "group32-lds", "hub1-lds", "hub2-lds", "wide-lds", "widescan-lds", "fallback-lds", "fallback-hbm", "fbsssp-lds",
+@pytest.fixture(params=["auto-lds", "auto-hbm", "lane-lds", "lanenl-lds", "lanetab-lds", "group-lds", "group16-lds", "group32-lds", "hub1-lds", "hub2-lds", "wide-lds", "widescan-lds", "fallback-lds", "fallback-hbm", "fbsssp-lds",
                         "sssp-lds", "sssp-hbm", "generic-lds", "generic-hbm"])
 def grid_state(request, monkeypatch):
     """Every solver path x both grid-state regimes:
@@ -38,6 +38,8 @@ def grid_state(request, monkeypatch):
     group32  — the same with groups of 32 lanes (the last round through ds_swizzle)
     lane     — auto with the lane kernel whenever it applies (MR_HUB_LANE=1); on the
                standard layout it computes ranks and looks up specials itself
+    lanenl   — the same with Fleetfoot 1..3 on the lane kernel for every order, Time
+               first included (MR_LANE_NONLIN=1)
     lanetab  — the same reading every cell's {sinfo, rank} record (MR_RANK_TABLE=1)
     hub1     — hub solver with one source per wave (no lane or group kernel)
     hub2     — hub solver with two sources per wave (no lane or group kernel)
@@ -63,6 +65,10 @@ def grid_state(request, monkeypatch):
     monkeypatch.delenv("MR_RANK_TABLE", raising=False)
     monkeypatch.delenv("MR_HUB_GROUP", raising=False)
     monkeypatch.delenv("MR_HUB_GROUP_FORCE", raising=False)
+    monkeypatch.delenv("MR_LANE_NONLIN", raising=False)
+    if algo == "lanenl":
+        monkeypatch.setenv("MR_LANE_NONLIN", "1")
+        algo = "lane"
     if algo in ("group", "group16", "group32"):
         monkeypatch.setenv("MR_HUB_GROUP_FORCE", "1")
         monkeypatch.setenv("MR_HUB_GROUP", algo[5:] or "8")
@@ -487,16 +493,22 @@ def test_overflow_pool(eng, oracle_lib, grid_state, max_cmds):
         assert any(len(e[3]) > max_cmds for e in exp)
 
 
+@pytest.mark.parametrize("kernel", ["hub", "lane"])
 @pytest.mark.parametrize("ff", [1, 2, 3])
 @pytest.mark.parametrize("sort_by", [(SORT_LEGS, SORT_MONEY), (SORT_LEGS, SORT_TIME), (SORT_MONEY, SORT_LEGS),
                                      (SORT_MONEY, SORT_TIME), (SORT_TIME, SORT_LEGS), (SORT_TIME, SORT_MONEY)])
-def test_fleetfoot_hub(eng, oracle_lib, monkeypatch, ff, sort_by):
+def test_fleetfoot_hub(eng, oracle_lib, monkeypatch, ff, sort_by, kernel):
     """Non-linear run times (Fleetfoot 1..3) through the hub solver: every closed-form
     label certified against near-ties of the time gap, uncertain sources re-solved by
     the SSSP kernel.  Bit-exact against the oracle, with both one and many
-    destinations per source, and most sources answered by the hub itself."""
-    for v in ("MR_ALGO", "MR_HUB_FALLBACK_ALL", "MR_HUB_SPW", "MR_HUB_WIDE", "MR_HUB_NONLIN", "MR_GRID_STATE"):
+    destinations per source, and most sources answered by the hub itself.  kernel:
+    hub_kernel alone, or the lane kernel's Fleetfoot instantiation for every source with
+    at most 32 queries (MR_HUB_LANE=1, MR_LANE_NONLIN=1; 22- and 32-entry tables)."""
+    for v in ("MR_ALGO", "MR_HUB_FALLBACK_ALL", "MR_HUB_SPW", "MR_HUB_WIDE", "MR_HUB_NONLIN", "MR_GRID_STATE",
+              "MR_HUB_GROUP", "MR_HUB_GROUP_FORCE"):
         monkeypatch.delenv(v, raising=False)
+    monkeypatch.setenv("MR_HUB_LANE", "0" if kernel == "hub" else "1")
+    monkeypatch.setenv("MR_LANE_NONLIN", "0" if kernel == "hub" else "1")
     for size, k, clustered, seed in ((33, 4, False, 31), (65, 6, True, 32), (129, 4, False, 33)):
         m = SyntheticMap(size, campfires_per_homeland=k, seed=seed + ff, clustered=clustered)
         params = Params(fleetfoot=ff, sort_by=sort_by, route_guru=ff, hq_position=m.campfires()[2])
@@ -516,6 +528,10 @@ def test_fleetfoot_hub(eng, oracle_lib, monkeypatch, ff, sort_by):
         st = plan.stats()
         assert st["solver"] == "hub"
         assert st["fallback_sources"] <= st["num_sources"] // 4, st
+        if kernel == "lane":
+            assert st["lane_sources"] == st["num_sources"] - 1 and st["lanes_per_source"] == 1, st
+        else:
+            assert st["lane_sources"] == 0 and st["lanes_per_source"] == 0, st
 
 
 def test_device_records_grouped_by_source(eng):
