@@ -1454,6 +1454,8 @@ __device__ __forceinline__ void finish_launch(const KArgs *__restrict__ a, uint3
         c[kCtrLastWritten] = wr;
         c[kCtrLastOvf] = ov;
         c[kCtrLastCert] = atomicAdd(c + kCtrCertDone, 0u);
+        c[kCtrLastRelist] = atomicAdd(c + kCtrRelist, 0u);
+        c[kCtrRelist] = 0;
         c[kCtrCertDone] = 0;
         c[kCtrOvf] = 0;
         c[kCtrDequeue] = 0;
@@ -1829,18 +1831,49 @@ struct HubSolver : Core<false> {
                 ux = k < ky ? bx : bx + sx * (k - ky);
             }
         };
-        // Periodic skip: on a run of steps where q moves away from the path (its distance
-        // grows by one a step, no axis crossed) every quantity below is constant or
-        // periodic in k with period den (run_time(k + den) = run_time(k) + 180 num), so
-        // once den consecutive steps of a run are checked the rest of the run is skipped
-        // and the scan resumes at the first step that leaves it (tests/test_path_tie_skip.py
-        // restates this loop and checks it against the cell-by-cell scan).
+        // Skips: on a run of steps where q moves away from the path (its distance grows by
+        // one a step, no axis crossed) every quantity below is constant or periodic in k
+        // with period den (run_time(k + den) = run_time(k) + 180 num), so a run of at least
+        // den steps is decided by one period of the time gaps and skipped whole (a shorter
+        // one after den checked steps); a stretch approaching q cannot flip and is skipped
+        // too (tests/test_path_tie_skip.py restates this loop and checks it against the
+        // cell-by-cell scan).
+        // the order after Time at a cell (dd, kk: q's and b's legs there): -1 q ahead, +1 b
+        // ahead, 0 undecided (the command lists)
+        auto tail = [&](long long dd, long long kk) -> int {
+            if (after == 0) {
+                if (lq + dd != lb + kk) return lq + dd < lb + kk ? -1 : 1;
+            } else if (after == 1) {
+                if (mq != mb) return mq < mb ? -1 : 1;
+            }
+            const long long nq = dd > 0 ? nq1 : nq0, nbb = kk > 0 ? nb1 : nb0;
+            if (nq != nbb) return nq < nbb ? -1 : 1;
+            return (dd > 0 && kk > 0) ? lists : 0;
+        };
         const int den = int(p.ff_den);
         int ux, uy, run = 0;
         cell(0, ux, uy);
         uint32_t dq = walk_dist(qx, qy, ux, uy);
         for (int k = 0; k < K;) {
             if (ux == 0 && uy == 0) return true;
+            {  // Approach skip: moving towards q's column (row), q's distance drops by one a step
+                // until the walk reaches it (or the step before the axis being crossed: the
+                // Center detour's term stays constant), and only a step on which it grows can flip
+                const bool ax = x_first ? k < kx : k >= ky;
+                const int seg = ax ? (x_first ? kx : K) : (x_first ? K : ky);
+                const int c0 = ax ? ux : uy, qc = ax ? qx : qy, sd = ax ? sx : sy;
+                if (sd * (c0 - qc) < 0) {
+                    int j = min(seg, k + abs(c0 - qc));
+                    if (c0 * sd < 0) j = min(j, k + abs(c0) - 1);
+                    if (j > k + 1) {
+                        k = j;
+                        run = 0;
+                        cell(k, ux, uy);
+                        dq = walk_dist(qx, qy, ux, uy);
+                        continue;
+                    }
+                }
+            }
             int wx, wy;
             cell(k + 1, wx, wy);
             const uint32_t dqn = walk_dist(qx, qy, wx, wy);
@@ -1850,18 +1883,6 @@ struct HubSolver : Core<false> {
                 const long long delta = ((long long)run_time(dqn) - fq) - ((long long)run_time(uint32_t(k) + 1) - fb);
                 const long long gap = tq + fq - tb - fb;
                 if ((gap == -1 || gap == 0) && delta >= 0) {
-                    // the order after Time at u (dq, k) and at the next cell (dqn, k + 1):
-                    // -1 q ahead, +1 b ahead, 0 undecided (the command lists)
-                    auto tail = [&](long long dd, long long kk) -> int {
-                        if (after == 0) {
-                            if (lq + dd != lb + kk) return lq + dd < lb + kk ? -1 : 1;
-                        } else if (after == 1) {
-                            if (mq != mb) return mq < mb ? -1 : 1;
-                        }
-                        const long long nq = dd > 0 ? nq1 : nq0, nbb = kk > 0 ? nb1 : nb0;
-                        if (nq != nbb) return nq < nbb ? -1 : 1;
-                        return (dd > 0 && kk > 0) ? lists : 0;
-                    };
                     const bool q_beats_u = gap == -1 || tail(dq, k) != 1;
                     const long long gw = gap + delta;
                     const bool b_beats_w = gw > 0 || (gw == 0 && tail(dqn, k + 1) != -1);
@@ -1871,13 +1892,39 @@ struct HubSolver : Core<false> {
             const bool along_x = x_first ? k < kx : k >= ky;
             const bool plain = k >= 1 && (along_x ? (ux != 0 && wx != 0 && sx * (ux - qx) >= 0)
                                                   : (uy != 0 && wy != 0 && sy * (uy - qy) >= 0));
-            run = plain ? run + 1 : 0;
-            if (run >= den) {
-                // the next step that is not plain: the segment's end, or the step before
-                // the one whose cell lies on the axis being crossed
-                int j = along_x ? (x_first ? kx : K) : (x_first ? K : ky);
+            // the next step that is not plain: the segment's end, or the step before the one
+            // whose cell lies on the axis being crossed
+            int j = along_x ? (x_first ? kx : K) : (x_first ? K : ky);
+            {
                 const int c0 = along_x ? ux : uy, sd = along_x ? sx : sy;
                 if (c0 * sd < 0) j = min(j, k + abs(c0) - 1);
+            }
+            // A plain run of at least den steps from here (q off the walk, so the tail is the
+            // run's): its steps see every residue of k mod den, and the time gaps at a step
+            // and the next are d0 + F(r), d0 + F(r + 1), F(r) = f(r + m) - f(r) with m = dq - k
+            // constant on the run.  One period of F decides whether some step of the run
+            // flips; the run is then skipped whole.
+            if (plain && tie_before && dq > 0 && j - k >= den) {
+                const int m = int(dq) - k, T = tail(dq, k);
+                const long long d0 = tq - tb;
+                const int base = den * ((max(0, -m) + den - 1) / den);  // (r + m >= 0)
+                for (int i = 0; i < den; ++i) {
+                    const int r = base + i;
+                    const long long g = d0 + (long long)run_time(uint32_t(r + m)) - (long long)run_time(uint32_t(r));
+                    const long long gw = d0 + (long long)run_time(uint32_t(r + 1 + m)) - (long long)run_time(uint32_t(r + 1));
+                    if ((g == -1 || g == 0) && gw >= g && (g == -1 || T != 1) && (gw > 0 || (gw == 0 && T != -1)))
+                        return true;
+                }
+                k = j;
+                run = 0;
+                cell(k, ux, uy);
+                dq = walk_dist(qx, qy, ux, uy);
+                continue;
+            }
+            run = plain ? run + 1 : 0;
+            // (Legs before Time: the legs gap is constant on a plain run too, so a run that
+            // starts untied stays untied and is skipped at once)
+            if (run >= den || (plain && !tie_before)) {
                 if (j > k + 1) {
                     k = j;
                     run = 0;
@@ -2154,13 +2201,16 @@ struct HubSolver : Core<false> {
         wave_sync();
     }
 
-    // Segment h solves source base + h (none past the end).
-    __device__ __forceinline__ void solve(uint32_t base) {
+    // Segment h solves source base + h (none past the end, `total`): indices past nsrc
+    // name the sources the lane kernel relisted (KArgs::relist).
+    __device__ __forceinline__ void solve(uint32_t base, uint32_t total) {
         const DevParams &p = P;
         const uint32_t t = seg_lane();
-        const uint32_t s_idx = base + lane_id() / LPS;
-        const bool have = s_idx < a->nsrc;
-        const uint32_t si = have ? s_idx : base;
+        const uint32_t s_raw = base + lane_id() / LPS, nsrc = a->nsrc;
+        const bool have = s_raw < total;
+        const uint32_t r_raw = have ? s_raw : base;
+        const uint32_t s_idx = r_raw < nsrc ? r_raw : a->relist[r_raw - nsrc];
+        const uint32_t si = s_idx;
         const bool mine = have && t >= 1 && t <= p.NS;
         src = a->src_v[si];
         src_rk = rank[src];
@@ -2396,13 +2446,19 @@ __device__ __forceinline__ void hub_body(const KArgs *__restrict__ a, char *smem
     // sources are strided over the launch's waves (no dequeue atomics: one word
     // would saturate at ~88 dequeues/us, MI355X_MICROARCH.md)
     const uint32_t waves = nblocks * (kBS / 64), wid = block * (kBS / 64) + (threadIdx.x >> 6);
+    // the sources [src_off, nsrc), then those the lane kernel of this pass relisted (its
+    // launch precedes this one on the stream; the count is reset only by the pass's last
+    // kernel's last workgroup, after every workgroup here has read it)
+    const uint32_t total = a->nsrc + (a->relist ? __hip_atomic_load(a->counter + kCtrRelist, __ATOMIC_RELAXED,
+                                                                      __HIP_MEMORY_SCOPE_AGENT)
+                                                : 0u);
     for (uint32_t k = 0;; ++k) {
         const unsigned long long base = a->src_off + ((unsigned long long)k * waves + wid) * SPW;
 #ifdef MR_STAMPS
         H.hmark(8);
 #endif
-        if (base >= a->nsrc) break;
-        H.solve(uint32_t(base));
+        if (base >= total) break;
+        H.solve(uint32_t(base), total);
     }
     H.flush_err();
     __shared__ uint32_t wsum;

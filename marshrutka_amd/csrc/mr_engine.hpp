@@ -153,6 +153,8 @@ struct KArgs {
     const uint32_t *near;
     uint32_t nreg;
     uint32_t *fb_list;           // sources the hub solver hands to the SSSP kernel (counter[2] of them)
+    uint32_t *relist;            // non-null: the lane kernel hands an uncertain source to hub_kernel
+                                 // (relist[counter[kCtrRelist]++]) instead of the SSSP kernel
     uint32_t fb_mode;            // 1: this SSSP launch solves fb_list[counter[3]++] only
     uint32_t fb_all;             // tests: the hub solver hands every source to the SSSP kernel
     uint32_t dbg_blocks;         // diagnostic builds: SSSP workgroups (hub stamps follow their slots)
@@ -235,7 +237,9 @@ enum : uint32_t {
     kCtrCert = 10,        // certified-fallback slots given in this pass (cert_select_kernel)
     kCtrCertDone = 11,    // fallback sources the certificate answered in this pass
     kCtrLastCert = 12,    // kCtrCertDone of the last completed pass
-    kCtrWords = 13
+    kCtrRelist = 13,      // lane-kernel sources handed to hub_kernel in this pass (KArgs::relist)
+    kCtrLastRelist = 14,  // kCtrRelist of the last completed pass
+    kCtrWords = 15
 };
 // per certificate slot and check workgroup: the least leading metric of a failing cell
 // (labels below the least over the workgroups are exact), failing cells, their bounding

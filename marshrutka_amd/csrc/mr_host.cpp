@@ -947,7 +947,8 @@ static bool dev_group_ok(const mr_grid *g, uint32_t n) {
 // The lane kernel's Fleetfoot run time ceil(c k / den) as umulhi(c k + den - 1, magic) >>
 // shift (LaneHub::rtime): the least shift whose magic ceil(2^(32 + shift) / den) fits 32
 // bits and gives the exact quotient for every k <= kmax (checked here, k by k: every walk
-// on the grid is shorter than 2 S + 8 legs).  False: no such pair (the plan then stays off
+// on the grid is shorter than 2 S + 8 legs, and the path scan's period check reads up to
+// 2 den + 1 past one: kmax = 2 S + 256).  False: no such pair (the plan then stays off
 // the lane kernel).
 static bool ff_magic(uint32_t c, uint32_t den, uint32_t kmax, uint32_t &magic, uint32_t &shift) {
     magic = 1;
@@ -997,7 +998,7 @@ static int build_plan(const mr_grid *g, const mr_params *prm, const mr_query *qs
     p.ff_den = ffd[ff];
     p.W = uint32_t((180ull * p.ff_num) / p.ff_den);  // floor(r*180): min StandardMove increment
     p.ff_c = 180u * p.ff_num;
-    hp.ff_magic_ok = ff_magic(p.ff_c, p.ff_den, 2u * g->S + 8u, p.ff_magic, p.ff_shift);
+    hp.ff_magic_ok = ff_magic(p.ff_c, p.ff_den, 2u * g->S + 256u, p.ff_magic, p.ff_shift);
     p.rgt = caravan_unit_time(prm->route_guru);
     p.soe_cost = prm->scroll_of_escape_cost;
     p.shq_cost = prm->scroll_of_escape_hq_cost;
@@ -1738,6 +1739,7 @@ struct mr_plan {
     uint32_t *d_near = nullptr, *d_fb = nullptr;
     uint32_t *d_near_sp = nullptr, *d_rb_off = nullptr, *d_rb_cell = nullptr;  // wide hub tables
     uint32_t *d_lane_blob = nullptr;  // lane / group kernels: the plan's LDS block (lane_blob_build)
+    uint32_t *d_relist = nullptr;     // lane kernel (Fleetfoot): uncertain sources for hub_kernel (KArgs::relist)
     OutCmd *d_ovf = nullptr;              // command-overflow pool (labels longer than max_cmds)
     uint32_t hub_blocks = 0, fb_blocks = 0, spw = 1, cus = 256, fill_per_cu = 8;
     unsigned long long *d_dbg = nullptr;  // diagnostic builds: per-workgroup phase cycles
@@ -1843,7 +1845,7 @@ struct mr_plan {
                         (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
                         (void *)d_counter, (void *)d_args, (void *)d_dbg, (void *)d_args_fb, (void *)d_near,
                         (void *)d_fb, (void *)d_args_hub_last, (void *)d_args_fill, (void *)d_rec,
-                        (void *)d_args_lane, (void *)d_args_lane_last,
+                        (void *)d_args_lane, (void *)d_args_lane_last, (void *)d_relist,
                         (void *)d_tab,
                         (void *)d_lex, (void *)d_sstate, (void *)d_near_sp, (void *)d_rb_off, (void *)d_rb_cell, (void *)d_ovf,
                         (void *)d_lane_blob})
@@ -1927,7 +1929,10 @@ static int upload_args(mr_plan *pl) {
             c.out_rec = pl->d_cert_rec;
             if (!put(pl->d_args_cert, c)) return MR_ERR_DEVICE;
         }
-        if (pl->d_args_lane && (!put(pl->d_args_lane, k) || !put(pl->d_args_lane_last, l))) return MR_ERR_DEVICE;
+        // (the lane kernel as the pass's only launch has no hub launch after it to relist into)
+        KArgs ll = l;
+        ll.relist = nullptr;
+        if (pl->d_args_lane && (!put(pl->d_args_lane, k) || !put(pl->d_args_lane_last, ll))) return MR_ERR_DEVICE;
     }
     return ok && hipStreamSynchronize(pl->stream) == hipSuccess ? MR_OK : MR_ERR_DEVICE;
 }
@@ -2221,13 +2226,11 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
                                 : (nsrc_g <= 1024 ? 32u : (nsrc_g <= 4096 ? 16u : 8u));
     const bool lane_ok = hp.hub && !hp.wide && !all_mode && hp.near && lane_bounds_ok(hp.p);
     // Fleetfoot 1..3 on the lane kernel (its NL instantiation: the walk certification of
-    // hub_kernel's §3a'') for orders that do not lead with Time.  A Time-first order's
-    // near ties leave a source uncertain now and then (1 in 118k at 1025^2), and hub_kernel
-    // hands such a source to the certificate (§3d: ~4 ms) where a lane-kernel source goes
-    // to the SSSP kernel (16-25 ms).  MR_LANE_NONLIN=0: never, =1: every order.
+    // hub_kernel's §3a'').  A source it cannot certify (Time first: 1 in 118k at 1025^2)
+    // is relisted for a hub_kernel launch right after it, whose fallback reaches the
+    // certificate (§3d) instead of the SSSP kernel.  MR_LANE_NONLIN=0: never.
     const char *lnl = std::getenv("MR_LANE_NONLIN");
-    const bool lane_nl = hp.nonlin && hp.ff_magic_ok && !(lnl && !std::strcmp(lnl, "0")) &&
-                         ((lnl && !std::strcmp(lnl, "1")) || hp.p.perm[0] != 2u);
+    const bool lane_nl = hp.nonlin && hp.ff_magic_ok && !(lnl && !std::strcmp(lnl, "0"));
     if (lane_ok && (!hp.nonlin || lane_nl) && !group_force && !lane_off && hub_lane_entries(hp.p.NS) != 0 &&
         lane_layout_ok(hp) && (lane_force || lane_sources(hp) >= lane_min_sources()))
         pl->n_lane = hp.dev_grouped ? partition_on_device(pl) : partition_sources(hp);
@@ -2444,7 +2447,10 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         if (hb > 160 * 1024) return bail(fail(MR_ERR_LIMIT, "hub tables exceed LDS"));
         const int hper = std::max(1, hp.wide ? hub_wide_blocks_per_cu(hp.p.perm, NS, hb)
                                              : hub_blocks_per_cu(hp.p.perm, pl->spw, hp.nonlin, hb));
-        const uint64_t per_block = 4ull * pl->spw, hub_src = nsrc - pl->n_lane;
+        // (a lane kernel with Fleetfoot relists its uncertain sources for hub_kernel: room
+        // for a few hundred of them in one round)
+        const bool relist = pl->n_lane && !pl->lane_g && hp.nonlin;
+        const uint64_t per_block = 4ull * pl->spw, hub_src = std::max<uint64_t>(nsrc - pl->n_lane, relist ? 512u : 0u);
         pl->hub_blocks = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((hub_src + per_block - 1) / per_block,
                                                                            uint64_t(hper) * prop.multiProcessorCount)));
         if (const char *e = std::getenv("MR_HUB_BLOCKS")) pl->hub_blocks = uint32_t(std::max(1, std::atoi(e)));
@@ -2510,6 +2516,11 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
         if (pl->n_lane && (pmalloc(reinterpret_cast<void **>(&pl->d_args_lane), sizeof(KArgs)) != hipSuccess ||
                            pmalloc(reinterpret_cast<void **>(&pl->d_args_lane_last), sizeof(KArgs)) != hipSuccess))
             return bail(fail(MR_ERR_DEVICE, "kernel args"));
+        if (relist) {
+            if (pmalloc(reinterpret_cast<void **>(&pl->d_relist), size_t(pl->n_lane) * 4) != hipSuccess)
+                return bail(fail(MR_ERR_DEVICE, "relist"));
+            ka.relist = pl->d_relist;
+        }
         if (pl->n_lane) {  // the lane / group kernels' LDS block, built once per plan
             const uint32_t TM = pl->lane_g ? pl->lane_g * hub_group_slots(NS, pl->lane_g) : hub_lane_entries(NS);
             std::vector<uint32_t> blob;
@@ -2732,7 +2743,9 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         // (usually none; those workgroups exit at once).  Once a pass of this plan (same
         // inputs, deterministic result) had no fallback source, the hub launches end the
         // pass on their own.
-        const bool big = pl->ka.nsrc > pl->n_lane;
+        // (a Fleetfoot lane plan relaunches hub_kernel for the sources its lane kernel
+        // relisted, until a pass had none)
+        const bool big = pl->ka.nsrc > pl->n_lane || (pl->d_relist && !pl->fb_none);
         e = hipSuccess;
         if (pl->n_lane) {
             const KArgs *la = pl->fb_none && !big ? pl->d_args_lane_last : pl->d_args_lane;
@@ -2788,7 +2801,7 @@ static bool plan_sync(mr_plan *pl) {
 static int read_counters(mr_plan *pl, uint32_t ctr[kCtrWords]) {
     if (!plan_sync(pl) || hipMemcpy(ctr, pl->d_counter, kCtrWords * 4, hipMemcpyDeviceToHost) != hipSuccess)
         return fail(MR_ERR_DEVICE, "copy counter");
-    if (pl->hp.hub && pl->runs && !pl->ka.fb_all && ctr[kCtrLastFb] == 0) pl->fb_none = true;
+    if (pl->hp.hub && pl->runs && !pl->ka.fb_all && ctr[kCtrLastFb] == 0 && ctr[kCtrLastRelist] == 0) pl->fb_none = true;
     return MR_OK;
 }
 

@@ -381,8 +381,9 @@ struct LaneHub {
 
     // The time of a run of k StandardMove legs (AggregatedCost, src/cost.rs:122-124): 180 k
     // s, or with Fleetfoot 1..3 (NL) ceil(180 k num / den) (src/skill.rs:65-71) as a
-    // multiply-high by the plan's magic, exact for k <= 2 S + 8 (checked on the host,
-    // ff_magic in mr_host.cpp: every walk on the grid is shorter)
+    // multiply-high by the plan's magic, exact for k <= 2 S + 256 (checked on the host,
+    // ff_magic in mr_host.cpp: every walk on the grid is shorter, and path_tie's period
+    // check reads f at most 2 den + 1 past a walk's length)
     __device__ __forceinline__ uint32_t rtime(uint32_t k) const {
         if (!NL) return 180u * k;
         return __umulhi(P.ff_c * k + P.ff_den - 1u, P.ff_magic) >> P.ff_shift;
@@ -605,6 +606,24 @@ struct LaneHub {
         uint32_t dq = walk_dist(qx, qy, ux, uy);
         for (int k = 0; k < K;) {
             if (ux == 0 && uy == 0) return true;
+            {  // Approach skip: moving towards q's column (row), q's distance drops by one a step
+                // until the walk reaches it (or the step before the axis being crossed: the
+                // Center detour's term stays constant), and only a step on which it grows can flip
+                const bool ax = x_first ? k < kx : k >= ky;
+                const int seg = ax ? (x_first ? kx : K) : (x_first ? K : ky);
+                const int c0 = ax ? ux : uy, qc = ax ? qx : qy, sd = ax ? sxd : syd;
+                if (sd * (c0 - qc) < 0) {
+                    int j = min(seg, k + abs(c0 - qc));
+                    if (c0 * sd < 0) j = min(j, k + abs(c0) - 1);
+                    if (j > k + 1) {
+                        k = j;
+                        run = 0;
+                        cell(k, ux, uy);
+                        dq = walk_dist(qx, qy, ux, uy);
+                        continue;
+                    }
+                }
+            }
             int wx, wy;
             cell(k + 1, wx, wy);
             const uint32_t dqn = walk_dist(qx, qy, wx, wy);
@@ -623,11 +642,39 @@ struct LaneHub {
             const bool along_x = x_first ? k < kx : k >= ky;
             const bool plain = k >= 1 && (along_x ? (ux != 0 && wx != 0 && sxd * (ux - qx) >= 0)
                                                   : (uy != 0 && wy != 0 && syd * (uy - qy) >= 0));
-            run = plain ? run + 1 : 0;
-            if (run >= den) {
-                int j = along_x ? (x_first ? kx : K) : (x_first ? K : ky);
+            // the next step that is not plain: the segment's end, or the step before the one
+            // whose cell lies on the axis being crossed
+            int j = along_x ? (x_first ? kx : K) : (x_first ? K : ky);
+            {
                 const int c0 = along_x ? ux : uy, sd = along_x ? sxd : syd;
                 if (c0 * sd < 0) j = min(j, k + abs(c0) - 1);
+            }
+            // A plain run of at least den steps from here (q off the walk, so the tail is
+            // the run's): its steps see every residue of k mod den, and the time gaps at a
+            // step and the next are d0 + F(r), d0 + F(r + 1), F(r) = f(r + m) - f(r) with m
+            // = dq - k constant on the run.  One period of F decides whether some step of
+            // the run flips; the run is then skipped whole (tests/test_path_tie_skip.py).
+            if (plain && tie_before && dq > 0 && j - k >= den) {
+                const int m = int(dq) - k, T = tail(dq, k);
+                const long long d0 = tq - tb;
+                const int base = den * ((max(0, -m) + den - 1) / den);  // (r + m >= 0)
+                for (int i = 0; i < den; ++i) {
+                    const uint32_t r = uint32_t(base + i);
+                    const long long g = d0 + (long long)rtime(uint32_t(int(r) + m)) - (long long)rtime(r);
+                    const long long gw = d0 + (long long)rtime(uint32_t(int(r) + 1 + m)) - (long long)rtime(r + 1u);
+                    if ((g == -1 || g == 0) && gw >= g && (g == -1 || T != 1) && (gw > 0 || (gw == 0 && T != -1)))
+                        return true;
+                }
+                k = j;
+                run = 0;
+                cell(k, ux, uy);
+                dq = walk_dist(qx, qy, ux, uy);
+                continue;
+            }
+            run = plain ? run + 1 : 0;
+            // (Legs before Time: the legs gap is constant on a plain run too, so a run that
+            // starts untied stays untied and is skipped at once)
+            if (run >= den || (plain && !tie_before)) {
                 if (j > k + 1) {
                     k = j;
                     run = 0;
@@ -1019,7 +1066,10 @@ struct LaneHub {
             if (NL && !unc && !(a->dbg_flags & 8u) && !walk_certain(bx, get(bx), wx, wy)) unc = true;
         }
         const bool fallback = fb_sp || unc;
-        if (fallback) push_fallback(a, counter, s_idx, kNone32);
+        // an uncertain source goes to hub_kernel when the plan relaunches it for such
+        // sources (its fallback reaches the certificate), else to the SSSP kernel
+        if (fallback && a->relist && !a->fb_all) a->relist[atomicAdd(counter + kCtrRelist, 1u)] = s_idx;
+        else if (fallback) push_fallback(a, counter, s_idx, kNone32);
         return fallback ? 0u : qb - qa;
     }
 };

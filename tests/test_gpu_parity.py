@@ -38,8 +38,8 @@ def grid_state(request, monkeypatch):
     group32  — the same with groups of 32 lanes (the last round through ds_swizzle)
     lane     — auto with the lane kernel whenever it applies (MR_HUB_LANE=1); on the
                standard layout it computes ranks and looks up specials itself
-    lanenl   — the same with Fleetfoot 1..3 on the lane kernel for every order, Time
-               first included (MR_LANE_NONLIN=1)
+    lanenl   — the same (Fleetfoot 1..3 on the lane kernel is the default; the mode
+               keeps the name of the switch, MR_LANE_NONLIN=1)
     lanetab  — the same reading every cell's {sinfo, rank} record (MR_RANK_TABLE=1)
     hub1     — hub solver with one source per wave (no lane or group kernel)
     hub2     — hub solver with two sources per wave (no lane or group kernel)

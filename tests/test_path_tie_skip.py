@@ -7,8 +7,12 @@ distance grows by one a step, no axis crossed), every quantity the flip test rea
 is constant or periodic in the step index with period den (the Fleetfoot ratio's
 denominator: run_time(k + den) = run_time(k) + 180 num).  So once den consecutive
 steps of such a run have been checked, the rest of the run can be skipped; the scan
-resumes exactly at the first step that leaves the run.  `path_tie_skip` below is a
-line-by-line restatement of the device loop; it must agree with the full scan."""
+resumes exactly at the first step that leaves the run; a run of at least den steps is
+decided at its start by one period of the time gaps (every residue of k mod den occurs
+on it) and skipped whole.  A stretch on which the walk
+approaches q's column (row) is skipped whole: q's distance drops there,
+and only a step on which it grows can flip.  `path_tie_skip` below is a line-by-line
+restatement of the device loop; it must agree with the full scan."""
 import random
 
 import pytest
@@ -51,9 +55,25 @@ def path_tie_skip(mq, nq, gq, q_src, mb, nb, gb, b_src, gv, perm, ff, x_first, l
     while k < K:
         if u == (0, 0):
             return True
+        # Approach skip: moving along a segment towards q's column (row), q's distance drops
+        # by one a step until the walk reaches it (or the step before the axis being
+        # crossed: the Center detour's term stays constant), so no step of it can flip
+        along_x = (k < kx) if x_first else (k >= ky)
+        seg_end = (kx if x_first else K) if along_x else (K if x_first else ky)
+        c0, qc, sd = (u[0], qx, sx) if along_x else (u[1], qy, sy)
+        if sd * (c0 - qc) < 0:
+            j = min(seg_end, k + abs(c0 - qc))
+            if c0 * sd < 0:
+                j = min(j, k + abs(c0) - 1)
+            if j > k + 1:
+                k, run = j, 0
+                u = cell(k)
+                dq = walk_dist(gq, u)
+                continue
         w = cell(k + 1)
         dqn = walk_dist(gq, w)
-        if not (LEGS in before and mq[LEGS] + dq != mb[LEGS] + k) and dqn > dq:
+        tie_before = not (LEGS in before and mq[LEGS] + dq != mb[LEGS] + k)
+        if tie_before and dqn > dq:
             delta = run_time(dqn, ff) - run_time(dq, ff) - (run_time(k + 1, ff) - run_time(k, ff))
             gap = mq[TIME] + run_time(dq, ff) - mb[TIME] - run_time(k, ff)
             if gap in (-1, 0) and delta >= 0:
@@ -69,20 +89,40 @@ def path_tie_skip(mq, nq, gq, q_src, mb, nb, gb, b_src, gv, perm, ff, x_first, l
             plain = k >= 1 and u[1] != 0 and w[1] != 0 and sy * (u[1] - qy) >= 0
         seg_end = (kx if x_first else K) if along_x else (K if x_first else ky)
         run = run + 1 if plain else 0
-        if run >= den:
-            # the next step that is not plain: the segment's end, or the step before the
-            # one whose cell lies on the axis being crossed
-            j = seg_end
-            if along_x:
-                c0 = cell(k)[0]
-                if c0 * sx < 0:  # the x = 0 axis ahead
-                    jz = k + abs(c0)  # the step index whose cell has x = 0
-                    j = min(j, jz - 1)
-            else:
-                c0 = cell(k)[1]
-                if c0 * sy < 0:
-                    jz = k + abs(c0)
-                    j = min(j, jz - 1)
+        # the next step that is not plain: the segment's end, or the step before the one
+        # whose cell lies on the axis being crossed
+        j = seg_end
+        if along_x:
+            c0 = cell(k)[0]
+            if c0 * sx < 0:  # the x = 0 axis ahead
+                jz = k + abs(c0)  # the step index whose cell has x = 0
+                j = min(j, jz - 1)
+        else:
+            c0 = cell(k)[1]
+            if c0 * sy < 0:
+                jz = k + abs(c0)
+                j = min(j, jz - 1)
+        # A plain run of at least den steps from here (q off the walk, so the tail below
+        # is the run's): its steps see every residue of k mod den, and the time gaps at a
+        # step and the next are d0 + F(r), d0 + F(r + 1) with F(r) = f(r + m) - f(r)
+        # (m = dq - k, constant on the run, F periodic in r).  One period of F decides
+        # whether some step of the run flips; the run is then skipped whole.
+        if plain and tie_before and dq > 0 and j - k >= den:
+            m, T, d0 = dq - k, tail(dq, k), mq[TIME] - mb[TIME]
+            base = den * (-(-max(0, -m) // den))  # (r + m >= 0: f's argument)
+            for i in range(den):
+                r = base + i
+                g = d0 + run_time(r + m, ff) - run_time(r, ff)
+                gw = d0 + run_time(r + 1 + m, ff) - run_time(r + 1, ff)
+                if g in (-1, 0) and gw >= g and (g == -1 or T != 1) and (gw > 0 or (gw == 0 and T != -1)):
+                    return True
+            k, run = j, 0
+            u = cell(k)
+            dq = walk_dist(gq, u)
+            continue
+        # (with Legs before Time the legs gap is constant on a plain run too: a run that
+        # starts untied stays untied and is skipped at once)
+        if run >= den or (plain and not tie_before):
             if j > k + 1:
                 k, run = j, 0
                 u = cell(k)

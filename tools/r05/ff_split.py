@@ -1,6 +1,6 @@
-"""GPU probe: where the non-linear hub's pass time goes — certification of destinations
-on/off (MR_DBG_FLAGS=8 skips it: labels unchecked, timing only) and the linear hub_kernel
-at the same batch.  Not product code."""
+"""GPU probe: where the non-linear lane kernel's pass time goes — the settled specials'
+certification (MR_DBG_FLAGS=4 skips it), the destinations' (=8), both (=12); labels
+unchecked, timing only.  Not product code."""
 import os
 import sys
 
@@ -21,19 +21,20 @@ def t(g, qs, params, env, steps=5):
     for _ in range(steps):
         plan.run()
     ms, n = plan.kernel_ms()
-    return ms, plan.stats()["solver"], plan.stats()["fallback_sources"]
+    st = plan.stats()
+    return f"{ms:.3f} ms (lane {st['lane_sources']}, fb {st['fallback_sources']})"
 
 
 def main(size=1025, nq=125000):
     m = SyntheticMap(size, campfires_per_homeland=4, seed=2024)
     g = pf.MapGrid(m.cells())
     qs = random_queries(m, nq, 7)
-    for s in [(0, 2), (2, 0), (1, 0)]:
-        print(f"ff=0 sort={s} hub_kernel {t(g, qs, Params(sort_by=s), {'MR_HUB_LANE': '0', 'MR_HUB_GROUP': '0'})}",
-              flush=True)
-        for ff in (1, 3):
-            p = Params(fleetfoot=ff, sort_by=s)
-            print(f"ff={ff} sort={s} full {t(g, qs, p, {})} nocert {t(g, qs, p, {'MR_DBG_FLAGS': '8'})}", flush=True)
+    for s, ff in [((0, 2), 1), ((0, 2), 2), ((2, 0), 1), ((1, 0), 3), ((1, 0), 1)]:
+        p = Params(fleetfoot=ff, sort_by=s)
+        row = [f"ff={ff} sort={s}"]
+        for dbg in ("0", "4", "8", "12"):
+            row.append(f"dbg{dbg} {t(g, qs, p, {'MR_LANE_NONLIN': '1', 'MR_DBG_FLAGS': dbg})}")
+        print("  ".join(row), flush=True)
 
 
 if __name__ == "__main__":
