@@ -316,13 +316,21 @@ __global__ __launch_bounds__(kSelectBS) void cert_select_kernel(const KArgs *__r
 #define MR_SWEEP_BUCKETS 4096
 #endif
 #ifndef MR_SWEEP_POOL
-#define MR_SWEEP_POOL 20480
+#define MR_SWEEP_POOL 16384
 #endif
 constexpr uint32_t kSweepBS = 1024;      // threads of the sweep's one workgroup per slot
 constexpr uint32_t kSweepBuckets = MR_SWEEP_BUCKETS;  // leading-metric buckets a window may span
 constexpr int kSweepMargin = 2;            // cells added round the failing cells' box
-constexpr uint32_t kSweepRunTimes = 8200;  // run-time table (walks of up to 2 S + 3 legs at S = 4097)
+#ifndef MR_SWEEP_RT
+#define MR_SWEEP_RT 4100
+#endif
+#ifndef MR_SWEEP_LQ
+#define MR_SWEEP_LQ MR_SWEEP_POOL
+#endif
+constexpr uint32_t kSweepRunTimes = MR_SWEEP_RT;  // run-time table (walks of up to 2 S + 3 legs at S = 2048;
+                                           // longer ones divide)
 constexpr uint32_t kSweepPool = MR_SWEEP_POOL;  // LDS words: the window's words, or its mark bitmap
+static_assert(kSweepPool <= 65536, "an LDS window's queues hold 16-bit cell indices");
 
 // One workgroup per slot: the failing box (+ margin) in order of the leading metric of its
 // cells, bucket by bucket (buckets of the least StandardMove increment: a cell never
@@ -336,7 +344,11 @@ constexpr uint32_t kSweepPool = MR_SWEEP_POOL;  // LDS words: the window's words
 // LDS (marks in bit 30) and writes them back at the end; a larger one (up to 32 x
 // kSweepPool cells) keeps its marks in an LDS bitmap and its words in the slot's buffer,
 // owned by this workgroup (one CU) during the sweep, so workgroup-scope accesses and the
-// barrier order the buckets.  Wider windows are left to the SSSP kernel.  (ff 2 at 1025^2,
+// barrier order the buckets.  An LDS window's queues are in LDS too (16-bit cell indices),
+// so its buckets touch no global memory; a bitmap window's are in the slot's list buffer.
+// A queued cell's four neighbour words are read once, for its least extension and for
+// queueing them (an unmarked neighbour is not rewritten in this bucket).  Wider windows
+// are left to the SSSP kernel.  (ff 2 at 1025^2,
 // 100k of the window's 441k cells in 810 of its 1 329 buckets.)
 __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__restrict__ a) {
     __shared__ CertEntry E[64];
@@ -344,6 +356,7 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
     __shared__ uint32_t fill[kSweepBuckets];  // its length so far
     __shared__ uint32_t FT[kSweepRunTimes];   // run times of 0 .. kSweepRunTimes - 1 legs
     __shared__ uint32_t pool[kSweepPool];
+    __shared__ uint16_t lq[MR_SWEEP_LQ];  // an LDS window's queues (window cell indices)
     __shared__ uint32_t red[2];
     const uint32_t slot = blockIdx.x, tid = threadIdx.x;
     const uint32_t nslot = min(a->cert_cap, __hip_atomic_load(a->counter + kCtrCert, __ATOMIC_RELAXED,
@@ -429,6 +442,8 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
         return;
     }
     const bool full = (a->dbg_flags & kDbgSweepFull) != 0;  // (A/B: every window cell queued)
+    const bool reread = (a->dbg_flags & kDbgSweepReread) != 0,
+               lql = in_lds && !(a->dbg_flags & kDbgSweepGList) && MR_SWEEP_LQ >= kSweepPool;
     for (uint32_t j = tid; j < nb; j += kSweepBS) {
         off[j] = 0;
         fill[j] = 0;
@@ -491,38 +506,75 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
         if (!seed) continue;
         if (!in_lds) atomicOr(&pool[i >> 5], 1u << (i & 31u));
         const uint32_t j = lead_of(raw & ~kCertDirty) / W - kmin;
-        list[(j ? off[j - 1] : 0u) + atomicAdd(&fill[j], 1u)] = uint32_t(y) << 16 | uint32_t(x);
+        const uint32_t at = (j ? off[j - 1] : 0u) + atomicAdd(&fill[j], 1u);
+        if (lql) lq[at] = uint16_t(i);
+        else list[at] = uint32_t(y) << 16 | uint32_t(x);
     }
     __syncthreads();
+    // bucket j's queue region and a push into it (a full region drops the push: the check
+    // after the sweep then finds the stale cell, and the SSSP kernel solves the source)
+    auto region = [&](uint32_t j) { return j ? off[j - 1] : 0u; };
+    auto push = [&](uint32_t j, int x, int y) {
+        const uint32_t at = atomicAdd(&fill[j], 1u);
+        if (at >= off[j] - region(j)) return;
+        if (lql) lq[region(j) + at] = uint16_t(widx(x, y));
+        else list[region(j) + at] = uint32_t(y) << 16 | uint32_t(x);
+    };
     // Bucket by bucket: each queued cell takes its neighbours' least extension; a change
-    // queues its unmarked neighbours of later buckets.
+    // queues its unmarked neighbours of later buckets.  A cell whose new word lies in a
+    // later bucket is queued again there: its label may rest on a neighbour of this
+    // bucket that changes concurrently, and only a later bucket's evaluation sees every
+    // cell it can rest on final.
     for (uint32_t j = 0; j < nb; ++j) {
-        const uint32_t n = fill[j];  // (uniform: written before the last barrier)
+        const uint32_t n = min(fill[j], off[j] - region(j));  // (uniform: written before the last barrier)
         if (n == 0) continue;
-        const uint32_t beg = j ? off[j - 1] : 0u;
+        const uint32_t beg = region(j);
         for (uint32_t i = beg + tid; i < beg + n; i += kSweepBS) {
-            const uint32_t v = list[i];
-            const int y = int(v >> 16), x = int(v & 0xFFFFu);
+            int x, y;
+            if (lql) {
+                const uint32_t wi = lq[i], r = wi / bw;
+                y = by0 + int(r);
+                x = bx0 + int(wi - r * bw);
+            } else {
+                const uint32_t v = list[i];
+                y = int(v >> 16);
+                x = int(v & 0xFFFFu);
+            }
+            // the neighbours' least extension (the Center has none), and their words (marks
+            // off) for the queueing below.  (The least extension goes through cert_best4*:
+            // the same loop written out here left the Fleetfoot 1 test source uncertified
+            // on the GPU, test_gpu_cert.py, for reasons not found)
+            const int nx[4] = {x - 1, x + 1, x, x}, ny[4] = {y, y, y - 1, y + 1};
+            uint32_t nwd[4];
+            bool on[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                on[q] = nx[q] >= 0 && nx[q] < S && ny[q] >= 0 && ny[q] < S && !(nx[q] == H && ny[q] == H);
+                nwd[q] = on[q] ? word(nx[q], ny[q]) : 0u;
+            }
+            const uint32_t old = word(x, y);
             CertLab best{};
-            bool any;
+            bool any = false;
             if (in_lds) cert_best4_lds(p, E, w, pitch, pool, bx0, by0, bx1, by1, x, y, best, any, FT, nft);
             else cert_best4<true>(p, E, w, pitch, x, y, best, any, FT, nft);
-            const uint32_t old = word(x, y);
             const uint32_t nw = any ? ((best.b << kStBShift) | best.k) : old;
             if (nw == old) continue;
             if (in_lds) pool[widx(x, y)] = nw | kCertDirty;  // (the mark stays: never queued again)
             else __hip_atomic_store(gptr(x, y), nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int nx[4] = {x - 1, x + 1, x, x}, ny[4] = {y, y, y - 1, y + 1};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                if (!inwin(nx[q], ny[q]) || (nx[q] == H && ny[q] == H)) continue;  // (outside the window: fixed)
-                const uint32_t cu = word(nx[q], ny[q]);
+                if (!on[q] || !inwin(nx[q], ny[q])) continue;  // (outside the window: fixed)
+                // (an unmarked neighbour is never processed in this bucket: its word read
+                // above is current; a marked one is skipped)
+                const uint32_t cu = reread ? word(nx[q], ny[q]) : nwd[q];
                 if (!plain_word(cu) || marked(nx[q], ny[q])) continue;  // (queued or processed already)
                 const uint32_t ju = lead_of(cu) / W - kmin;           // (an unmarked cell: its initial bucket)
                 if (ju <= j || ju >= nb) continue;                    // (an earlier or this bucket: not its reader)
                 if (!mark(nx[q], ny[q])) continue;                    // (another thread queued it)
-                list[off[ju - 1] + atomicAdd(&fill[ju], 1u)] = uint32_t(ny[q]) << 16 | uint32_t(nx[q]);
+                push(ju, nx[q], ny[q]);
             }
+            const uint32_t jn = lead_of(nw) / W - kmin;  // (the mark stays: nobody else queues it)
+            if (jn > j && jn < nb) push(jn, x, y);
         }
         __syncthreads();
     }

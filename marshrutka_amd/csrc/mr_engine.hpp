@@ -278,5 +278,6 @@ constexpr uint32_t kDbgInjectFlag = 16u;
 constexpr uint32_t kDbgGroupNoSolve = 32u, kDbgGroupNoReadoff = 64u, kDbgGroupNoTies = 128u;
 constexpr uint32_t kDbgSweepFull = 256u;   // the repair sweep queues every window cell (A/B)
 constexpr uint32_t kDbgSweepNoLds = 512u;  // the repair sweep keeps a small window's words in the slot's buffer
+constexpr uint32_t kDbgSweepReread = 1024u, kDbgSweepGList = 2048u;  // (A/B probes of the sweep)
 
 }  // namespace mr
