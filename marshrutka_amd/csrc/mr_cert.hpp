@@ -318,7 +318,10 @@ __global__ __launch_bounds__(kSelectBS) void cert_select_kernel(const KArgs *__r
 #ifndef MR_SWEEP_POOL
 #define MR_SWEEP_POOL 16384
 #endif
-constexpr uint32_t kSweepBS = 1024;      // threads of the sweep's one workgroup per slot
+#ifndef MR_SWEEP_BS
+#define MR_SWEEP_BS 1024
+#endif
+constexpr uint32_t kSweepBS = MR_SWEEP_BS;  // threads of the sweep's one workgroup per slot
 constexpr uint32_t kSweepBuckets = MR_SWEEP_BUCKETS;  // leading-metric buckets a window may span
 constexpr int kSweepMargin = 2;            // cells added round the failing cells' box
 #ifndef MR_SWEEP_RT

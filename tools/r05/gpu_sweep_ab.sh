@@ -1,13 +1,10 @@
 #!/bin/bash
-# A/B of the sweep variants on the flagged Fleetfoot 1 / 2 sources
+# timing A/B of sweep variants (Time-first Fleetfoot 1 and 2 at 1025^2 / 125k)
 set -o pipefail
 mkdir -p gpurun_out
-run() {  # tag lib flags
-  echo "$1 flags=$3"
-  MR_LIB_PATH=$2 MR_DBG_FLAGS=$3 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
-    tests/test_gpu_cert.py -k "flagged_source_certified_1025" > gpurun_out/ab_$1_$3.log 2>&1; tail -n 1 gpurun_out/ab_$1_$3.log
-}
-run main "" 0
-run main "" 512
-run main "" 3072
-run helper marshrutka_amd/lib/variants/helper/libmarshrutka_pf.so 0
+for v in main bs64 bs256 noreq; do
+  L=""; [ $v != main ] && L=marshrutka_amd/lib/variants/$v/libmarshrutka_pf.so
+  for FF in 1 2; do
+    echo -n "$v: "; MR_LIB_PATH=$L timeout -k 10 200 python tools/r05/ff_one.py $FF 1 2 6 || exit 1
+  done
+done
