@@ -12,7 +12,7 @@ LIB_DIR = os.path.join(HERE, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libmarshrutka_pf.so")
 # one translation unit per kernel family (device code shared through mr_device.hpp),
 # compiled in parallel and linked into one shared library
-SOURCES = ["mr_k_region.hip", "mr_k_groupq.hip", "mr_k_group.hip", "mr_k_lane.hip", "mr_k_lane24.hip", "mr_k_lane32.hip", "mr_k_lane_nl.hip", "mr_k_lane_nl2.hip", "mr_k_wide2.hip", "mr_k_wide5.hip", "mr_k_wide8.hip", "mr_k_hub_lin.hip", "mr_k_hub_nl.hip",
+SOURCES = ["mr_k_region.hip", "mr_k_groupq.hip", "mr_k_group.hip", "mr_k_group_nl.hip", "mr_k_lane.hip", "mr_k_lane24.hip", "mr_k_lane32.hip", "mr_k_lane_nl.hip", "mr_k_lane_nl2.hip", "mr_k_wide2.hip", "mr_k_wide5.hip", "mr_k_wide8.hip", "mr_k_hub_lin.hip", "mr_k_hub_nl.hip",
            "mr_k_hub.hip", "mr_k_wide.hip",
            "mr_k_solve.hip", "mr_k_fill.hip", "mr_k_cert.hip", "mr_k_decode.hip",
            "mr_host.cpp", "mr_html.cpp", "mr_render.cpp"]

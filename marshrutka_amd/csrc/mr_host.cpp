@@ -69,7 +69,7 @@ hipError_t partition_sources_device(uint32_t n, uint32_t V, const void *scratch,
                                     hipStream_t s);
 uint32_t hub_group_lds_bytes(uint32_t NS, uint32_t nreg, uint32_t G);
 hipError_t launch_hub_group(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t n,
-                            uint32_t G, hipStream_t stream);
+                            uint32_t G, bool nonlin, hipStream_t stream);
 hipError_t launch_cert_select(const KArgs *d_args, hipStream_t stream);
 hipError_t launch_cert_check(const KArgs *d_args, uint32_t gx, uint32_t slots, uint32_t mark, hipStream_t stream);
 hipError_t launch_cert_sweep(const KArgs *d_args, uint32_t slots, hipStream_t stream);
@@ -2228,13 +2228,17 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
     // Fleetfoot 1..3 on the lane kernel (its NL instantiation: the walk certification of
     // hub_kernel's §3a'').  A source it cannot certify (Time first: 1 in 118k at 1025^2)
     // is relisted for a hub_kernel launch right after it, whose fallback reaches the
-    // certificate (§3d) instead of the SSSP kernel.  MR_LANE_NONLIN=0: never.
+    // certificate (§3d) instead of the SSSP kernel.  MR_LANE_NONLIN=0: never; =1: the group
+    // kernel for Time-first orders too.
     const char *lnl = std::getenv("MR_LANE_NONLIN");
     const bool lane_nl = hp.nonlin && hp.ff_magic_ok && !(lnl && !std::strcmp(lnl, "0"));
     if (lane_ok && (!hp.nonlin || lane_nl) && !group_force && !lane_off && hub_lane_entries(hp.p.NS) != 0 &&
         lane_layout_ok(hp) && (lane_force || lane_sources(hp) >= lane_min_sources()))
         pl->n_lane = hp.dev_grouped ? partition_on_device(pl) : partition_sources(hp);
-    else if (lane_ok && !hp.nonlin && !group_off && !lane_force && hub_group_slots(hp.p.NS, group_g) != 0 &&
+    // (the group kernel takes Fleetfoot plans that do not lead with Time: on Time-first
+    // ones, c2-sized, hub_kernel's pass was 0.4-0.5 ms shorter, tools/r05/gpu_rates.sh)
+    else if (lane_ok && (!hp.nonlin || (lane_nl && (hp.p.perm[0] != 2u || (lnl && !std::strcmp(lnl, "1"))))) &&
+             !group_off && !lane_force && hub_group_slots(hp.p.NS, group_g) != 0 &&
              !std::getenv("MR_HUB_FALLBACK_ALL")) {
         pl->n_lane = nsrc_of(hp);
         pl->lane_g = group_g;
@@ -2449,7 +2453,7 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
                                              : hub_blocks_per_cu(hp.p.perm, pl->spw, hp.nonlin, hb));
         // (a lane kernel with Fleetfoot relists its uncertain sources for hub_kernel: room
         // for a few hundred of them in one round)
-        const bool relist = pl->n_lane && !pl->lane_g && hp.nonlin;
+        const bool relist = pl->n_lane && hp.nonlin;
         const uint64_t per_block = 4ull * pl->spw, hub_src = std::max<uint64_t>(nsrc - pl->n_lane, relist ? 512u : 0u);
         pl->hub_blocks = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((hub_src + per_block - 1) / per_block,
                                                                            uint64_t(hper) * prop.multiProcessorCount)));
@@ -2749,7 +2753,7 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
         e = hipSuccess;
         if (pl->n_lane) {
             const KArgs *la = pl->fb_none && !big ? pl->d_args_lane_last : pl->d_args_lane;
-            e = pl->lane_g ? launch_hub_group(la, pl->ka.p.perm, pl->ka.p.NS, pl->ka.nreg, pl->n_lane, pl->lane_g, s)
+            e = pl->lane_g ? launch_hub_group(la, pl->ka.p.perm, pl->ka.p.NS, pl->ka.nreg, pl->n_lane, pl->lane_g, pl->hp.nonlin, s)
                            : launch_hub_lane(la, pl->ka.p.perm, pl->ka.p.NS, pl->ka.nreg, pl->n_lane, pl->hp.nonlin, s);
         }
         if (e == hipSuccess && big) e = launch_hub_plan(pl, pl->fb_none ? pl->d_args_hub_last : pl->d_args, s);

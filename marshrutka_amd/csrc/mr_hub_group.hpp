@@ -117,13 +117,15 @@ __device__ __forceinline__ uint32_t bitv(uint32_t w, uint32_t e) {
     } while (0)
 #endif
 
-template <uint32_t PERM, uint32_t G, uint32_t E>
-struct GroupHub : LaneHub<PERM, G * E> {
+// NL: Fleetfoot 1..3 (LaneHub's run times and walk certification, the group's lanes
+// sharing the boundaries)
+template <uint32_t PERM, uint32_t G, uint32_t E, bool NL = false>
+struct GroupHub : LaneHub<PERM, G * E, NL> {
 #ifdef MR_STAMPS
     unsigned long long gst[8] = {0, 0, 0, 0, 0, 0, 0, 0}, gst_last = 0;
 #endif
     static constexpr uint32_t TM = G * E;  // table entries (slot i of lane j: entry i * G + j)
-    using Base = LaneHub<PERM, TM>;
+    using Base = LaneHub<PERM, TM, NL>;
     using Base::a;
     using Base::P;
     using Base::spl;
@@ -160,6 +162,7 @@ struct GroupHub : LaneHub<PERM, G * E> {
     using Base::settle_ctx;
     using Base::walk_to;
     using Base::meta_of;
+    using Base::rtime;
     using Base::mstride;
     using Base::mcolumn;
     using Own = typename Base::Own;
@@ -278,6 +281,36 @@ struct GroupHub : LaneHub<PERM, G * E> {
         if (gj < a->nreg) sr0 = reinterpret_cast<const uint2 *>(a->near)[(unsigned long long)src * a->nreg + gj];
     }
 
+    // ---- non-linear run times (NL): LaneHub::walk_certain with the group's lanes sharing
+    // the boundaries: each lane checks the boundaries among its own slots (their labels in
+    // registers), the group combines the clean paths.  Group-uniform: every lane of the
+    // group calls it with the same target.
+    __device__ __forceinline__ bool cert_group(uint32_t b, int vx, int vy) const {
+        int bx, by;
+        pos(b, bx, by);
+        if ((by == 0 && vy == 0 && bx != 0 && vx != 0 && (bx < 0) != (vx < 0)) ||
+            (bx == 0 && vx == 0 && by != 0 && vy != 0 && (by < 0) != (vy < 0)))
+            return false;  // shortest walks detour round the Center
+        const LLab xb = b == 0 ? start() : lt_get(b);
+        uint32_t paths = 3u;
+#pragma unroll
+        for (uint32_t i = 0; i < E; ++i) {
+            const uint32_t e = ent(i);
+            const bool isq = e == 0 ? src != P.vc : (e != 1 && ((bndm >> e) & 1u));  // (the Center starts no walks)
+            if (!isq || e == b) continue;
+            const LLab xq = e == 0 ? start() : Ls[i];
+            if (!Base::near_tie(xq, ex[i], ey[i], xb, bx, by, vx, vy)) continue;
+            int lists = 0;  // the order of q's and b's command lists when their lengths tie
+            if (e != 0 && b != 0 && lm_len(xq.m) == lm_len(xb.m))
+                lists = cmp_list(meta_of(e), e, own_of(e), meta_of(b), b, own_of(b));
+            uint32_t clean = 0;
+            for (uint32_t xf = 0; xf < 2; ++xf)
+                clean |= Base::path_tie(xq, e, ex[i], ey[i], xb, b, bx, by, vx, vy, xf == 0, lists) ? 0u : (1u << xf);
+            paths &= clean;
+        }
+        return !(group_any((paths & 1u) == 0u) && group_any((paths & 2u) == 0u));
+    }
+
     // ---- one source per group; every lane of the group calls it with the same source ---
     // returns the records this lane wrote (lane 0 of the group reports the source's)
     __device__ __forceinline__ uint32_t solve(bool have, uint32_t s_idx) {
@@ -313,7 +346,7 @@ struct GroupHub : LaneHub<PERM, G * E> {
             uint32_t any = m0;
             const uint32_t k = walk_dist(sx, sy, tS.x, tS.y);
             const uint32_t won = vmask(valid && walks0 && tS.v != src && e != 1);  // no walks into the Center
-            const LLab w = opt(won, mk(k, 0, 180u * k, lm_pack(1, 0, 1, kStandard)));
+            const LLab w = opt(won, mk(k, 0, rtime(k), lm_pack(1, 0, 1, kStandard)));
             consider(c, w);
             any |= won;
             {  // [SoE src -> e], or [Std{d} src -> u, SoE u -> e]
@@ -322,7 +355,7 @@ struct GroupHub : LaneHub<PERM, G * E> {
                 const bool on = walks0 && reg && ev != kNone32;
                 const uint32_t d = on ? ev : 0u;
                 const uint32_t om = vmask(on);
-                consider(c, opt(om, mk(d, p.soe_cost, 180u * d,
+                consider(c, opt(om, mk(d, p.soe_cost, rtime(d),
                                        d == 0 ? lm_pack(1, 0, 1, kSoE) : lm_pack(2, 0, 2, kStandard))));
                 any |= om;
             }
@@ -431,6 +464,27 @@ struct GroupHub : LaneHub<PERM, G * E> {
                 if (e >= 1 && e <= NS && ((done >> e) & 1u) && !label_avail(Ls[i].m, e)) unc = true;
             }
         }
+        // non-linear run times: every settled walk label must also be certain against near
+        // ties of the time gap (LaneHub::label_certain, the group's lanes sharing the
+        // boundaries; done and bndm are the group's)
+        if (NL && !group_any(unc) && !(a->dbg_flags & 4u)) {
+            for (uint32_t m = done & ~1u; m; m &= m - 1u) {
+                const uint32_t t = uint32_t(__builtin_ctz(m));
+                const uint32_t mt = meta_of(t);
+                if (lm_kind(mt) != kStandard) continue;
+                const uint32_t b = lm_par(mt);
+                int vx = spl[t].x, vy = spl[t].y;
+                if (lm_nt(mt) != 1) {
+                    const uint32_t u = Base::rank_inv[Base::near_of(b, spl[t].rid).y];
+                    vx = int(u % p.S) - int(p.H);
+                    vy = int(u / p.S) - int(p.H);
+                }
+                if (!cert_group(b, vx, vy)) {
+                    unc = true;
+                    break;
+                }
+            }
+        }
         const bool fb_sp = group_any(unc) || a->fb_all || (a->dbg_flags & kDbgGroupNoReadoff);
         MR_GSTAMP(6);  // (6: the tail commands and the certification of settled labels)
         // ---- destinations: each query by the whole group, its record by one lane --------
@@ -445,6 +499,7 @@ struct GroupHub : LaneHub<PERM, G * E> {
             W[gj] = j0 == 0 ? w_first : (j0 + gj < nq ? a->q_dst[qa + j0 + gj] : 0u);
             const uint32_t nb = min(G, nq - j0);
             uint32_t rk_ = 0, rw = 0, rbx = 0, rtie = 0;  // this lane's record: kind, destination, boundary, tie
+            uint32_t fbx = 0;                              // its final boundary (after the list compares)
             LLab rx = inf();
             for (uint32_t j = 0; j < nb; ++j) {
                 const uint32_t w = W[j];
@@ -468,7 +523,7 @@ struct GroupHub : LaneHub<PERM, G * E> {
                         const bool on = e == 0 ? walk0 : ((bndm >> e) & 1u) != 0;
                         const uint32_t kk = walk_dist(ex[i], ey[i], wx, wy);
                         const LLab b0 = e == 0 ? LLab{0u, 0u, 0u, 0u} : Ls[i];
-                        cs[i] = opt(vmask(on), add(b0, kk, 0, 180u * kk, b0.m));
+                        cs[i] = opt(vmask(on), add(b0, kk, 0, rtime(kk), b0.m));
                         ltm_take_i(cs[i], lx, e, sl);
                     }
                     x = lx;
@@ -513,7 +568,7 @@ struct GroupHub : LaneHub<PERM, G * E> {
                             int px, py;
                             pos(b, px, py);
                             const uint32_t kk = walk_dist(px, py, wx, wy);
-                            const LLab c = b == 0 ? mk(kk, 0, 180u * kk, lm_pack(1, 0, 1, kStandard)) : walk_to(lt_get(b), b, kk);
+                            const LLab c = b == 0 ? mk(kk, 0, rtime(kk), lm_pack(1, 0, 1, kStandard)) : walk_to(lt_get(b), b, kk);
                             if (cmp4(c, x) == 0 && cmp_list(c.m, kOwn, wo, x.m, kOwn, wo) < 0) {
                                 x = c;
                                 bx = b;
@@ -524,11 +579,25 @@ struct GroupHub : LaneHub<PERM, G * E> {
                     pos(bx, px, py);
                     emit_ct(x, bx, true, Cmd{(kStandard << 29) | walk_dist(px, py, wx, wy), Base::rk(bx), wr}, qi);
                     if (blk != 0 && !avail(bx, px, py, wx, wy)) uncd = true;
+                    fbx = bx;
+                }
+            }
+            // non-linear run times: each plain destination's winning walk must be certain,
+            // checked by the whole group (the queries' winners come over from their lanes)
+            if (NL && !(a->dbg_flags & 8u)) {
+                for (uint32_t j = 0; j < nb; ++j) {
+                    const uint32_t kj = uint32_t(__shfl(int(rk_), int(gbase + j), 64));
+                    const uint32_t bj = uint32_t(__shfl(int(fbx), int(gbase + j), 64));
+                    const uint32_t wj = uint32_t(__shfl(int(rw), int(gbase + j), 64));
+                    if (kj != 3 || group_any(uncd)) continue;
+                    if (!cert_group(bj, int(wj % p.S) - int(p.H), int(wj / p.S) - int(p.H))) uncd = true;
                 }
             }
         }
         const bool fallback = fb_sp || group_any(uncd);
-        if (fallback && gj == 0) push_fallback(a, counter, s_idx, kNone32);
+        // (an uncertain source goes to hub_kernel when the plan relaunches it, as on the lane kernel)
+        if (fallback && gj == 0 && a->relist && !a->fb_all) a->relist[atomicAdd(counter + kCtrRelist, 1u)] = s_idx;
+        else if (fallback && gj == 0) push_fallback(a, counter, s_idx, kNone32);
         MR_GSTAMP(5);  // (5: certification and the destinations)
         return (fallback || gj != 0) ? 0u : qb - qa;
     }
@@ -556,11 +625,11 @@ __host__ __device__ inline uint32_t group_lds_total(uint32_t NS, uint32_t nreg, 
     return group_off_w(NS, nreg, G, E) + kBS * 4u;
 }
 
-template <uint32_t PERM, uint32_t G, uint32_t E>
+template <uint32_t PERM, uint32_t G, uint32_t E, bool NL = false>
 __global__ __launch_bounds__(kBS) void hub_group_kernel(const KArgs *__restrict__ a) {
     constexpr uint32_t TM = G * E;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    GroupHub<PERM, G, E> H;
+    GroupHub<PERM, G, E, NL> H;
     // group q of wave w: source (64 / G) w + q of the sources [0, n_lane)
     const uint32_t grp = (blockIdx.x * (kBS / 64) + (threadIdx.x >> 6)) * (64u / G) + lane_id() / G;
     const uint32_t n = a->n_lane;

@@ -4,6 +4,9 @@
 
 namespace mr {
 
+// Fleetfoot 1..3 (hub_group_kernel<PERM, G, E, true>): mr_k_group_nl.hip
+const void *group_nl_fn(uint32_t G, uint32_t E, uint32_t perm);
+
 template <uint32_t G, uint32_t E>
 static const void *group_fn_ge(uint32_t perm) {
     switch (perm) {
@@ -31,11 +34,12 @@ uint32_t hub_group_lds_bytes(uint32_t NS, uint32_t nreg, uint32_t G) {
 }
 
 hipError_t launch_hub_group(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t n,
-                            uint32_t G, hipStream_t stream) {
+                            uint32_t G, bool nonlin, hipStream_t stream) {
     const uint32_t k = perm[0] * 9 + perm[1] * 3 + perm[2];
     const uint32_t E = hub_group_slots(NS, G);
     const void *fn = nullptr;
-    if (G == 8 && E == 3) fn = group_fn_ge<8, 3>(k);
+    if (nonlin) fn = E ? group_nl_fn(G, E, k) : nullptr;
+    else if (G == 8 && E == 3) fn = group_fn_ge<8, 3>(k);
     else if (G == 8 && E == 4) fn = group_fn_ge<8, 4>(k);
     else if (G == 16 && E == 2) fn = group_fn_ge<16, 2>(k);
     else if (G == 32 && E == 1) fn = group_fn_ge<32, 1>(k);

@@ -493,7 +493,7 @@ def test_overflow_pool(eng, oracle_lib, grid_state, max_cmds):
         assert any(len(e[3]) > max_cmds for e in exp)
 
 
-@pytest.mark.parametrize("kernel", ["hub", "lane"])
+@pytest.mark.parametrize("kernel", ["hub", "lane", "group8", "group32"])
 @pytest.mark.parametrize("ff", [1, 2, 3])
 @pytest.mark.parametrize("sort_by", [(SORT_LEGS, SORT_MONEY), (SORT_LEGS, SORT_TIME), (SORT_MONEY, SORT_LEGS),
                                      (SORT_MONEY, SORT_TIME), (SORT_TIME, SORT_LEGS), (SORT_TIME, SORT_MONEY)])
@@ -502,13 +502,18 @@ def test_fleetfoot_hub(eng, oracle_lib, monkeypatch, ff, sort_by, kernel):
     label certified against near-ties of the time gap, uncertain sources re-solved by
     the SSSP kernel.  Bit-exact against the oracle, with both one and many
     destinations per source, and most sources answered by the hub itself.  kernel:
-    hub_kernel alone, or the lane kernel's Fleetfoot instantiation for every source with
-    at most 32 queries (MR_HUB_LANE=1, MR_LANE_NONLIN=1; 22- and 32-entry tables)."""
+    hub_kernel alone, the lane kernel's Fleetfoot instantiation for every source with at
+    most 32 queries (MR_HUB_LANE=1, MR_LANE_NONLIN=1; 22- and 32-entry tables), or the
+    group kernel's with 8 / 32 lanes a source (MR_HUB_GROUP_FORCE=1)."""
     for v in ("MR_ALGO", "MR_HUB_FALLBACK_ALL", "MR_HUB_SPW", "MR_HUB_WIDE", "MR_HUB_NONLIN", "MR_GRID_STATE",
               "MR_HUB_GROUP", "MR_HUB_GROUP_FORCE"):
         monkeypatch.delenv(v, raising=False)
-    monkeypatch.setenv("MR_HUB_LANE", "0" if kernel == "hub" else "1")
+    monkeypatch.setenv("MR_HUB_LANE", "1" if kernel == "lane" else "0")
     monkeypatch.setenv("MR_LANE_NONLIN", "0" if kernel == "hub" else "1")
+    if kernel.startswith("group"):
+        monkeypatch.setenv("MR_HUB_LANE", "0")
+        monkeypatch.setenv("MR_HUB_GROUP_FORCE", "1")
+        monkeypatch.setenv("MR_HUB_GROUP", kernel[5:])
     for size, k, clustered, seed in ((33, 4, False, 31), (65, 6, True, 32), (129, 4, False, 33)):
         m = SyntheticMap(size, campfires_per_homeland=k, seed=seed + ff, clustered=clustered)
         params = Params(fleetfoot=ff, sort_by=sort_by, route_guru=ff, hq_position=m.campfires()[2])
@@ -530,8 +535,10 @@ def test_fleetfoot_hub(eng, oracle_lib, monkeypatch, ff, sort_by, kernel):
         assert st["fallback_sources"] <= st["num_sources"] // 4, st
         if kernel == "lane":
             assert st["lane_sources"] == st["num_sources"] - 1 and st["lanes_per_source"] == 1, st
-        else:
+        elif kernel == "hub":
             assert st["lane_sources"] == 0 and st["lanes_per_source"] == 0, st
+        else:
+            assert st["lanes_per_source"] == int(kernel[5:]), st
 
 
 def test_device_records_grouped_by_source(eng):
