@@ -2465,15 +2465,19 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
             pmalloc(reinterpret_cast<void **>(&pl->d_args_fill), sizeof(KArgs)) != hipSuccess)
             return bail(fail(MR_ERR_DEVICE, "kernel args"));
         // Certified fallback for query plans on hub_kernel (MR_CERT=0: off; MR_CERT_SLOTS:
-        // slots per pass, default 8): a flagged source's table goes to a slot, the fill
+        // slots per pass, default by grid size): a flagged source's table goes to a slot, the fill
         // writes its closed form over every cell, the check and one repair sweep decide
         // whether its labels need the SSSP kernel at all.
         const char *ce = std::getenv("MR_CERT");
         if (!all_mode && !hp.wide && !(ce && !std::strcmp(ce, "0"))) {
-            uint32_t cap = 8;
-            if (const char *e = std::getenv("MR_CERT_SLOTS")) cap = uint32_t(std::min(64, std::max(1, std::atoi(e))));
+            // slots: as many as 512 MB of cell words and sweep lists hold, 8 to 64 (1025^2:
+            // 60; 4097^2: 8).  A Time-first Fleetfoot 1 batch of 125k on c4's map hands
+            // over ~40 sources, and every one without a slot costs a whole SSSP solve.
             const size_t T = size_t(NS) + 1;
             const uint32_t pitch = (hp.p.S + 31) / 32 * 32;
+            const size_t slot_bytes = size_t(V) * 4 + size_t(hp.p.S) * pitch * 4 + T * (sizeof(Rec) + 4);
+            uint32_t cap = uint32_t(std::min<size_t>(64, std::max<size_t>(8, (size_t(512) << 20) / slot_bytes)));
+            if (const char *e = std::getenv("MR_CERT_SLOTS")) cap = uint32_t(std::min(64, std::max(1, std::atoi(e))));
             std::vector<uint32_t> ones(cap, 1u);
             // staging for every fallback entry up to kCertStageMax (mr_engine.hpp): a
             // pass with more hands nothing to the certificate

@@ -28,7 +28,7 @@ import pytest
 
 import label_digest as ld
 from golden_util import as_expected
-from marshrutka_amd.abi import SORT_MONEY, SORT_TIME, CellIndex, Params, mr_command, mr_result
+from marshrutka_amd.abi import SORT_LEGS, SORT_MONEY, SORT_TIME, CellIndex, Params, mr_command, mr_result
 from marshrutka_amd.mapgen import SyntheticMap, random_queries, random_query_cells
 
 pytestmark = pytest.mark.gpu
@@ -286,6 +286,62 @@ def test_fleetfoot_time_first_1025(eng, oracle_lib, c4_map, ff):
         sel = np.arange(off + i * 1000, off + (i + 1) * 1000)
         bad = ld.mismatches(got, {f: want[f][i] for f in want}, idx_got=sel, idx_exp=q_dst[sel])
         assert bad.size == 0, (str(s), len(bad), [str(m.index_at(int(q_dst[sel][j]))) for j in bad[:4]])
+
+
+@pytest.mark.parametrize("ff,sort_by", [(2, (SORT_LEGS, SORT_MONEY)), (1, (SORT_MONEY, SORT_TIME)),
+                                        (3, (SORT_TIME, SORT_MONEY)), (1, (SORT_TIME, SORT_LEGS))],
+                         ids=["ff2_legs_money", "ff1_money_time", "ff3_time_money", "ff1_time_legs"])
+def test_c4_lane_kernel_fleetfoot_vs_oracle(eng, c4_map, ff, sort_by):
+    """hub_lane_kernel's Fleetfoot instantiation (DESIGN.md section 3a'') against the
+    oracle at configs[3]'s map: 16 sources of every kind x 512 destinations (8 192 labels),
+    spread over plans of a 125k-query batch (lane-kernel size) plus at most 32 queries a
+    source, so every compared label is the lane kernel's read-off, or, for a source it
+    cannot certify, hub_kernel's after the relist (the certificate / SSSP kernel behind
+    it).  The plan stats prove every source ran on the lane kernel."""
+    import oracle_lib
+    oracle_lib.build()
+    m, arr = c4_map
+    V = m.size * m.size
+    params = Params(fleetfoot=ff, sort_by=sort_by)
+    uni_src, uni_dst = random_query_cells(m, 125_000, 5000 + ff)
+    qarr = m.query_array(uni_src, uni_dst, arr)
+    rng = random.Random(77 + ff)
+    srcs = _sources_of_every_kind(m, rng)
+    cf_cells = [m.cell_of(c) for c in m.campfires()]
+    dsts = [np.array(rng.sample(range(V), 512 - len(cf_cells)) + cf_cells, dtype=np.int64) for _ in srcs]
+    want = oracle_lib.OracleGrid.from_array(arr).sssp_digests(params, srcs, threads=ORACLE_THREADS)
+    cnt = np.bincount(uni_src, minlength=V)
+    caps = [32 - int(cnt[m.cell_of(s)]) for s in srcs]
+    assert min(caps) >= 16, caps
+    n_plans = max(-(-len(d) // c) for d, c in zip(dsts, caps))
+    g = eng.MapGrid.from_array(arr)
+    nb = len(uni_src)
+    compared = 0
+    for p in range(n_plans):
+        ex_src, ex_dst, owner = [], [], []
+        for i, (s, d, c) in enumerate(zip(srcs, dsts, caps)):
+            piece = d[p * c:(p + 1) * c]
+            ex_src.append(np.full(len(piece), m.cell_of(s), dtype=np.int64))
+            ex_dst.append(piece)
+            owner.append(np.full(len(piece), i, dtype=np.int64))
+        ex_src, ex_dst, owner = np.concatenate(ex_src), np.concatenate(ex_dst), np.concatenate(owner)
+        q = np.concatenate([qarr, m.query_array(ex_src, ex_dst, arr)])
+        plan = eng.Plan(g, params, None, max_cmds=6, query_array=q)
+        plan.run()
+        st = plan.stats()
+        assert st["solver"] == "hub" and st["lanes_per_source"] == 1, st
+        assert st["lane_sources"] == st["num_sources"], st  # (Time first hands over tens of sources here)
+        res, pool = plan.fetch_raw()
+        got = _tail_digests(res, pool, len(q), nb)
+        for i in range(len(srcs)):
+            sel = np.nonzero(owner == i)[0]
+            if sel.size == 0:
+                continue
+            bad = ld.mismatches(got, {f: want[f][i] for f in want}, idx_got=sel, idx_exp=ex_dst[sel])
+            assert bad.size == 0, (p, str(srcs[i]), len(bad), [str(m.index_at(int(ex_dst[sel][j]))) for j in bad[:4]])
+            compared += sel.size
+        del plan
+    assert compared == sum(len(d) for d in dsts) >= 8_000, compared
 
 
 @pytest.mark.parametrize("params", [Params(), Params(sort_by=(SORT_TIME, SORT_MONEY), route_guru=2)],
