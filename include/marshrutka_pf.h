@@ -281,7 +281,10 @@ typedef struct mr_plan_stats {
     uint32_t region_boundary_cells; /* MR_SOLVER_HUB_WIDE: cells scanned for each source's region row */
     uint32_t fill_launch;       /* all-destinations hub plans: MR_FILL_* (how the fill is launched) */
     uint32_t lane_sources;      /* hub solver: sources solved one per lane (hub_lane_kernel); the rest
-                                   (more than 32 queries each) a lane per query (ABI 5) */
+                                   (more than 32 queries each) a lane per query (ABI 5).  With
+                                   Fleetfoot 1..3 a source the lane or group kernel cannot certify
+                                   goes to hub_kernel in the same pass, and counts in
+                                   fallback_sources only if hub_kernel cannot certify it either */
     uint32_t certified_sources; /* of fallback_sources, those answered by the fixed-point certificate
                                    in the last pass (the rest ran the SSSP kernel; ABI 6) */
     uint32_t lanes_per_source;  /* hub solver: lanes that share one source's Dijkstra over the
