@@ -6,3 +6,8 @@ timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeou
 tail -3 gpurun_out/gpu_suite.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
 tail -3 gpurun_out/smoke.log
+# (optional second stage: the c2-size Fleetfoot rates)
+if [ "${RATES:-0}" = 1 ]; then
+  timeout -k 10 300 python -u tools/ff_rates.py 65 10000 5 > gpurun_out/ff_rates_c2.log 2>&1 || { tail -20 gpurun_out/ff_rates_c2.log; exit 1; }
+  grep "sort=(1" gpurun_out/ff_rates_c2.log
+fi
