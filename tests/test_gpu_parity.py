@@ -349,6 +349,7 @@ def test_fallback_sources_reported(eng, oracle_lib, monkeypatch):
     assert len(got) == pl.stats()["fallback_sources"] == pl.num_sources
     assert set(got) == {a for a, _ in qs}
     monkeypatch.delenv("MR_CERT")
+    monkeypatch.setenv("MR_CERT_SLOTS", "8")  # (the default on this grid size is 64: more than its sources)
     runs = []
     for _ in range(2):
         pl = eng.Plan(g, Params(), qs)
