@@ -542,6 +542,48 @@ def test_fleetfoot_hub(eng, oracle_lib, monkeypatch, ff, sort_by, kernel):
             assert st["lanes_per_source"] == int(kernel[5:]), st
 
 
+@pytest.mark.parametrize("kernel", ["lane", "group16"])
+@pytest.mark.parametrize("ff", [1, 2, 3])
+def test_fleetfoot_random_257(eng, oracle_lib, monkeypatch, ff, kernel):
+    """The Fleetfoot lane / group kernels on 257^2 maps (6 campfires a homeland: a 32-entry
+    table, or 4 clustered: 22 entries; SoE / SFm / caravans toggled; Route Guru; HQ on a campfire or none), every
+    order, against the oracle: 6 orders x 2 maps x 240 queries per case, each source with
+    at most a few queries, so the lane kernel answers all of them (or relists them for
+    hub_kernel)."""
+    for v in ("MR_ALGO", "MR_HUB_FALLBACK_ALL", "MR_HUB_SPW", "MR_HUB_WIDE", "MR_HUB_NONLIN", "MR_GRID_STATE",
+              "MR_HUB_GROUP", "MR_HUB_GROUP_FORCE"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setenv("MR_LANE_NONLIN", "1")
+    if kernel == "lane":
+        monkeypatch.setenv("MR_HUB_LANE", "1")
+    else:
+        monkeypatch.setenv("MR_HUB_LANE", "0")
+        monkeypatch.setenv("MR_HUB_GROUP_FORCE", "1")
+        monkeypatch.setenv("MR_HUB_GROUP", "16")
+    rng = random.Random(257 + ff)
+    for clustered in (False, True):
+        m = SyntheticMap(257, campfires_per_homeland=6 if not clustered else 4, seed=900 + ff + 10 * clustered,
+                         clustered=clustered)
+        g = eng.MapGrid(m.cells())
+        og = oracle_lib.OracleGrid(m.cells())
+        qs = random_queries(m, 240, 31 * ff + clustered)
+        for sort_by in SORTS:
+            if sort_by[0] == sort_by[1]:
+                continue
+            params = Params(fleetfoot=ff, sort_by=sort_by, route_guru=rng.choice([0, 2, 5]),
+                            use_soe=rng.random() < 0.8, use_sfm=rng.random() < 0.5, use_caravans=rng.random() < 0.8,
+                            hq_position=m.campfires()[rng.randrange(len(m.campfires()))] if rng.random() < 0.5 else None)
+            plan = eng.Plan(g, params, qs)
+            plan.run()
+            got = plan.fetch()
+            st = plan.stats()
+            assert st["solver"] == "hub", st
+            assert st["lanes_per_source"] == (1 if kernel == "lane" else 16), st
+            exp = og.find_path_batch(params, qs, threads=0)
+            bad = [(q, e, r) for q, e, r in zip(qs, exp, got) if as_expected(e) != as_expected(r)]
+            assert not bad, f"{kernel} ff={ff} {params}: {len(bad)}/{len(qs)} mismatches; first: {bad[0]}"
+
+
 def test_device_records_grouped_by_source(eng):
     """The compact device records (what the multi-GPU gather moves) are grouped by
     source; mr_plan_record_queries maps record k back to its query, and each record's
