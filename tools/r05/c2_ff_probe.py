@@ -1,3 +1,6 @@
+"""GPU probe (not product code): Time-first Fleetfoot 1-3 on the c2-sized batch (65^2, 10k
+queries): handed-over and certified sources and the pass time (run it under rocprofv3 for
+the certificate kernels' split)."""
 import os, sys
 sys.path.insert(0, os.getcwd())
 from marshrutka_amd import pathfinder as pf
