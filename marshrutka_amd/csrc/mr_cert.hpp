@@ -33,9 +33,16 @@ namespace mr {
 // per table entry of a slot (LDS): metrics, length, boundary rank (kNone32: not a
 // boundary), and for a walk label its boundary and run length
 struct CertEntry {
-    uint32_t m0, m1, m2, len, lex, wb, wk, pad;
-    uint32_t sb, sk, su, pad2;  // a Scroll-of-Escape-region label: its walk (b, k) and the cell (rank) it ends at
+    uint32_t m0, m1, m2, len, lex, wb, wk, par;  // par: the label's parent entry
+    uint32_t sb, sk, su, fl;  // a Scroll-of-Escape-region label: its walk (b, k) and the cell (rank) it ends at;
+                              // fl: kCertF* flags of the entry
+    uint32_t v;               // the entry's cell (entries >= 1)
+    int32_t x, y;             // its position
+    uint32_t reg;             // its region's campfire (table index; kNone10: none)
 };
+// CertEntry::fl: the Center or a border-1 cell (never demoted: CentralMoves merge), a
+// caravan hub, the HQ, a caravan into it costs 5 a unit, the label is the start label
+constexpr uint32_t kCertFCentral = 1u, kCertFHub = 2u, kCertFHQ = 4u, kCertFCoef5 = 8u, kCertFStart = 16u;
 // a walk label (b, k) as comparator keys: c1..c3 in comparator order, length, rank of b
 struct CertLab {
     uint32_t c1, c2, c3, len, lex, b, k;
@@ -92,9 +99,16 @@ __device__ __forceinline__ void cert_load_table(const KArgs *__restrict__ a, uin
         const Rec r = a->cert_tab[(unsigned long long)slot * T + t];
         const bool walk = r.ntail() == 1 && (r.kp0 >> 29) == kStandard && t != 0;
         const bool soe = r.ntail() == 2 && (r.kp0 >> 29) == kStandard && t != 0;  // walk, then SoE from its end
+        const SpecialStatic ss = a->sp[t != 0 ? t : 1u];
+        const uint32_t fl = (t != 0 && (ss.flags & (kSpCenter | kSpBorder1)) ? kCertFCentral : 0u) |
+                            (t != 0 && (ss.flags & kSpHub) ? kCertFHub : 0u) |
+                            (t != 0 && t == a->p.hq_t ? kCertFHQ : 0u) | (t != 0 && ss.coef5 ? kCertFCoef5 : 0u) |
+                            ((r.kp0 >> 29) == kNoMove ? kCertFStart : 0u);
         E[t] = CertEntry{r.m[0], r.m[1], r.m[2], r.len(), a->cert_lex[(unsigned long long)slot * T + t],
-                         walk ? r.parent() : kCertNoB, walk ? (r.kp0 & 0x1FFFFFFFu) : 0u, 0u,
-                         soe ? r.parent() : kCertNoB, soe ? (r.kp0 & 0x1FFFFFFFu) : 0u, soe ? r.u : kNone32, 0u};
+                         walk ? r.parent() : kCertNoB, walk ? (r.kp0 & 0x1FFFFFFFu) : 0u, r.parent(),
+                         soe ? r.parent() : kCertNoB, soe ? (r.kp0 & 0x1FFFFFFFu) : 0u, soe ? r.u : kNone32, fl,
+                         t != 0 ? ss.v : kNone32, t != 0 ? ss.x : 0, t != 0 ? ss.y : 0,
+                         t != 0 ? ss.region : kNone10};
     }
 }
 
@@ -153,17 +167,61 @@ __device__ __forceinline__ void cert_best4_lds(const DevParams &p, const CertEnt
 
 // One launch over every slot's cells (blockIdx.y = slot): failing cells lower the slot's
 // key, count, and widen its box.
+//
+// Demoted specials.  A special whose hub label is a walk can be
+// wrong the way a plain cell's closed form is: a walk that its own boundary cannot
+// realise.  The first check (mark) then turns such a failing special (not the Center or a
+// border-1 cell, whose CentralMoves merge) into a plain cell: its word becomes its walk
+// (b, k), marked, and the sweep recomputes it from its neighbours like any other.  A
+// demoted special keeps its other in-edges, so the later check tests them too: no
+// caravan from a hub and no SHQ may reach it first, and a Scroll of Escape into it (a
+// region campfire) is tested against its new word.  The labels the hub built from a
+// demoted special (its caravans, SoE, CentralMoves) were built from its old label: a
+// special whose parent was demoted fails its pull test.
 __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict__ a, uint32_t mark) {
     __shared__ CertEntry E[64];
+    __shared__ uint32_t dem[64];  // entries whose cell holds a plain (demoted) word: that word, else kNone32
     const uint32_t slot = blockIdx.y;
     const uint32_t nslot = min(a->cert_cap, __hip_atomic_load(a->counter + kCtrCert, __ATOMIC_RELAXED,
                                                                __HIP_MEMORY_SCOPE_AGENT));
     if (slot >= nslot) return;
     const DevParams p = a->p;
     cert_load_table(a, slot, E);
-    __syncthreads();
-    const uint32_t S = p.S, pitch = a->rec_pitch;
+    const uint32_t S = p.S, pitch = a->rec_pitch, T = p.NS + 1;
     const CellWord *w = a->cert_rec + (unsigned long long)slot * S * pitch;
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < 64; t += kBS) {
+        uint32_t d = kNone32;
+        if (t >= 1 && t < T && !mark) {  // (the first check demotes; it sees none)
+            const uint32_t vv = E[t].v, yy = vv / S;
+            const uint32_t raw = cert_clean(w[(size_t)yy * pitch + (vv - yy * S)]);
+            if (raw != kViaSource && !(raw & kViaSpecial)) d = raw;
+        }
+        dem[t] = d;
+    }
+    __syncthreads();
+    // entry h's current label as raw metrics (legs, money, time), length, start label
+    auto cur = [&](uint32_t h, uint32_t &l, uint32_t &mo, uint32_t &ti, uint32_t &len, bool &start) {
+        if (dem[h] != kNone32) {
+            const uint32_t b = (dem[h] >> kStBShift) & kNone10, k = dem[h] & kStKMask;
+            l = E[b].m0 + k;
+            mo = E[b].m1;
+            ti = E[b].m2 + run_time_ff(k, p.ff_num, p.ff_den);
+            len = b == 0 ? 1u : E[b].len + 1u;
+            start = false;
+        } else {
+            l = E[h].m0;
+            mo = E[h].m1;
+            ti = E[h].m2;
+            len = E[h].len;
+            start = (E[h].fl & kCertFStart) != 0;
+        }
+    };
+    // (c1, c2, c3, length) of o strictly before those of the raw metrics (l, mo, ti), len
+    auto before = [&](const CertLab &o, uint32_t l, uint32_t mo, uint32_t ti, uint32_t len) {
+        const uint32_t e1 = pick(p, 0, l, mo, ti), e2 = pick(p, 1, l, mo, ti), e3 = pick(p, 2, l, mo, ti);
+        return o.c1 != e1 ? o.c1 < e1 : (o.c2 != e2 ? o.c2 < e2 : (o.c3 != e3 ? o.c3 < e3 : o.len < len));
+    };
     uint32_t key = 0xFFFFFFFFu, nf = 0, x0 = 0xFFFFFFFFu, x1 = 0, y0 = 0xFFFFFFFFu, y1 = 0;
     for (uint32_t v = blockIdx.x * kBS + threadIdx.x; v < p.V; v += gridDim.x * kBS) {
         const uint32_t y = v / S, x = v - y * S;
@@ -180,27 +238,94 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
                 const CertLab o = cert_walk(p, E, e.wb, e.wk);
                 own1 = o.c1;
                 fail = fail || !any || !cert_same(o, best);
+                // (the first check demotes it: its walk as a plain word, marked for the sweep)
+                if (fail && mark && !(e.fl & kCertFCentral))
+                    const_cast<CellWord *>(w)[(size_t)y * pitch + x] = ((e.wb << kStBShift) | e.wk) | kCertDirty;
             } else {  // built over the specials: no neighbour's walk may reach it first (a tie on
-                      // metrics and length would need the command lists: counted as a failure)
+                      // metrics and length would need the command lists: counted as a failure),
+                      // and its parent must still hold the label the hub built it from
                 const uint32_t o1 = pick(p, 0, e.m0, e.m1, e.m2), o2 = pick(p, 1, e.m0, e.m1, e.m2),
                                o3 = pick(p, 2, e.m0, e.m1, e.m2);
                 own1 = o1;
                 const bool below = o1 != best.c1 ? o1 < best.c1
                                                  : (o2 != best.c2 ? o2 < best.c2 : (o3 != best.c3 ? o3 < best.c3 : e.len < best.len));
-                fail = fail || (any && !below);
+                fail = fail || (any && !below) || (e.par < 64u && dem[e.par] != kNone32);
             }
         } else {  // a plain cell: exactly its neighbours' least extension
             const uint32_t b = (cw >> kStBShift) & kNone10, k = cw & kStKMask;
             const CertLab o = cert_walk(p, E, b, k);
             own1 = o.c1;
             fail = fail || !any || !cert_same(o, best);
+            // a demoted special: no caravan from a hub and no SHQ may reach it first (ties
+            // would need the command lists: counted as failures)
+            const uint32_t tv = (mark || p.NS == 0) ? kNone10 : (a->sinfo[v] & kNone10);
+            if (tv != kNone10 && tv < T) {
+                const CertEntry &et = E[tv];
+                if (p.use_caravans && (et.fl & kCertFHub)) {
+                    const uint32_t coef = (et.fl & kCertFCoef5) ? 5u : 2u;
+                    for (uint32_t i = 0; i < p.n_hubs; ++i) {
+                        const uint32_t h = a->hubs[i];
+                        if (h == tv || h >= T) continue;
+                        uint32_t l, mo, ti, len;
+                        bool start;
+                        cur(h, l, mo, ti, len, start);
+                        const uint32_t d = uint32_t(abs(E[h].x - et.x) + abs(E[h].y - et.y));
+                        if (start) {
+                            l = 0;
+                            mo = coef * d;
+                            ti = p.rgt * d;
+                            len = 1;
+                        } else {
+                            mo += coef * d;
+                            ti += p.rgt * d;
+                            len += 1;
+                        }
+                        if (!before(o, l, mo, ti, len)) fail = true;
+                    }
+                }
+                if ((et.fl & kCertFHQ) && !before(o, 0u, p.shq_cost, 0u, 1u)) fail = true;
+                // a Scroll of Escape into it from a special of its region, or from the source
+                if (p.use_soe) {
+                    for (uint32_t h = 1; h < T; ++h) {
+                        if (h == tv || E[h].reg != tv) continue;
+                        uint32_t l, mo, ti, len;
+                        bool start;
+                        cur(h, l, mo, ti, len, start);
+                        if (start) {
+                            l = 0;
+                            mo = p.soe_cost;
+                            ti = 0;
+                            len = 1;
+                        } else {
+                            mo += p.soe_cost;
+                            len += 1;
+                        }
+                        if (!before(o, l, mo, ti, len)) fail = true;
+                    }
+                    const uint32_t sv = a->cert_src[slot];
+                    if (((a->sinfo[sv] >> 10) & kNone10) == tv && !before(o, 0u, p.soe_cost, 0u, 1u)) fail = true;
+                }
+            }
             // Its Scroll of Escape into its region's campfire c (the repair sweep may have
             // changed the cell after the hub built c's label from the closed form): c's
             // SoE-region label must start from this cell's word when it names this cell
             // (pull), and no other cell's SoE may reach c first (push; a tie on metrics and
             // length would need the command lists: counted as a failure).
             const uint32_t rc = p.use_soe ? (a->sinfo[v] >> 10) & kNone10 : kNone10;
-            if (rc != kNone10) {
+            if (rc != kNone10 && rc < T && dem[rc] != kNone32) {
+                // the campfire was demoted: its label is its walk word's; the scroll from this
+                // cell must not reach it first (a tie: the lists would decide, a failure)
+                if (rc != (a->sinfo[v] & kNone10)) {
+                    const uint32_t wm0 = E[b].m0 + k, wm1 = E[b].m1 + p.soe_cost,
+                                   wm2 = E[b].m2 + run_time_ff(k, p.ff_num, p.ff_den);
+                    const uint32_t rb = (dem[rc] >> kStBShift) & kNone10, rk = dem[rc] & kStKMask;
+                    const CertLab cl = cert_walk(p, E, rb, rk);
+                    if (!before(cl, wm0, wm1, wm2, o.len + 1u)) {
+                        own1 = min(own1, min(cl.c1, pick(p, 0, wm0, wm1, wm2)));
+                        fail = true;
+                    }
+                }
+            } else if (rc != kNone10) {
                 const CertEntry &e = E[rc];
                 const CertLab &w = o;
                 // metrics of the walk, then + the scroll's money
