@@ -73,6 +73,7 @@ hipError_t launch_hub_group(const KArgs *d_args, const uint32_t perm[3], uint32_
 hipError_t launch_cert_select(const KArgs *d_args, hipStream_t stream);
 hipError_t launch_cert_check(const KArgs *d_args, uint32_t gx, uint32_t slots, uint32_t mark, hipStream_t stream);
 hipError_t launch_cert_sweep(const KArgs *d_args, uint32_t slots, hipStream_t stream);
+hipError_t launch_ovf_order(const KArgs *d_args, uint32_t nrec, OutCmd *tmp, hipStream_t stream);
 hipError_t decode_records_device(const OutResult *res, const OutCmd *slots, const OutCmd *ovf, uint32_t novf,
                                  const uint32_t *q_id, uint32_t nrec, uint32_t nq, uint32_t mc,
                                  const mr_cell_index *idx_rank, uint32_t V, uint32_t rgt, uint32_t soe, uint32_t shq,
@@ -1741,6 +1742,10 @@ struct mr_plan {
     uint32_t *d_lane_blob = nullptr;  // lane / group kernels: the plan's LDS block (lane_blob_build)
     uint32_t *d_relist = nullptr;     // lane kernel (Fleetfoot): uncertain sources for hub_kernel (KArgs::relist)
     OutCmd *d_ovf = nullptr;              // command-overflow pool (labels longer than max_cmds)
+    // outputs bound with an overflow buffer (a collective gathers them raw): each pass
+    // ends with ovf_order_kernel, which puts the pool in record order (d_ovf_tmp: its staging)
+    OutCmd *d_ovf_tmp = nullptr;
+    bool ovf_order = false;
     uint32_t hub_blocks = 0, fb_blocks = 0, spw = 1, cus = 256, fill_per_cu = 8;
     unsigned long long *d_dbg = nullptr;  // diagnostic builds: per-workgroup phase cycles
     uint32_t algo = kAlgoGeneric;
@@ -1848,7 +1853,7 @@ struct mr_plan {
                         (void *)d_args_lane, (void *)d_args_lane_last, (void *)d_relist,
                         (void *)d_tab,
                         (void *)d_lex, (void *)d_sstate, (void *)d_near_sp, (void *)d_rb_off, (void *)d_rb_cell, (void *)d_ovf,
-                        (void *)d_lane_blob})
+                        (void *)d_lane_blob, (void *)d_ovf_tmp})
             if (p) (void)pfree(p);
         if (ev_last && ev_last_orphan) (void)hipEventDestroy(ev_last);
         for (auto &e : timed) {
@@ -2786,6 +2791,8 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
     } else {
         e = launch_solve(pl->d_args, pl->grid_in_lds, pl->algo, pl->ka.p.NS, pl->ka.p.V, pl->blocks, s);
     }
+    // raw outputs for a collective: the overflow pool in record order (byte-deterministic)
+    if (e == hipSuccess && pl->ovf_order && !pl->all_mode) e = launch_ovf_order(pl->d_args, nrec_of(pl->hp), pl->d_ovf_tmp, s);
     (void)hipEventRecord(e1, s);
     // the pass's end event doubles as the plan's last event (plan_sync): a record of
     // its own cost ~6 us of command-processor time per pass
@@ -2876,8 +2883,15 @@ extern "C" int mr_plan_bind_outputs_ex(mr_plan *pl, void *d_results, void *d_com
     pl->ka.out_res = reinterpret_cast<OutResult *>(d_results);
     pl->ka.out_cmd = reinterpret_cast<OutCmd *>(d_commands);
     if (d_overflow && overflow_cap) {  // overflow_cap 0 keeps the plan's own pool
+        // the pool in record order after every pass (ovf_order_kernel): its staging buffer
+        pfree(pl->d_ovf_tmp);
+        pl->d_ovf_tmp = nullptr;
+        pl->ovf_order = false;
+        if (pmalloc(reinterpret_cast<void **>(&pl->d_ovf_tmp), size_t(overflow_cap) * sizeof(OutCmd)) != hipSuccess)
+            return fail(MR_ERR_DEVICE, "bind_outputs: overflow staging");
         pl->ka.ovf = reinterpret_cast<OutCmd *>(d_overflow);
         pl->ka.ovf_cap = overflow_cap;
+        pl->ovf_order = true;
     }
     if (upload_args(pl) != MR_OK) return fail(MR_ERR_DEVICE, "kernel args");
     return MR_OK;

@@ -129,4 +129,70 @@ hipError_t decode_records_device(const OutResult *res, const OutCmd *slots, cons
     return e;
 }
 
+// ---- byte-deterministic overflow pool -----------------------------------
+// A pass hands out overflow-pool offsets by atomicAdd, in arrival order, so the raw
+// records and the pool differ from run to run in those offsets (the decoded labels do
+// not).  For a plan whose raw outputs a collective gathers (mr_plan_bind_outputs_ex with
+// an overflow buffer) this one-workgroup kernel runs after the pass: it renumbers the
+// offsets as the exclusive prefix sum of the overflowing records' command counts in
+// record order, moves each record's commands there through tmp, and publishes the pool's
+// new length.  A pass that overflowed nothing costs one load.  (When the pool ran out, the
+// records that got no room depend on arrival order: MR_ERR_CAPACITY, not made
+// deterministic.)
+constexpr uint32_t kOrdBS = 1024;
+
+// record k's overflow segment {from, len} (false: not an overflow record, or a malformed tag)
+__device__ __forceinline__ bool ovf_segment(const KArgs *__restrict__ a, uint32_t k, uint32_t nov, uint32_t &from,
+                                            uint32_t &len) {
+    const OutResult o = a->out_res[k];
+    if (int(o.ncmd_status >> 16) - 16 != int(kStatusOverflow)) return false;
+    const OutCmd tag = a->out_cmd[(unsigned long long)k * a->p.max_cmds];
+    len = o.ncmd_status & 0xFFFFu;
+    from = tag.from;
+    return tag.kp == kOvfTag && tag.to == len && (unsigned long long)from + len <= nov;
+}
+
+__global__ __launch_bounds__(kOrdBS) void ovf_order_kernel(const KArgs *__restrict__ a, uint32_t nrec,
+                                                           OutCmd *__restrict__ tmp) {
+    __shared__ uint32_t part[kOrdBS];
+    uint32_t *c = a->counter;
+    const uint32_t nov = min(c[kCtrLastOvf], a->ovf_cap);
+    if (nov == 0 || a->p.max_cmds == 0) return;
+    const uint32_t t = threadIdx.x;
+    const uint32_t lo = uint32_t((unsigned long long)nrec * t / kOrdBS),
+                   hi = uint32_t((unsigned long long)nrec * (t + 1) / kOrdBS);
+    uint32_t sum = 0;
+    for (uint32_t k = lo; k < hi; ++k) {
+        uint32_t f, l;
+        if (ovf_segment(a, k, nov, f, l)) sum += l;
+    }
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < kOrdBS; d <<= 1) {  // inclusive scan of the threads' sums
+        const uint32_t v = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    const uint32_t total = part[kOrdBS - 1];
+    uint32_t off = part[t] - sum;
+    OutCmd *ovf = a->ovf;
+    for (uint32_t k = lo; k < hi; ++k) {  // (each thread rewrites only its own records' tags)
+        uint32_t f, l;
+        if (!ovf_segment(a, k, nov, f, l)) continue;
+        for (uint32_t j = 0; j < l; ++j) tmp[off + j] = ovf[f + j];
+        a->out_cmd[(unsigned long long)k * a->p.max_cmds].from = off;
+        off += l;
+    }
+    __threadfence();
+    __syncthreads();
+    for (uint32_t i = t; i < total; i += kOrdBS) ovf[i] = tmp[i];
+    if (t == 0) c[kCtrLastOvf] = total;
+}
+
+hipError_t launch_ovf_order(const KArgs *d_args, uint32_t nrec, OutCmd *tmp, hipStream_t stream) {
+    hipLaunchKernelGGL(ovf_order_kernel, dim3(1), dim3(kOrdBS), 0, stream, d_args, nrec, tmp);
+    return hipGetLastError();
+}
+
 }  // namespace mr

@@ -494,6 +494,51 @@ def test_overflow_pool(eng, oracle_lib, grid_state, max_cmds):
         assert any(len(e[3]) > max_cmds for e in exp)
 
 
+def test_overflow_pool_bound_in_record_order(eng, oracle_lib, grid_state):
+    """Outputs bound to one caller buffer with an overflow pool (what the N > 1 gather
+    moves raw, mr_plan_bind_outputs_ex): every pass leaves the pool in record order
+    (ovf_order_kernel). Each overflowing record's tag points at the prefix sum of
+    the command counts of the overflowing records before it. So the raw bytes are the
+    same from pass to pass and from plan to plan, and they decode to the oracle's labels."""
+    import numpy as np
+    import torch
+    m = SyntheticMap(25, campfires_per_homeland=6, seed=9, clustered=True)
+    g = eng.MapGrid(m.cells())
+    og = oracle_lib.OracleGrid(m.cells())
+    mc = 2
+    for params in (Params(), Params(sort_by=(SORT_TIME, SORT_MONEY))):
+        qs = random_queries(m, 300, 17)
+        exp = [as_expected(e) for e in og.find_path_batch(params, qs, threads=0)]
+        n, rw, cw, ovf_cap = len(qs), 4, 4 * mc, 8 * len(qs)
+        snaps = []
+        for _plan in range(2):
+            plan = eng.Plan(g, params, qs, max_cmds=mc)
+            buf = torch.zeros(n * (rw + cw) + ovf_cap * 4, dtype=torch.int32, device="cuda")
+            p0 = buf.data_ptr()
+            plan.bind_outputs(p0, p0 + n * rw * 4, p0 + n * (rw + cw) * 4, ovf_cap)
+            for _pass in range(2):
+                plan.run()
+                plan.wait()
+                snaps.append(buf.cpu().numpy().view(np.uint32).copy())
+            words = snaps[-1]
+            res = words[: n * rw].reshape(n, rw)
+            slots = words[n * rw: n * (rw + cw)].reshape(n, mc, 4)
+            st, ln = res[:, 3] >> 16, res[:, 3] & 0xFFFF
+            ov = st == 80
+            assert ov.sum() > n // 4
+            offs = np.concatenate([[0], np.cumsum(ln[ov])[:-1]]).astype(np.uint32)
+            assert (slots[ov, 0, 0] == 0xFFFFFFFF).all() and (slots[ov, 0, 2] == ln[ov]).all()
+            assert (slots[ov, 0, 1] == offs).all(), "overflow offsets not in record order"
+            labels = eng.decode_records(g, params, res, slots, n, mc, words[n * (rw + cw):])
+            q_of = plan.record_queries()
+            got = [None] * n
+            for k in range(n):
+                got[q_of[k]] = as_expected(labels[k])
+            assert got == exp
+            assert [as_expected(r) for r in plan.fetch()] == exp
+        assert all((s == snaps[0]).all() for s in snaps), "raw outputs differ between passes / plans"
+
+
 @pytest.mark.parametrize("kernel", ["hub", "lane", "group8", "group32"])
 @pytest.mark.parametrize("ff", [1, 2, 3])
 @pytest.mark.parametrize("sort_by", [(SORT_LEGS, SORT_MONEY), (SORT_LEGS, SORT_TIME), (SORT_MONEY, SORT_LEGS),
