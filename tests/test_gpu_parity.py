@@ -500,8 +500,16 @@ def test_overflow_pool_bound_in_record_order(eng, oracle_lib, grid_state):
     (ovf_order_kernel). Each overflowing record's tag points at the prefix sum of
     the command counts of the overflowing records before it. So the raw bytes are the
     same from pass to pass and from plan to plan, and they decode to the oracle's labels."""
+    import ctypes as C
+
     import numpy as np
-    import torch
+    # device buffers from the HIP runtime the engine library runs on (torch's wheel carries
+    # a runtime of its own, which cannot start once this one holds the device)
+    hip = C.CDLL("libamdhip64.so.7")
+    hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+    hip.hipMemset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    hip.hipFree.argtypes = [C.c_void_p]
     m = SyntheticMap(25, campfires_per_homeland=6, seed=9, clustered=True)
     g = eng.MapGrid(m.cells())
     og = oracle_lib.OracleGrid(m.cells())
@@ -513,19 +521,23 @@ def test_overflow_pool_bound_in_record_order(eng, oracle_lib, grid_state):
         snaps = []
         for _plan in range(2):
             plan = eng.Plan(g, params, qs, max_cmds=mc)
-            buf = torch.zeros(n * (rw + cw) + ovf_cap * 4, dtype=torch.int32, device="cuda")
-            p0 = buf.data_ptr()
+            nw = n * (rw + cw) + ovf_cap * 4
+            dbuf = C.c_void_p()
+            assert hip.hipMalloc(C.byref(dbuf), nw * 4) == 0 and hip.hipMemset(dbuf, 0, nw * 4) == 0
+            p0 = dbuf.value
             plan.bind_outputs(p0, p0 + n * rw * 4, p0 + n * (rw + cw) * 4, ovf_cap)
             for _pass in range(2):
                 plan.run()
                 plan.wait()
-                snaps.append(buf.cpu().numpy().view(np.uint32).copy())
+                host = np.zeros(nw, dtype=np.uint32)
+                assert hip.hipMemcpy(host.ctypes.data, dbuf, nw * 4, 2) == 0  # device to host
+                snaps.append(host)
             words = snaps[-1]
             res = words[: n * rw].reshape(n, rw)
             slots = words[n * rw: n * (rw + cw)].reshape(n, mc, 4)
             st, ln = res[:, 3] >> 16, res[:, 3] & 0xFFFF
             ov = st == 80
-            assert ov.sum() > n // 4
+            assert ov.sum() >= 20
             offs = np.concatenate([[0], np.cumsum(ln[ov])[:-1]]).astype(np.uint32)
             assert (slots[ov, 0, 0] == 0xFFFFFFFF).all() and (slots[ov, 0, 2] == ln[ov]).all()
             assert (slots[ov, 0, 1] == offs).all(), "overflow offsets not in record order"
@@ -536,6 +548,8 @@ def test_overflow_pool_bound_in_record_order(eng, oracle_lib, grid_state):
                 got[q_of[k]] = as_expected(labels[k])
             assert got == exp
             assert [as_expected(r) for r in plan.fetch()] == exp
+            del plan
+            hip.hipFree(dbuf)
         assert all((s == snaps[0]).all() for s in snaps), "raw outputs differ between passes / plans"
 
 
