@@ -173,6 +173,42 @@ __device__ __forceinline__ uint32_t ltm_take_idx(const LLab &c, LLab &d, uint32_
         : "vcc");
     return k;
 }
+// the same with the mask and no index (offer: the index word was a dummy kept in a register)
+__device__ __forceinline__ uint32_t ltm_take_m(const LLab &c, LLab &d) {
+    uint32_t t, k;
+    asm("v_sub_co_u32_sdwa %0, vcc, %6, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %7, %3, vcc\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %8, %4, vcc\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %9, %5, vcc\n\t"
+        "v_cndmask_b32_e64 %1, 0, -1, vcc\n\t"
+        "v_cndmask_b32_e32 %5, %5, %9, vcc\n\t"
+        "v_cndmask_b32_e32 %4, %4, %8, vcc\n\t"
+        "v_cndmask_b32_e32 %3, %3, %7, vcc\n\t"
+        "v_cndmask_b32_e32 %2, %2, %6, vcc"
+        : "=&v"(t), "=&v"(k), "+&v"(d.m), "+&v"(d.c3), "+&v"(d.c2), "+&v"(d.c1)
+        : "v"(c.m), "v"(c.c3), "v"(c.c2), "v"(c.c1)
+        : "vcc");
+    return k;
+}
+// c when c < d on (c1, c2, c3, length), else d, into new registers.  For the first two
+// candidates of an entry, whose words are shared across the unrolled entries (the settled
+// label's, the meta constants): ltm_take would first copy d (up to four v_mov an entry).
+__device__ __forceinline__ LLab ltm_min(const LLab &c, const LLab &d) {
+    uint32_t t;
+    LLab r;
+    asm("v_sub_co_u32_sdwa %0, vcc, %5, %9 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %6, %10, vcc\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %7, %11, vcc\n\t"
+        "v_subb_co_u32_e32 %0, vcc, %8, %12, vcc\n\t"
+        "v_cndmask_b32_e32 %1, %9, %5, vcc\n\t"
+        "v_cndmask_b32_e32 %2, %10, %6, vcc\n\t"
+        "v_cndmask_b32_e32 %3, %11, %7, vcc\n\t"
+        "v_cndmask_b32_e32 %4, %12, %8, vcc"
+        : "=&v"(t), "=&v"(r.m), "=&v"(r.c3), "=&v"(r.c2), "=&v"(r.c1)
+        : "v"(c.m), "v"(c.c3), "v"(c.c2), "v"(c.c1), "v"(d.m), "v"(d.c3), "v"(d.c2), "v"(d.c1)
+        : "vcc");
+    return r;
+}
 // the same without the mask (the scans: only the index is wanted)
 __device__ __forceinline__ void ltm_take_i(const LLab &c, LLab &d, uint32_t ci, uint32_t &i) {
     uint32_t t;
@@ -421,10 +457,10 @@ struct LaneHub {
         }
         f.c = f.w;
         f.any = f.won;
+        // (the first two candidates combine into new registers: ltm_min)
         if (t <= 5) {  // CentralMove: the Center (entry 1) <-> the border-1 cells (entries 2..5)
             const uint32_t on = bitm(z.cenm, t);
-            f.c = opt(on, z.cen);
-            if (t != 1) consider(f.c, f.w);
+            f.c = t != 1 ? ltm_min(f.w, opt(on, z.cen)) : opt(on, z.cen);
             f.any |= on;
         }
         // Which entries are hubs / region campfires is known from the table layout the
@@ -433,7 +469,7 @@ struct LaneHub {
         // instead cost ~80 VGPRs of split live ranges in the unrolled loop.)
         if (t == 1 || t >= 6) {  // caravans between hubs (src/pathfinder.rs:140-160, :251-273)
             const uint32_t on = bitm(z.car, t);
-            consider(f.c, opt(on, add(z.ls, 0, A.z, A.w, z.mCar)));
+            f.c = ltm_min(opt(on, add(z.ls, 0, A.z, A.w, z.mCar)), f.c);
             f.any |= on;
         }
         if (t >= 6 && t < 6 + kLaneRegs) {  // Scroll of Escape (src/pathfinder.rs:162-170)
@@ -456,8 +492,7 @@ struct LaneHub {
         const uint32_t lt = ltm(f.c, T);
         ll_sel(lt, T, f.c);
 #else
-        uint32_t dummy = 0;
-        const uint32_t lt = ltm_take_idx(f.c, T, 0u, dummy);
+        const uint32_t lt = ltm_take_m(f.c, T);
 #endif
         tent |= lt & bit;
         // blocker bit: a walk candidate with the (new) tentative metrics; the walk is >= the
