@@ -854,6 +854,16 @@ struct LaneHub {
         // (src/pathfinder.rs:162-178)
         const bool walks0 = have && src != p.vc;
         const LLab st0 = start();
+        // The source's region row (at most kLaneRegs regions on this kernel's layout,
+        // lane_layout_ok), loaded at once.  Read per entry below, each load sat in its own
+        // branch and was waited for: a row of dependent round trips to memory per source.
+        // (A lane without a source has s_idx of a real one: its row is readable.)
+        uint32_t rowx[kLaneRegs];
+        {
+            const uint32_t nr = min(nreg, kLaneRegs);
+#pragma unroll
+            for (uint32_t r = 0; r < kLaneRegs; ++r) rowx[r] = r < nr ? srow[r].x : kNone32;
+        }
 #pragma unroll
         for (uint32_t t = 1; t < TM; ++t) {
             const bool valid = have && t <= NS;
@@ -871,7 +881,12 @@ struct LaneHub {
             }
             {  // [SoE src -> t], or [Std{d} src -> u, SoE u -> t]
                 const bool reg = valid && p.use_soe && tS.rid != kNone10;
-                const uint32_t e = reg ? srow[reg ? tS.rid : 0u].x : kNone32;
+                // (tS is a static record: the same in every lane)
+                const uint32_t rid = __builtin_amdgcn_readfirstlane(tS.rid);
+                uint32_t ev = kNone32;
+#pragma unroll
+                for (uint32_t r = 0; r < kLaneRegs; ++r) ev = rid == r ? rowx[r] : ev;
+                const uint32_t e = reg ? ev : kNone32;
                 const bool on = walks0 && reg && e != kNone32;
                 const uint32_t d = on ? e : 0u;
                 const uint32_t om = vmask(on);
