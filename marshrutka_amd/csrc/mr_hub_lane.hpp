@@ -69,6 +69,21 @@ __host__ __device__ constexpr uint32_t lane_waves(uint32_t TM) { return TM <= 22
 #ifndef MR_LANE_PF
 #define MR_LANE_PF 1
 #endif
+// relaxations of entries with no candidate in any lane of the wave skipped (1) or run as
+// no-ops (0)
+#ifndef MR_LANE_SKIP
+#define MR_LANE_SKIP 1
+#endif
+// OR of v over the wave (uniform): four DPP rounds within each row of 16 lanes, then the
+// four rows' words by readlane
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x140, 0xF, 0xF, false));  // row_mirror
+    return uint32_t(__builtin_amdgcn_readlane(int(v), 0) | __builtin_amdgcn_readlane(int(v), 16) |
+                    __builtin_amdgcn_readlane(int(v), 32) | __builtin_amdgcn_readlane(int(v), 48));
+}
 // meta: length (8 b) | kind of the first tail command (3 b) << 8 | parent entry (5 b)
 // << 11 | (tail count - 1) << 16 | CentralMove count (2 b) << 17
 __device__ __forceinline__ uint32_t lm_len(uint32_t m) { return m & 0xFFu; }
@@ -973,6 +988,11 @@ struct LaneHub {
             if (s != 0) M[s * mstride + mcolumn] = z.ls.m;  // (the settled meta, for the chains)
             // no candidate out of any lane's settle (the last settles): nothing to relax
             if (!__any((z.walk | z.cenm | z.car | z.soe | z.reg) != 0)) continue;
+#if MR_LANE_SKIP
+            // the entries some lane of the wave has a candidate into (a wave-uniform mask):
+            // the others' relaxations are no-ops in every lane and are skipped
+            const uint32_t live_w = wave_or_u32(z.walk | z.cenm | z.car | z.soe | z.reg);
+#endif
             const uint4 *rowa = PA + z.s * TM;
             const uint2 *rowb = PB + z.s * TM;
             // Each step also stores into the per-wave LDS copy MC the meta of this
@@ -998,6 +1018,9 @@ struct LaneHub {
                     pa[(ahead - 1) % R] = rowa[ahead];
                     if (ahead >= 6 && ahead < 6 + kLaneRegs) pb[(ahead - 1) % R] = rowb[ahead];
                 }
+#if MR_LANE_SKIP
+                if (!((live_w >> t) & 1u)) continue;
+#endif
                 const uint2 B = (t >= 6 && t < 6 + kLaneRegs) ? pb[(t - 1) % R] : make_uint2(0, 0);
                 const FromS f = from_s(z, t, pa[(t - 1) % R], B);
                 offer(t, f, ties);
