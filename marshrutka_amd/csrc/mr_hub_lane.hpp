@@ -928,6 +928,9 @@ struct LaneHub {
         for (uint32_t it = 0; it < NS; ++it) {
             const uint32_t cand = tent & ~done;
             if (!__any(cand != 0)) break;
+#if MR_LANE_SKIP
+            const uint32_t cand_w = wave_or_u32(cand);  // (entries no lane can settle: skipped)
+#endif
             // the settle candidate: least (c1, c2, c3, length), two interleaved chains
             // (odd and even entries) for the latency, then merged; ta / tb: the chain's
             // best has an exact tie (MR_LANE_SETTLE_TIES only)
@@ -935,6 +938,9 @@ struct LaneHub {
             uint32_t sa = 0, sb = 0, ta = 0, tb = 0;
 #pragma unroll
             for (uint32_t t = 1; t < TM; ++t) {
+#if MR_LANE_SKIP
+                if (!((cand_w >> t) & 1u)) continue;
+#endif
                 LLab &lx = (t & 1u) ? la : lb;
                 uint32_t &sx_ = (t & 1u) ? sa : sb;
                 uint32_t &tx = (t & 1u) ? ta : tb;
