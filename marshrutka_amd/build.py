@@ -16,7 +16,7 @@ SOURCES = ["mr_k_region.hip", "mr_k_groupq.hip", "mr_k_group.hip", "mr_k_group_n
            "mr_k_hub.hip", "mr_k_wide.hip",
            "mr_k_solve.hip", "mr_k_fill.hip", "mr_k_cert.hip", "mr_k_decode.hip",
            "mr_host.cpp", "mr_html.cpp", "mr_render.cpp"]
-HEADERS = ["mr_engine.hpp", "mr_pool.hpp", "mr_device.hpp", "mr_hub_lane.hpp", "mr_hub_group.hpp", "mr_cert.hpp", os.path.join("..", "..", "include", "marshrutka_pf.h")]
+HEADERS = ["mr_engine.hpp", "mr_pool.hpp", "mr_device.hpp", "mr_hub_lane.hpp", "mr_hub_group.hpp", "mr_cert.hpp", "mr_cert_tile.hpp", os.path.join("..", "..", "include", "marshrutka_pf.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall",
          "-Wno-unused-result", "-munsafe-fp-atomics"]

@@ -223,6 +223,9 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
         return o.c1 != e1 ? o.c1 < e1 : (o.c2 != e2 ? o.c2 < e2 : (o.c3 != e3 ? o.c3 < e3 : o.len < len));
     };
     uint32_t key = 0xFFFFFFFFu, nf = 0, x0 = 0xFFFFFFFFu, x1 = 0, y0 = 0xFFFFFFFFu, y1 = 0;
+    __shared__ uint32_t dem_bits[2];  // entries this workgroup demotes (mark: the first check)
+    if (threadIdx.x < 2) dem_bits[threadIdx.x] = 0;
+    __syncthreads();
     for (uint32_t v = blockIdx.x * kBS + threadIdx.x; v < p.V; v += gridDim.x * kBS) {
         const uint32_t y = v / S, x = v - y * S;
         const uint32_t cw = cert_clean(w[(size_t)y * pitch + x]);
@@ -238,9 +241,10 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
                 const CertLab o = cert_walk(p, E, e.wb, e.wk);
                 own1 = o.c1;
                 fail = fail || !any || !cert_same(o, best);
-                // (the first check demotes it: its walk as a plain word, marked for the sweep)
-                if (fail && mark && !(e.fl & kCertFCentral))
-                    const_cast<CellWord *>(w)[(size_t)y * pitch + x] = ((e.wb << kStBShift) | e.wk) | kCertDirty;
+                // (the first check demotes it: cert_window_kernel writes its walk as a plain
+                // word before the sweep; recorded here, so this check's readers all see the
+                // special's word)
+                if (fail && mark && !(e.fl & kCertFCentral)) atomicOr(&dem_bits[t >> 5], 1u << (t & 31u));
             } else {  // built over the specials: no neighbour's walk may reach it first (a tie on
                       // metrics and length would need the command lists: counted as a failure),
                       // and its parent must still hold the label the hub built it from
@@ -372,6 +376,7 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
     if (threadIdx.x < kCertSt) red[threadIdx.x] = (threadIdx.x == kCertKey || threadIdx.x == kCertX0 ||
                                                    threadIdx.x == kCertY0) ? 0xFFFFFFFFu : 0u;
     __syncthreads();
+    if (threadIdx.x < 2) red[kCertDem0 + threadIdx.x] = dem_bits[threadIdx.x];
     if (__any(nf != 0)) {
         key = wave_min_u32(key);
         x0 = wave_min_u32(x0);
@@ -490,6 +495,8 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
     const uint32_t nslot = min(a->cert_cap, __hip_atomic_load(a->counter + kCtrCert, __ATOMIC_RELAXED,
                                                                __HIP_MEMORY_SCOPE_AGENT));
     if (slot >= nslot) return;
+    // (cert_window_kernel gave this slot to the tile sweep, or to nobody)
+    if (a->cert_win && a->cert_win[(unsigned long long)slot * kWinWords + kWinMode] != kWinOld) return;
     // the check's state: the least / greatest over its workgroups' partials
     __shared__ uint32_t st[kCertSt];
     if (tid < kCertSt) st[tid] = (tid == kCertKey || tid == kCertX0 || tid == kCertY0) ? 0xFFFFFFFFu : 0u;

@@ -214,6 +214,12 @@ struct KArgs {
     // lane and group kernels: the plan's LDS block (lane_blob_bytes, mr_hub_lane.hpp), built
     // once on the host (lane_blob_build) and copied by every workgroup
     const uint4 *lane_blob;
+    // the certificate's repair (mr_cert_tile.hpp): per slot kWinWords window words
+    // (cert_window_kernel), and the tile sweep's publish areas, two kTileT x kTileT keys
+    // per workgroup of its launch (cert_pub_wgs of them)
+    uint32_t *cert_win;
+    unsigned long long *cert_pub;
+    uint32_t cert_pub_wgs;
 };
 // fb_cert[i] of a staged entry before cert_select_kernel gives it a slot (or none)
 constexpr uint32_t kFbStaged = 0xFFFFFFFEu;
@@ -243,8 +249,42 @@ enum : uint32_t {
 };
 // per certificate slot and check workgroup: the least leading metric of a failing cell
 // (labels below the least over the workgroups are exact), failing cells, their bounding
-// box (grid coordinates)
-enum : uint32_t { kCertKey = 0, kCertFails = 1, kCertX0 = 2, kCertX1 = 3, kCertY0 = 4, kCertY1 = 5, kCertSt = 8 };
+// box (grid coordinates), and the walk-labelled specials it demoted to plain cells (a
+// bit per table entry; applied by cert_window_kernel, so every reader of one check sees
+// the same words)
+enum : uint32_t {
+    kCertKey = 0, kCertFails = 1, kCertX0 = 2, kCertX1 = 3, kCertY0 = 4, kCertY1 = 5, kCertDem0 = 6, kCertDem1 = 7,
+    kCertSt = 8
+};
+// the certificate's tile sweep (mr_cert_tile.hpp)
+constexpr uint32_t kTileT = 64;        // a team tile's side
+constexpr uint32_t kTileH = 24;        // halo width = steps between exchanges
+constexpr uint32_t kTileP = 128;       // LDS row pitch of a region (>= kTileT + 2 kTileH; a power of two)
+constexpr uint32_t kTileR = 112;       // LDS rows of a region (>= kTileT + 2 kTileH)
+constexpr uint32_t kTileN = kTileP * kTileR;
+constexpr uint32_t kTileBS = 512;      // threads of a tile workgroup
+constexpr uint32_t kTileList = 2048;   // entries of a bucket list (more: that step scans densely)
+constexpr uint32_t kTileEv = 1024;     // fixed cells bordering window cells, per region
+constexpr uint32_t kTileFD = 4096;     // run-time increments tabulated (longer runs divide)
+constexpr uint32_t kTileMaxSteps = 8192;
+constexpr uint32_t kTileMaxTiles = 256;  // tiles of one window (its team)
+constexpr unsigned long long kTileHi = 1ull << 63, kTileNoExt = ~kTileHi;  // (fixed, nothing to push)
+constexpr uint32_t kTileGMax = 1u << 22;  // G - B0 at or past this: far beyond any step (no push)
+constexpr uint32_t kTileDone = 0xFFFFFFFFu;  // a tile's flag once its cells are final
+
+// per slot window words (cert_window_kernel writes them, the sweeps read them)
+enum : uint32_t {
+    kWinMode = 0,  // kWinNone / kWinTile / kWinOld / kWinWide
+    kWinX0 = 1, kWinY0 = 2, kWinX1 = 3, kWinY1 = 4,
+    kWinNtx = 5, kWinNty = 6, kWinB0 = 7,
+    kWinFail = 8,   // the tile sweep gave up (step cap, a spin timeout, an LDS table too small)
+    kWinSteps = 10, // steps of the slot's last tile to finish
+    kWinTStep = 11, kWinTXchg = 12, kWinNXchg = 13,  // tile 0: time in steps / exchanges (10 ns), exchanges
+    kWinFlag = 16,  // per tile: exchanges published (kTileDone: final)
+    kWinStat = 16 + kTileMaxTiles,  // per tile 4 words: time in steps / exchanges (10 ns), settles, steps
+    kWinWords = 16 + 5 * kTileMaxTiles
+};
+enum : uint32_t { kWinNone = 0, kWinTile = 1, kWinOld = 2, kWinWide = 3 };
 // result status (OutResult high half - 16) of a label whose commands went to the
 // overflow pool: its first command slot holds {kOvfTag, offset, count}
 constexpr uint32_t kStatusOverflow = 64u, kOvfTag = 0xFFFFFFFFu;

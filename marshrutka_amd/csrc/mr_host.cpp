@@ -53,8 +53,9 @@ hipError_t launch_hub_lane(const KArgs *d_args, const uint32_t perm[3], uint32_t
 uint32_t hub_group_slots(uint32_t NS, uint32_t G);
 uint32_t lane_blob_build(const SpecialStatic *sp, uint32_t NS, uint32_t nreg, uint32_t TM, uint32_t rgt,
                          uint32_t ff_num, uint32_t ff_den, const uint32_t *near_sp, std::vector<uint32_t> &blob);
+uint64_t region_table_seg_words(uint32_t S, uint32_t nreg);
 hipError_t region_table_build(const uint16_t *reg, const uint32_t *rank, uint32_t S, uint32_t nreg, void *tab,
-                              void *axis, hipStream_t stream);
+                              void *axis, void *seg, hipStream_t stream);
 struct GroupGeom {
     long long vc, ux[4], uy[4], ub[4];
     uint32_t H, V;
@@ -73,6 +74,9 @@ hipError_t launch_hub_group(const KArgs *d_args, const uint32_t perm[3], uint32_
 hipError_t launch_cert_select(const KArgs *d_args, hipStream_t stream);
 hipError_t launch_cert_check(const KArgs *d_args, uint32_t gx, uint32_t slots, uint32_t mark, hipStream_t stream);
 hipError_t launch_cert_sweep(const KArgs *d_args, uint32_t slots, hipStream_t stream);
+hipError_t launch_cert_window(const KArgs *d_args, uint32_t slots, hipStream_t stream);
+hipError_t launch_cert_tile(const KArgs *d_args, uint32_t wgs, hipStream_t stream);
+int cert_tile_occupancy();
 hipError_t launch_ovf_order(const KArgs *d_args, uint32_t nrec, OutCmd *tmp, hipStream_t stream);
 hipError_t decode_records_device(const OutResult *res, const OutCmd *slots, const OutCmd *ovf, uint32_t novf,
                                  const uint32_t *q_id, uint32_t nrec, uint32_t nq, uint32_t mc,
@@ -194,9 +198,10 @@ struct mr_grid {
     // wide hub solver without the region table: a special cell's row of {distance, rank}
     // per region, scanned from the boundary cells once per (homeland, cell)
     mutable std::unordered_map<uint32_t, std::vector<uint32_t>> near_sp_cache[4];
-    // device copies of the region tables, uploaded on first use and shared by the
-    // grid's plans (the grid outlives its plans)
-    mutable uint32_t *d_near[4] = {nullptr, nullptr, nullptr, nullptr};
+    // device copies of the region tables, built on first use and shared by the grid's
+    // plans (the grid outlives its plans): one per (device, homeland), so a plan never
+    // reads a table that lives on another device
+    mutable std::map<std::pair<int, int>, uint32_t *> d_near;
     // device copies shared by the grid's plans on one device (the first plan's): the rank
     // tables, and per (query homeland, HQ cell) the special / region word of every cell
     // (sinfo: it depends on the special order, fixed by those two)
@@ -211,8 +216,8 @@ struct mr_grid {
     mutable mr_cell_index *d_idx_rank = nullptr;  // device fetch: the CellIndex of every rank
     ~mr_grid() {
         if (d_idx_rank) (void)hipFree(d_idx_rank);
-        for (uint32_t *p : d_near)
-            if (p) (void)hipFree(p);
+        for (auto &kv : d_near)
+            if (kv.second) (void)hipFree(kv.second);
         for (uint32_t *p : {d_rank, d_rank_inv})
             if (p) (void)hipFree(p);
         for (const SinfoDev &e : d_sinfo) {
@@ -651,14 +656,18 @@ static const std::vector<uint32_t> &region_list(const mr_grid *g, int h) {
     return g->regions[h];
 }
 
-// The region table of homeland h on the current device, built there once per grid
-// (mr_k_region.hip: a separable L1 transform of (distance, rank) in three passes) from
-// the region of every cell (the nearest campfire, computed at grid creation) and the
-// device rank table.  The grid's plans share it; nullptr on a device error.
+// The region table of homeland h on the current device, built there once per grid and
+// device (mr_k_region.hip: a separable L1 transform of (distance, rank) in three passes)
+// from the region of every cell (the nearest campfire, computed at grid creation) and
+// the device rank table d_rank (which must live on the current device).  The grid's
+// plans on that device share it; nullptr on a device error.
 static const uint32_t *region_table_device(const mr_grid *g, int h, const uint32_t *d_rank) {
     const std::vector<uint32_t> &regs = region_list(g, h);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> lk(g->near_mu);
-    if (g->d_near[h]) return g->d_near[h];
+    auto it = g->d_near.find({dev, h});
+    if (it != g->d_near.end()) return it->second;
     const double t0 = now_ms();
     const uint32_t V = g->V, S = g->S, nreg = uint32_t(regs.size());
     std::unordered_map<uint32_t, uint16_t> rid;
@@ -685,24 +694,29 @@ static const uint32_t *region_table_device(const mr_grid *g, int h, const uint32
     }
     uint32_t *d = nullptr;
     uint16_t *d_reg = nullptr;
-    void *d_axis = nullptr;
+    void *d_axis = nullptr, *d_seg = nullptr;
     hipStream_t st = nullptr;
+    // (MR_REGION_SERIAL=1: the serial kernels, A/B)
+    static const bool serial = std::getenv("MR_REGION_SERIAL") != nullptr;
+    const uint64_t segw = serial ? 0 : region_table_seg_words(S, nreg);
     bool ok = nreg > 0 && dev_malloc(reinterpret_cast<void **>(&d), size_t(V) * nreg * 8) == hipSuccess &&
               dev_malloc(reinterpret_cast<void **>(&d_reg), size_t(V) * 2) == hipSuccess &&
               dev_malloc(&d_axis, size_t(2) * S * nreg * 8) == hipSuccess &&
+              (!segw || dev_malloc(&d_seg, size_t(segw) * 8) == hipSuccess) &&
               hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
               hipMemcpyAsync(d_reg, reg.data(), size_t(V) * 2, hipMemcpyHostToDevice, st) == hipSuccess &&
-              region_table_build(d_reg, d_rank, S, nreg, d, d_axis, st) == hipSuccess &&
+              region_table_build(d_reg, d_rank, S, nreg, d, d_axis, d_seg, st) == hipSuccess &&
               hipStreamSynchronize(st) == hipSuccess;
     if (st) (void)hipStreamDestroy(st);
     if (d_reg) (void)hipFree(d_reg);
     if (d_axis) (void)hipFree(d_axis);
+    if (d_seg) (void)hipFree(d_seg);
     if (!ok) {
         (void)hipGetLastError();
         if (d) (void)hipFree(d);
         return nullptr;
     }
-    g->d_near[h] = d;
+    g->d_near[{dev, h}] = d;
     g->region_ms[h] = now_ms() - t0;
     return d;
 }
@@ -1801,8 +1815,10 @@ struct mr_plan {
     // certified fallback (query hub plans): per slot a label table,
     // boundary ranks, source, cell words, check state and sweep list; the fill's
     // argument block over the slots
-    uint32_t cert_cap = 0, cert_fill_gx = 1, cert_check_gx = 1;
+    uint32_t cert_cap = 0, cert_fill_gx = 1, cert_check_gx = 1, cert_tile_wgs = 0;
     Rec *d_cert_tab = nullptr;
+    uint32_t *d_cert_win = nullptr;               // per slot the repair window (cert_window_kernel)
+    unsigned long long *d_cert_pub = nullptr;     // the tile sweep's publish areas
     uint32_t *d_cert_lex = nullptr, *d_cert_src = nullptr, *d_cert_st = nullptr, *d_cert_aux = nullptr,
              *d_fb_cert = nullptr, *d_cert_ones = nullptr;
     CellWord *d_cert_rec = nullptr;
@@ -1844,7 +1860,7 @@ struct mr_plan {
         for (void *p : {(void *)d_cert_tab, (void *)d_cert_lex, (void *)d_cert_src, (void *)d_cert_st,
                         (void *)d_cert_aux, (void *)d_fb_cert, (void *)d_cert_ones, (void *)d_cert_rec,
                         (void *)d_args_cert, (void *)d_cert_stage_tab, (void *)d_cert_stage_lex,
-                        (void *)d_cert_stage_src})
+                        (void *)d_cert_stage_src, (void *)d_cert_win, (void *)d_cert_pub})
             if (p) (void)pfree(p);
         for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_rank_inv, (void *)d_src, (void *)d_qb, (void *)d_qd,
                         (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
@@ -2529,6 +2545,24 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
                 return bail(fail(MR_ERR_DEVICE, "certificate slots"));
             ka.cert_st = pl->d_cert_st;
             ka.cert_parts = pl->cert_check_gx;
+            // the repair: per slot its window; the tile sweep's persistent grid (one
+            // workgroup a CU, each with two publish areas).  MR_CERT_TILE=0: the round-5
+            // sweep for every slot (A/B)
+            static const bool no_tile = [] {
+                const char *e = std::getenv("MR_CERT_TILE");
+                return e && std::atoi(e) == 0;
+            }();
+            const int occ = no_tile ? 0 : cert_tile_occupancy();
+            pl->cert_tile_wgs = occ > 0 ? uint32_t(occ) * uint32_t(prop.multiProcessorCount) : 0u;
+            // (+ one word: cert_window_kernel's completion count, zero between launches)
+            if (pmalloc(reinterpret_cast<void **>(&pl->d_cert_win), (size_t(cap) * kWinWords + 1) * 4) != hipSuccess ||
+                hipMemset(pl->d_cert_win, 0, (size_t(cap) * kWinWords + 1) * 4) != hipSuccess ||
+                (pl->cert_tile_wgs && pmalloc(reinterpret_cast<void **>(&pl->d_cert_pub),
+                                              size_t(pl->cert_tile_wgs) * 2 * kTileT * kTileT * 8) != hipSuccess))
+                return bail(fail(MR_ERR_DEVICE, "certificate slots"));
+            ka.cert_win = pl->d_cert_win;
+            ka.cert_pub = pl->d_cert_pub;
+            ka.cert_pub_wgs = pl->cert_tile_wgs;
         }
         if (pl->n_lane && (pmalloc(reinterpret_cast<void **>(&pl->d_args_lane), sizeof(KArgs)) != hipSuccess ||
                            pmalloc(reinterpret_cast<void **>(&pl->d_args_lane_last), sizeof(KArgs)) != hipSuccess))
@@ -2782,6 +2816,10 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
             // the first check marks its failing cells: the sweep's seeds
             if (e == hipSuccess) e = launch_cert_check(pl->d_args, pl->cert_check_gx, pl->cert_cap, nosweep ? 0u : 1u, s);
             if (!nosweep) {
+                // the repair: each slot's window, the tile sweep (Legs / Time first), the
+                // round-5 sweep for the others
+                if (e == hipSuccess) e = launch_cert_window(pl->d_args, pl->cert_cap, s);
+                if (e == hipSuccess && pl->cert_tile_wgs) e = launch_cert_tile(pl->d_args, pl->cert_tile_wgs, s);
                 if (e == hipSuccess) e = launch_cert_sweep(pl->d_args, pl->cert_cap, s);
                 if (e == hipSuccess) e = launch_cert_check(pl->d_args, pl->cert_check_gx, pl->cert_cap, 0u, s);
             }
@@ -2956,9 +2994,25 @@ extern "C" int mr_plan_get_stats(mr_plan *pl, mr_plan_stats *out) {
                     y1 = std::max(y1, q[kCertY1]);
                 }
                 const uint32_t v = src[k] < pl->grid->V ? src[k] : 0;
-                std::fprintf(stderr, "MR_CERT_DEBUG slot %u src (%d,%d): fails %u key %u box x %d..%d y %d..%d\n", k,
-                             pl->grid->gx(v), pl->grid->gy(v), fails, key, int(x0) - int(pl->grid->H),
-                             int(x1) - int(pl->grid->H), int(y0) - int(pl->grid->H), int(y1) - int(pl->grid->H));
+                uint32_t wn[16] = {0};
+                if (pl->d_cert_win) (void)hipMemcpy(wn, pl->d_cert_win + size_t(k) * kWinWords, sizeof(wn), hipMemcpyDeviceToHost);
+                std::fprintf(stderr,
+                             "MR_CERT_DEBUG slot %u src (%d,%d): fails %u key %u box x %d..%d y %d..%d | repair mode %u "
+                             "tiles %ux%u steps %u fail %u | tile 0: steps %.1f us, %u exchanges %.1f us\n",
+                             k, pl->grid->gx(v), pl->grid->gy(v), fails, key, int(x0) - int(pl->grid->H),
+                             int(x1) - int(pl->grid->H), int(y0) - int(pl->grid->H), int(y1) - int(pl->grid->H), wn[kWinMode],
+                             wn[kWinNtx], wn[kWinNty], wn[kWinSteps], wn[kWinFail], wn[kWinTStep] * 0.01, wn[kWinNXchg],
+                             wn[kWinTXchg] * 0.01);
+                if (wn[kWinMode] == kWinTile) {  // the tiles' step / exchange times and settles
+                    const uint32_t nt = std::min(wn[kWinNtx] * wn[kWinNty], kTileMaxTiles);
+                    std::vector<uint32_t> ts(size_t(nt) * 4);
+                    if (hipMemcpy(ts.data(), pl->d_cert_win + size_t(k) * kWinWords + kWinStat, ts.size() * 4,
+                                  hipMemcpyDeviceToHost) == hipSuccess)
+                        for (uint32_t t = 0; t < nt; ++t)
+                            std::fprintf(stderr, "MR_CERT_DEBUG   tile %u: steps %u in %.1f us, exchanges %.1f us (publish %.1f, wait %.1f)\n", t,
+                                         ts[4 * t + 3], ts[4 * t] * 0.01, ts[4 * t + 1] * 0.01, (ts[4 * t + 2] >> 16) * 0.01,
+                                         (ts[4 * t + 2] & 0xFFFFu) * 0.01);
+                }
             }
     }
     out->solver = pl->hp.hub ? (pl->hp.wide ? MR_SOLVER_HUB_WIDE : MR_SOLVER_HUB)
