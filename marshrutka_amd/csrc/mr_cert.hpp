@@ -43,6 +43,7 @@ struct CertEntry {
 // CertEntry::fl: the Center or a border-1 cell (never demoted: CentralMoves merge), a
 // caravan hub, the HQ, a caravan into it costs 5 a unit, the label is the start label
 constexpr uint32_t kCertFCentral = 1u, kCertFHub = 2u, kCertFHQ = 4u, kCertFCoef5 = 8u, kCertFStart = 16u;
+constexpr uint32_t kCertFLastCentral = 32u;  // the label ends in a CentralMove (another one merges into it)
 // a walk label (b, k) as comparator keys: c1..c3 in comparator order, length, rank of b
 struct CertLab {
     uint32_t c1, c2, c3, len, lex, b, k;
@@ -103,7 +104,8 @@ __device__ __forceinline__ void cert_load_table(const KArgs *__restrict__ a, uin
         const uint32_t fl = (t != 0 && (ss.flags & (kSpCenter | kSpBorder1)) ? kCertFCentral : 0u) |
                             (t != 0 && (ss.flags & kSpHub) ? kCertFHub : 0u) |
                             (t != 0 && t == a->p.hq_t ? kCertFHQ : 0u) | (t != 0 && ss.coef5 ? kCertFCoef5 : 0u) |
-                            ((r.kp0 >> 29) == kNoMove ? kCertFStart : 0u);
+                            ((r.kp0 >> 29) == kNoMove ? kCertFStart : 0u) |
+                            (r.ntail() == 1 && (r.kp0 >> 29) == kCentral ? kCertFLastCentral : 0u);
         E[t] = CertEntry{r.m[0], r.m[1], r.m[2], r.len(), a->cert_lex[(unsigned long long)slot * T + t],
                          walk ? r.parent() : kCertNoB, walk ? (r.kp0 & 0x1FFFFFFFu) : 0u, r.parent(),
                          soe ? r.parent() : kCertNoB, soe ? (r.kp0 & 0x1FFFFFFFu) : 0u, soe ? r.u : kNone32, fl,
@@ -185,10 +187,32 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
     const uint32_t nslot = min(a->cert_cap, __hip_atomic_load(a->counter + kCtrCert, __ATOMIC_RELAXED,
                                                                __HIP_MEMORY_SCOPE_AGENT));
     if (slot >= nslot) return;
+    // (the second round: a done slot keeps its state; a slot that only sweeps again skips
+    // the check before the sweep)
+    if (a->cert_redo && (!a->cert_redo[slot] || (mark && a->cert_redo[slot] != kRedoFill))) return;
     const DevParams p = a->p;
     cert_load_table(a, slot, E);
     const uint32_t S = p.S, pitch = a->rec_pitch, T = p.NS + 1;
     const CellWord *w = a->cert_rec + (unsigned long long)slot * S * pitch;
+    uint32_t *win = a->cert_win ? a->cert_win + (unsigned long long)slot * kWinWords : nullptr;
+    // Entries promoted this pass (their label is now a caravan, cert_promote_kernel) and
+    // every entry built on them: the hub built those from the promoted entries' old labels,
+    // so they fail (a label resting on them has a lead metric no smaller: the key bounds it)
+    __shared__ unsigned long long taint;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long tm = win ? ((unsigned long long)win[kWinProm1] << 32) | win[kWinProm0] : 0ull;
+        for (uint32_t it = 0; tm && it < 64u; ++it) {
+            bool grew = false;
+            for (uint32_t e = 1; e < min(T, 64u); ++e)
+                if (!((tm >> e) & 1ull) && E[e].par < 64u && ((tm >> E[e].par) & 1ull)) {
+                    tm |= 1ull << e;
+                    grew = true;
+                }
+            if (!grew) break;
+        }
+        taint = tm;
+    }
     __syncthreads();
     for (uint32_t t = threadIdx.x; t < 64; t += kBS) {
         uint32_t d = kNone32;
@@ -233,6 +257,7 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
         CertLab best{};
         bool any;
         bool fail = !cert_best4<false>(p, E, w, pitch, int(x), int(y), best, any);
+        uint32_t why = fail ? 1u : 0u;  // (diagnostics: which tests failed, kWinWhy)
         uint32_t own1;
         if (cw & kViaSpecial) {
             const uint32_t t = cw & kNone10;
@@ -240,11 +265,16 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
             if (e.wb != kCertNoB) {  // a walk into a special: supported by a neighbour, beaten by none
                 const CertLab o = cert_walk(p, E, e.wb, e.wk);
                 own1 = o.c1;
-                fail = fail || !any || !cert_same(o, best);
+                why |= (!any || !cert_same(o, best)) ? 2u : 0u;
+                why |= (e.par < 64u && ((taint >> e.par) & 1ull)) ? 4u : 0u;
+                fail = fail || !any || !cert_same(o, best) || (e.par < 64u && ((taint >> e.par) & 1ull));
                 // (the first check demotes it: cert_window_kernel writes its walk as a plain
                 // word before the sweep; recorded here, so this check's readers all see the
                 // special's word)
-                if (fail && mark && !(e.fl & kCertFCentral)) atomicOr(&dem_bits[t >> 5], 1u << (t & 31u));
+                // (the last check records one that fails its walk test too: the second round
+                // demotes it then and sweeps again, from the repaired words)
+                // (a border-1 cell too: its CentralMove in-edge is tested with the others)
+                if (fail && (mark || (why & 2u))) atomicOr(&dem_bits[t >> 5], 1u << (t & 31u));
             } else {  // built over the specials: no neighbour's walk may reach it first (a tie on
                       // metrics and length would need the command lists: counted as a failure),
                       // and its parent must still hold the label the hub built it from
@@ -253,12 +283,15 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
                 own1 = o1;
                 const bool below = o1 != best.c1 ? o1 < best.c1
                                                  : (o2 != best.c2 ? o2 < best.c2 : (o3 != best.c3 ? o3 < best.c3 : e.len < best.len));
-                fail = fail || (any && !below) || (e.par < 64u && dem[e.par] != kNone32);
+                why |= (any && !below) ? 8u : 0u;
+                why |= (e.par < 64u && (dem[e.par] != kNone32 || ((taint >> e.par) & 1ull))) ? 16u : 0u;
+                fail = fail || (any && !below) || (e.par < 64u && (dem[e.par] != kNone32 || ((taint >> e.par) & 1ull)));
             }
         } else {  // a plain cell: exactly its neighbours' least extension
             const uint32_t b = (cw >> kStBShift) & kNone10, k = cw & kStKMask;
             const CertLab o = cert_walk(p, E, b, k);
             own1 = o.c1;
+            why |= (!any || !cert_same(o, best)) ? 32u : 0u;
             fail = fail || !any || !cert_same(o, best);
             // a demoted special: no caravan from a hub and no SHQ may reach it first (ties
             // would need the command lists: counted as failures)
@@ -267,6 +300,11 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
                 const CertEntry &et = E[tv];
                 if (p.use_caravans && (et.fl & kCertFHub)) {
                     const uint32_t coef = (et.fl & kCertFCoef5) ? 5u : 2u;
+                    // the least caravan from a hub whose own label is the hub's (a tie between
+                    // two such caravans would need the lists: no promotion)
+                    CertLab bc{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0, 0};
+                    uint32_t bh = kNone32;
+                    bool btie = false;
                     for (uint32_t i = 0; i < p.n_hubs; ++i) {
                         const uint32_t h = a->hubs[i];
                         if (h == tv || h >= T) continue;
@@ -284,10 +322,57 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
                             ti += p.rgt * d;
                             len += 1;
                         }
-                        if (!before(o, l, mo, ti, len)) fail = true;
+                        if (!before(o, l, mo, ti, len)) {
+                            fail = true;
+                            why |= 64u;
+                        }
+                        if (dem[h] != kNone32 || (h < 64u && ((taint >> h) & 1ull))) continue;
+                        const CertLab c{pick(p, 0, l, mo, ti), pick(p, 1, l, mo, ti), pick(p, 2, l, mo, ti), len, 0, 0, 0};
+                        const bool lt = c.c1 != bc.c1 ? c.c1 < bc.c1
+                                                      : (c.c2 != bc.c2 ? c.c2 < bc.c2 : (c.c3 != bc.c3 ? c.c3 < bc.c3 : c.len < bc.len));
+                        const bool eq = c.c1 == bc.c1 && c.c2 == bc.c2 && c.c3 == bc.c3 && c.len == bc.len;
+                        if (lt) {
+                            bc = c;
+                            bh = h;
+                            btie = false;
+                        } else if (eq) {
+                            btie = true;
+                        }
+                    }
+                    // the caravan strictly before the repaired walk (metrics, length): the
+                    // special's label is that caravan unless something else beats both —
+                    // cert_promote_kernel makes it so and the next round checks it all again
+                    // (not the HQ, not a Scroll-of-Escape target: their other in-edges are not
+                    // rebuilt there)
+                    const bool cb = bc.c1 != o.c1 ? bc.c1 < o.c1
+                                                  : (bc.c2 != o.c2 ? bc.c2 < o.c2 : (bc.c3 != o.c3 ? bc.c3 < o.c3 : bc.len < o.len));
+                    if (win && bh != kNone32 && !btie && cb && !(et.fl & kCertFHQ) && a->sp[tv].rid == kNone10 && tv < 64u)
+                        win[kWinPromo + tv] = bh + 1u;
+                }
+                // a demoted border-1 cell: the Center's label + a CentralMove (10 s; merged
+                // into a CentralMove the label ends in) must not reach it first
+                if ((a->sp[tv].flags & kSpBorder1) && T > 1u) {
+                    uint32_t l, mo, ti, len;
+                    bool start;
+                    cur(1, l, mo, ti, len, start);
+                    if (start) {
+                        l = 0;
+                        mo = 0;
+                        ti = 10;
+                        len = 1;
+                    } else {
+                        ti += 10;
+                        len += (E[1].fl & kCertFLastCentral) ? 0u : 1u;
+                    }
+                    if (!before(o, l, mo, ti, len)) {
+                        fail = true;
+                        why |= 4096u;
                     }
                 }
-                if ((et.fl & kCertFHQ) && !before(o, 0u, p.shq_cost, 0u, 1u)) fail = true;
+                if ((et.fl & kCertFHQ) && !before(o, 0u, p.shq_cost, 0u, 1u)) {
+                    fail = true;
+                    why |= 128u;
+                }
                 // a Scroll of Escape into it from a special of its region, or from the source
                 if (p.use_soe) {
                     for (uint32_t h = 1; h < T; ++h) {
@@ -304,10 +389,16 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
                             mo += p.soe_cost;
                             len += 1;
                         }
-                        if (!before(o, l, mo, ti, len)) fail = true;
+                        if (!before(o, l, mo, ti, len)) {
+                            fail = true;
+                            why |= 256u;
+                        }
                     }
                     const uint32_t sv = a->cert_src[slot];
-                    if (((a->sinfo[sv] >> 10) & kNone10) == tv && !before(o, 0u, p.soe_cost, 0u, 1u)) fail = true;
+                    if (((a->sinfo[sv] >> 10) & kNone10) == tv && !before(o, 0u, p.soe_cost, 0u, 1u)) {
+                        fail = true;
+                        why |= 512u;
+                    }
                 }
             }
             // Its Scroll of Escape into its region's campfire c (the repair sweep may have
@@ -327,6 +418,7 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
                     if (!before(cl, wm0, wm1, wm2, o.len + 1u)) {
                         own1 = min(own1, min(cl.c1, pick(p, 0, wm0, wm1, wm2)));
                         fail = true;
+                        why |= 1024u;
                     }
                 }
             } else if (rc != kNone10) {
@@ -356,7 +448,17 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
                 if (bad) {
                     own1 = min(own1, min(c1, x1));
                     fail = true;
+                    why |= 2048u;
                 }
+            }
+        }
+        if (fail && !mark && win) {  // (diagnostics: the first few failing cells of the last check)
+            const uint32_t at = atomicAdd(win + kWinWhy, 1u);
+            if (at < 7u) {
+                win[kWinWhy + 1 + 4 * at] = x | (y << 16);
+                win[kWinWhy + 2 + 4 * at] = why | ((cw & kViaSpecial) && cw != kViaSource ? 0x80000000u : 0u);
+                win[kWinWhy + 3 + 4 * at] = own1;
+                win[kWinWhy + 4 + 4 * at] = any ? best.c1 : 0xFFFFFFFFu;
             }
         }
         if (fail) {
@@ -440,6 +542,11 @@ __global__ __launch_bounds__(kSelectBS) void cert_select_kernel(const KArgs *__r
         if (t == 0) a->cert_src[slot] = a->cert_stage_src[i];
     }
     if (tid == 0) a->counter[kCtrCert] = min(nstaged, a->cert_cap);
+    if (a->cert_win)  // (a new pass: nothing promoted yet)
+        for (uint32_t s = tid; s < a->cert_cap; s += kSelectBS) {
+            a->cert_win[(unsigned long long)s * kWinWords + kWinProm0] = 0;
+            a->cert_win[(unsigned long long)s * kWinWords + kWinProm1] = 0;
+        }
 }
 
 #ifndef MR_SWEEP_BUCKETS
@@ -454,6 +561,7 @@ __global__ __launch_bounds__(kSelectBS) void cert_select_kernel(const KArgs *__r
 constexpr uint32_t kSweepBS = MR_SWEEP_BS;  // threads of the sweep's one workgroup per slot
 constexpr uint32_t kSweepBuckets = MR_SWEEP_BUCKETS;  // leading-metric buckets a window may span
 constexpr int kSweepMargin = 2;            // cells added round the failing cells' box
+constexpr int kSweepMarginAgain = 24;      // the same in a sweep-only second round
 #ifndef MR_SWEEP_RT
 #define MR_SWEEP_RT 4100
 #endif
@@ -497,6 +605,7 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
     if (slot >= nslot) return;
     // (cert_window_kernel gave this slot to the tile sweep, or to nobody)
     if (a->cert_win && a->cert_win[(unsigned long long)slot * kWinWords + kWinMode] != kWinOld) return;
+    if (a->cert_redo && !a->cert_redo[slot]) return;
     // the check's state: the least / greatest over its workgroups' partials
     __shared__ uint32_t st[kCertSt];
     if (tid < kCertSt) st[tid] = (tid == kCertKey || tid == kCertX0 || tid == kCertY0) ? 0xFFFFFFFFu : 0u;
@@ -521,8 +630,9 @@ __global__ __launch_bounds__(kSweepBS) void cert_sweep_kernel(const KArgs *__res
         red[1] = 0;
     }
     const int S = int(p.S), H = int(p.H);
-    const int bx0 = max(0, int(st[kCertX0]) - kSweepMargin), bx1 = min(S - 1, int(st[kCertX1]) + kSweepMargin);
-    const int by0 = max(0, int(st[kCertY0]) - kSweepMargin), by1 = min(S - 1, int(st[kCertY1]) + kSweepMargin);
+    const int mg = (a->cert_redo && a->cert_redo[slot] == kRedoSweep) ? kSweepMarginAgain : kSweepMargin;
+    const int bx0 = max(0, int(st[kCertX0]) - mg), bx1 = min(S - 1, int(st[kCertX1]) + mg);
+    const int by0 = max(0, int(st[kCertY0]) - mg), by1 = min(S - 1, int(st[kCertY1]) + mg);
     const uint32_t bw = uint32_t(bx1 - bx0 + 1), area = bw * uint32_t(by1 - by0 + 1);
     const uint32_t pitch = a->rec_pitch;
     CellWord *w = a->cert_rec + (unsigned long long)slot * p.S * pitch;

@@ -51,7 +51,9 @@ __device__ __forceinline__ void cert_window_slot(const KArgs *__restrict__ a, ui
     __shared__ uint32_t b0;
     const uint32_t tid = threadIdx.x;
     uint32_t *win = a->cert_win + (unsigned long long)slot * kWinWords;
-    for (uint32_t i = tid; i < kWinWords; i += 256) win[i] = 0;
+    if (a->cert_redo && !a->cert_redo[slot]) return;  // (the second round: this slot is done)
+    for (uint32_t i = tid; i < kWinWords; i += 256)
+        if (i != kWinProm0 && i != kWinProm1) win[i] = 0;
     const uint32_t nslot = min(a->cert_cap, __hip_atomic_load(a->counter + kCtrCert, __ATOMIC_RELAXED,
                                                                __HIP_MEMORY_SCOPE_AGENT));
     if (slot >= nslot) return;
@@ -83,8 +85,11 @@ __device__ __forceinline__ void cert_window_slot(const KArgs *__restrict__ a, ui
         w[(size_t)y * pitch + (v - y * p.S)] = ((E[t].wb << kStBShift) | E[t].wk) | kCertDirty;
     }
     const int S = int(p.S), H = int(p.H);
-    const int bx0 = max(0, int(st[kCertX0]) - kSweepMargin), bx1 = min(S - 1, int(st[kCertX1]) + kSweepMargin);
-    const int by0 = max(0, int(st[kCertY0]) - kSweepMargin), by1 = min(S - 1, int(st[kCertY1]) + kSweepMargin);
+    // (a sweep-only round repairs what the last sweep's window left: cells just past its
+    // edge, downstream of a special demoted late; a wider margin takes them in at once)
+    const int mg = (a->cert_redo && a->cert_redo[slot] == kRedoSweep) ? kSweepMarginAgain : kSweepMargin;
+    const int bx0 = max(0, int(st[kCertX0]) - mg), bx1 = min(S - 1, int(st[kCertX1]) + mg);
+    const int by0 = max(0, int(st[kCertY0]) - mg), by1 = min(S - 1, int(st[kCertY1]) + mg);
     const uint32_t bw = uint32_t(bx1 - bx0 + 1), bh = uint32_t(by1 - by0 + 1);
     const bool money_first = p.perm[0] == 1u;
     uint32_t ntx = 1, nty = 1;
@@ -187,12 +192,14 @@ __global__ __launch_bounds__(256) void cert_window_kernel(const KArgs *__restric
             uint32_t tiles = 0;
             for (uint32_t s = 0; s < gridDim.x; ++s) {
                 const uint32_t *win = a->cert_win + (unsigned long long)s * kWinWords;
+                if (a->cert_redo && !a->cert_redo[s]) continue;
                 if (__hip_atomic_load(win + kWinMode, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kWinTile)
                     tiles += win[kWinNtx] * win[kWinNty];
             }
             if (tiles > a->cert_pub_wgs)
                 for (uint32_t s = 0; s < gridDim.x; ++s) {
                     uint32_t *win = a->cert_win + (unsigned long long)s * kWinWords;
+                    if (a->cert_redo && !a->cert_redo[s]) continue;
                     if (win[kWinMode] == kWinTile && win[kWinNtx] * win[kWinNty] > 1u) win[kWinMode] = kWinOld;
                 }
             *ctr = 0;
@@ -233,7 +240,7 @@ __global__ __launch_bounds__(kTileBS) void cert_tile_kernel(const KArgs *__restr
         uint32_t used = 0, n = 0;
         for (uint32_t s = 0; s < nslot; ++s) {
             const uint32_t *win = a->cert_win + (unsigned long long)s * kWinWords;
-            if (win[kWinMode] != kWinTile) continue;
+            if (win[kWinMode] != kWinTile || (a->cert_redo && !a->cert_redo[s])) continue;
             const uint32_t nt = win[kWinNtx] * win[kWinNty];
             if (used + nt > P) used = 0;  // the next round
             if (blockIdx.x >= used && blockIdx.x < used + nt && n < 64) {
@@ -709,6 +716,130 @@ __global__ __launch_bounds__(kTileBS) void cert_tile_kernel(const KArgs *__restr
             *pw = (b << kStBShift) | (k1 - 1u);
         }
         __syncthreads();
+    }
+}
+
+// Between the two rounds (one wave per slot): a demoted special whose repaired walk a
+// caravan beats (the last check named the hub, kWinPromo) gets that caravan as its label
+// (src/pathfinder.rs:141-160, TotalCost += Caravan, src/cost.rs:208-315), becomes a
+// boundary (its cell word names its own entry again), and the boundaries' ranks by
+// (length, command list) are taken again.  The slot is then redone: closed form, check,
+// repair, check (cert_redo[slot] = 1); the check fails every entry the hub built on a
+// promoted one.  Other slots keep their result (cert_redo[slot] = 0).
+__global__ __launch_bounds__(64) void cert_promote_kernel(const KArgs *__restrict__ a, uint32_t *redo) {
+    __shared__ Rec R[64];
+    __shared__ uint32_t lex[64];
+    __shared__ uint32_t prom_lo, prom_hi;
+    const uint32_t slot = blockIdx.x, lane = threadIdx.x;
+    uint32_t *win = a->cert_win + (unsigned long long)slot * kWinWords;
+    const uint32_t nslot = min(a->cert_cap, __hip_atomic_load(a->counter + kCtrCert, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT));
+    const uint32_t T = a->p.NS + 1;
+    const uint32_t promo = slot < nslot && T <= 64u && lane < T ? win[kWinPromo + lane] : 0u;
+    const unsigned long long any = __ballot(promo != 0u);
+    // a slot whose last check still failed sweeps again from its repaired words, over the
+    // failing cells' box with a wider margin (specials that check demoted become plain)
+    uint32_t nf = 0;
+    if (slot < nslot && !any)
+        for (uint32_t j = lane; j < a->cert_parts; j += 64)
+            nf |= a->cert_st[((unsigned long long)slot * a->cert_parts + j) * kCertSt + kCertFails];
+    const bool again = __ballot(nf != 0u) != 0ull;
+    if (lane == 0) redo[slot] = any ? kRedoFill : (again ? kRedoSweep : 0u);
+    if (!any) return;
+    const unsigned long long tb = (unsigned long long)slot * T;
+    if (lane < T) {
+        R[lane] = a->cert_tab[tb + lane];
+        lex[lane] = a->cert_lex[tb + lane];
+    }
+    if (lane == 0) {
+        prom_lo = win[kWinProm0] | uint32_t(any);
+        prom_hi = win[kWinProm1] | uint32_t(any >> 32);
+    }
+    wave_sync();
+    const DevParams p = a->p;
+    const SpecialStatic *sp = a->sp;
+    if (promo) {
+        const uint32_t t = lane, h = promo - 1u;
+        const Rec rh = R[h];
+        const SpecialStatic st = sp[t], sh = sp[h];
+        const uint32_t d = uint32_t(abs(sh.x - st.x) + abs(sh.y - st.y)), coef = st.coef5 ? 5u : 2u;
+        const uint32_t kp = (kCaravan << 29) | (d << 1) | st.coef5;
+        Rec r;
+        if ((rh.kp0 >> 29) == kNoMove) {  // from the start label: the NoMove is replaced
+            r.m[0] = 0;
+            r.m[1] = coef * d;
+            r.m[2] = p.rgt * d;
+            r.meta = Rec::pack(1, 0, 1, 2);
+            r.from0 = rh.from0;
+        } else {
+            r.m[0] = rh.m[0];
+            r.m[1] = rh.m[1] + coef * d;
+            r.m[2] = rh.m[2] + p.rgt * d;
+            r.meta = Rec::pack(rh.len() + 1u, h, 1, 2);
+            r.from0 = sh.rk;
+        }
+        r.kp0 = kp;
+        r.u = st.rk;
+        R[t] = r;
+        // its cell names its own entry again (a boundary)
+        const uint32_t v = st.v, y = v / p.S;
+        a->cert_rec[(unsigned long long)slot * p.S * a->rec_pitch + (size_t)y * a->rec_pitch + (v - y * p.S)] = kViaSpecial | t;
+    }
+    wave_sync();
+    // the boundaries' ranks by (length, command list), the source first (export_cert in
+    // mr_device.hpp): lists of equal length compare from their first differing command,
+    // found walking both chains back from the end
+    auto tail = [&](uint32_t e, int i) -> Cmd {
+        const Rec &r = R[e];
+        return i == 0 ? Cmd{r.kp0, r.from0, r.u} : Cmd{kSoE << 29, r.u, sp[e].rk};
+    };
+    auto cmp_lists = [&](uint32_t x, uint32_t y) -> int {
+        uint32_t xe = x, ye = y;
+        int xt = int(R[x].ntail()) - 1, yt = int(R[y].ntail()) - 1, res = 0;
+        for (uint32_t guard = 0; guard < 4096u; ++guard) {
+            if (xe == ye && xt == yt) return res;
+            const Cmd cx = tail(xe, xt), cy = tail(ye, yt);
+            if (cx.kp != cy.kp) res = cx.kp < cy.kp ? -1 : 1;
+            else if (cx.from != cy.from) res = cx.from < cy.from ? -1 : 1;
+            else if (cx.to != cy.to) res = cx.to < cy.to ? -1 : 1;
+            if (xt > 0) --xt;
+            else {
+                const uint32_t pp = R[xe].parent();
+                if (pp == 0) return res;
+                xe = pp;
+                xt = int(R[pp].ntail()) - 1;
+            }
+            if (yt > 0) --yt;
+            else {
+                const uint32_t pp = R[ye].parent();
+                if (pp == 0) return res;
+                ye = pp;
+                yt = int(R[pp].ntail()) - 1;
+            }
+        }
+        return res;
+    };
+    const bool bnd = lane < T && (lane == 0 || lex[lane] != kNone32 || promo != 0u);
+    uint32_t r = kNone32;
+    if (bnd) {
+        r = 0;
+        for (uint32_t i = 0; i < T; ++i) {
+            if (i == lane || !(i == 0 || lex[i] != kNone32 || ((any >> i) & 1ull))) continue;
+            bool less;
+            if (i == 0 || lane == 0) less = i == 0;
+            else if (R[i].len() != R[lane].len()) less = R[i].len() < R[lane].len();
+            else less = cmp_lists(i, lane) < 0;
+            r += less ? 1u : 0u;
+        }
+    }
+    wave_sync();
+    if (lane < T) {
+        a->cert_lex[tb + lane] = r;
+        if (promo) a->cert_tab[tb + lane] = R[lane];
+    }
+    if (lane == 0) {
+        win[kWinProm0] = prom_lo;
+        win[kWinProm1] = prom_hi;
     }
 }
 

@@ -220,7 +220,14 @@ struct KArgs {
     uint32_t *cert_win;
     unsigned long long *cert_pub;
     uint32_t cert_pub_wgs;
+    // the certificate's second round (promoted specials, mr_cert_tile.hpp): non-null in the
+    // argument block of the round's kernels, which skip the slots with cert_redo[slot] == 0
+    uint32_t *cert_redo;
 };
+// cert_redo[slot]: kRedoFill — promoted specials: the closed form again, both checks and the
+// repair; kRedoSweep — specials the last check demoted: the repair from the current words
+// and the last check only
+constexpr uint32_t kRedoFill = 1u, kRedoSweep = 2u;
 // fb_cert[i] of a staged entry before cert_select_kernel gives it a slot (or none)
 constexpr uint32_t kFbStaged = 0xFFFFFFFEu;
 // fb_list[i] | kFbCertified: the SSSP launch emitted entry i from its certificate slot
@@ -280,9 +287,12 @@ enum : uint32_t {
     kWinFail = 8,   // the tile sweep gave up (step cap, a spin timeout, an LDS table too small)
     kWinSteps = 10, // steps of the slot's last tile to finish
     kWinTStep = 11, kWinTXchg = 12, kWinNXchg = 13,  // tile 0: time in steps / exchanges (10 ns), exchanges
+    kWinProm0 = 14, kWinProm1 = 15,  // entries promoted this pass (a bit each; zeroed by cert_select_kernel)
     kWinFlag = 16,  // per tile: exchanges published (kTileDone: final)
     kWinStat = 16 + kTileMaxTiles,  // per tile 4 words: time in steps / exchanges (10 ns), settles, steps
-    kWinWords = 16 + 5 * kTileMaxTiles
+    kWinPromo = 16 + 5 * kTileMaxTiles,  // per entry: the hub whose caravan beats its repaired walk, + 1
+    kWinWhy = kWinPromo + 64,  // diagnostics: failing cells of the last check (count, 7 x {x | y << 16, tests, keys})
+    kWinWords = kWinWhy + 32
 };
 enum : uint32_t { kWinNone = 0, kWinTile = 1, kWinOld = 2, kWinWide = 3 };
 // result status (OutResult high half - 16) of a label whose commands went to the

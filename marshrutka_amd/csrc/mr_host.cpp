@@ -76,6 +76,8 @@ hipError_t launch_cert_check(const KArgs *d_args, uint32_t gx, uint32_t slots, u
 hipError_t launch_cert_sweep(const KArgs *d_args, uint32_t slots, hipStream_t stream);
 hipError_t launch_cert_window(const KArgs *d_args, uint32_t slots, hipStream_t stream);
 hipError_t launch_cert_tile(const KArgs *d_args, uint32_t wgs, hipStream_t stream);
+hipError_t launch_cert_promote(const KArgs *d_args, uint32_t slots, uint32_t *redo, hipStream_t stream);
+constexpr int kCertRounds = 2;  // certificate rounds after the first (cert_promote_kernel decides each slot's)
 int cert_tile_occupancy();
 hipError_t launch_ovf_order(const KArgs *d_args, uint32_t nrec, OutCmd *tmp, hipStream_t stream);
 hipError_t decode_records_device(const OutResult *res, const OutCmd *slots, const OutCmd *ovf, uint32_t novf,
@@ -1818,6 +1820,8 @@ struct mr_plan {
     uint32_t cert_cap = 0, cert_fill_gx = 1, cert_check_gx = 1, cert_tile_wgs = 0;
     Rec *d_cert_tab = nullptr;
     uint32_t *d_cert_win = nullptr;               // per slot the repair window (cert_window_kernel)
+    uint32_t *d_cert_redo = nullptr;              // per slot: redone in the second round (cert_promote_kernel)
+    KArgs *d_args_r2 = nullptr, *d_args_cert_r2 = nullptr;  // the second round's argument blocks
     unsigned long long *d_cert_pub = nullptr;     // the tile sweep's publish areas
     uint32_t *d_cert_lex = nullptr, *d_cert_src = nullptr, *d_cert_st = nullptr, *d_cert_aux = nullptr,
              *d_fb_cert = nullptr, *d_cert_ones = nullptr;
@@ -1860,7 +1864,8 @@ struct mr_plan {
         for (void *p : {(void *)d_cert_tab, (void *)d_cert_lex, (void *)d_cert_src, (void *)d_cert_st,
                         (void *)d_cert_aux, (void *)d_fb_cert, (void *)d_cert_ones, (void *)d_cert_rec,
                         (void *)d_args_cert, (void *)d_cert_stage_tab, (void *)d_cert_stage_lex,
-                        (void *)d_cert_stage_src, (void *)d_cert_win, (void *)d_cert_pub})
+                        (void *)d_cert_stage_src, (void *)d_cert_win, (void *)d_cert_pub, (void *)d_cert_redo,
+                        (void *)d_args_r2, (void *)d_args_cert_r2})
             if (p) (void)pfree(p);
         for (void *p : {(void *)d_sinfo, (void *)d_rank, (void *)d_rank_inv, (void *)d_src, (void *)d_qb, (void *)d_qd,
                         (void *)d_qi, (void *)d_sp, (void *)d_hubs, (void *)d_res, (void *)d_cmd, (void *)d_ws,
@@ -1908,7 +1913,7 @@ static int upload_args(mr_plan *pl) {
     // every block queued on the plan's stream, then one synchronisation (a blocking copy
     // each cost ~10 us: up to six per plan); the host copies live in `held` until then.
     // Callers hold a drained plan, so nothing of the stream's is in flight.
-    KArgs held[6];
+    KArgs held[8];
     uint32_t nh = 0;
     bool ok = true;
     auto put = [&](KArgs *d, const KArgs &k) {
@@ -1949,6 +1954,12 @@ static int upload_args(mr_plan *pl) {
             c.out_lex = pl->d_cert_lex;
             c.out_rec = pl->d_cert_rec;
             if (!put(pl->d_args_cert, c)) return MR_ERR_DEVICE;
+            if (pl->d_args_r2) {  // the second round: only the slots cert_promote_kernel marked
+                KArgs r = k;
+                r.cert_redo = pl->d_cert_redo;
+                c.src_state = pl->d_cert_redo;
+                if (!put(pl->d_args_r2, r) || !put(pl->d_args_cert_r2, c)) return MR_ERR_DEVICE;
+            }
         }
         // (the lane kernel as the pass's only launch has no hub launch after it to relist into)
         KArgs ll = l;
@@ -2563,6 +2574,15 @@ static int plan_create(const mr_grid *g, const mr_params *prm, const mr_query *q
             ka.cert_win = pl->d_cert_win;
             ka.cert_pub = pl->d_cert_pub;
             ka.cert_pub_wgs = pl->cert_tile_wgs;
+            // the second round after promotions (MR_CERT_PROMOTE=0: none)
+            static const bool no_promote = [] {
+                const char *e = std::getenv("MR_CERT_PROMOTE");
+                return e && std::atoi(e) == 0;
+            }();
+            if (!no_promote && (pmalloc(reinterpret_cast<void **>(&pl->d_cert_redo), size_t(cap) * 4) != hipSuccess ||
+                                pmalloc(reinterpret_cast<void **>(&pl->d_args_r2), sizeof(KArgs)) != hipSuccess ||
+                                pmalloc(reinterpret_cast<void **>(&pl->d_args_cert_r2), sizeof(KArgs)) != hipSuccess))
+                return bail(fail(MR_ERR_DEVICE, "certificate slots"));
         }
         if (pl->n_lane && (pmalloc(reinterpret_cast<void **>(&pl->d_args_lane), sizeof(KArgs)) != hipSuccess ||
                            pmalloc(reinterpret_cast<void **>(&pl->d_args_lane_last), sizeof(KArgs)) != hipSuccess))
@@ -2822,6 +2842,17 @@ extern "C" int mr_plan_run(mr_plan *pl, void *stream) {
                 if (e == hipSuccess && pl->cert_tile_wgs) e = launch_cert_tile(pl->d_args, pl->cert_tile_wgs, s);
                 if (e == hipSuccess) e = launch_cert_sweep(pl->d_args, pl->cert_cap, s);
                 if (e == hipSuccess) e = launch_cert_check(pl->d_args, pl->cert_check_gx, pl->cert_cap, 0u, s);
+                // further rounds for the slots whose last check still failed: the closed form
+                // again after a promotion, else the sweep again from the repaired words
+                for (int round = 0; round < kCertRounds && e == hipSuccess && pl->d_args_r2; ++round) {
+                    e = launch_cert_promote(pl->d_args, pl->cert_cap, pl->d_cert_redo, s);
+                    if (e == hipSuccess) e = launch_fill(pl->d_args_cert_r2, pl->ka.p.perm, pl->cert_fill_gx, 1, s);
+                    if (e == hipSuccess) e = launch_cert_check(pl->d_args_r2, pl->cert_check_gx, pl->cert_cap, 1u, s);
+                    if (e == hipSuccess) e = launch_cert_window(pl->d_args_r2, pl->cert_cap, s);
+                    if (e == hipSuccess && pl->cert_tile_wgs) e = launch_cert_tile(pl->d_args_r2, pl->cert_tile_wgs, s);
+                    if (e == hipSuccess) e = launch_cert_sweep(pl->d_args_r2, pl->cert_cap, s);
+                    if (e == hipSuccess) e = launch_cert_check(pl->d_args_r2, pl->cert_check_gx, pl->cert_cap, 0u, s);
+                }
             }
         }
         if (e == hipSuccess && !pl->fb_none)
@@ -2998,11 +3029,20 @@ extern "C" int mr_plan_get_stats(mr_plan *pl, mr_plan_stats *out) {
                 if (pl->d_cert_win) (void)hipMemcpy(wn, pl->d_cert_win + size_t(k) * kWinWords, sizeof(wn), hipMemcpyDeviceToHost);
                 std::fprintf(stderr,
                              "MR_CERT_DEBUG slot %u src (%d,%d): fails %u key %u box x %d..%d y %d..%d | repair mode %u "
-                             "tiles %ux%u steps %u fail %u | tile 0: steps %.1f us, %u exchanges %.1f us\n",
+                             "tiles %ux%u steps %u fail %u promoted %08x%08x | tile 0: steps %.1f us, %u exchanges %.1f us\n",
                              k, pl->grid->gx(v), pl->grid->gy(v), fails, key, int(x0) - int(pl->grid->H),
                              int(x1) - int(pl->grid->H), int(y0) - int(pl->grid->H), int(y1) - int(pl->grid->H), wn[kWinMode],
-                             wn[kWinNtx], wn[kWinNty], wn[kWinSteps], wn[kWinFail], wn[kWinTStep] * 0.01, wn[kWinNXchg],
+                             wn[kWinNtx], wn[kWinNty], wn[kWinSteps], wn[kWinFail], wn[kWinProm1], wn[kWinProm0],
+                             wn[kWinTStep] * 0.01, wn[kWinNXchg],
                              wn[kWinTXchg] * 0.01);
+                {
+                    uint32_t wy[29] = {0};
+                    if (hipMemcpy(wy, pl->d_cert_win + size_t(k) * kWinWords + kWinWhy, sizeof(wy), hipMemcpyDeviceToHost) == hipSuccess)
+                        for (uint32_t f = 0; f < std::min(wy[0], 7u); ++f)
+                            std::fprintf(stderr, "MR_CERT_DEBUG   failing cell (%d,%d)%s tests %#x own %u best %u\n",
+                                         int(wy[1 + 4 * f] & 0xFFFFu) - int(pl->grid->H), int(wy[1 + 4 * f] >> 16) - int(pl->grid->H),
+                                         (wy[2 + 4 * f] >> 31) ? " special" : "", wy[2 + 4 * f] & 0x7FFFFFFFu, wy[3 + 4 * f], wy[4 + 4 * f]);
+                }
                 if (wn[kWinMode] == kWinTile) {  // the tiles' step / exchange times and settles
                     const uint32_t nt = std::min(wn[kWinNtx] * wn[kWinNty], kTileMaxTiles);
                     std::vector<uint32_t> ts(size_t(nt) * 4);

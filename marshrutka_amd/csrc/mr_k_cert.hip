@@ -36,6 +36,12 @@ hipError_t launch_cert_tile(const KArgs *d_args, uint32_t wgs, hipStream_t strea
     return hipLaunchKernel((const void *)&cert_tile_kernel, dim3(wgs), dim3(kTileBS), args, 0, stream);
 }
 
+// between the certificate's two rounds: one wave per slot
+hipError_t launch_cert_promote(const KArgs *d_args, uint32_t slots, uint32_t *redo, hipStream_t stream) {
+    void *args[] = {const_cast<KArgs **>(&d_args), &redo};
+    return hipLaunchKernel((const void *)&cert_promote_kernel, dim3(slots), dim3(64), args, 0, stream);
+}
+
 // resident workgroups of the tile sweep per CU (1 expected)
 int cert_tile_occupancy() {
     int n = 0;
