@@ -260,6 +260,12 @@ uint32_t mr_plan_num_sources(const mr_plan *plan);
  * Waits for the plan's passes.  A cost signal for balancing sources over ranks
  * (marshrutka_amd/shard.py SourceCosts); no reference counterpart. */
 int mr_plan_fallback_sources(mr_plan *plan, mr_cell_index *out, uint32_t cap, uint32_t *n);
+/* Every source the hub handed over in the last pass (its closed form not certain), in
+ * source order, whichever path then answered it: certified[k] = 1 for one the
+ * fixed-point certificate answered from its slot, 0 for one the SSSP kernel solved.  Up
+ * to cap entries into out / certified (either may be NULL), their count in *n.  Waits for
+ * the plan's passes (tests, diagnostics). */
+int mr_plan_handed_over_sources(mr_plan *plan, mr_cell_index *out, uint8_t *certified, uint32_t cap, uint32_t *n);
 
 /* Which solver a plan runs and how the last pass went (diagnostics, bench). */
 enum {

@@ -187,6 +187,13 @@ extern "C" {
     pub fn mr_plan_record_queries(plan: *const mr_plan, query_of_record: *mut u32, n: u32) -> c_int;
     pub fn mr_plan_num_sources(plan: *const mr_plan) -> u32;
     pub fn mr_plan_fallback_sources(plan: *mut mr_plan, out: *mut mr_cell_index, cap: u32, n: *mut u32) -> c_int;
+    pub fn mr_plan_handed_over_sources(
+        plan: *mut mr_plan,
+        out: *mut mr_cell_index,
+        certified: *mut u8,
+        cap: u32,
+        n: *mut u32,
+    ) -> c_int;
     pub fn mr_plan_get_stats(plan: *mut mr_plan, out: *mut mr_plan_stats) -> c_int;
     pub fn mr_plan_kernel_ms(plan: *mut mr_plan, n_launches: *mut u32) -> f64;
     pub fn mr_plan_destroy(plan: *mut mr_plan);

@@ -43,7 +43,6 @@ struct CertEntry {
 // CertEntry::fl: the Center or a border-1 cell (never demoted: CentralMoves merge), a
 // caravan hub, the HQ, a caravan into it costs 5 a unit, the label is the start label
 constexpr uint32_t kCertFCentral = 1u, kCertFHub = 2u, kCertFHQ = 4u, kCertFCoef5 = 8u, kCertFStart = 16u;
-constexpr uint32_t kCertFLastCentral = 32u;  // the label ends in a CentralMove (another one merges into it)
 // a walk label (b, k) as comparator keys: c1..c3 in comparator order, length, rank of b
 struct CertLab {
     uint32_t c1, c2, c3, len, lex, b, k;
@@ -104,8 +103,7 @@ __device__ __forceinline__ void cert_load_table(const KArgs *__restrict__ a, uin
         const uint32_t fl = (t != 0 && (ss.flags & (kSpCenter | kSpBorder1)) ? kCertFCentral : 0u) |
                             (t != 0 && (ss.flags & kSpHub) ? kCertFHub : 0u) |
                             (t != 0 && t == a->p.hq_t ? kCertFHQ : 0u) | (t != 0 && ss.coef5 ? kCertFCoef5 : 0u) |
-                            ((r.kp0 >> 29) == kNoMove ? kCertFStart : 0u) |
-                            (r.ntail() == 1 && (r.kp0 >> 29) == kCentral ? kCertFLastCentral : 0u);
+                            ((r.kp0 >> 29) == kNoMove ? kCertFStart : 0u);
         E[t] = CertEntry{r.m[0], r.m[1], r.m[2], r.len(), a->cert_lex[(unsigned long long)slot * T + t],
                          walk ? r.parent() : kCertNoB, walk ? (r.kp0 & 0x1FFFFFFFu) : 0u, r.parent(),
                          soe ? r.parent() : kCertNoB, soe ? (r.kp0 & 0x1FFFFFFFu) : 0u, soe ? r.u : kNone32, fl,
@@ -273,8 +271,10 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
                 // special's word)
                 // (the last check records one that fails its walk test too: the second round
                 // demotes it then and sweeps again, from the repaired words)
-                // (a border-1 cell too: its CentralMove in-edge is tested with the others)
-                if (fail && (mark || (why & 2u))) atomicOr(&dem_bits[t >> 5], 1u << (t & 31u));
+                // (not a border-1 cell: the Center's label and through it the other border-1
+                // cells' rest on its label, and only a new Dijkstra over the specials would
+                // rebuild them — tried: the failure moves to those cells)
+                if (fail && !(e.fl & kCertFCentral) && (mark || (why & 2u))) atomicOr(&dem_bits[t >> 5], 1u << (t & 31u));
             } else {  // built over the specials: no neighbour's walk may reach it first (a tie on
                       // metrics and length would need the command lists: counted as a failure),
                       // and its parent must still hold the label the hub built it from
@@ -348,26 +348,6 @@ __global__ __launch_bounds__(kBS) void cert_check_kernel(const KArgs *__restrict
                                                   : (bc.c2 != o.c2 ? bc.c2 < o.c2 : (bc.c3 != o.c3 ? bc.c3 < o.c3 : bc.len < o.len));
                     if (win && bh != kNone32 && !btie && cb && !(et.fl & kCertFHQ) && a->sp[tv].rid == kNone10 && tv < 64u)
                         win[kWinPromo + tv] = bh + 1u;
-                }
-                // a demoted border-1 cell: the Center's label + a CentralMove (10 s; merged
-                // into a CentralMove the label ends in) must not reach it first
-                if ((a->sp[tv].flags & kSpBorder1) && T > 1u) {
-                    uint32_t l, mo, ti, len;
-                    bool start;
-                    cur(1, l, mo, ti, len, start);
-                    if (start) {
-                        l = 0;
-                        mo = 0;
-                        ti = 10;
-                        len = 1;
-                    } else {
-                        ti += 10;
-                        len += (E[1].fl & kCertFLastCentral) ? 0u : 1u;
-                    }
-                    if (!before(o, l, mo, ti, len)) {
-                        fail = true;
-                        why |= 4096u;
-                    }
                 }
                 if ((et.fl & kCertFHQ) && !before(o, 0u, p.shq_cost, 0u, 1u)) {
                     fail = true;

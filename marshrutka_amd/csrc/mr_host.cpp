@@ -2982,22 +2982,45 @@ extern "C" int mr_plan_record_queries(const mr_plan *pl, uint32_t *query_of_reco
 
 extern "C" double mr_plan_fill_ms(const mr_plan *pl) { return pl ? pl->fill_ms : 0.0; }
 
-extern "C" int mr_plan_fallback_sources(mr_plan *pl, mr_cell_index *out, uint32_t cap, uint32_t *n) {
-    if (!pl || !n || (cap && !out)) return fail(MR_ERR_INVALID_ARG, "null argument");
-    *n = 0;
+// The last pass's fallback entries (source indices, kFbCertified on those the certificate
+// answered), sorted by source
+static int handed_over(mr_plan *pl, std::vector<uint32_t> &fb) {
+    fb.clear();
     if (!plan_sync(pl)) return fail(MR_ERR_DEVICE, "sync");
     uint32_t ctr[kCtrWords];
     if (int st = read_counters(pl, ctr)) return st;
     const uint32_t nf = pl->hp.hub && pl->d_fb ? std::min(ctr[kCtrLastFb], pl->ka.nsrc) : 0u;
-    std::vector<uint32_t> fb(nf);
+    fb.resize(nf);
     if (nf && hipMemcpy(fb.data(), pl->d_fb, size_t(nf) * 4, hipMemcpyDeviceToHost) != hipSuccess)
         return fail(MR_ERR_DEVICE, "copy fallback list");
-    // entries the certificate answered carry kFbCertified: no search was run for them
-    fb.erase(std::remove_if(fb.begin(), fb.end(), [](uint32_t s) { return (s & kFbCertified) != 0; }), fb.end());
-    std::sort(fb.begin(), fb.end());
+    std::sort(fb.begin(), fb.end(), [](uint32_t a, uint32_t b) { return (a & ~kFbCertified) < (b & ~kFbCertified); });
     if (!fb.empty())
         if (int st = host_arrays(pl)) return st;
+    return MR_OK;
+}
+
+extern "C" int mr_plan_fallback_sources(mr_plan *pl, mr_cell_index *out, uint32_t cap, uint32_t *n) {
+    if (!pl || !n || (cap && !out)) return fail(MR_ERR_INVALID_ARG, "null argument");
+    *n = 0;
+    std::vector<uint32_t> fb;
+    if (int st = handed_over(pl, fb)) return st;
+    // entries the certificate answered carry kFbCertified: no search was run for them
+    fb.erase(std::remove_if(fb.begin(), fb.end(), [](uint32_t s) { return (s & kFbCertified) != 0; }), fb.end());
     for (uint32_t k = 0; k < fb.size() && k < cap; ++k) out[k] = pl->grid->idx[pl->hp.src_v[fb[k]]];
+    *n = uint32_t(fb.size());
+    return MR_OK;
+}
+
+extern "C" int mr_plan_handed_over_sources(mr_plan *pl, mr_cell_index *out, uint8_t *certified, uint32_t cap,
+                                           uint32_t *n) {
+    if (!pl || !n) return fail(MR_ERR_INVALID_ARG, "null argument");
+    *n = 0;
+    std::vector<uint32_t> fb;
+    if (int st = handed_over(pl, fb)) return st;
+    for (uint32_t k = 0; k < fb.size() && k < cap; ++k) {
+        if (out) out[k] = pl->grid->idx[pl->hp.src_v[fb[k] & ~kFbCertified]];
+        if (certified) certified[k] = (fb[k] & kFbCertified) ? 1u : 0u;
+    }
     *n = uint32_t(fb.size());
     return MR_OK;
 }

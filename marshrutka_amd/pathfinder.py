@@ -26,7 +26,7 @@ LIB_PATH = os.environ.get("MR_LIB_PATH") or os.path.join(os.path.dirname(os.path
 EXPORTED_SYMBOLS = [
     "mr_grid_create", "mr_grid_destroy", "mr_grid_square_size", "mr_params_default", "mr_find_path",
     "mr_find_path_batch", "mr_plan_create", "mr_plan_create_ex", "mr_plan_run", "mr_plan_fetch", "mr_plan_device_outputs",
-    "mr_plan_num_sources", "mr_plan_record_queries", "mr_plan_fallback_sources", "mr_plan_wait", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_cache_trim", "mr_host_register", "mr_host_unregister", "mr_plan_bind_outputs", "mr_plan_bind_outputs_ex", "mr_decode_records", "mr_abi_version", "mr_last_error",
+    "mr_plan_num_sources", "mr_plan_record_queries", "mr_plan_fallback_sources", "mr_plan_handed_over_sources", "mr_plan_wait", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_cache_trim", "mr_host_register", "mr_host_unregister", "mr_plan_bind_outputs", "mr_plan_bind_outputs_ex", "mr_decode_records", "mr_abi_version", "mr_last_error",
     "mr_device_available", "mr_parse_map_html", "mr_parse_error", "mr_grid_from_html",
     "mr_command_time", "mr_duration_display", "mr_render_schedule", "mr_grid_region_table",
     "mr_sssp_plan_create", "mr_sssp_records", "mr_sssp_device_records", "mr_sssp_record_pitch", "mr_sssp_device_tables", "mr_sssp_label", "mr_sssp_labels", "mr_plan_fill_ms",
@@ -89,6 +89,9 @@ def lib():
         L.mr_plan_record_queries.restype = C.c_int
         L.mr_plan_fallback_sources.argtypes = [vp, C.POINTER(mr_cell_index), C.c_uint32, C.POINTER(C.c_uint32)]
         L.mr_plan_fallback_sources.restype = C.c_int
+        L.mr_plan_handed_over_sources.argtypes = [vp, C.POINTER(mr_cell_index), C.POINTER(C.c_uint8), C.c_uint32,
+                                                  C.POINTER(C.c_uint32)]
+        L.mr_plan_handed_over_sources.restype = C.c_int
         L.mr_plan_get_stats.argtypes = [vp, C.POINTER(mr_plan_stats)]
         L.mr_plan_get_stats.restype = C.c_int
         L.mr_plan_kernel_ms.argtypes = [vp, C.POINTER(C.c_uint32)]
@@ -459,6 +462,20 @@ class Plan:
         if st != MR_OK:
             raise EngineError(st, last_error())
         return [CellIndex(c.kind, c.sub, c.x, c.y) for c in out[: n.value]]
+
+    def handed_over_sources(self) -> List[Tuple[CellIndex, bool]]:
+        """Every source the hub handed over in the last pass, with whether the certificate
+        answered it (True) or the SSSP kernel solved it (mr_plan_handed_over_sources)."""
+        n = C.c_uint32()
+        st = lib().mr_plan_handed_over_sources(self.handle, None, None, 0, C.byref(n))
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+        out = (mr_cell_index * max(1, n.value))()
+        cert = (C.c_uint8 * max(1, n.value))()
+        st = lib().mr_plan_handed_over_sources(self.handle, out, cert, n.value, C.byref(n))
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+        return [(CellIndex(c.kind, c.sub, c.x, c.y), bool(f)) for c, f in zip(out[: n.value], cert[: n.value])]
 
     def run(self, stream: int = 0) -> None:
         st = lib().mr_plan_run(self.handle, C.c_void_p(stream) if stream else None)

@@ -248,9 +248,9 @@ def test_c4_busy_sources_hub_kernel(eng, c4_map, c4_batch, c4_sources):
         assert bad.size == 0, (str(s), len(bad), [str(m.index_at(int(ex_dst[sel][j]))) for j in bad[:4]])
 
 
-@pytest.mark.parametrize("ff", [1, 3])
+@pytest.mark.parametrize("ff", [1, 2, 3])
 def test_fleetfoot_time_first_1025(eng, oracle_lib, c4_map, ff):
-    """Non-linear run times (Fleetfoot 1, 3) with Time first at configs[3]'s size: the
+    """Non-linear run times (Fleetfoot 1, 2, 3) with Time first at configs[3]'s size: the
     certified hub path (DESIGN.md section 3a'') plus the SSSP kernel for the sources it
     hands over.  A 20k-query batch property-checked in full (the time of a StandardMove
     run through the Fleetfoot ceil), and every destination of 8 sources x 1 000 against
@@ -285,6 +285,80 @@ def test_fleetfoot_time_first_1025(eng, oracle_lib, c4_map, ff):
     for i, s in enumerate(srcs):
         sel = np.arange(off + i * 1000, off + (i + 1) * 1000)
         bad = ld.mismatches(got, {f: want[f][i] for f in want}, idx_got=sel, idx_exp=q_dst[sel])
+        assert bad.size == 0, (str(s), len(bad), [str(m.index_at(int(q_dst[sel][j]))) for j in bad[:4]])
+
+
+# sources the hub hands over, of a 125k Time-first batch on configs[3]'s map, that the
+# certificate still leaves to the SSSP kernel: at Fleetfoot 3, sources whose repaired words
+# still fail at border-1 cells (a border-1 cell's label is not
+# demoted).  A source is emitted from its slot when every label asked of it lies below the
+# failing key, so with 1 000 destinations (the forced plan) both such sources need the
+# SSSP kernel, and with the batch's few destinations one of them does not.
+C4_MAP_SSSP_MAX = {1: 0, 2: 0, 3: 1}
+C4_MAP_SSSP_MAX_1000 = {1: 0, 2: 0, 3: 2}
+
+
+@pytest.mark.parametrize("ff", [1, 2, 3])
+def test_c4_map_time_first_handed_over(eng, oracle_lib, c4_map, ff):
+    """configs[3]'s own map (seed 4096), a 125k-query Time-first batch at Fleetfoot 1-3
+    (tools/r06/ff_c4map.py): the hub hands over tens of sources (42 / 10 / 3).  Per source,
+    mr_plan_handed_over_sources says which path answered it (certificate or SSSP kernel),
+    consistent with the plan stats, and the certificate must answer all but
+    C4_MAP_SSSP_MAX of them.  Every handed-over source's own queries of the batch are
+    compared with the oracle, and so are >= 1 000 destinations of each, in a second plan
+    that sends every source through a certificate slot (MR_HUB_FALLBACK_ALL): the label of
+    every compared cell is the certificate's (or, where it still fails, the SSSP kernel's)."""
+    m, arr = c4_map
+    V = m.size * m.size
+    params = Params(fleetfoot=ff, sort_by=(SORT_TIME, SORT_LEGS))
+    src, dst = random_query_cells(m, 125_000, 5001)
+    g = eng.MapGrid.from_array(arr)
+    plan = eng.Plan(g, params, None, max_cmds=8, query_array=m.query_array(src, dst, arr))
+    plan.run()
+    plan.run()  # (a second pass: the path a source takes does not change)
+    st = plan.stats()
+    handed = plan.handed_over_sources()
+    assert st["solver"] == "hub" and len(handed) == st["fallback_sources"] > 0, (st, len(handed))
+    n_cert = sum(1 for _, c in handed if c)
+    assert n_cert == st["certified_sources"], (st, n_cert)
+    assert len(handed) - n_cert <= C4_MAP_SSSP_MAX[ff], (ff, [str(s) for s, c in handed if not c])
+    sssp = {str(s) for s in plan.fallback_sources()}
+    assert sssp == {str(s) for s, c in handed if not c}
+    srcs = [s for s, _ in handed]
+    og = oracle_lib.OracleGrid.from_array(arr)
+    want = og.sssp_digests(params, srcs, threads=ORACLE_THREADS)
+    # the batch's own queries of those sources
+    res, pool = plan.fetch_raw()
+    got = ld.digests(res, pool, len(src))
+    for i, s in enumerate(srcs):
+        sel = np.flatnonzero(src == m.cell_of(s))
+        assert sel.size > 0
+        bad = ld.mismatches(got, {f: want[f][i] for f in want}, idx_got=sel, idx_exp=dst[sel])
+        assert bad.size == 0, (str(s), len(bad))
+    # >= 1 000 destinations each, every source through a certificate slot
+    rng = random.Random(ff)
+    cf_cells = [m.cell_of(c) for c in m.campfires()]
+    q_src, q_dst = [], []
+    for s in srcs:
+        d = rng.sample(range(V), 1000) + cf_cells
+        q_src += [m.cell_of(s)] * len(d)
+        q_dst += d
+    q_src, q_dst = np.array(q_src, dtype=np.int64), np.array(q_dst, dtype=np.int64)
+    os.environ["MR_HUB_FALLBACK_ALL"] = "1"
+    try:
+        p2 = eng.Plan(g, params, None, max_cmds=8, query_array=m.query_array(q_src, q_dst, arr))
+        p2.run()
+        st2 = p2.stats()
+        h2 = p2.handed_over_sources()
+        res2, pool2 = p2.fetch_raw()
+    finally:
+        os.environ.pop("MR_HUB_FALLBACK_ALL", None)
+    assert len(h2) == len(srcs) and st2["certified_sources"] >= len(srcs) - C4_MAP_SSSP_MAX_1000[ff], st2
+    got2 = ld.digests(res2, pool2, len(q_src))
+    per = 1000 + len(cf_cells)
+    for i, s in enumerate(srcs):
+        sel = np.arange(i * per, (i + 1) * per)
+        bad = ld.mismatches(got2, {f: want[f][i] for f in want}, idx_got=sel, idx_exp=q_dst[sel])
         assert bad.size == 0, (str(s), len(bad), [str(m.index_at(int(q_dst[sel][j]))) for j in bad[:4]])
 
 
