@@ -218,12 +218,12 @@ def algorithmic_bytes(plan, stats, V):
     return float(b), name, survey
 
 
-def check_gather(pipe, plan, k, grid, params, shards, orders, counts, rows, rw, cw, ovf_cap, rank, world):
-    """After the timed region (N > 1): rank 0 decodes every record of the last batch
-    as gathered (result records, command slots, overflow pool of each rank) on the
-    host, puts record j of rank r at its query shards[r][orders[r][j]], and compares
-    the labels with each rank's own fetch of that batch (mr_plan_fetch, in the rank's
-    query order): one digest per rank.  Returns the check's summary on rank 0."""
+def check_gather(pipe, plan, k, grid, params, shards, orders, counts, rows, rw, wpool_cap, rank, world):
+    """After the timed region (N > 1): rank 0 decodes every wire row of the last batch as
+    gathered (rows, then the pool of long labels, of each rank) on the host
+    (mr_decode_wire), puts row j of rank r at its query shards[r][orders[r][j]], and
+    compares the labels with each rank's own fetch of that batch (mr_plan_fetch, in the
+    rank's query order): one digest per rank.  Returns the check's summary on rank 0."""
     import numpy as np
     import torch.distributed as dist
     from marshrutka_amd import pathfinder
@@ -233,23 +233,23 @@ def check_gather(pipe, plan, k, grid, params, shards, orders, counts, rows, rw, 
     if rank != 0:
         return None
     bad_status, mismatched, seen = 0, 0, np.zeros(sum(counts), dtype=bool)
+    mc = (rw - 1) // 2
     for r, buf in enumerate(pipe.out[k]):
         words = buf.to("cpu").numpy().view("uint32")
         n = counts[r]
-        rres = words[: n * rw]
-        slots = words[rows * rw: rows * rw + n * cw]
-        ovf = words[rows * (rw + cw): rows * (rw + cw) + ovf_cap * 4]
-        st = rres.reshape(-1, rw)[:, 3] >> 16
-        bad_status += int(((st != 16) & (st != 17) & (st != 80)).sum())
-        out, opool = pathfinder.decode_records_raw(grid, params, rres, slots, n, cw // 4, ovf)
-        order = np.asarray(orders[r][:n], dtype=np.int64)  # record j answers local query order[j]
+        out, opool = pathfinder.decode_wire_raw(grid, params, words[: n * rw], n, mc,
+                                                words[rows * rw: rows * rw + wpool_cap * 2])
+        st = np.array([out[j].status for j in range(n)])
+        bad_status += int(((st != 0) & (st != 1)).sum())
+        order = np.asarray(orders[r][:n], dtype=np.int64)  # row j answers local query order[j]
         inv = np.empty(n, dtype=np.int64)
-        inv[order] = np.arange(n)  # local query i is record inv[i]
+        inv[order] = np.arange(n)  # local query i is row inv[i]
         seen[np.asarray(shards[r], dtype=np.int64)[order]] = True
         if pathfinder.labels_digest(out, opool, n, inv) != digests[r]:
             mismatched += 1
     return {"rows": sum(counts), "bad_status": bad_status, "queries_covered": int(seen.sum()),
-            "ranks_matching_own_fetch": world - mismatched, "ranks": world}
+            "ranks_matching_own_fetch": world - mismatched, "ranks": world,
+            "wire_bytes_per_query": rw * 4 + wpool_cap * 8 / max(1, rows)}
 
 
 def as_expected(label):
@@ -430,18 +430,16 @@ def main():
                  for _ in range(depth)]
         plan = plans[0]
         n_src = plan.num_sources
-        _, rbytes, _, cbytes = plan.device_outputs()
     pipe = None
     if dist_on and not all_dst:
-        # result records, command slots and the overflow pool in one flat torch-owned
-        # device buffer per plan, padded to the largest shard: one RCCL gather per batch
-        # moves every record of the batch with all its commands
-        rows, nq = max(counts), max(1, len(mine))
-        rw, cw = rbytes // nq // 4, cbytes // nq // 4
-        ovf_cap = max(1024, rows // 8)  # commands (16 B) for labels longer than the slots
-        bufs = [torch.zeros(rows * (rw + cw) + ovf_cap * 4, dtype=torch.int32, device="cuda") for _ in plans]
-        for p_, b in zip(plans, bufs):
-            p_.bind_outputs(b.data_ptr(), b.data_ptr() + rows * rw * 4, b.data_ptr() + rows * (rw + cw) * 4, ovf_cap)
+        # each pass re-encoded as wire rows (mr_plan_wire_records: 4 + 8 max_cmds bytes a
+        # query, the metrics left to the decoder) and the pool of long labels, in one flat
+        # torch-owned device buffer per plan, padded to the largest shard: one RCCL gather
+        # per batch moves every label of the batch with all its commands
+        rows = max(counts)
+        rw = pathfinder.wire_row_words(plan.max_cmds)
+        wpool_cap = max(1024, rows // 8)  # commands (8 B) of labels longer than the slots
+        bufs = [torch.zeros(rows * rw + wpool_cap * 2, dtype=torch.int32, device="cuda") for _ in plans]
         pipe = PipelinedGather(bufs, rank, world, host_staging=backend == "gloo")
         # record k of rank r's buffer answers query shards[r][order_r[k]]: the grouping
         # order is fixed per plan, so it crosses once, outside the timed region
@@ -458,6 +456,8 @@ def main():
             pipe.reuse(k)  # the stream waits until batch k-2's gather has read this buffer
         plans[k].run(stream.cuda_stream)
         if pipe is not None:
+            b = bufs[k].data_ptr()
+            plans[k].wire_records(b, b + rows * rw * 4, wpool_cap, stream.cuda_stream)
             pipe.issue(k)
 
     for _ in range(args.warmup):
@@ -487,7 +487,7 @@ def main():
     gather_check = None
     if pipe is not None:
         gather_check = check_gather(pipe, plans[(it[0] - 1) % len(plans)], (it[0] - 1) % len(plans), grid, params,
-                                    shards, orders, counts, rows, rw, cw, ovf_cap, rank, world)
+                                    shards, orders, counts, rows, rw, wpool_cap, rank, world)
     kn = [p_.kernel_ms() for p_ in plans]
     nl = sum(n for _, n in kn)
     kms = sum(ms * n for ms, n in kn) / nl if nl else 0.0

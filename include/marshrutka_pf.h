@@ -248,6 +248,25 @@ int mr_plan_bind_outputs_ex(mr_plan *plan, void *d_results, void *d_commands, vo
 int mr_decode_records(const mr_grid *grid, const mr_params *params, const void *results, const void *commands,
                       uint32_t n, uint32_t max_cmds, const void *overflow, uint64_t overflow_n,
                       mr_result *out, mr_command *pool, uint64_t pool_cap);
+/* Wire records: the plan's last pass re-encoded on the device for a gather, in record
+ * order, mr_wire_row_bytes(max_cmds) = 4 + 8 * max_cmds bytes per query (36 B at
+ * max_cmds 4, against 80 B of mr_plan_device_outputs): the first command's `from` cell and
+ * the command count (or the status) in one word, then {kind|payload, `to` cell} per command.
+ * The metrics and the other `from` cells are left out: mr_decode_wire recomputes them from
+ * the commands exactly (TotalCost::add_assign, src/cost.rs:299-313; a command starts where
+ * the previous one ended, src/pathfinder.rs:223-234).  A label longer than max_cmds has its
+ * commands at d_pool (8 B each, pool_cap commands); one that does not fit reads
+ * MR_ERR_CAPACITY.  Enqueued on `stream` (null: the plan's) after the plan's last pass;
+ * rows and pool are rewritten by the next call.  Needs a grid of at most 2^25 cells.
+ * No reference counterpart (the reference returns labels in process). */
+uint32_t mr_wire_row_bytes(uint32_t max_cmds);
+int mr_plan_wire_records(mr_plan *plan, void *d_rows, void *d_pool, uint32_t pool_cap, void *stream);
+/* Host decoding of n wire rows (and their pool of pool_n commands) over the same grid
+ * and params: out[k] and its commands at cmds[out[k].command_offset ..], exactly what
+ * mr_decode_records gives for the same records.  MR_ERR_CAPACITY if cmd_cap is too small;
+ * MR_ERR_DEVICE for a row that is not well formed.  Needs no device. */
+int mr_decode_wire(const mr_grid *grid, const mr_params *params, const void *rows, uint32_t n, uint32_t max_cmds,
+                   const void *pool, uint64_t pool_n, mr_result *out, mr_command *cmds, uint64_t cmd_cap);
 /* query_of_record[k] = the input query whose output is record k of
  * mr_plan_device_outputs (0xFFFFFFFF past the valid queries), k < n. */
 int mr_plan_record_queries(const mr_plan *plan, uint32_t *query_of_record, uint32_t n);

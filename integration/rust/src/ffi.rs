@@ -184,6 +184,12 @@ extern "C" {
     pub fn mr_decode_records(grid: *const mr_grid, params: *const mr_params, results: *const c_void,
                              commands: *const c_void, n: u32, max_cmds: u32, overflow: *const c_void,
                              overflow_n: u64, out: *mut mr_result, pool: *mut mr_command, pool_cap: u64) -> c_int;
+    pub fn mr_wire_row_bytes(max_cmds: u32) -> u32;
+    pub fn mr_plan_wire_records(plan: *mut mr_plan, d_rows: *mut c_void, d_pool: *mut c_void, pool_cap: u32,
+                                stream: *mut c_void) -> c_int;
+    pub fn mr_decode_wire(grid: *const mr_grid, params: *const mr_params, rows: *const c_void, n: u32, max_cmds: u32,
+                          pool: *const c_void, pool_n: u64, out: *mut mr_result, cmds: *mut mr_command,
+                          cmd_cap: u64) -> c_int;
     pub fn mr_plan_record_queries(plan: *const mr_plan, query_of_record: *mut u32, n: u32) -> c_int;
     pub fn mr_plan_num_sources(plan: *const mr_plan) -> u32;
     pub fn mr_plan_fallback_sources(plan: *mut mr_plan, out: *mut mr_cell_index, cap: u32, n: *mut u32) -> c_int;

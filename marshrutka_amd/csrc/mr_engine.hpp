@@ -295,6 +295,17 @@ enum : uint32_t {
     kWinWords = kWinWhy + 32
 };
 enum : uint32_t { kWinNone = 0, kWinTile = 1, kWinOld = 2, kWinWide = 3 };
+// Wire records (mr_plan_wire_records / mr_decode_wire): a pass's records re-encoded for
+// transfer, 1 + 2 max_cmds 32-bit words each, in record order.  Word 0: the rank of the
+// first command's `from` cell (kWireRankBits) | code << kWireRankBits, code = n_commands
+// for MR_OK (< kWireOvf), kWireOvf for a label whose commands are in the wire pool (slot 0
+// = {offset, count}), kWireStatus + 32 + status for any other status.  Then per command
+// {kind << 29 | payload, rank of its `to` cell}: a command's `from` is the previous one's
+// `to`, and the metrics are the commands' sums (TotalCost::add_assign recomputes them the
+// same way, src/cost.rs:299-313), so neither crosses the wire.  The pool: 2 words a command.
+constexpr uint32_t kWireRankBits = 25, kWireRankMask = (1u << kWireRankBits) - 1u;
+constexpr uint32_t kWireOvf = 64u, kWireStatus = 65u;
+
 // result status (OutResult high half - 16) of a label whose commands went to the
 // overflow pool: its first command slot holds {kOvfTag, offset, count}
 constexpr uint32_t kStatusOverflow = 64u, kOvfTag = 0xFFFFFFFFu;

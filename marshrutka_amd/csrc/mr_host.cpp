@@ -80,6 +80,9 @@ hipError_t launch_cert_promote(const KArgs *d_args, uint32_t slots, uint32_t *re
 constexpr int kCertRounds = 2;  // certificate rounds after the first (cert_promote_kernel decides each slot's)
 int cert_tile_occupancy();
 hipError_t launch_ovf_order(const KArgs *d_args, uint32_t nrec, OutCmd *tmp, hipStream_t stream);
+hipError_t launch_wire(const OutResult *res, const OutCmd *slots, const OutCmd *ovf, const uint32_t *nov, uint32_t ovf_cap,
+                       uint32_t nrec, uint32_t nq, uint32_t mc, uint32_t *rows, uint32_t *wpool, uint32_t wpool_cap,
+                       hipStream_t stream);
 hipError_t decode_records_device(const OutResult *res, const OutCmd *slots, const OutCmd *ovf, uint32_t novf,
                                  const uint32_t *q_id, uint32_t nrec, uint32_t nq, uint32_t mc,
                                  const mr_cell_index *idx_rank, uint32_t V, uint32_t rgt, uint32_t soe, uint32_t shq,
@@ -3537,6 +3540,99 @@ extern "C" int mr_decode_records(const mr_grid *g, const mr_params *prm, const v
     return ret;
 }
 
+extern "C" uint32_t mr_wire_row_bytes(uint32_t max_cmds) { return 4u + 8u * max_cmds; }
+
+extern "C" int mr_plan_wire_records(mr_plan *pl, void *d_rows, void *d_pool, uint32_t pool_cap, void *stream) {
+    if (!pl || (pl->hp.nq && !d_rows) || (pool_cap && !d_pool)) return fail(MR_ERR_INVALID_ARG, "null argument");
+    if (pl->all_mode) return fail(MR_ERR_INVALID_ARG, "wire_records: not a query plan");
+    if (pl->grid->V > kWireRankMask + 1u) return fail(MR_ERR_INVALID_ARG, "wire_records: grid too large for wire records");
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : pl->stream;
+    // ordered after the plan's last pass, whichever stream that ran on
+    if (pl->ev_last && pl->last_stream != s && hipStreamWaitEvent(s, pl->ev_last, 0) != hipSuccess)
+        return fail(MR_ERR_DEVICE, "wait for the last pass");
+    const uint32_t nq = pl->hp.nq, nrec = pl->runs ? nrec_of(pl->hp) : 0u;
+    if (launch_wire(pl->ka.out_res, pl->ka.out_cmd, pl->ka.ovf, pl->d_counter + kCtrLastOvf, pl->ka.ovf_cap, nrec, nq,
+                    pl->hp.p.max_cmds, static_cast<uint32_t *>(d_rows), static_cast<uint32_t *>(d_pool), pool_cap, s) !=
+        hipSuccess)
+        return fail(MR_ERR_DEVICE, "wire kernel");
+    return MR_OK;
+}
+
+// Metrics of a label from its commands (the reference's TotalCost sums, src/cost.rs:299-313;
+// a StandardMove run's time is its Fleetfoot ceil, src/skill.rs:21-30).
+static void wire_metrics(const CmdScale &cs, const uint32_t *cmd, uint32_t n, mr_result &r) {
+    static const uint32_t ffn[4] = {1, 50, 100, 25}, ffd[4] = {1, 53, 109, 28};
+    const uint32_t ff = cs.ff <= 3 ? cs.ff : 0;
+    uint64_t legs = 0, money = 0, t = 0;
+    for (uint32_t j = 0; j < n; ++j) {
+        const uint32_t kind = cmd[2 * j] >> 29, pay = cmd[2 * j] & 0x1FFFFFFFu;
+        switch (kind) {
+            case kCentral: t += uint64_t(10) * pay; break;
+            case kStandard:
+                legs += pay;
+                t += (uint64_t(180) * pay * ffn[ff] + ffd[ff] - 1) / ffd[ff];
+                break;
+            case kCaravan:
+                t += uint64_t(cs.rgt) * (pay >> 1);
+                money += uint64_t(pay >> 1) * ((pay & 1u) ? 5u : 2u);
+                break;
+            case kSoE: money += cs.soe; break;
+            case kSHQ: money += cs.shq; break;
+            case kSFm: money += cs.sfm; break;
+            default: break;
+        }
+    }
+    r.legs = uint32_t(legs);
+    r.money = uint32_t(money);
+    r.time_s = int64_t(t);
+}
+
+extern "C" int mr_decode_wire(const mr_grid *g, const mr_params *prm, const void *rows, uint32_t n, uint32_t max_cmds,
+                              const void *pool, uint64_t pool_n, mr_result *out, mr_command *cmds, uint64_t cmd_cap) {
+    if (!g || !prm || (n && (!rows || !out)) || (pool_n && !pool)) return fail(MR_ERR_INVALID_ARG, "null argument");
+    const CmdScale cs = cmd_scale(*prm);
+    const uint32_t rw = 1u + 2u * max_cmds;
+    const uint32_t *w = static_cast<const uint32_t *>(rows), *wp = static_cast<const uint32_t *>(pool);
+    uint64_t off = 0;
+    int ret = MR_OK;
+    for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t *row = w + size_t(k) * rw;
+        mr_result &r = out[k];
+        std::memset(&r, 0, sizeof(r));
+        r.command_offset = uint32_t(off);
+        const uint32_t code = row[0] >> kWireRankBits;
+        uint32_t from = row[0] & kWireRankMask, nc = 0;
+        const uint32_t *src = row + 1;
+        if (code >= kWireStatus) {
+            r.status = int32_t(code) - int32_t(kWireStatus) - 32;
+            if (r.status != MR_NOT_FOUND && ret == MR_OK) ret = r.status;
+            continue;
+        }
+        if (code == kWireOvf) {
+            if (!max_cmds || uint64_t(row[1]) + row[2] > pool_n) return fail(MR_ERR_DEVICE, "wire pool record");
+            src = wp + 2ull * row[1];
+            nc = row[2];
+        } else {
+            if (code > max_cmds) return fail(MR_ERR_DEVICE, "wire record longer than its command slots");
+            nc = code;
+        }
+        r.status = MR_OK;
+        r.n_commands = nc;
+        wire_metrics(cs, src, nc, r);
+        if (cmds && off + nc <= cmd_cap) {
+            for (uint32_t j = 0; j < nc; ++j) {
+                const OutCmd c{src[2 * j], from, src[2 * j + 1], 0u};
+                if (!expand_cmd(g, cs, c, cmds[off + j])) return fail(MR_ERR_DEVICE, "command names no cell");
+                from = c.to;
+            }
+        } else {
+            ret = MR_ERR_CAPACITY;
+        }
+        off += nc;
+    }
+    return ret;
+}
+
 extern "C" void mr_plan_destroy(mr_plan *pl) {
 #ifdef MR_STAMPS
     if (pl && pl->d_dbg) {  // diagnostic summary: phase cycles summed over workgroups (last launch)
@@ -3678,9 +3774,9 @@ extern "C" int mr_sssp_records(mr_plan *pl, uint32_t i, mr_label_record *out) {
     std::vector<CellWord> words(V);
     std::vector<Rec> tab;
     const uint32_t S = pl->ka.p.S, pitch = pl->ka.rec_pitch;
-    if (hipMemcpy2D(words.data(), S * sizeof(CellWord), pl->d_rec + size_t(si) * S * pitch, pitch * sizeof(CellWord),
-                    S * sizeof(CellWord), S, hipMemcpyDeviceToHost) != hipSuccess)
-        return fail(MR_ERR_DEVICE, "copy records");
+    if (hipError_t e = hipMemcpy2D(words.data(), S * sizeof(CellWord), pl->d_rec + size_t(si) * S * pitch,
+                                   pitch * sizeof(CellWord), S * sizeof(CellWord), S, hipMemcpyDeviceToHost))
+        return fail(MR_ERR_DEVICE, std::string("copy records: ") + hipGetErrorString(e));
     if (int st = sssp_table(pl, si, tab)) return st;
     for (uint32_t v = 0; v < V; ++v)
         if (!expand_word(pl->hp, tab, words[v], out[v])) return fail(MR_ERR_DEVICE, "cell word names no table entry");
@@ -3797,9 +3893,9 @@ extern "C" int mr_sssp_labels(mr_plan *pl, uint32_t i, mr_result *results, mr_co
     const uint32_t V = pl->ka.p.V, S = pl->ka.p.S, pitch = pl->ka.rec_pitch;
     std::vector<CellWord> words(V);
     std::vector<Rec> tab;
-    if (hipMemcpy2D(words.data(), S * sizeof(CellWord), pl->d_rec + size_t(si) * S * pitch, pitch * sizeof(CellWord),
-                    S * sizeof(CellWord), S, hipMemcpyDeviceToHost) != hipSuccess)
-        return fail(MR_ERR_DEVICE, "copy records");
+    if (hipError_t e = hipMemcpy2D(words.data(), S * sizeof(CellWord), pl->d_rec + size_t(si) * S * pitch,
+                                   pitch * sizeof(CellWord), S * sizeof(CellWord), S, hipMemcpyDeviceToHost))
+        return fail(MR_ERR_DEVICE, std::string("copy records: ") + hipGetErrorString(e));
     if (int st = sssp_table(pl, si, tab)) return st;
     const CmdScale cs = cmd_scale(pl->hp);
     std::vector<OutCmd> seq;

@@ -129,6 +129,73 @@ hipError_t decode_records_device(const OutResult *res, const OutCmd *slots, cons
     return e;
 }
 
+// ---- wire records (mr_engine.hpp): the records of a pass re-encoded for transfer -------------
+// One thread per record: 4 + 8 max_cmds bytes instead of 16 + 16 max_cmds (c4: 36 B a query
+// against 80), the metrics left to the decoder; an overflowing label's commands go to the
+// wire pool at the same offsets (wpool_cap commands; past it the record reads
+// MR_ERR_CAPACITY).  nov: the pass's overflow-pool length, read on the device.
+__global__ void wire_kernel(const OutResult *__restrict__ res, const OutCmd *__restrict__ slots,
+                            const OutCmd *__restrict__ ovf, const uint32_t *__restrict__ nov_p, uint32_t ovf_cap,
+                            uint32_t nrec, uint32_t nq, uint32_t mc, uint32_t *__restrict__ rows,
+                            uint32_t *__restrict__ wpool, uint32_t wpool_cap) {
+    const uint32_t nov = min(*nov_p, ovf_cap), rw = 1u + 2u * mc;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nq; k += gridDim.x * blockDim.x) {
+        // rows past the records (queries with an invalid cell index) read MR_ERR_INVALID_INDEX
+        const OutResult o = k < nrec ? res[k] : OutResult{0u, 0u, 0u, uint32_t(16 + MR_ERR_INVALID_INDEX) << 16};
+        const int st = int(o.ncmd_status >> 16) - 16;
+        const uint32_t n = o.ncmd_status & 0xFFFFu;
+        const OutCmd *src = slots + (unsigned long long)k * mc;
+        uint32_t *row = rows + (unsigned long long)k * rw;
+        uint32_t hdr, s0 = 0, s1 = 0;
+        bool copy = false;
+        if (st == MR_OK && n <= mc && n < kWireOvf) {
+            hdr = (n ? (src[0].from & kWireRankMask) : 0u) | (n << kWireRankBits);
+            copy = true;
+        } else if (st == int(kStatusOverflow) && mc) {
+            const OutCmd tag = src[0];
+            if (tag.kp == kOvfTag && tag.to == n && (unsigned long long)tag.from + n <= nov &&
+                (unsigned long long)tag.from + n <= wpool_cap && n) {
+                hdr = (ovf[tag.from].from & kWireRankMask) | (kWireOvf << kWireRankBits);
+                s0 = tag.from;
+                s1 = n;
+                for (uint32_t j = 0; j < n; ++j) {
+                    const OutCmd c = ovf[tag.from + j];
+                    wpool[2ull * (tag.from + j)] = c.kp;
+                    wpool[2ull * (tag.from + j) + 1] = c.to;
+                }
+            } else {
+                hdr = (kWireStatus + 32u + uint32_t(MR_ERR_CAPACITY)) << kWireRankBits;
+            }
+        } else {
+            hdr = (kWireStatus + 32u + uint32_t(st == MR_OK ? MR_ERR_DEVICE : st)) << kWireRankBits;
+        }
+        row[0] = hdr;
+        for (uint32_t j = 0; j < mc; ++j) {
+            uint32_t kp = 0, to = 0;
+            if (copy && j < n) {
+                const OutCmd c = src[j];
+                kp = c.kp;
+                to = c.to;
+            } else if (j == 0) {
+                kp = s0;
+                to = s1;
+            }
+            row[1 + 2 * j] = kp;
+            row[2 + 2 * j] = to;
+        }
+    }
+}
+
+hipError_t launch_wire(const OutResult *res, const OutCmd *slots, const OutCmd *ovf, const uint32_t *nov, uint32_t ovf_cap,
+                       uint32_t nrec, uint32_t nq, uint32_t mc, uint32_t *rows, uint32_t *wpool, uint32_t wpool_cap,
+                       hipStream_t stream) {
+    if (!nq) return hipSuccess;
+    const uint32_t blocks = std::max(1u, std::min(8192u, (nq + 255) / 256));
+    hipLaunchKernelGGL(wire_kernel, dim3(blocks), dim3(256), 0, stream, res, slots, ovf, nov, ovf_cap, nrec, nq, mc, rows,
+                       wpool, wpool_cap);
+    return hipGetLastError();
+}
+
 // ---- byte-deterministic overflow pool -----------------------------------
 // A pass hands out overflow-pool offsets by atomicAdd, in arrival order, so the raw
 // records and the pool differ from run to run in those offsets (the decoded labels do

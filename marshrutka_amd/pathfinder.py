@@ -26,7 +26,7 @@ LIB_PATH = os.environ.get("MR_LIB_PATH") or os.path.join(os.path.dirname(os.path
 EXPORTED_SYMBOLS = [
     "mr_grid_create", "mr_grid_destroy", "mr_grid_square_size", "mr_params_default", "mr_find_path",
     "mr_find_path_batch", "mr_plan_create", "mr_plan_create_ex", "mr_plan_run", "mr_plan_fetch", "mr_plan_device_outputs",
-    "mr_plan_num_sources", "mr_plan_record_queries", "mr_plan_fallback_sources", "mr_plan_handed_over_sources", "mr_plan_wait", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_cache_trim", "mr_host_register", "mr_host_unregister", "mr_plan_bind_outputs", "mr_plan_bind_outputs_ex", "mr_decode_records", "mr_abi_version", "mr_last_error",
+    "mr_plan_num_sources", "mr_plan_record_queries", "mr_plan_fallback_sources", "mr_plan_handed_over_sources", "mr_plan_wait", "mr_plan_get_stats", "mr_plan_kernel_ms", "mr_plan_destroy", "mr_cache_trim", "mr_host_register", "mr_host_unregister", "mr_plan_bind_outputs", "mr_plan_bind_outputs_ex", "mr_decode_records", "mr_wire_row_bytes", "mr_plan_wire_records", "mr_decode_wire", "mr_abi_version", "mr_last_error",
     "mr_device_available", "mr_parse_map_html", "mr_parse_error", "mr_grid_from_html",
     "mr_command_time", "mr_duration_display", "mr_render_schedule", "mr_grid_region_table",
     "mr_sssp_plan_create", "mr_sssp_records", "mr_sssp_device_records", "mr_sssp_record_pitch", "mr_sssp_device_tables", "mr_sssp_label", "mr_sssp_labels", "mr_plan_fill_ms",
@@ -83,6 +83,13 @@ def lib():
         L.mr_decode_records.argtypes = [vp, C.POINTER(mr_params), vp, vp, C.c_uint32, C.c_uint32, vp, C.c_uint64,
                                         C.POINTER(mr_result), C.POINTER(mr_command), C.c_uint64]
         L.mr_decode_records.restype = C.c_int
+        L.mr_wire_row_bytes.argtypes = [C.c_uint32]
+        L.mr_wire_row_bytes.restype = C.c_uint32
+        L.mr_plan_wire_records.argtypes = [vp, vp, vp, C.c_uint32, vp]
+        L.mr_plan_wire_records.restype = C.c_int
+        L.mr_decode_wire.argtypes = [vp, C.POINTER(mr_params), vp, C.c_uint32, C.c_uint32, vp, C.c_uint64,
+                                     C.POINTER(mr_result), C.POINTER(mr_command), C.c_uint64]
+        L.mr_decode_wire.restype = C.c_int
         L.mr_plan_num_sources.argtypes = [vp]
         L.mr_plan_num_sources.restype = C.c_uint32
         L.mr_plan_record_queries.argtypes = [vp, C.POINTER(C.c_uint32), C.c_uint32]
@@ -354,6 +361,31 @@ def decode_records_raw(grid: MapGrid, params: Params, results, commands, n: int,
     return out, pool
 
 
+def wire_row_words(max_cmds: int) -> int:
+    """32-bit words of one wire row (mr_wire_row_bytes / 4)."""
+    return int(lib().mr_wire_row_bytes(max_cmds)) // 4
+
+
+def decode_wire_raw(grid: MapGrid, params: Params, rows, n: int, max_cmds: int, pool=None):
+    """n wire rows (Plan.wire_records layout) and their pool as host buffers, decoded on the
+    host (mr_decode_wire): returns (mr_result array, mr_command pool), row k -> entry k —
+    the same as decode_records_raw gives for the plan's compact records."""
+    import numpy as np
+    w = np.ascontiguousarray(rows, dtype=np.uint32).reshape(-1)
+    wp = np.ascontiguousarray(pool if pool is not None else np.zeros(0), dtype=np.uint32).reshape(-1)
+    if w.size < n * (1 + 2 * max_cmds):
+        raise EngineError(abi.MR_ERR_INVALID_ARG, "decode_wire: buffer shorter than n rows")
+    out = (mr_result * max(n, 1))()
+    cap = int(n * max_cmds + wp.size // 2 + 1)
+    cmds = (mr_command * cap)()
+    p = params.to_c()
+    st = lib().mr_decode_wire(grid.handle, C.byref(p), w.ctypes.data if w.size else None, n, max_cmds,
+                              wp.ctypes.data if wp.size else None, wp.size // 2, out, cmds, cap)
+    if st not in (MR_OK, abi.MR_ERR_INVALID_INDEX, abi.MR_ERR_CAPACITY):  # (per-row statuses are in out[k])
+        raise EngineError(st, last_error())
+    return out, cmds
+
+
 def decode_records(grid: MapGrid, params: Params, results, commands, n: int, max_cmds: int,
                    overflow=None) -> List[Optional[TotalCost]]:
     """decode_records_raw as labels.  A record whose status is not OK / NOT_FOUND raises."""
@@ -515,6 +547,15 @@ class Plan:
         overflow pool of overflow_cap commands): one collective then moves them all."""
         st = lib().mr_plan_bind_outputs_ex(self.handle, C.c_void_p(d_results), C.c_void_p(d_commands),
                                            C.c_void_p(d_overflow) if d_overflow else None, overflow_cap)
+        if st != MR_OK:
+            raise EngineError(st, last_error())
+
+    def wire_records(self, d_rows: int, d_pool: int = 0, pool_cap: int = 0, stream=None) -> None:
+        """Enqueues the wire encoding of the last pass (mr_plan_wire_records) into caller
+        device memory: n rows of wire_row_words(max_cmds) words at d_rows and the pool of
+        long labels (pool_cap commands, 8 B each) at d_pool — what a gather then moves."""
+        st = lib().mr_plan_wire_records(self.handle, C.c_void_p(d_rows), C.c_void_p(d_pool) if d_pool else None,
+                                        pool_cap, C.c_void_p(stream) if stream else None)
         if st != MR_OK:
             raise EngineError(st, last_error())
 

@@ -150,6 +150,113 @@ def test_decode_records_on_host(eng):
         eng.decode_records(g, p, res, bad, 3, 2, pool)
 
 
+def test_decode_wire_on_host(eng):
+    """mr_decode_wire: wire rows (first `from` rank | count, then {kind|payload, `to`}) with
+    the metrics left out decode to the same full labels as the compact records."""
+    import numpy as np
+    from marshrutka_amd.abi import GREEN, Command, TotalCost
+    m = SyntheticMap(7, campfires_per_homeland=1, seed=4)
+    g = eng.MapGrid(m.cells())
+    rk = _ranks(m)
+    b33, c, g33 = CellIndex.homeland(BLUE, 3, 3), CellIndex.center(), CellIndex.homeland(GREEN, 3, 3)
+    car = lambda d, five: (3 << 29) | (d << 1) | five  # noqa: E731
+    want = TotalCost(0, 42, 2880, [Command(3, 1440, 0, 12, 0, b33, c), Command(3, 1440, 0, 30, 0, c, g33)])
+    p = Params(route_guru=0)
+    # max_cmds 2: the label in its slots, NOT_FOUND, the label in the pool at offset 3,
+    # a capacity row (what the encoder writes for a label past the pool)
+    st = lambda s_: (65 + 32 + s_) << 25  # noqa: E731
+    rows = np.array([[rk[b33] | 2 << 25, car(6, 0), rk[c], car(6, 1), rk[g33]],
+                     [st(1), 0, 0, 0, 0],
+                     [rk[b33] | 64 << 25, 3, 2, 0, 0],
+                     [st(-4), 0, 0, 0, 0]], dtype=np.uint32)
+    pool = np.zeros((5, 2), dtype=np.uint32)
+    pool[3:5] = [[car(6, 0), rk[c]], [car(6, 1), rk[g33]]]
+    out, cmds = eng.decode_wire_raw(g, p, rows, 4, 2, pool)
+    lab = [eng.result_from_c(out[k], cmds) if out[k].status == 0 else out[k].status for k in range(4)]
+    assert lab[0].as_tuple() == want.as_tuple() and lab[2].as_tuple() == want.as_tuple()
+    assert lab[1] == 1 and lab[3] == -4
+    assert eng.wire_row_words(4) == 9  # 36 B a query at max_cmds 4
+    with pytest.raises(eng.EngineError, match="DEVICE"):  # a pool reference past the pool
+        eng.decode_wire_raw(g, p, rows, 4, 2, pool[:4])
+
+
+@pytest.mark.parametrize("ff,rg", [(0, 0), (1, 3), (2, 5), (3, 1), (7, 2)])
+def test_decode_wire_matches_decode_records(eng, ff, rg):
+    """Random command chains of every kind: the wire decoder's recomputed metrics
+    (Fleetfoot ceil per StandardMove run, caravan time and coefficient, scroll prices)
+    and commands equal mr_decode_records over the same labels with the metrics given."""
+    import random as _r
+    from fractions import Fraction
+
+    import numpy as np
+    m = SyntheticMap(15, campfires_per_homeland=3, seed=ff + 11)
+    g = eng.MapGrid(m.cells())
+    V = len(m.all_indices())
+    p = Params(fleetfoot=ff, route_guru=rg, scroll_of_escape_cost=7, scroll_of_escape_hq_cost=11,
+               scroll_of_escape_forum_cost=13)
+    ffr = {0: Fraction(1), 1: Fraction(50, 53), 2: Fraction(100, 109), 3: Fraction(25, 28)}.get(ff, Fraction(1))
+    rgt = {0: 240, 1: 190, 2: 168, 3: 146, 4: 124, 5: 102}[rg]  # ceil(240 * RouteGuru ratio)
+    rng = _r.Random(ff * 31 + rg)
+    n, mc = 300, 3
+    res = np.zeros((n, 4), dtype=np.uint32)
+    slots = np.zeros((n, mc, 4), dtype=np.uint32)
+    rows = np.zeros((n, 1 + 2 * mc), dtype=np.uint32)
+    ovf, wpool = [], []
+    for k in range(n):
+        if rng.random() < 0.05:
+            res[k, 3] = 17 << 16
+            rows[k, 0] = (65 + 32 + 1) << 25
+            continue
+        nc = rng.randint(0, 6)
+        at = rng.randrange(V)
+        first = at
+        legs = money = t = 0
+        seq = []
+        for _ in range(nc):
+            kind = rng.randint(1, 6)
+            if kind == 1:
+                pay = rng.randint(1, 20)
+                t += 10 * pay
+            elif kind == 2:
+                pay = rng.randint(1, 400)
+                legs += pay
+                t += -((-ffr * 180 * pay).numerator // (ffr * 180 * pay).denominator)
+            elif kind == 3:
+                d, five = rng.randint(1, 600), rng.randint(0, 1)
+                pay = d << 1 | five
+                t += rgt * d
+                money += d * (5 if five else 2)
+            else:
+                pay = 0
+                money += {4: 7, 5: 11, 6: 13}[kind]
+            to = rng.randrange(V)
+            seq.append([(kind << 29) | pay, at, to, 0])
+            at = to
+        res[k] = [legs, money, t, (16 << 16) | nc]
+        if nc <= mc:
+            slots[k, :nc] = seq if nc else 0
+            rows[k, 0] = (first if nc else 0) | nc << 25
+            for j, s_ in enumerate(seq):
+                rows[k, 1 + 2 * j:3 + 2 * j] = [s_[0], s_[2]]
+        else:
+            res[k, 3] = (80 << 16) | nc
+            slots[k, 0] = [0xFFFFFFFF, len(ovf), nc, 0]
+            rows[k, 0] = first | 64 << 25
+            rows[k, 1:3] = [len(ovf), nc]
+            ovf += seq
+            wpool += [[s_[0], s_[2]] for s_ in seq]
+    ovf = np.array(ovf, dtype=np.uint32).reshape(-1, 4)
+    wpool = np.array(wpool, dtype=np.uint32).reshape(-1, 2)
+    a_out, a_pool = eng.decode_records_raw(g, p, res, slots, n, mc, ovf)
+    b_out, b_pool = eng.decode_wire_raw(g, p, rows, n, mc, wpool)
+    for k in range(n):
+        fa = [getattr(a_out[k], f) for f, _ in a_out[k]._fields_]
+        fb = [getattr(b_out[k], f) for f, _ in b_out[k]._fields_]
+        assert fa == fb, k
+    ncmd = sum(a_out[k].n_commands for k in range(n))
+    assert bytes(memoryview(a_pool)[:ncmd]) == bytes(memoryview(b_pool)[:ncmd])
+
+
 def test_labels_digest_follows_query_order(eng):
     """labels_digest (the N > 1 gather check): the same labels stored in another
     order hash alike once the order is given, and differently without it."""

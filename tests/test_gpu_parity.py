@@ -553,6 +553,57 @@ def test_overflow_pool_bound_in_record_order(eng, oracle_lib, grid_state):
         assert all((s == snaps[0]).all() for s in snaps), "raw outputs differ between passes / plans"
 
 
+@pytest.mark.parametrize("mc,ff,sort_by", [(2, 0, (SORT_LEGS, SORT_MONEY)), (4, 2, (SORT_TIME, SORT_MONEY)),
+                                            (3, 3, (SORT_MONEY, SORT_TIME)), (16, 1, (SORT_TIME, SORT_LEGS))])
+def test_wire_records_match_oracle(eng, oracle_lib, grid_state, mc, ff, sort_by):
+    """mr_plan_wire_records (what the N > 1 gather moves, 4 + 8 max_cmds bytes a query)
+    decoded on the host by mr_decode_wire: every label equals the oracle's and the plan's
+    own fetch — metrics recomputed from the commands, `from` cells from the chain, long
+    labels through the wire pool, rows past the records (invalid queries) INVALID_INDEX."""
+    import ctypes as C
+
+    import numpy as np
+    from marshrutka_amd.abi import MR_ERR_INVALID_INDEX
+    hip = C.CDLL("libamdhip64.so.7")
+    hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+    hip.hipMemset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    hip.hipFree.argtypes = [C.c_void_p]
+    m = SyntheticMap(33, campfires_per_homeland=5, seed=21 + mc, clustered=True)
+    g = eng.MapGrid(m.cells())
+    og = oracle_lib.OracleGrid(m.cells())
+    params = Params(fleetfoot=ff, sort_by=sort_by, use_sfm=mc == 3, route_guru=mc % 6)
+    qs = random_queries(m, 400, 5 + mc)
+    exp = [as_expected(e) for e in og.find_path_batch(params, qs, threads=0)]
+    qs_all = qs + [(CellIndex.center(), CellIndex.homeland(BLUE, 99, 99))] * 3
+    n, rw, pcap = len(qs_all), eng.wire_row_words(mc), 4 * len(qs_all)
+    nw = n * rw + 2 * pcap
+    dbuf = C.c_void_p()
+    assert hip.hipMalloc(C.byref(dbuf), nw * 4) == 0 and hip.hipMemset(dbuf, 0, nw * 4) == 0
+    try:
+        plan = eng.Plan(g, params, qs_all, max_cmds=mc)
+        for _pass in range(2):
+            plan.run()
+            plan.wire_records(dbuf.value, dbuf.value + n * rw * 4, pcap)
+            plan.wait()
+            host = np.zeros(nw, dtype=np.uint32)
+            assert hip.hipMemcpy(host.ctypes.data, dbuf, nw * 4, 2) == 0
+            out, cmds = eng.decode_wire_raw(g, params, host[: n * rw], n, mc, host[n * rw:])
+            q_of = plan.record_queries()
+            got = [None] * len(qs)
+            for k in range(n):
+                if k >= len(qs):
+                    assert out[k].status == MR_ERR_INVALID_INDEX and q_of[k] == 0xFFFFFFFF
+                    continue
+                got[q_of[k]] = as_expected(eng.result_from_c(out[k], cmds)) if out[k].status == 0 else None
+            assert got == exp
+        assert mc != 2 or any(len(e[3]) > mc for e in exp if e)
+        assert [as_expected(r) for r in plan.fetch()[: len(qs)]] == exp
+        del plan
+    finally:
+        hip.hipFree(dbuf)
+
+
 @pytest.mark.parametrize("kernel", ["hub", "lane", "group8", "group32"])
 @pytest.mark.parametrize("ff", [1, 2, 3])
 @pytest.mark.parametrize("sort_by", [(SORT_LEGS, SORT_MONEY), (SORT_LEGS, SORT_TIME), (SORT_MONEY, SORT_LEGS),
