@@ -232,7 +232,7 @@ __global__ __launch_bounds__(kTileBS) void cert_tile_kernel(const KArgs *__restr
     __shared__ uint32_t gbase[64], legs_id[64];    // per boundary its G; per id its boundary's legs
     __shared__ uint8_t inv[64];                    // id -> table entry
     __shared__ uint32_t fixedb[kTileN / 32];       // cells that are not window plain cells
-    __shared__ uint32_t jobs[64][2], njobs, nev, ev_ptr, flag, unset, nsettle;
+    __shared__ uint32_t jobs[64][2], njobs, nev, ev_ptr, flag, unset;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, P = gridDim.x;
     const uint32_t nslot = min(a->cert_cap, __hip_atomic_load(a->counter + kCtrCert, __ATOMIC_RELAXED,
                                                                __HIP_MEMORY_SCOPE_AGENT));
@@ -286,7 +286,6 @@ __global__ __launch_bounds__(kTileBS) void cert_tile_kernel(const KArgs *__restr
             nev = 0;
             ev_ptr = 0;
             flag = 0;
-            nsettle = 0;
         }
         __syncthreads();
         // keys: ranks of the boundaries (id unique: the lists differ), money ranks
@@ -470,7 +469,6 @@ __global__ __launch_bounds__(kTileBS) void cert_tile_kernel(const KArgs *__restr
                     if (lane == 0) ev_ptr = p0;
                 }
                 const uint32_t nl = cnt[j & 3u];
-                if (tid == 0) nsettle += nl;
                 if (nl <= kTileList) {
                     for (uint32_t e = tid; e < nl; e += kTileBS) {
                         const uint32_t n = lst[j & 3u][e];

@@ -81,8 +81,12 @@ constexpr int kCertRounds = 2;  // certificate rounds after the first (cert_prom
 int cert_tile_occupancy();
 hipError_t launch_ovf_order(const KArgs *d_args, uint32_t nrec, OutCmd *tmp, hipStream_t stream);
 hipError_t launch_wire(const OutResult *res, const OutCmd *slots, const OutCmd *ovf, const uint32_t *nov, uint32_t ovf_cap,
-                       uint32_t nrec, uint32_t nq, uint32_t mc, uint32_t *rows, uint32_t *wpool, uint32_t wpool_cap,
-                       hipStream_t stream);
+                       uint32_t nrec, uint32_t nq, uint32_t mc, const uint32_t *q_id, uint32_t *rows, uint32_t *wpool,
+                       uint32_t wpool_cap, hipStream_t stream);
+hipError_t wire_fetch_device(const OutResult *res, const OutCmd *slots, const OutCmd *ovf, const uint32_t *nov,
+                             uint32_t ovf_cap, const uint32_t *q_id, uint32_t nrec, uint32_t nq, uint32_t mc, uint32_t *cnt,
+                             uint32_t *off, void *temp, size_t *temp_bytes, uint32_t *rows, uint32_t *wpool,
+                             uint32_t wpool_cap, hipStream_t stream);
 hipError_t decode_records_device(const OutResult *res, const OutCmd *slots, const OutCmd *ovf, uint32_t novf,
                                  const uint32_t *q_id, uint32_t nrec, uint32_t nq, uint32_t mc,
                                  const mr_cell_index *idx_rank, uint32_t V, uint32_t rgt, uint32_t soe, uint32_t shq,
@@ -207,6 +211,8 @@ struct mr_grid {
     // plans (the grid outlives its plans): one per (device, homeland), so a plan never
     // reads a table that lives on another device
     mutable std::map<std::pair<int, int>, uint32_t *> d_near;
+    // CellIndex of each rank, built on first use by a wire fetch (idx_of_rank)
+    mutable std::vector<mr_cell_index> idx_rank_h;
     // device copies shared by the grid's plans on one device (the first plan's): the rank
     // tables, and per (query homeland, HQ cell) the special / region word of every cell
     // (sinfo: it depends on the special order, fixed by those two)
@@ -3445,10 +3451,13 @@ static bool plan_fetch_device(mr_plan *pl, mr_result *results, mr_command *pool,
     return true;
 }
 
+static bool plan_fetch_wire(mr_plan *pl, mr_result *results, mr_command *pool, uint64_t pool_cap, int &ret);
+
 extern "C" int mr_plan_fetch(mr_plan *pl, mr_result *results, mr_command *pool, uint64_t pool_cap) {
     if (!pl || (pl->hp.nq && !results)) return fail(MR_ERR_INVALID_ARG, "null argument");
     {
         int ret = MR_OK;
+        if (plan_fetch_wire(pl, results, pool, pool_cap, ret)) return ret;
         if (plan_fetch_device(pl, results, pool, pool_cap, ret)) return ret;
     }
     const double tm0 = timing_on() ? now_ms() : 0.0;
@@ -3552,7 +3561,8 @@ extern "C" int mr_plan_wire_records(mr_plan *pl, void *d_rows, void *d_pool, uin
         return fail(MR_ERR_DEVICE, "wait for the last pass");
     const uint32_t nq = pl->hp.nq, nrec = pl->runs ? nrec_of(pl->hp) : 0u;
     if (launch_wire(pl->ka.out_res, pl->ka.out_cmd, pl->ka.ovf, pl->d_counter + kCtrLastOvf, pl->ka.ovf_cap, nrec, nq,
-                    pl->hp.p.max_cmds, static_cast<uint32_t *>(d_rows), static_cast<uint32_t *>(d_pool), pool_cap, s) !=
+                    pl->hp.p.max_cmds, nullptr, static_cast<uint32_t *>(d_rows), static_cast<uint32_t *>(d_pool), pool_cap,
+                    s) !=
         hipSuccess)
         return fail(MR_ERR_DEVICE, "wire kernel");
     return MR_OK;
@@ -3587,6 +3597,45 @@ static void wire_metrics(const CmdScale &cs, const uint32_t *cmd, uint32_t n, mr
     r.time_s = int64_t(t);
 }
 
+// Decodes wire row `row` (max_cmds mc, the pool wp of pool_n commands) into r, its commands
+// into cmds[off..] when they fit cmd_cap (else *ret = MR_ERR_CAPACITY).  MR_OK, or
+// MR_ERR_DEVICE for a row that is not well formed.
+static int decode_wire_row(const mr_grid *g, const CmdScale &cs, const uint32_t *row, uint32_t mc, const uint32_t *wp,
+                           uint64_t pool_n, mr_result &r, mr_command *cmds, uint64_t cmd_cap, uint64_t &off, int &ret) {
+    std::memset(&r, 0, sizeof(r));
+    r.command_offset = uint32_t(off);
+    const uint32_t code = row[0] >> kWireRankBits;
+    uint32_t from = row[0] & kWireRankMask, nc = 0;
+    const uint32_t *src = row + 1;
+    if (code >= kWireStatus) {
+        r.status = int32_t(code) - int32_t(kWireStatus) - 32;
+        if (r.status != MR_NOT_FOUND && ret == MR_OK) ret = r.status;
+        return MR_OK;
+    }
+    if (code == kWireOvf) {
+        if (!mc || uint64_t(row[1]) + row[2] > pool_n) return fail(MR_ERR_DEVICE, "wire pool record");
+        src = wp + 2ull * row[1];
+        nc = row[2];
+    } else {
+        if (code > mc) return fail(MR_ERR_DEVICE, "wire record longer than its command slots");
+        nc = code;
+    }
+    r.status = MR_OK;
+    r.n_commands = nc;
+    wire_metrics(cs, src, nc, r);
+    if (cmds && off + nc <= cmd_cap) {
+        for (uint32_t j = 0; j < nc; ++j) {
+            const OutCmd c{src[2 * j], from, src[2 * j + 1], 0u};
+            if (!expand_cmd(g, cs, c, cmds[off + j])) return fail(MR_ERR_DEVICE, "command names no cell");
+            from = c.to;
+        }
+    } else {
+        ret = MR_ERR_CAPACITY;
+    }
+    off += nc;
+    return MR_OK;
+}
+
 extern "C" int mr_decode_wire(const mr_grid *g, const mr_params *prm, const void *rows, uint32_t n, uint32_t max_cmds,
                               const void *pool, uint64_t pool_n, mr_result *out, mr_command *cmds, uint64_t cmd_cap) {
     if (!g || !prm || (n && (!rows || !out)) || (pool_n && !pool)) return fail(MR_ERR_INVALID_ARG, "null argument");
@@ -3595,42 +3644,245 @@ extern "C" int mr_decode_wire(const mr_grid *g, const mr_params *prm, const void
     const uint32_t *w = static_cast<const uint32_t *>(rows), *wp = static_cast<const uint32_t *>(pool);
     uint64_t off = 0;
     int ret = MR_OK;
-    for (uint32_t k = 0; k < n; ++k) {
-        const uint32_t *row = w + size_t(k) * rw;
-        mr_result &r = out[k];
-        std::memset(&r, 0, sizeof(r));
-        r.command_offset = uint32_t(off);
-        const uint32_t code = row[0] >> kWireRankBits;
-        uint32_t from = row[0] & kWireRankMask, nc = 0;
-        const uint32_t *src = row + 1;
-        if (code >= kWireStatus) {
-            r.status = int32_t(code) - int32_t(kWireStatus) - 32;
-            if (r.status != MR_NOT_FOUND && ret == MR_OK) ret = r.status;
-            continue;
-        }
-        if (code == kWireOvf) {
-            if (!max_cmds || uint64_t(row[1]) + row[2] > pool_n) return fail(MR_ERR_DEVICE, "wire pool record");
-            src = wp + 2ull * row[1];
-            nc = row[2];
-        } else {
-            if (code > max_cmds) return fail(MR_ERR_DEVICE, "wire record longer than its command slots");
-            nc = code;
-        }
-        r.status = MR_OK;
-        r.n_commands = nc;
-        wire_metrics(cs, src, nc, r);
-        if (cmds && off + nc <= cmd_cap) {
-            for (uint32_t j = 0; j < nc; ++j) {
-                const OutCmd c{src[2 * j], from, src[2 * j + 1], 0u};
-                if (!expand_cmd(g, cs, c, cmds[off + j])) return fail(MR_ERR_DEVICE, "command names no cell");
-                from = c.to;
-            }
-        } else {
-            ret = MR_ERR_CAPACITY;
-        }
-        off += nc;
-    }
+    for (uint32_t k = 0; k < n; ++k)
+        if (int st = decode_wire_row(g, cs, w + size_t(k) * rw, max_cmds, wp, pool_n, out[k], cmds, cmd_cap, off, ret))
+            return st;
     return ret;
+}
+
+// the grid's CellIndex-by-rank table on the host (one lookup a command instead of two)
+static const mr_cell_index *idx_of_rank(const mr_grid *g) {
+    std::lock_guard<std::mutex> lk(g->near_mu);
+    if (g->idx_rank_h.size() != g->V) {
+        std::vector<mr_cell_index> t(g->V);
+        for (uint32_t r = 0; r < g->V; ++r) t[r] = g->idx[g->rank_inv[r]];
+        g->idx_rank_h.swap(t);
+    }
+    return g->idx_rank_h.data();
+}
+
+static inline uint64_t cell_bits(const mr_cell_index &c) {
+    uint64_t b;
+    std::memcpy(&b, &c, 8);
+    return b;
+}
+static inline void nt_store(void *dst, const uint64_t *q, int n) {
+    uint64_t *d = static_cast<uint64_t *>(dst);
+    for (int i = 0; i < n; ++i) __builtin_nontemporal_store(q[i], d + i);
+}
+
+// decode_wire_row for the fetch: the same outputs, written with streaming stores (the
+// caller's arrays are written once and not read back here: no read-for-ownership of
+// their lines), cells from the rank table, a command's `from` as the previous `to`.
+// Returns MR_OK or MR_ERR_DEVICE (a row that is not well formed; *bad names it).
+static int fetch_wire_row(const uint32_t *row, uint32_t mc, const uint32_t *wp, uint64_t pool_n, const mr_cell_index *cell,
+                          uint32_t V, const CmdScale &cs, const uint32_t ffn, const uint32_t ffd, mr_result &r,
+                          mr_command *cmds, uint64_t cmd_cap, uint64_t &off, int &ret, const char *&bad) {
+    const uint32_t code = row[0] >> kWireRankBits;
+    uint32_t from = row[0] & kWireRankMask, nc = 0;
+    const uint32_t *src = row + 1;
+    uint64_t q[5];
+    if (code >= kWireStatus) {
+        const int32_t st = int32_t(code) - int32_t(kWireStatus) - 32;
+        if (st != MR_NOT_FOUND && ret == MR_OK) ret = st;
+        q[0] = q[1] = 0;
+        q[2] = uint64_t(uint32_t(off)) << 32;
+        q[3] = uint64_t(uint32_t(st));
+        nt_store(&r, q, 4);
+        return MR_OK;
+    }
+    if (code == kWireOvf) {
+        if (!mc || uint64_t(row[1]) + row[2] > pool_n) return (bad = "wire pool record"), MR_ERR_DEVICE;
+        src = wp + 2ull * row[1];
+        nc = row[2];
+    } else {
+        if (code > mc) return (bad = "wire record longer than its command slots"), MR_ERR_DEVICE;
+        nc = code;
+    }
+    const bool put = cmds && off + nc <= cmd_cap;
+    if (!put) ret = MR_ERR_CAPACITY;
+    uint64_t legs = 0, money = 0, t = 0;
+    if (nc && from >= V) return (bad = "command names no cell"), MR_ERR_DEVICE;
+    uint64_t fbits = nc ? cell_bits(cell[from]) : 0;
+    for (uint32_t j = 0; j < nc; ++j) {
+        const uint32_t kp = src[2 * j], to = src[2 * j + 1], kind = kp >> 29, pay = kp & 0x1FFFFFFFu;
+        if (kind > kSFm || to >= V) return (bad = "command names no cell"), MR_ERR_DEVICE;
+        uint32_t cl = 0, cm = 0, cf = 0;
+        uint64_t ct = 0;
+        switch (kind) {
+            case kCentral: ct = uint64_t(10) * pay; break;
+            case kStandard:
+                cl = pay;
+                ct = uint64_t(180) * pay;
+                cf = cs.ff;
+                t += (ct * ffn + ffd - 1) / ffd;
+                ct = uint64_t(180) * pay;
+                break;
+            case kCaravan:
+                ct = uint64_t(cs.rgt) * (pay >> 1);
+                cm = (pay >> 1) * ((pay & 1u) ? 5u : 2u);
+                break;
+            case kSoE: cm = cs.soe; break;
+            case kSHQ: cm = cs.shq; break;
+            case kSFm: cm = cs.sfm; break;
+            default: break;
+        }
+        legs += cl;
+        money += cm;
+        if (kind != kStandard) t += ct;
+        const uint64_t tbits = cell_bits(cell[to]);
+        if (put) {
+            q[0] = uint64_t(kind) | uint64_t(cl) << 32;
+            q[1] = uint64_t(cm) | uint64_t(cf) << 32;
+            q[2] = ct;
+            q[3] = fbits;
+            q[4] = tbits;
+            nt_store(&cmds[off + j], q, 5);
+        }
+        fbits = tbits;
+    }
+    q[0] = uint64_t(uint32_t(legs)) | uint64_t(uint32_t(money)) << 32;
+    q[1] = t;
+    q[2] = uint64_t(nc) | uint64_t(uint32_t(off)) << 32;
+    q[3] = uint64_t(uint32_t(MR_OK));
+    nt_store(&r, q, 4);
+    off += nc;
+    return MR_OK;
+}
+
+// mr_plan_fetch through wire rows: the pass re-encoded on the device in query order
+// (wire_kernel, 4 + 8 max_cmds bytes a query instead of the 32 B result and 32 B per
+// command the device decoder writes), copied in chunks into the pinned stage, and decoded
+// on the host pool while the next chunk is in flight; a chunk's command offsets continue
+// the previous chunk's.  Same outputs and status rules as plan_fetch_device.  Returns
+// false (nothing written) when it does not apply.
+static bool plan_fetch_wire(mr_plan *pl, mr_result *results, mr_command *pool, uint64_t pool_cap, int &ret) {
+    const HostPlan &hp = pl->hp;
+    const uint32_t nq = hp.nq, nrec = nrec_of(hp), mc = hp.p.max_cmds, rw = 2u + 2u * mc;  // (+ the offset word)
+    const char *fw = std::getenv("MR_FETCH_WIRE");  // (0: the device decoder, plan_fetch_device)
+    if ((fw && !std::strcmp(fw, "0")) || !pool || !nq || pl->all_mode || pl->grid->V > kWireRankMask + 1u || !pl->d_qi)
+        return false;
+    if (const char *e = std::getenv("MR_HOST_DECODE"))
+        if (!std::strcmp(e, "1")) return false;
+    const double tm0 = timing_on() ? now_ms() : 0.0;
+    uint32_t flags = 0, ctr[kCtrWords];
+    if ((ret = check_device_errors(pl, flags, ctr)) != MR_OK) return true;  // (syncs the plan)
+    const uint32_t nov = std::min(ctr[kCtrLastOvf], pl->ka.ovf_cap);
+    const size_t rows_b = size_t(nq) * rw * 4, pool_b = size_t(nov) * 8, cnt_b = (size_t(nq) * 4 + 255) / 256 * 256;
+    size_t temp_b = 0;
+    (void)wire_fetch_device(nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0, nq, mc, nullptr, nullptr, nullptr, &temp_b,
+                            nullptr, nullptr, 0, pl->stream);
+    const size_t rows_at = 2 * cnt_b + (temp_b + 255) / 256 * 256;
+    void *d_wire = nullptr;
+    if (pmalloc(&d_wire, rows_at + rows_b + pool_b + 8) != hipSuccess) return false;
+    char *dw = static_cast<char *>(d_wire);
+    uint32_t *d_cnt = reinterpret_cast<uint32_t *>(dw), *d_off = reinterpret_cast<uint32_t *>(dw + cnt_b);
+    uint32_t *d_rows = reinterpret_cast<uint32_t *>(dw + rows_at), *d_pool = d_rows + size_t(nq) * rw;
+    PinnedStage &stg = stage_down();
+    std::lock_guard<std::mutex> lk(stg.mu);
+    char *h = static_cast<char *>(stg.get(rows_b + pool_b + 8));
+    if (!h) {
+        pfree(d_wire);
+        return false;
+    }
+    const uint32_t *h_rows = reinterpret_cast<const uint32_t *>(h), *h_pool = h_rows + size_t(nq) * rw;
+    // chunks of rows copied one after the other, the pool first (the rows of any chunk may
+    // point into it); each host part decodes its share of a chunk once that has landed
+    const uint32_t nch = nq >= (1u << 18) ? 8u : 1u;
+    std::vector<hipEvent_t> ev(nch, nullptr);
+    hipError_t e = wire_fetch_device(pl->ka.out_res, pl->ka.out_cmd, pl->ka.ovf, pl->d_counter + kCtrLastOvf, pl->ka.ovf_cap,
+                                     pl->d_qi, nrec, nq, mc, d_cnt, d_off, dw + 2 * cnt_b, &temp_b, d_rows, d_pool, nov,
+                                     pl->stream);
+    if (e == hipSuccess && pool_b) e = hipMemcpyAsync(h + rows_b, d_pool, pool_b, hipMemcpyDeviceToHost, pl->stream);
+    for (uint32_t c = 0; c < nch && e == hipSuccess; ++c) {
+        const size_t lo = size_t(chunk_lo(nq, nch, c)) * rw * 4, hi = size_t(chunk_lo(nq, nch, c + 1)) * rw * 4;
+        e = hipMemcpyAsync(h + lo, reinterpret_cast<char *>(d_rows) + lo, hi - lo, hipMemcpyDeviceToHost, pl->stream);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[c], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(ev[c], pl->stream);
+    }
+    const double tm1 = timing_on() ? now_ms() : 0.0;
+    HostPool &hpool = HostPool::get();
+    const CmdScale cs = cmd_scale(hp);
+    static const uint32_t ffn_t[4] = {1, 50, 100, 25}, ffd_t[4] = {1, 53, 109, 28};
+    const uint32_t ffn = ffn_t[cs.ff <= 3 ? cs.ff : 0], ffd = ffd_t[cs.ff <= 3 ? cs.ff : 0];
+    const mr_cell_index *cell = idx_of_rank(pl->grid);
+    const uint32_t V = pl->grid->V;
+    const uint32_t parts = nq >= 65536u ? hpool.size() : 1u;
+    // per (chunk, part): the first error status in its queries, or MR_ERR_CAPACITY
+    std::vector<int32_t> p_ret(size_t(nch) * parts, MR_OK), p_err(parts, MR_OK);
+    std::vector<const char *> p_msg(parts, nullptr);
+    std::vector<hipError_t> p_e(parts, hipSuccess);
+    if (e == hipSuccess)
+        hpool.run(parts, [&](uint32_t pt) {
+            for (uint32_t c = 0; c < nch; ++c) {
+                if (hipError_t x = hipEventSynchronize(ev[c])) {
+                    p_e[pt] = x;
+                    break;
+                }
+                const uint32_t q0 = chunk_lo(nq, nch, c), nc = chunk_lo(nq, nch, c + 1) - q0;
+                const uint32_t i0 = q0 + chunk_lo(nc, parts, pt), i1 = q0 + chunk_lo(nc, parts, pt + 1);
+                // (device-grouped plans: the invalid queries from their sorted list)
+                auto inv = std::lower_bound(hp.invalid.begin(), hp.invalid.end(), i0);
+                int32_t rt = MR_OK;
+                for (uint32_t i = i0; i < i1; ++i) {
+                    mr_result &r = results[i];
+                    int32_t qs = MR_OK;
+                    if (hp.dev_grouped) {
+                        if (inv != hp.invalid.end() && *inv == i) {
+                            qs = MR_ERR_INVALID_INDEX;
+                            ++inv;
+                        }
+                    } else {
+                        qs = hp.q_status[i];
+                    }
+                    if (qs != MR_OK) {
+                        const uint64_t z[4] = {0, 0, 0, uint64_t(uint32_t(qs))};
+                        nt_store(&r, z, 4);
+                        if (rt == MR_OK) rt = qs;
+                        continue;
+                    }
+                    const uint32_t *row = h_rows + size_t(i) * rw;
+                    uint64_t o = row[rw - 1];
+                    int rr = MR_OK;
+                    const char *bad = nullptr;
+                    if (int st = fetch_wire_row(row, mc, h_pool, nov, cell, V, cs, ffn, ffd, r, pool, pool_cap, o, rr, bad)) {
+                        p_err[pt] = st;
+                        p_msg[pt] = bad;
+                        __builtin_ia32_sfence();
+                        return;
+                    }
+                    if (rr == MR_ERR_CAPACITY) rt = MR_ERR_CAPACITY;  // (a short pool wins over other errors)
+                    else if (rt == MR_OK && rr != MR_OK) rt = rr;
+                }
+                p_ret[size_t(c) * parts + pt] = rt;
+            }
+            __builtin_ia32_sfence();  // (the streaming stores drain before the pool's completion count)
+        });
+    ret = MR_OK;
+    int32_t err = MR_OK;
+    const char *msg = nullptr;
+    for (uint32_t pt = 0; pt < parts; ++pt) {
+        if (e == hipSuccess && p_e[pt] != hipSuccess) e = p_e[pt];
+        if (err == MR_OK && p_err[pt] != MR_OK) {
+            err = p_err[pt];
+            msg = p_msg[pt];
+        }
+    }
+    for (int32_t x : p_ret) {  // (chunk-major, part-minor: query order)
+        if (x == MR_ERR_CAPACITY) ret = MR_ERR_CAPACITY;
+        else if (ret == MR_OK) ret = x;
+    }
+    // the device block goes back to the cache, which hands it out with no implicit sync
+    (void)hipStreamSynchronize(pl->stream);
+    for (hipEvent_t x : ev)
+        if (x) (void)hipEventDestroy(x);
+    pfree(d_wire);
+    if (e != hipSuccess) return (ret = fail(MR_ERR_DEVICE, std::string("wire fetch: ") + hipGetErrorString(e))), true;
+    if (err != MR_OK) return (ret = fail(err, msg ? msg : "wire row")), true;
+    if (timing_on())
+        std::fprintf(stderr, "MR_TIMING fetch n=%u (wire, %u chunks, %u parts): enqueue %.2f ms, copies + host decode %.2f ms\n",
+                     nq, nch, parts, tm1 - tm0, now_ms() - tm1);
+    return true;
 }
 
 extern "C" void mr_plan_destroy(mr_plan *pl) {

@@ -136,16 +136,22 @@ hipError_t decode_records_device(const OutResult *res, const OutCmd *slots, cons
 // MR_ERR_CAPACITY).  nov: the pass's overflow-pool length, read on the device.
 __global__ void wire_kernel(const OutResult *__restrict__ res, const OutCmd *__restrict__ slots,
                             const OutCmd *__restrict__ ovf, const uint32_t *__restrict__ nov_p, uint32_t ovf_cap,
-                            uint32_t nrec, uint32_t nq, uint32_t mc, uint32_t *__restrict__ rows,
-                            uint32_t *__restrict__ wpool, uint32_t wpool_cap) {
-    const uint32_t nov = min(*nov_p, ovf_cap), rw = 1u + 2u * mc;
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nq; k += gridDim.x * blockDim.x) {
+                            uint32_t nrec, uint32_t nq, uint32_t mc, const uint32_t *__restrict__ q_id,
+                            const uint32_t *__restrict__ q_off, uint32_t *__restrict__ rows, uint32_t *__restrict__ wpool,
+                            uint32_t wpool_cap) {
+    // (q_off: the fetch's rows, one word longer, ending in the query's offset in the output
+    // pool, so that any row decodes on its own)
+    const uint32_t nov = min(*nov_p, ovf_cap), rw = 1u + 2u * mc + (q_off ? 1u : 0u);
+    // (q_id: rows in query order, record k at row q_id[k]; the rows of queries without a
+    // record are left alone)
+    const uint32_t nrow = q_id ? nrec : nq;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nrow; k += gridDim.x * blockDim.x) {
         // rows past the records (queries with an invalid cell index) read MR_ERR_INVALID_INDEX
         const OutResult o = k < nrec ? res[k] : OutResult{0u, 0u, 0u, uint32_t(16 + MR_ERR_INVALID_INDEX) << 16};
         const int st = int(o.ncmd_status >> 16) - 16;
         const uint32_t n = o.ncmd_status & 0xFFFFu;
         const OutCmd *src = slots + (unsigned long long)k * mc;
-        uint32_t *row = rows + (unsigned long long)k * rw;
+        uint32_t *row = rows + (unsigned long long)(q_id ? q_id[k] : k) * rw;
         uint32_t hdr, s0 = 0, s1 = 0;
         bool copy = false;
         if (st == MR_OK && n <= mc && n < kWireOvf) {
@@ -183,17 +189,41 @@ __global__ void wire_kernel(const OutResult *__restrict__ res, const OutCmd *__r
             row[1 + 2 * j] = kp;
             row[2 + 2 * j] = to;
         }
+        if (q_off) row[1 + 2 * mc] = q_off[q_id ? q_id[k] : k];
     }
 }
 
 hipError_t launch_wire(const OutResult *res, const OutCmd *slots, const OutCmd *ovf, const uint32_t *nov, uint32_t ovf_cap,
-                       uint32_t nrec, uint32_t nq, uint32_t mc, uint32_t *rows, uint32_t *wpool, uint32_t wpool_cap,
-                       hipStream_t stream) {
-    if (!nq) return hipSuccess;
-    const uint32_t blocks = std::max(1u, std::min(8192u, (nq + 255) / 256));
-    hipLaunchKernelGGL(wire_kernel, dim3(blocks), dim3(256), 0, stream, res, slots, ovf, nov, ovf_cap, nrec, nq, mc, rows,
-                       wpool, wpool_cap);
+                       uint32_t nrec, uint32_t nq, uint32_t mc, const uint32_t *q_id, uint32_t *rows, uint32_t *wpool,
+                       uint32_t wpool_cap, hipStream_t stream) {
+    const uint32_t nrow = q_id ? nrec : nq;
+    if (!nrow) return hipSuccess;
+    const uint32_t blocks = std::max(1u, std::min(8192u, (nrow + 255) / 256));
+    hipLaunchKernelGGL(wire_kernel, dim3(blocks), dim3(256), 0, stream, res, slots, ovf, nov, ovf_cap, nrec, nq, mc, q_id,
+                       nullptr, rows, wpool, wpool_cap);
     return hipGetLastError();
+}
+
+// The fetch's wire rows (mr_host.cpp plan_fetch_wire): in query order, each ending in the
+// query's command offset (the exclusive prefix of the counts in query order), so the host
+// decodes rows in any order on any thread.  cnt / off: nq words of scratch; temp scan
+// scratch of *temp_bytes (a null temp returns the size needed).
+hipError_t wire_fetch_device(const OutResult *res, const OutCmd *slots, const OutCmd *ovf, const uint32_t *nov,
+                             uint32_t ovf_cap, const uint32_t *q_id, uint32_t nrec, uint32_t nq, uint32_t mc, uint32_t *cnt,
+                             uint32_t *off, void *temp, size_t *temp_bytes, uint32_t *rows, uint32_t *wpool,
+                             uint32_t wpool_cap, hipStream_t stream) {
+    if (!temp) return hipcub::DeviceScan::ExclusiveSum(nullptr, *temp_bytes, cnt, off, int(nq), stream);
+    hipError_t e = hipMemsetAsync(cnt, 0, size_t(nq) * 4, stream);
+    const uint32_t blocks = std::max(1u, std::min(8192u, (nrec + 255) / 256));
+    if (e == hipSuccess && nrec)
+        hipLaunchKernelGGL(decode_count_kernel, dim3(blocks), dim3(256), 0, stream, res, q_id, nrec, cnt);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, cnt, off, int(nq), stream);
+    if (e == hipSuccess && nrec)
+        hipLaunchKernelGGL(wire_kernel, dim3(blocks), dim3(256), 0, stream, res, slots, ovf, nov, ovf_cap, nrec, nq, mc, q_id,
+                           off, rows, wpool, wpool_cap);
+    if (e == hipSuccess) e = hipGetLastError();
+    return e;
 }
 
 // ---- byte-deterministic overflow pool -----------------------------------

@@ -745,11 +745,14 @@ def test_device_fetch_matches_host_decode(eng, monkeypatch, max_cmds):
     qs[77] = (qs[77][0], CellIndex(2, 1, 999, 0))
     for params in (Params(), Params(fleetfoot=2, sort_by=(SORT_TIME, SORT_MONEY), use_sfm=True)):
         out = {}
-        for mode in ("device", "pinned", "host"):
+        for mode in ("device", "pinned", "wire", "host"):
             if mode == "host":
                 monkeypatch.setenv("MR_HOST_DECODE", "1")
             else:
                 monkeypatch.delenv("MR_HOST_DECODE", raising=False)
+            # "wire" (the default): rows re-encoded on the device, decoded on the host
+            # pool; "device" / "pinned": the device decoder (MR_FETCH_WIRE=0)
+            monkeypatch.setenv("MR_FETCH_WIRE", "1" if mode == "wire" else "0")
             plan = eng.Plan(g, params, qs, max_cmds=max_cmds)
             plan.run()
             for cap in (len(qs) * 24, 500):
@@ -764,7 +767,7 @@ def test_device_fetch_matches_host_decode(eng, monkeypatch, max_cmds):
                     pf.unpin_host(pool)
                 out[(mode, cap)] = (st, bytes(res), bytes(pool))
         for cap in (len(qs) * 24, 500):
-            for mode in ("device", "pinned"):
+            for mode in ("device", "pinned", "wire"):
                 d, h = out[(mode, cap)], out[("host", cap)]
                 assert d[0] == h[0], (mode, cap, d[0], h[0])
                 assert d[1] == h[1], (mode, cap)
