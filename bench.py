@@ -449,16 +449,21 @@ def main():
         plans = [plan]
     it = [0]
 
+    # N > 1: the wire encoding and the gather of batch i run on a stream of their own, so
+    # that they overlap the pass of batch i+1 (the other plan); the plan's next pass waits
+    # for its encoding (mr_plan_wire_records)
+    wstream = torch.cuda.Stream() if pipe is not None else None
+
     def step():
         k = it[0] % len(plans)
         it[0] += 1
-        if pipe is not None:
-            pipe.reuse(k)  # the stream waits until batch k-2's gather has read this buffer
         plans[k].run(stream.cuda_stream)
         if pipe is not None:
             b = bufs[k].data_ptr()
-            plans[k].wire_records(b, b + rows * rw * 4, wpool_cap, stream.cuda_stream)
-            pipe.issue(k)
+            with torch.cuda.stream(wstream):
+                pipe.reuse(k)  # wstream waits until batch k-2's gather has read this buffer
+                plans[k].wire_records(b, b + rows * rw * 4, wpool_cap, wstream.cuda_stream)
+                pipe.issue(k)
 
     for _ in range(args.warmup):
         step()

@@ -3565,6 +3565,20 @@ extern "C" int mr_plan_wire_records(mr_plan *pl, void *d_rows, void *d_pool, uin
                     s) !=
         hipSuccess)
         return fail(MR_ERR_DEVICE, "wire kernel");
+    // on a stream of its own (overlapping the next plan's pass), the encoding reads the
+    // plan's outputs after the pass: the plan's next pass waits for it as for a pass
+    if (pl->ev_last && pl->last_stream != s) {
+        hipEvent_t ev = nullptr;
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess || hipEventRecord(ev, s) != hipSuccess) {
+            if (ev) (void)hipEventDestroy(ev);
+            (void)hipStreamSynchronize(s);  // (ordered the slow way)
+            return MR_OK;
+        }
+        if (pl->ev_last_orphan) (void)hipEventDestroy(pl->ev_last);
+        pl->ev_last = ev;
+        pl->ev_last_orphan = true;
+        pl->last_stream = s;
+    }
     return MR_OK;
 }
 

@@ -138,58 +138,76 @@ __global__ void wire_kernel(const OutResult *__restrict__ res, const OutCmd *__r
                             const OutCmd *__restrict__ ovf, const uint32_t *__restrict__ nov_p, uint32_t ovf_cap,
                             uint32_t nrec, uint32_t nq, uint32_t mc, const uint32_t *__restrict__ q_id,
                             const uint32_t *__restrict__ q_off, uint32_t *__restrict__ rows, uint32_t *__restrict__ wpool,
-                            uint32_t wpool_cap) {
+                            uint32_t wpool_cap, bool stage_rows) {
     // (q_off: the fetch's rows, one word longer, ending in the query's offset in the output
     // pool, so that any row decodes on its own)
     const uint32_t nov = min(*nov_p, ovf_cap), rw = 1u + 2u * mc + (q_off ? 1u : 0u);
     // (q_id: rows in query order, record k at row q_id[k]; the rows of queries without a
     // record are left alone)
     const uint32_t nrow = q_id ? nrec : nq;
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nrow; k += gridDim.x * blockDim.x) {
-        // rows past the records (queries with an invalid cell index) read MR_ERR_INVALID_INDEX
-        const OutResult o = k < nrec ? res[k] : OutResult{0u, 0u, 0u, uint32_t(16 + MR_ERR_INVALID_INDEX) << 16};
-        const int st = int(o.ncmd_status >> 16) - 16;
-        const uint32_t n = o.ncmd_status & 0xFFFFu;
-        const OutCmd *src = slots + (unsigned long long)k * mc;
-        uint32_t *row = rows + (unsigned long long)(q_id ? q_id[k] : k) * rw;
-        uint32_t hdr, s0 = 0, s1 = 0;
-        bool copy = false;
-        if (st == MR_OK && n <= mc && n < kWireOvf) {
-            hdr = (n ? (src[0].from & kWireRankMask) : 0u) | (n << kWireRankBits);
-            copy = true;
-        } else if (st == int(kStatusOverflow) && mc) {
-            const OutCmd tag = src[0];
-            if (tag.kp == kOvfTag && tag.to == n && (unsigned long long)tag.from + n <= nov &&
-                (unsigned long long)tag.from + n <= wpool_cap && n) {
-                hdr = (ovf[tag.from].from & kWireRankMask) | (kWireOvf << kWireRankBits);
-                s0 = tag.from;
-                s1 = n;
-                for (uint32_t j = 0; j < n; ++j) {
-                    const OutCmd c = ovf[tag.from + j];
-                    wpool[2ull * (tag.from + j)] = c.kp;
-                    wpool[2ull * (tag.from + j) + 1] = c.to;
+    // rows in record order are built in LDS (a row per thread; rw odd, so the threads' rows
+    // start in distinct banks) and stored by the workgroup as one contiguous run: a thread
+    // storing its own 36 B row scatters every store instruction over 36 lines
+    extern __shared__ uint32_t wsh[];
+    const bool stage = !q_id && stage_rows;
+    const uint32_t bd = blockDim.x, tid = threadIdx.x;
+    for (uint32_t base = blockIdx.x * bd; base < nrow; base += gridDim.x * bd) {
+        const uint32_t k = base + tid;
+        if (k >= nrow) {
+            if (!stage) continue;
+        } else {
+            // rows past the records (queries with an invalid cell index) read MR_ERR_INVALID_INDEX
+            const OutResult o = k < nrec ? res[k] : OutResult{0u, 0u, 0u, uint32_t(16 + MR_ERR_INVALID_INDEX) << 16};
+            const int st = int(o.ncmd_status >> 16) - 16;
+            const uint32_t n = o.ncmd_status & 0xFFFFu;
+            const OutCmd *src = slots + (unsigned long long)k * mc;
+            uint32_t *row = stage ? wsh + tid * rw : rows + (unsigned long long)(q_id ? q_id[k] : k) * rw;
+            uint32_t hdr, s0 = 0, s1 = 0;
+            bool copy = false;
+            if (st == MR_OK && n <= mc && n < kWireOvf) {
+                hdr = (n ? (src[0].from & kWireRankMask) : 0u) | (n << kWireRankBits);
+                copy = true;
+            } else if (st == int(kStatusOverflow) && mc) {
+                const OutCmd tag = src[0];
+                if (tag.kp == kOvfTag && tag.to == n && (unsigned long long)tag.from + n <= nov &&
+                    (unsigned long long)tag.from + n <= wpool_cap && n) {
+                    hdr = (ovf[tag.from].from & kWireRankMask) | (kWireOvf << kWireRankBits);
+                    s0 = tag.from;
+                    s1 = n;
+                    for (uint32_t j = 0; j < n; ++j) {
+                        const OutCmd c = ovf[tag.from + j];
+                        wpool[2ull * (tag.from + j)] = c.kp;
+                        wpool[2ull * (tag.from + j) + 1] = c.to;
+                    }
+                } else {
+                    hdr = (kWireStatus + 32u + uint32_t(MR_ERR_CAPACITY)) << kWireRankBits;
                 }
             } else {
-                hdr = (kWireStatus + 32u + uint32_t(MR_ERR_CAPACITY)) << kWireRankBits;
+                hdr = (kWireStatus + 32u + uint32_t(st == MR_OK ? MR_ERR_DEVICE : st)) << kWireRankBits;
             }
-        } else {
-            hdr = (kWireStatus + 32u + uint32_t(st == MR_OK ? MR_ERR_DEVICE : st)) << kWireRankBits;
-        }
-        row[0] = hdr;
-        for (uint32_t j = 0; j < mc; ++j) {
-            uint32_t kp = 0, to = 0;
-            if (copy && j < n) {
-                const OutCmd c = src[j];
-                kp = c.kp;
-                to = c.to;
-            } else if (j == 0) {
-                kp = s0;
-                to = s1;
+            row[0] = hdr;
+            for (uint32_t j = 0; j < mc; ++j) {
+                uint32_t kp = 0, to = 0;
+                if (copy && j < n) {
+                    const OutCmd c = src[j];
+                    kp = c.kp;
+                    to = c.to;
+                } else if (j == 0) {
+                    kp = s0;
+                    to = s1;
+                }
+                row[1 + 2 * j] = kp;
+                row[2 + 2 * j] = to;
             }
-            row[1 + 2 * j] = kp;
-            row[2 + 2 * j] = to;
+            if (q_off) row[1 + 2 * mc] = q_off[q_id ? q_id[k] : k];
         }
-        if (q_off) row[1 + 2 * mc] = q_off[q_id ? q_id[k] : k];
+        if (stage) {
+            __syncthreads();
+            const uint32_t nw = min(bd, nrow - base) * rw;
+            uint32_t *dst = rows + (unsigned long long)base * rw;
+            for (uint32_t w = tid; w < nw; w += bd) dst[w] = wsh[w];
+            __syncthreads();
+        }
     }
 }
 
@@ -198,9 +216,12 @@ hipError_t launch_wire(const OutResult *res, const OutCmd *slots, const OutCmd *
                        uint32_t wpool_cap, hipStream_t stream) {
     const uint32_t nrow = q_id ? nrec : nq;
     if (!nrow) return hipSuccess;
-    const uint32_t blocks = std::max(1u, std::min(8192u, (nrow + 255) / 256));
-    hipLaunchKernelGGL(wire_kernel, dim3(blocks), dim3(256), 0, stream, res, slots, ovf, nov, ovf_cap, nrec, nq, mc, q_id,
-                       nullptr, rows, wpool, wpool_cap);
+    // (staged rows: 256 threads while their rows fit 64 KB of LDS, else 64, else unstaged)
+    const uint32_t rw = 1u + 2u * mc, bd = rw <= 64u ? 256u : 64u;
+    const bool stage = !q_id && size_t(bd) * rw * 4 <= 65536;
+    const uint32_t blocks = std::max(1u, std::min(8192u, (nrow + bd - 1) / bd));
+    hipLaunchKernelGGL(wire_kernel, dim3(blocks), dim3(bd), stage ? size_t(bd) * rw * 4 : 0, stream, res, slots, ovf, nov,
+                       ovf_cap, nrec, nq, mc, q_id, nullptr, rows, wpool, wpool_cap, stage);
     return hipGetLastError();
 }
 
@@ -221,7 +242,7 @@ hipError_t wire_fetch_device(const OutResult *res, const OutCmd *slots, const Ou
     if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, cnt, off, int(nq), stream);
     if (e == hipSuccess && nrec)
         hipLaunchKernelGGL(wire_kernel, dim3(blocks), dim3(256), 0, stream, res, slots, ovf, nov, ovf_cap, nrec, nq, mc, q_id,
-                           off, rows, wpool, wpool_cap);
+                           off, rows, wpool, wpool_cap, false);
     if (e == hipSuccess) e = hipGetLastError();
     return e;
 }
