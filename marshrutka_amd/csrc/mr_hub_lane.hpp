@@ -75,14 +75,20 @@ __host__ __device__ constexpr uint32_t lane_waves(uint32_t TM) { return TM <= 22
 #define MR_LANE_SKIP 1
 #endif
 // OR of v over the wave (uniform): four DPP rounds within each row of 16 lanes, then the
-// four rows' words by readlane
+// four rows' words by readlane.  Exact only with every lane active (the DPP reads of an
+// inactive lane give 0 with bound_ctrl off, and lanes 0/16/32/48 are read whatever EXEC
+// says); the relax loop's callers keep EXEC full (MR_LANE_SKIP: lanes without a source run
+// the loop to its end), and with EXEC not full the result is ~0 — every entry treated as
+// needed, so a skip can only be lost, never taken wrongly
 __device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+    const bool full = __builtin_amdgcn_read_exec() == ~0ull;
     v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
     v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
     v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
     v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x140, 0xF, 0xF, false));  // row_mirror
-    return uint32_t(__builtin_amdgcn_readlane(int(v), 0) | __builtin_amdgcn_readlane(int(v), 16) |
-                    __builtin_amdgcn_readlane(int(v), 32) | __builtin_amdgcn_readlane(int(v), 48));
+    const uint32_t r = uint32_t(__builtin_amdgcn_readlane(int(v), 0) | __builtin_amdgcn_readlane(int(v), 16) |
+                                __builtin_amdgcn_readlane(int(v), 32) | __builtin_amdgcn_readlane(int(v), 48));
+    return full ? r : ~0u;
 }
 // meta: length (8 b) | kind of the first tail command (3 b) << 8 | parent entry (5 b)
 // << 11 | (tail count - 1) << 16 | CentralMove count (2 b) << 17

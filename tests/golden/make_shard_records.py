@@ -1,7 +1,8 @@
 """Generates tests/golden/shard_records.npz on an MI355X: the device records of a
 two-rank split of a query batch, each rank's shard solved by its own plan into one
 flat buffer laid out as bench.py's N > 1 path lays it out (result records, command
-slots, overflow pool; marshrutka_amd/shard.py), plus the one-rank labels of the
+slots, overflow pool; marshrutka_amd/shard.py), the same passes as wire rows
+(mr_plan_wire_records, what bench.py gathers), plus the one-rank labels of the
 whole batch.  tests/test_shard_dist.py gathers these buffers over gloo and decodes
 them with mr_decode_records on the host.  Run: python tests/golden/make_shard_records.py
 (a GPU box; the fixture is data, committed)."""
@@ -57,8 +58,17 @@ def main():
             plan.wait()
             torch.cuda.synchronize()
             arrays[f"run{j}_rank{r}"] = buf.cpu().numpy()
+            # the same pass as wire rows (what bench.py gathers since round 6):
+            # mr_plan_wire_records, then the pool of long labels
+            wrw = pathfinder.wire_row_words(max_cmds)
+            wpool_cap = max(1024, rows // 8)
+            wbuf = torch.zeros(rows * wrw + wpool_cap * 2, dtype=torch.int32, device="cuda")
+            plan.wire_records(wbuf.data_ptr(), wbuf.data_ptr() + rows * wrw * 4, wpool_cap)
+            plan.wait()
+            torch.cuda.synchronize()
+            arrays[f"run{j}_rank{r}_wire"] = wbuf.cpu().numpy()
             run["orders"].append(plan.record_queries())
-            run.update(rows=rows, rw=rw, cw=cw, ovf_cap=ovf_cap)
+            run.update(rows=rows, rw=rw, cw=cw, ovf_cap=ovf_cap, wrw=wrw, wpool_cap=wpool_cap)
         pl = pathfinder.Plan(g, params, qs, max_cmds=16)  # the one-rank run of the whole batch
         pl.run()
         whole = pl.fetch()

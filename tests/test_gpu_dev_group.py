@@ -129,3 +129,21 @@ def test_device_grouping_c4_batch(eng, monkeypatch):
     finally:
         eng.unpin_host(buf)
     _same(a, c)
+
+
+@pytest.mark.parametrize("every", [1, 2])
+def test_device_grouping_many_invalid(eng, monkeypatch, every):
+    """More than 4 096 invalid queries in a device-grouped batch: the plan
+    copies every grouped id back and rebuilds the invalid list on the host
+    (group_on_device's long path).  Statuses, records and labels equal the host grouping's."""
+    m = SyntheticMap(65, campfires_per_homeland=4, seed=2024)
+    arr = m.cells_array()
+    g = eng.MapGrid.from_array(arr)
+    src, dst = random_query_cells(m, 12_000, 91)
+    q, bad = _with_invalid(m, m.query_array(src, dst, arr), every=every)
+    assert len(bad) > 4096
+    a = _run(eng, monkeypatch, True, g, Params(), q)
+    b = _run(eng, monkeypatch, False, g, Params(), q)
+    _same(a, b)
+    st = np.frombuffer(a["res"].tobytes(), dtype=np.int32).reshape(len(q), 8)[:, 6]
+    assert np.all(st[bad] == MR_ERR_INVALID_INDEX) and np.all(np.delete(st, bad) == MR_OK)

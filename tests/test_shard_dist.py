@@ -142,7 +142,7 @@ def test_cost_aware_lpt_spreads_fallback_sources():
 FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "shard_records.npz")
 
 
-def _records_worker(rank, world, port, ret):
+def _records_worker(rank, world, port, ret, wire=False):
     import json
     import numpy as np
     import torch.distributed as dist
@@ -160,7 +160,8 @@ def _records_worker(rank, world, port, ret):
         meta = json.loads(str(z["meta"]))
         summary = []
         for j, run in enumerate(meta["runs"]):
-            pg = PipelinedGather([torch.from_numpy(z[f"run{j}_rank{rank}"].copy())], rank, world, host_staging=True)
+            key = f"run{j}_rank{rank}" + ("_wire" if wire else "")
+            pg = PipelinedGather([torch.from_numpy(z[key].copy())], rank, world, host_staging=True)
             pg.issue(0)
             pg.drain()
             if rank != 0:
@@ -174,10 +175,18 @@ def _records_worker(rank, world, port, ret):
             for r, buf in enumerate(pg.out[0]):
                 words = buf.numpy().view(np.uint32)
                 n = run["counts"][r]
-                res = words[: n * rw]
-                slots = words[rows * rw: rows * rw + n * cw]
-                ovf = words[rows * (rw + cw): rows * (rw + cw) + ovf_cap * 4]
-                for k, lab in enumerate(pathfinder.decode_records(g, params, res, slots, n, cw // 4, ovf)):
+                if wire:
+                    wrw = run["wrw"]
+                    out, cmds = pathfinder.decode_wire_raw(g, params, words[: n * wrw], n, run["max_cmds"],
+                                                           words[rows * wrw: rows * wrw + run["wpool_cap"] * 2])
+                    labs = [None if out[k].status == 1 else pathfinder.result_from_c(out[k], cmds) for k in range(n)]
+                    assert all(out[k].status in (0, 1) for k in range(n))
+                else:
+                    res = words[: n * rw]
+                    slots = words[rows * rw: rows * rw + n * cw]
+                    ovf = words[rows * (rw + cw): rows * (rw + cw) + ovf_cap * 4]
+                    labs = pathfinder.decode_records(g, params, res, slots, n, cw // 4, ovf)
+                for k, lab in enumerate(labs):
                     q = meta["shards"][r][run["orders"][r][k]]
                     got[q] = as_expected(lab)
                     covered += 1
@@ -204,6 +213,29 @@ def test_engine_records_gather_gloo_world2():
     ret = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_records_worker, args=(r, 2, port, ret)) for r in range(2)]
+    for p in procs:
+        p.start()
+    summary = ret.get(timeout=180)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert len(summary) == 2
+    for covered, bad in summary:
+        assert covered == 400 and bad == 0, summary
+
+
+def test_engine_wire_gather_gloo_world2():
+    """The same with the wire rows bench.py gathers (mr_plan_wire_records on the MI355X:
+    4 + 8 max_cmds bytes a query, then the pool of long labels), decoded on rank 0 by
+    mr_decode_wire: every label equals the one-rank run, labels longer than 3 commands
+    (wire pool) included."""
+    import numpy as np
+    import torch.multiprocessing as mp
+    assert "run0_rank0_wire" in np.load(FIX).files, "regenerate tests/golden/shard_records.npz"
+    ctx = mp.get_context("spawn")
+    ret = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_records_worker, args=(r, 2, port, ret, True)) for r in range(2)]
     for p in procs:
         p.start()
     summary = ret.get(timeout=180)

@@ -13,8 +13,8 @@ from marshrutka_amd.mapgen import SyntheticMap, random_queries  # noqa: E402
 SORTS = [(0, 2), (0, 1), (2, 0), (2, 1), (1, 0), (1, 2)]  # Legs=0 Time=1 Money=2
 
 
-def main(size=65, nq=10000, steps=5):
-    m = SyntheticMap(size, campfires_per_homeland=4, seed=2024)
+def main(size=65, nq=10000, steps=5, seed=2024):
+    m = SyntheticMap(size, campfires_per_homeland=4, seed=seed)
     g = pf.MapGrid(m.cells())
     qs = random_queries(m, nq, 7)
     for ff in (0, 1, 2, 3):
@@ -29,7 +29,7 @@ def main(size=65, nq=10000, steps=5):
             wall = (time.time() - t) / steps
             st = plan.stats()
             ms, n = plan.kernel_ms()
-            print(f"S={size} ff={ff} sort={s}: solver {st['solver']} fallback {st['fallback_sources']}/"
+            print(f"S={size} seed={seed} ff={ff} sort={s}: solver {st['solver']} fallback {st['fallback_sources']}/"
                   f"{st['num_sources']} kernel {ms:.3f} ms  {nq / (ms * 1e-3) / 1e6:.2f} M q/s (wall {wall * 1e3:.2f} ms)",
                   flush=True)
 
