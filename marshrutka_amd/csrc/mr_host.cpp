@@ -64,10 +64,10 @@ size_t group_scratch_bytes(uint32_t n, uint32_t V);
 hipError_t group_queries_device(const void *q, uint32_t n, const GroupGeom &geo, uint32_t lane_max_q, void *scratch,
                                 uint32_t *src_v, uint32_t *q_begin, uint32_t *q_dst, uint32_t *q_id, uint32_t *cnt,
                                 uint32_t *inv, uint32_t inv_cap, hipStream_t s);
-hipError_t partition_sources_device(uint32_t n, uint32_t V, const void *scratch, const uint32_t *src_v,
-                                    const uint32_t *q_begin, const uint32_t *q_dst, const uint32_t *q_id,
-                                    const uint32_t *cnt, uint32_t *src2, uint32_t *qb2, uint32_t *qd2, uint32_t *qi2,
-                                    hipStream_t s);
+hipError_t partition_sources_device(uint32_t n, uint32_t V, uint32_t ns, uint32_t lane_max_q, const void *scratch,
+                                    const uint32_t *src_v, const uint32_t *q_begin, const uint32_t *q_dst,
+                                    const uint32_t *q_id, const uint32_t *cnt, uint32_t *src2, uint32_t *qb2,
+                                    uint32_t *qd2, uint32_t *qi2, hipStream_t s);
 uint32_t hub_group_lds_bytes(uint32_t NS, uint32_t nreg, uint32_t G);
 hipError_t launch_hub_group(const KArgs *d_args, const uint32_t perm[3], uint32_t NS, uint32_t nreg, uint32_t n,
                             uint32_t G, bool nonlin, hipStream_t stream);
@@ -2024,18 +2024,22 @@ static uint32_t lane_min_sources() {
 }
 
 // Hub plans on the lane kernel: the sources with at most kLaneMaxQ queries first (one
-// source per lane, hub_lane_kernel), the others after them (hub_kernel, a lane per
-// query); each source's records stay contiguous.  Returns the count of the first group.
+// source per lane, hub_lane_kernel), by query count (a wave runs its destination loop as
+// often as its busiest lane's source has queries: c4's uniform batch, 1.55 queries a
+// source, ran it ~4 times a wave in source order), then the others (hub_kernel, a lane
+// per query); each class in source order, each source's records contiguous (the device
+// partition, mr_k_groupq.hip, gives the same order).  Returns the count of the first group.
 static uint32_t partition_sources(HostPlan &hp) {
     const uint32_t ns = uint32_t(hp.src_v.size());
-    std::vector<uint32_t> order;
-    order.reserve(ns);
-    for (uint32_t i = 0; i < ns; ++i)
-        if (hp.q_begin[i + 1] - hp.q_begin[i] <= kLaneMaxQ) order.push_back(i);
-    const uint32_t n_lane = uint32_t(order.size());
-    if (n_lane == ns) return n_lane;
-    for (uint32_t i = 0; i < ns; ++i)
-        if (hp.q_begin[i + 1] - hp.q_begin[i] > kLaneMaxQ) order.push_back(i);
+    std::vector<uint32_t> order(ns), start(kLaneMaxQ + 3, 0);
+    auto cls = [&](uint32_t i) {
+        const uint32_t c = hp.q_begin[i + 1] - hp.q_begin[i];
+        return c <= kLaneMaxQ ? c : kLaneMaxQ + 1u;
+    };
+    for (uint32_t i = 0; i < ns; ++i) ++start[cls(i) + 1];
+    for (uint32_t c = 1; c < start.size(); ++c) start[c] += start[c - 1];
+    const uint32_t n_lane = start[kLaneMaxQ + 1];
+    for (uint32_t i = 0; i < ns; ++i) order[start[cls(i)]++] = i;
     std::vector<uint32_t> src, qb, qd, qi;
     spare_take(src, ns);
     spare_take(qb, ns + 1);
@@ -2172,13 +2176,14 @@ static int group_on_device(mr_plan *pl, const mr_query *qs, uint32_t n) {
 // Phase 2 (plans on hub_lane_kernel): the small sources first, into a new block
 static uint32_t partition_on_device(mr_plan *pl) {
     HostPlan &hp = pl->hp;
-    if (hp.n_small == hp.nsrc) return hp.n_small;
+    if (hp.nsrc == 0) return 0;
     size_t at[5];
     qblock_layout(hp.nq, at);
     uint32_t *blk = nullptr;
     if (pmalloc(reinterpret_cast<void **>(&blk), at[4] * 4) != hipSuccess) return kNone32;
-    hipError_t e = partition_sources_device(hp.nq, pl->grid->V, pl->d_gscratch, pl->d_src, pl->d_qb, pl->d_qd, pl->d_qi,
-                                            pl->d_gcnt, blk + at[0], blk + at[1], blk + at[2], blk + at[3], pl->stream);
+    hipError_t e = partition_sources_device(hp.nq, pl->grid->V, hp.nsrc, kLaneMaxQ, pl->d_gscratch, pl->d_src, pl->d_qb,
+                                            pl->d_qd, pl->d_qi, pl->d_gcnt, blk + at[0], blk + at[1], blk + at[2],
+                                            blk + at[3], pl->stream);
     const hipError_t es = hipStreamSynchronize(pl->stream);
     if (e == hipSuccess) e = es;
     if (e != hipSuccess) {
@@ -3917,9 +3922,9 @@ extern "C" void mr_plan_destroy(mr_plan *pl) {
                              "MR_STAMPS hub (sum over waves): sources=%llu iterations=%llu boundaries=%llu cycles: "
                              "init=%llu select=%llu edges=%llu boundary=%llu emit=%llu dequeue=%llu\n",
                              h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]);
-            if (pl->lane_g && h[9])
+            if (h[9])
                 std::fprintf(stderr,
-                             "MR_STAMPS group (per wave, %llu waves, last pass): setup=%.0f own_edges=%.0f scan_min=%.0f "
+                             "MR_STAMPS lane/group (per wave, %llu waves, last pass): setup=%.0f own_edges=%.0f scan_min=%.0f "
                              "settle=%.0f relax=%.0f cmds_cert=%.0f destinations=%.0f\n",
                              h[9], double(h[10]) / h[9], double(h[11]) / h[9], double(h[12]) / h[9], double(h[13]) / h[9],
                              double(h[14]) / h[9], double(h[7]) / h[9], double(h[15]) / h[9]);

@@ -263,8 +263,26 @@ __device__ __forceinline__ uint32_t ltm3(const LLab &x, const LLab &y) {
 // money, caravan time (uint4), SoE-region distance from s into t's region and its walk
 // time (uint2; 0 where there is none), and per row s the entries t whose SoE-region
 // candidate applies (distance known and nonzero)
+// diagnostic builds (-DMR_STAMPS): the lane kernel's phase cycles per wave (s_memtime),
+// summed like the group kernel's (mr_hub_group.hpp MR_GSTAMP; mr_plan_destroy prints them)
+#ifdef MR_STAMPS
+#define MR_LSTAMP(i)                                                  \
+    do {                                                              \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+        lst[i] += now_ - lst_last;                                    \
+        lst_last = now_;                                              \
+    } while (0)
+#else
+#define MR_LSTAMP(i) \
+    do {             \
+    } while (0)
+#endif
+
 template <uint32_t PERM, uint32_t TM, bool NL = false>
 struct LaneHub {
+#ifdef MR_STAMPS
+    unsigned long long lst[8] = {0, 0, 0, 0, 0, 0, 0, 0}, lst_last = 0;
+#endif
     static constexpr uint32_t C1 = PERM / 9, C2 = (PERM / 3) % 3, C3 = PERM % 3;
     const KArgs *__restrict__ a;
     DevParams P;
@@ -930,6 +948,7 @@ struct LaneHub {
             wt |= won & ~ltm3(c, w) & (1u << t);
             MR_LANE_FENCE();
         }
+        MR_LSTAMP(1);  // (1: the source's own edges)
         // ---- Dijkstra over the specials, one settle per lane per iteration ----------
         for (uint32_t it = 0; it < NS; ++it) {
             const uint32_t cand = tent & ~done;
@@ -962,6 +981,7 @@ struct LaneHub {
 #endif
                 MR_LANE_FENCE();
             }
+            MR_LSTAMP(2);  // (2: the settle scan)
             Settle z;
             z.ls = la;
             uint32_t s, tie = 0;
@@ -998,6 +1018,7 @@ struct LaneHub {
             }
             settle_ctx(z, s, ((wt >> s) & 1u) != 0);
             if (s != 0) M[s * mstride + mcolumn] = z.ls.m;  // (the settled meta, for the chains)
+            MR_LSTAMP(3);  // (3: the settle's ties and bookkeeping)
             // no candidate out of any lane's settle (the last settles): nothing to relax
             if (!__any((z.walk | z.cenm | z.car | z.soe | z.reg) != 0)) continue;
 #if MR_LANE_SKIP
@@ -1053,6 +1074,7 @@ struct LaneHub {
 #pragma unroll
                 for (uint32_t t = 1; t < TM; ++t) L[t].m = msel(bitm(repl, t), ml[t * 64u], L[t].m);
             }
+            MR_LSTAMP(4);  // (4: the relaxations and their ties)
         }
         if (!have) return 0;
         // ---- certification: with blockers, every settled walk label must be certain ----
@@ -1072,6 +1094,7 @@ struct LaneHub {
                 if (!label_certain(meta_of(t), t)) unc = true;
             }
         }
+        MR_LSTAMP(6);  // (6: the certification of settled labels)
         const uint32_t qa = a->q_begin[s_idx], qb = a->q_begin[s_idx + 1];
         const bool fb_sp = unc || a->fb_all;
         // ---- destinations: the source, a special's own label, or the best walk ------------
@@ -1235,14 +1258,36 @@ template <uint32_t PERM, uint32_t TM, bool NL = false>
 __global__ __launch_bounds__(kBS, lane_waves(TM)) void hub_lane_kernel(const KArgs *__restrict__ a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     LaneHub<PERM, TM, NL> H;
+#ifdef MR_STAMPS
+    H.lst_last = __builtin_amdgcn_s_memtime();
+#endif
     lane_setup<TM>(a, smem, H);
     H.MC = reinterpret_cast<uint32_t *>(smem + lane_lds_total(a->p.NS, a->nreg, TM)) + (threadIdx.x >> 6) * (TM * 64u);
+#ifdef MR_STAMPS
+    {
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();
+        H.lst[0] += now_ - H.lst_last;  // (0: the table copy)
+        H.lst_last = now_;
+    }
+#endif
     // lane l of wave w: source 64 w + l of the lane kernel's sources [0, n_lane)
     const uint32_t s_idx = (blockIdx.x * (kBS / 64) + (threadIdx.x >> 6)) * 64u + lane_id();
     const uint32_t n = a->n_lane;
     const bool have = s_idx < n;
     uint32_t written = 0;
     if (__any(have)) written = H.solve(have, have ? s_idx : (n ? n - 1 : 0));
+#ifdef MR_STAMPS
+    {
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();
+        H.lst[5] += now_ - H.lst_last;  // (5: the destinations, from the certification's end)
+        if (a->dbg && lane_id() == 0) {
+            unsigned long long *h = a->dbg + (unsigned long long)a->dbg_blocks * 10 + 9;
+            atomicAdd(h, 1ull);
+            for (int i = 0; i < 6; ++i) atomicAdd(h + 1 + i, H.lst[i]);
+            atomicAdd(h - 2, H.lst[6]);
+        }
+    }
+#endif
     __shared__ uint32_t wsum;
     if (threadIdx.x == 0) wsum = 0;
     __syncthreads();

@@ -136,27 +136,6 @@ __global__ void gq_totals_kernel(const uint4 *__restrict__ in, const uint4 *__re
     cnt[3] = ex[ns - 1].y + in[ns - 1].y;
 }
 
-// the small sources first: per source its new index and first position
-__global__ __launch_bounds__(kGBS) void gq_part_src_kernel(const uint32_t *__restrict__ src_v,
-                                                           const uint32_t *__restrict__ q_begin,
-                                                           const uint4 *__restrict__ info, const uint4 *__restrict__ ex,
-                                                           const uint32_t *__restrict__ cnt, uint32_t n,
-                                                           uint32_t *__restrict__ src2, uint32_t *__restrict__ qb2,
-                                                           uint32_t *__restrict__ newoff) {
-    const uint32_t ns = cnt[1], n_small = cnt[2], nq_small = cnt[3];
-    for (uint32_t s = blockIdx.x * kGBS + threadIdx.x; s < ns; s += gridDim.x * kGBS) {
-        const uint4 e = ex[s];
-        const bool small = info[s].x != 0;
-        const uint32_t j = small ? e.x : n_small + (s - e.x);
-        const uint32_t off = small ? e.y : nq_small + e.z;
-        src2[j] = src_v[s];
-        qb2[j] = off;
-        newoff[s] = off;
-        if (s == 0) qb2[ns] = cnt[0];
-    }
-    (void)n;
-}
-
 __global__ __launch_bounds__(kGBS) void gq_part_q_kernel(const uint32_t *__restrict__ q_dst,
                                                          const uint32_t *__restrict__ q_id,
                                                          const uint32_t *__restrict__ q_begin,
@@ -169,6 +148,44 @@ __global__ __launch_bounds__(kGBS) void gq_part_q_kernel(const uint32_t *__restr
         const uint32_t s = sid[k] - 1u, at = newoff[s] + (k - q_begin[s]);
         qd2[at] = q_dst[k];
         qi2[at] = q_id[k];
+    }
+}
+
+// the lane kernel's order (phase 2): per source its class key (its query count when at
+// most lane_max_q, else lane_max_q + 1: after every small one) and its index
+__global__ __launch_bounds__(kGBS) void gq_class_kernel(const uint32_t *__restrict__ q_begin, uint32_t ns,
+                                                        uint32_t lane_max_q, uint32_t *__restrict__ key,
+                                                        uint32_t *__restrict__ val) {
+    for (uint32_t s = blockIdx.x * kGBS + threadIdx.x; s < ns; s += gridDim.x * kGBS) {
+        const uint32_t c = q_begin[s + 1] - q_begin[s];
+        key[s] = c <= lane_max_q ? c : lane_max_q + 1u;
+        val[s] = s;
+    }
+}
+
+// position j of the new order: its source's query count
+__global__ __launch_bounds__(kGBS) void gq_count_sorted_kernel(const uint32_t *__restrict__ q_begin,
+                                                               const uint32_t *__restrict__ order, uint32_t ns,
+                                                               uint32_t *__restrict__ c) {
+    for (uint32_t j = blockIdx.x * kGBS + threadIdx.x; j < ns; j += gridDim.x * kGBS) {
+        const uint32_t s = order[j];
+        c[j] = q_begin[s + 1] - q_begin[s];
+    }
+}
+
+// the sources in the new order: index, first position, and each old source's new first
+// position (for the queries)
+__global__ __launch_bounds__(kGBS) void gq_reorder_src_kernel(const uint32_t *__restrict__ src_v,
+                                                              const uint32_t *__restrict__ order,
+                                                              const uint32_t *__restrict__ off, uint32_t ns,
+                                                              const uint32_t *__restrict__ cnt, uint32_t *__restrict__ src2,
+                                                              uint32_t *__restrict__ qb2, uint32_t *__restrict__ newoff) {
+    for (uint32_t j = blockIdx.x * kGBS + threadIdx.x; j < ns; j += gridDim.x * kGBS) {
+        const uint32_t s = order[j];
+        src2[j] = src_v[s];
+        qb2[j] = off[j];
+        newoff[s] = off[j];
+        if (j == 0) qb2[ns] = cnt[0];
     }
 }
 
@@ -254,23 +271,47 @@ hipError_t group_queries_device(const void *q, uint32_t n, const GroupGeom &geo,
     return hipGetLastError();
 }
 
-// Phase 2 (plans on hub_lane_kernel): the sources of at most lane_max_q queries first,
-// into src2 / qb2 / qd2 / qi2 (the same sizes).  Reads phase 1's scratch and counts.
-hipError_t partition_sources_device(uint32_t n, uint32_t V, const void *scratch, const uint32_t *src_v,
-                                    const uint32_t *q_begin, const uint32_t *q_dst, const uint32_t *q_id,
-                                    const uint32_t *cnt, uint32_t *src2, uint32_t *qb2, uint32_t *qd2, uint32_t *qi2,
-                                    hipStream_t s) {
+// Phase 2 (plans on hub_lane_kernel): the sources in the lane kernel's order into src2 /
+// qb2 / qd2 / qi2 (the same sizes): by query count, 1 to lane_max_q, then the sources of
+// more queries (hub_kernel's), each class in source order.  A wave of the lane kernel runs
+// its destination loop as often as its busiest lane's source has queries: grouped by
+// count, its 64 sources have the same.  Reads phase 1's scratch and counts; ns: the sources.
+hipError_t partition_sources_device(uint32_t n, uint32_t V, uint32_t ns, uint32_t lane_max_q, const void *scratch,
+                                    const uint32_t *src_v, const uint32_t *q_begin, const uint32_t *q_dst,
+                                    const uint32_t *q_id, const uint32_t *cnt, uint32_t *src2, uint32_t *qb2,
+                                    uint32_t *qd2, uint32_t *qi2, hipStream_t s) {
     const uint32_t bits = 32u - uint32_t(__builtin_clz(V));
     const GroupScratchLayout L = group_layout(n, bits);
-    const char *b = static_cast<const char *>(scratch);
+    char *b = static_cast<char *>(const_cast<void *>(scratch));
     const uint32_t *sid = reinterpret_cast<const uint32_t *>(b + L.sid);
-    const uint4 *info = reinterpret_cast<const uint4 *>(b + L.info), *ex = reinterpret_cast<const uint4 *>(b + L.ex);
-    // the new first positions per source reuse the (consumed) key_in words
-    uint32_t *newoff = const_cast<uint32_t *>(reinterpret_cast<const uint32_t *>(b + L.key_in));
-    const uint32_t gb = grid_of(n);
-    hipLaunchKernelGGL(gq_part_src_kernel, dim3(gb), dim3(kGBS), 0, s, src_v, q_begin, info, ex, cnt, n, src2, qb2, newoff);
+    // phase 1's consumed words: the new first positions per source (key_in), the class
+    // keys and source indices before and after the sort, the sorted counts and their scan
+    uint32_t *newoff = reinterpret_cast<uint32_t *>(b + L.key_in);
+    uint32_t *k_in = reinterpret_cast<uint32_t *>(b + L.key_out), *k_out = reinterpret_cast<uint32_t *>(b + L.dstv);
+    uint32_t *v_in = reinterpret_cast<uint32_t *>(b + L.val_in), *v_out = reinterpret_cast<uint32_t *>(b + L.val_out);
+    uint32_t *c_sorted = reinterpret_cast<uint32_t *>(b + L.info), *off = reinterpret_cast<uint32_t *>(b + L.ex);
+    void *temp = b + L.temp;
+    size_t tb = L.temp_bytes;
+    const uint32_t gs = grid_of(ns), gb = grid_of(n);
+    const uint32_t kbits = 32u - uint32_t(__builtin_clz(lane_max_q + 1u));
+    {  // (phase 1's temp storage, sized for n keys of the cells' width, holds these)
+        size_t need_sort = 0, need_scan = 0;
+        (void)hipcub::DeviceRadixSort::SortPairs(nullptr, need_sort, k_in, k_out, v_in, v_out, int(ns), 0, int(kbits), s);
+        (void)hipcub::DeviceScan::ExclusiveSum(nullptr, need_scan, c_sorted, off, int(ns), s);
+        if (need_sort > tb || need_scan > tb) return hipErrorInvalidValue;
+    }
+    hipLaunchKernelGGL(gq_class_kernel, dim3(gs), dim3(kGBS), 0, s, q_begin, ns, lane_max_q, k_in, v_in);
     hipError_t e = hipGetLastError();
+    // stable: equal classes keep the source order (by cell)
+    if (e == hipSuccess)
+        e = hipcub::DeviceRadixSort::SortPairs(temp, tb, k_in, k_out, v_in, v_out, int(ns), 0, int(kbits), s);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(gq_count_sorted_kernel, dim3(gs), dim3(kGBS), 0, s, q_begin, v_out, ns, c_sorted);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    tb = L.temp_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(temp, tb, c_sorted, off, int(ns), s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(gq_reorder_src_kernel, dim3(gs), dim3(kGBS), 0, s, src_v, v_out, off, ns, cnt, src2, qb2, newoff);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(gq_part_q_kernel, dim3(gb), dim3(kGBS), 0, s, q_dst, q_id, q_begin, sid, newoff, cnt, qd2, qi2);
     return hipGetLastError();
 }
