@@ -23,6 +23,7 @@ for b in bufs:
 plan = pathfinder.Plan(grid, Params(), None, max_cmds=4, query_array=qa)
 plan.run()
 plan.wait()
+fresh = os.environ.get("FRESH") == "1"
 for mode, pin in (("1", 0), ("0", 0), ("1", 1), ("0", 1), ("1", 0)):
     os.environ["MR_FETCH_WIRE"] = mode
     if pin:
@@ -30,6 +31,11 @@ for mode, pin in (("1", 0), ("0", 0), ("1", 1), ("0", 1), ("1", 0)):
             pathfinder.pin_host(b)
     ts = []
     for _ in range(4):
+        if fresh:  # a new plan per fetch (bench.py's end_to_end)
+            del plan
+            plan = pathfinder.Plan(grid, Params(), None, max_cmds=4, query_array=qa)
+            plan.run()
+            plan.wait()
         t0 = time.perf_counter()
         plan.fetch_raw(bufs)
         ts.append((time.perf_counter() - t0) * 1e3)
