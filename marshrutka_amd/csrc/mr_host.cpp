@@ -4037,6 +4037,22 @@ static bool expand_word(const HostPlan &hp, const std::vector<Rec> &tab, CellWor
     return true;
 }
 
+// A source's cell words in row-major order (S x S, the device rows' padding dropped):
+// one contiguous copy of its padded rows, compacted on the host.  (A pitched
+// hipMemcpy2D into pageable memory here twice ended in an illegal memory access on the
+// GPU box, intermittently, with every kernel of the plan long finished.)
+static int copy_source_words(mr_plan *pl, uint32_t si, std::vector<CellWord> &words) {
+    const uint32_t S = pl->ka.p.S, pitch = pl->ka.rec_pitch;
+    std::vector<CellWord> rows(size_t(S) * pitch);
+    if (hipError_t e = hipMemcpy(rows.data(), pl->d_rec + size_t(si) * S * pitch, rows.size() * sizeof(CellWord),
+                                 hipMemcpyDeviceToHost))
+        return fail(MR_ERR_DEVICE, std::string("copy records: ") + hipGetErrorString(e));
+    words.resize(size_t(S) * S);
+    for (uint32_t y = 0; y < S; ++y)
+        std::memcpy(&words[size_t(y) * S], &rows[size_t(y) * pitch], S * sizeof(CellWord));
+    return MR_OK;
+}
+
 extern "C" int mr_sssp_records(mr_plan *pl, uint32_t i, mr_label_record *out) {
     uint32_t si = 0;
     if (int st = sssp_source(pl, i, si)) return st;
@@ -4044,10 +4060,7 @@ extern "C" int mr_sssp_records(mr_plan *pl, uint32_t i, mr_label_record *out) {
     const uint32_t V = pl->ka.p.V;
     std::vector<CellWord> words(V);
     std::vector<Rec> tab;
-    const uint32_t S = pl->ka.p.S, pitch = pl->ka.rec_pitch;
-    if (hipError_t e = hipMemcpy2D(words.data(), S * sizeof(CellWord), pl->d_rec + size_t(si) * S * pitch,
-                                   pitch * sizeof(CellWord), S * sizeof(CellWord), S, hipMemcpyDeviceToHost))
-        return fail(MR_ERR_DEVICE, std::string("copy records: ") + hipGetErrorString(e));
+    if (int st = copy_source_words(pl, si, words)) return st;
     if (int st = sssp_table(pl, si, tab)) return st;
     for (uint32_t v = 0; v < V; ++v)
         if (!expand_word(pl->hp, tab, words[v], out[v])) return fail(MR_ERR_DEVICE, "cell word names no table entry");
@@ -4161,12 +4174,10 @@ extern "C" int mr_sssp_labels(mr_plan *pl, uint32_t i, mr_result *results, mr_co
     if (int st = sssp_source(pl, i, si)) return st;
     if (!results) return fail(MR_ERR_INVALID_ARG, "null results");
     const mr_grid *g = pl->grid;
-    const uint32_t V = pl->ka.p.V, S = pl->ka.p.S, pitch = pl->ka.rec_pitch;
+    const uint32_t V = pl->ka.p.V;
     std::vector<CellWord> words(V);
     std::vector<Rec> tab;
-    if (hipError_t e = hipMemcpy2D(words.data(), S * sizeof(CellWord), pl->d_rec + size_t(si) * S * pitch,
-                                   pitch * sizeof(CellWord), S * sizeof(CellWord), S, hipMemcpyDeviceToHost))
-        return fail(MR_ERR_DEVICE, std::string("copy records: ") + hipGetErrorString(e));
+    if (int st = copy_source_words(pl, si, words)) return st;
     if (int st = sssp_table(pl, si, tab)) return st;
     const CmdScale cs = cmd_scale(pl->hp);
     std::vector<OutCmd> seq;
