@@ -3781,6 +3781,12 @@ static bool plan_fetch_wire(mr_plan *pl, mr_result *results, mr_command *pool, u
     const char *fw = std::getenv("MR_FETCH_WIRE");  // (0: the device decoder, plan_fetch_device)
     if ((fw && !std::strcmp(fw, "0")) || !pool || !nq || pl->all_mode || pl->grid->V > kWireRankMask + 1u || !pl->d_qi)
         return false;
+    // page-locked caller arrays (mr_host_register) take the device decoder's direct DMA:
+    // it costs the host no threads, and the host's writes here slow down when the
+    // process's other threads hold its CPU share (MR_FETCH_WIRE=1: the wire path anyway)
+    if (!(fw && !std::strcmp(fw, "1")) && host_pinned(results, size_t(nq) * sizeof(mr_result)) &&
+        host_pinned(pool, size_t(std::min<uint64_t>(pool_cap, uint64_t(nrec) * mc)) * sizeof(mr_command)))
+        return false;
     if (const char *e = std::getenv("MR_HOST_DECODE"))
         if (!std::strcmp(e, "1")) return false;
     const double tm0 = timing_on() ? now_ms() : 0.0;
@@ -3807,7 +3813,9 @@ static bool plan_fetch_wire(mr_plan *pl, mr_result *results, mr_command *pool, u
     const uint32_t *h_rows = reinterpret_cast<const uint32_t *>(h), *h_pool = h_rows + size_t(nq) * rw;
     // chunks of rows copied one after the other, the pool first (the rows of any chunk may
     // point into it); each host part decodes its share of a chunk once that has landed
-    const uint32_t nch = nq >= (1u << 18) ? 8u : 1u;
+    // (one chunk: the caller waits for the copies, then the pool decodes; the pool's threads
+    // waiting on per-chunk events spun through the process's CPU share on busy hosts)
+    const uint32_t nch = 1u;
     std::vector<hipEvent_t> ev(nch, nullptr);
     hipError_t e = wire_fetch_device(pl->ka.out_res, pl->ka.out_cmd, pl->ka.ovf, pl->d_counter + kCtrLastOvf, pl->ka.ovf_cap,
                                      pl->d_qi, nrec, nq, mc, d_cnt, d_off, dw + 2 * cnt_b, &temp_b, d_rows, d_pool, nov,
@@ -3827,6 +3835,7 @@ static bool plan_fetch_wire(mr_plan *pl, mr_result *results, mr_command *pool, u
     const mr_cell_index *cell = idx_of_rank(pl->grid);
     const uint32_t V = pl->grid->V;
     const uint32_t parts = nq >= 65536u ? hpool.size() : 1u;
+    if (e == hipSuccess) e = hipEventSynchronize(ev[nch - 1]);
     // per (chunk, part): the first error status in its queries, or MR_ERR_CAPACITY
     std::vector<int32_t> p_ret(size_t(nch) * parts, MR_OK), p_err(parts, MR_OK);
     std::vector<const char *> p_msg(parts, nullptr);
