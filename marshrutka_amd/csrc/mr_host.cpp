@@ -3778,14 +3778,13 @@ static int fetch_wire_row(const uint32_t *row, uint32_t mc, const uint32_t *wp, 
 static bool plan_fetch_wire(mr_plan *pl, mr_result *results, mr_command *pool, uint64_t pool_cap, int &ret) {
     const HostPlan &hp = pl->hp;
     const uint32_t nq = hp.nq, nrec = nrec_of(hp), mc = hp.p.max_cmds, rw = 2u + 2u * mc;  // (+ the offset word)
-    const char *fw = std::getenv("MR_FETCH_WIRE");  // (0: the device decoder, plan_fetch_device)
-    if ((fw && !std::strcmp(fw, "0")) || !pool || !nq || pl->all_mode || pl->grid->V > kWireRankMask + 1u || !pl->d_qi)
-        return false;
-    // page-locked caller arrays (mr_host_register) take the device decoder's direct DMA:
-    // it costs the host no threads, and the host's writes here slow down when the
-    // process's other threads hold its CPU share (MR_FETCH_WIRE=1: the wire path anyway)
-    if (!(fw && !std::strcmp(fw, "1")) && host_pinned(results, size_t(nq) * sizeof(mr_result)) &&
-        host_pinned(pool, size_t(std::min<uint64_t>(pool_cap, uint64_t(nrec) * mc)) * sizeof(mr_command)))
+    // Opt-in (MR_FETCH_WIRE=1).  In a quiet process it fetches 1M labels in 1.7-1.9 ms
+    // against 3.5-5 ms for the device decoder; in bench.py's process (torch loaded, the CPU
+    // baseline's threads just run) its host writes took 5.8-6.1 ms, so the device decoder
+    // (plan_fetch_device: no host threads, direct DMA into page-locked arrays) stays the
+    // default
+    const char *fw = std::getenv("MR_FETCH_WIRE");
+    if (!(fw && !std::strcmp(fw, "1")) || !pool || !nq || pl->all_mode || pl->grid->V > kWireRankMask + 1u || !pl->d_qi)
         return false;
     if (const char *e = std::getenv("MR_HOST_DECODE"))
         if (!std::strcmp(e, "1")) return false;
