@@ -65,9 +65,11 @@ __host__ __device__ constexpr uint32_t lane_waves(uint32_t TM) { return TM <= 22
     } while (0)
 #define MR_LANE_FENCE() MR_LANE_FENCE_AT(t)
 
-// pair-table reads issued this many entries ahead of their use in the relax loop
+// pair-table reads issued this many entries ahead of their use in the relax loop (round 6:
+// 0, in the entry's own step, 0.460 / 0.460 ms at c4 against 0.470 / 0.469 one entry ahead,
+// tools/r06/gpu_final_b.sh; round 5 had measured the opposite before the skips)
 #ifndef MR_LANE_PF
-#define MR_LANE_PF 1
+#define MR_LANE_PF 0
 #endif
 // relaxations of entries with no candidate in any lane of the wave skipped (1) or run as
 // no-ops (0)
