@@ -64,7 +64,7 @@ size_t group_scratch_bytes(uint32_t n, uint32_t V);
 hipError_t group_queries_device(const void *q, uint32_t n, const GroupGeom &geo, uint32_t lane_max_q, void *scratch,
                                 uint32_t *src_v, uint32_t *q_begin, uint32_t *q_dst, uint32_t *q_id, uint32_t *cnt,
                                 uint32_t *inv, uint32_t inv_cap, hipStream_t s);
-hipError_t partition_sources_device(uint32_t n, uint32_t V, uint32_t ns, uint32_t lane_max_q, const void *scratch,
+hipError_t partition_sources_device(uint32_t n, uint32_t V, uint32_t ns, uint32_t lane_max_q, bool desc, const void *scratch,
                                     const uint32_t *src_v, const uint32_t *q_begin, const uint32_t *q_dst,
                                     const uint32_t *q_id, const uint32_t *cnt, uint32_t *src2, uint32_t *qb2,
                                     uint32_t *qd2, uint32_t *qi2, hipStream_t s);
@@ -2023,6 +2023,13 @@ static uint32_t lane_min_sources() {
     return uint32_t(cus) * 160u;
 }
 
+// The lane kernel's count order: the busiest sources first (MR_LANE_ORDER=asc: the
+// least busy first), so the last waves of a launch are the shortest ones
+static bool lane_order_desc() {
+    const char *e = std::getenv("MR_LANE_ORDER");
+    return !(e && !std::strcmp(e, "asc"));
+}
+
 // Hub plans on the lane kernel: the sources with at most kLaneMaxQ queries first (one
 // source per lane, hub_lane_kernel), by query count (a wave runs its destination loop as
 // often as its busiest lane's source has queries: c4's uniform batch, 1.55 queries a
@@ -2032,9 +2039,10 @@ static uint32_t lane_min_sources() {
 static uint32_t partition_sources(HostPlan &hp) {
     const uint32_t ns = uint32_t(hp.src_v.size());
     std::vector<uint32_t> order(ns), start(kLaneMaxQ + 3, 0);
+    const bool desc = lane_order_desc();
     auto cls = [&](uint32_t i) {
         const uint32_t c = hp.q_begin[i + 1] - hp.q_begin[i];
-        return c <= kLaneMaxQ ? c : kLaneMaxQ + 1u;
+        return c <= kLaneMaxQ ? (desc ? kLaneMaxQ + 1u - c : c) : kLaneMaxQ + 1u;
     };
     for (uint32_t i = 0; i < ns; ++i) ++start[cls(i) + 1];
     for (uint32_t c = 1; c < start.size(); ++c) start[c] += start[c - 1];
@@ -2181,7 +2189,7 @@ static uint32_t partition_on_device(mr_plan *pl) {
     qblock_layout(hp.nq, at);
     uint32_t *blk = nullptr;
     if (pmalloc(reinterpret_cast<void **>(&blk), at[4] * 4) != hipSuccess) return kNone32;
-    hipError_t e = partition_sources_device(hp.nq, pl->grid->V, hp.nsrc, kLaneMaxQ, pl->d_gscratch, pl->d_src, pl->d_qb,
+    hipError_t e = partition_sources_device(hp.nq, pl->grid->V, hp.nsrc, kLaneMaxQ, lane_order_desc(), pl->d_gscratch, pl->d_src, pl->d_qb,
                                             pl->d_qd, pl->d_qi, pl->d_gcnt, blk + at[0], blk + at[1], blk + at[2],
                                             blk + at[3], pl->stream);
     const hipError_t es = hipStreamSynchronize(pl->stream);

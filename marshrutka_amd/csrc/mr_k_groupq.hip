@@ -154,11 +154,11 @@ __global__ __launch_bounds__(kGBS) void gq_part_q_kernel(const uint32_t *__restr
 // the lane kernel's order (phase 2): per source its class key (its query count when at
 // most lane_max_q, else lane_max_q + 1: after every small one) and its index
 __global__ __launch_bounds__(kGBS) void gq_class_kernel(const uint32_t *__restrict__ q_begin, uint32_t ns,
-                                                        uint32_t lane_max_q, uint32_t *__restrict__ key,
+                                                        uint32_t lane_max_q, bool desc, uint32_t *__restrict__ key,
                                                         uint32_t *__restrict__ val) {
     for (uint32_t s = blockIdx.x * kGBS + threadIdx.x; s < ns; s += gridDim.x * kGBS) {
         const uint32_t c = q_begin[s + 1] - q_begin[s];
-        key[s] = c <= lane_max_q ? c : lane_max_q + 1u;
+        key[s] = c <= lane_max_q ? (desc ? lane_max_q + 1u - c : c) : lane_max_q + 1u;
         val[s] = s;
     }
 }
@@ -276,7 +276,7 @@ hipError_t group_queries_device(const void *q, uint32_t n, const GroupGeom &geo,
 // more queries (hub_kernel's), each class in source order.  A wave of the lane kernel runs
 // its destination loop as often as its busiest lane's source has queries: grouped by
 // count, its 64 sources have the same.  Reads phase 1's scratch and counts; ns: the sources.
-hipError_t partition_sources_device(uint32_t n, uint32_t V, uint32_t ns, uint32_t lane_max_q, const void *scratch,
+hipError_t partition_sources_device(uint32_t n, uint32_t V, uint32_t ns, uint32_t lane_max_q, bool desc, const void *scratch,
                                     const uint32_t *src_v, const uint32_t *q_begin, const uint32_t *q_dst,
                                     const uint32_t *q_id, const uint32_t *cnt, uint32_t *src2, uint32_t *qb2,
                                     uint32_t *qd2, uint32_t *qi2, hipStream_t s) {
@@ -300,7 +300,7 @@ hipError_t partition_sources_device(uint32_t n, uint32_t V, uint32_t ns, uint32_
         (void)hipcub::DeviceScan::ExclusiveSum(nullptr, need_scan, c_sorted, off, int(ns), s);
         if (need_sort > tb || need_scan > tb) return hipErrorInvalidValue;
     }
-    hipLaunchKernelGGL(gq_class_kernel, dim3(gs), dim3(kGBS), 0, s, q_begin, ns, lane_max_q, k_in, v_in);
+    hipLaunchKernelGGL(gq_class_kernel, dim3(gs), dim3(kGBS), 0, s, q_begin, ns, lane_max_q, desc, k_in, v_in);
     hipError_t e = hipGetLastError();
     // stable: equal classes keep the source order (by cell)
     if (e == hipSuccess)
